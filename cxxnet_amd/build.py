@@ -1,0 +1,121 @@
+"""In-tree native build for cxxnet_amd.
+
+Produces, under ``cxxnet_amd/_native/``:
+  * ``_cxxnet_rt<EXT_SUFFIX>``  -- pybind11 module: config parser, NetConfig,
+    checkpoint PODs, data IO, metrics (g++, no GPU dependency).
+  * ``libcxxnet_kernels.so``     -- every hand-written HIP kernel for gfx950,
+    exported through a flat C ABI (hipcc --offload-arch=gfx950).
+  * ``libcxxnetwrapper.so``      -- the CXN* C ABI (embeds CPython).
+
+Run ``python -m cxxnet_amd.build`` (or ``__graft_entry__.build()``).  Builds are
+incremental: a target is rebuilt when any of its sources/headers is newer.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+OUT = os.path.join(PKG, "_native")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.path.join(ROCM, "bin", "hipcc")
+ARCH = os.environ.get("CXXNET_OFFLOAD_ARCH", "gfx950")
+
+RT_NAME = "_cxxnet_rt" + sysconfig.get_config_var("EXT_SUFFIX")
+KERNEL_LIB = "libcxxnet_kernels.so"
+WRAPPER_LIB = "libcxxnetwrapper.so"
+
+
+def _newer(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build failed:\n" + " ".join(cmd) + "\n" + r.stdout)
+    return r.stdout
+
+
+def build_runtime(verbose=False, force=False) -> str:
+    import pybind11
+
+    src = os.path.join(CSRC, "runtime", "bindings.cpp")
+    deps = [src] + glob.glob(os.path.join(CSRC, "runtime", "*.h"))
+    target = os.path.join(OUT, RT_NAME)
+    if force or _newer(target, deps):
+        os.makedirs(OUT, exist_ok=True)
+        cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wall", "-Wno-unused-result",
+               "-fvisibility=hidden",
+               "-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"],
+               src, "-o", target + ".tmp", "-lz", "-lpthread"]
+        _run(cmd, verbose)
+        os.replace(target + ".tmp", target)
+    return target
+
+
+def build_kernels(verbose=False, force=False, jobs=8) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    hdrs = glob.glob(os.path.join(CSRC, "kernels", "*.h"))
+    target = os.path.join(OUT, KERNEL_LIB)
+    objdir = os.path.join(OUT, "obj")
+    os.makedirs(objdir, exist_ok=True)
+    common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+              "-munsafe-fp-atomics", "-Wno-unused-result",
+              "-I" + os.path.join(CSRC, "kernels")]
+    objs = []
+    jobs_list = []
+    for s in srcs:
+        o = os.path.join(objdir, os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _newer(o, [s] + hdrs):
+            jobs_list.append(common + ["-c", s, "-o", o])
+    if jobs_list:
+        with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+            list(ex.map(lambda c: _run(c, verbose), jobs_list))
+    if force or _newer(target, objs) or jobs_list:
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", target + ".tmp"], verbose)
+        os.replace(target + ".tmp", target)
+    return target
+
+
+def build_wrapper(verbose=False, force=False) -> str:
+    src = os.path.join(CSRC, "capi", "cxxnet_wrapper.cpp")
+    if not os.path.exists(src):
+        return ""
+    deps = [src] + glob.glob(os.path.join(CSRC, "capi", "*.h"))
+    target = os.path.join(OUT, WRAPPER_LIB)
+    if force or _newer(target, deps):
+        libdir = sysconfig.get_config_var("LIBDIR")
+        ver = sysconfig.get_config_var("LDVERSION")
+        cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wall",
+               "-I" + sysconfig.get_paths()["include"], "-I" + os.path.join(CSRC, "capi"),
+               src, "-o", target + ".tmp", "-L" + libdir, "-lpython" + ver,
+               "-Wl,-rpath," + libdir]
+        _run(cmd, verbose)
+        os.replace(target + ".tmp", target)
+    return target
+
+
+def build_all(verbose=False, force=False):
+    rt = build_runtime(verbose, force)
+    k = build_kernels(verbose, force)
+    w = build_wrapper(verbose, force)
+    return rt, k, w
+
+
+if __name__ == "__main__":
+    force = "--force" in sys.argv
+    for p in build_all(verbose=True, force=force):
+        if p:
+            print("built", p)

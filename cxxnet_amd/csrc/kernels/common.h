@@ -1,0 +1,63 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define CXN_API extern "C" __attribute__((visibility("default")))
+
+typedef unsigned short bf16_t;  // storage type for bf16 tensors
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(static_cast<uint32_t>(v) << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = static_cast<__bf16>(f);  // lowers to v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+// 8 x bf16 packed in a uint4 (16 B) -- the unit of every vectorised access.
+__device__ __forceinline__ void unpack8(const uint4 &v, float *f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return static_cast<uint32_t>(f2bf(a)) | (static_cast<uint32_t>(f2bf(b)) << 16);
+}
+__device__ __forceinline__ uint4 pack8(const float *f) {
+  return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+}
+
+// Division by a runtime-invariant divisor with a multiply-high (n < 2^31).
+struct FastDiv {
+  uint32_t d, mul, shift;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  f.shift = l;
+  f.mul = static_cast<uint32_t>(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f) {
+  return (__umulhi(n, f.mul) + n) >> f.shift;
+}
+
+// XCD-aware bijective remap of a 1-D block id: consecutive logical tiles land on
+// the same XCD (blocks b and b+8 share an XCD under round-robin dispatch), so
+// neighbouring tiles share that XCD's L2.  Speed-only; any placement is correct.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t orig, uint32_t nwg) {
+  if (nwg < 16) return orig;
+  const uint32_t q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+static inline int cdiv(long a, long b) { return static_cast<int>((a + b - 1) / b); }

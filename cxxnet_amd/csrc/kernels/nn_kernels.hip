@@ -1,0 +1,586 @@
+// Memory-bound layer kernels for gfx950, all on NHWC bf16 activations with
+// 16-byte (8 x bf16) vector accesses per lane.
+//
+//   layout      : NCHW fp32 -> NHWC bf16 (input, channel pad), NHWC -> NCHW, conv weight flip
+//   pooling     : max/sum/avg fwd + gather-form bwd (reference src/layer/pooling_layer-inl.hpp:42-111)
+//   lrn         : cross-channel LRN fwd/bwd      (reference src/layer/lrn_layer-inl.hpp:53-74)
+//   activation  : relu/sigmoid/tanh/xelu fwd/bwd (reference src/layer/op.h, activation_layer-inl.hpp)
+//   dropout     : counter-hash mask, no mask storage (reference src/layer/dropout_layer-inl.hpp:44-57)
+//   softmax     : row softmax + (p - onehot) * scale grad on device (reference loss/softmax_layer-inl.hpp)
+//   bias grad   : column sums of an [rows][C] bf16 matrix into fp32 (reference K5/K11)
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+__device__ __forceinline__ int grid_stride_start() { return blockIdx.x * blockDim.x + threadIdx.x; }
+__device__ __forceinline__ int grid_stride() { return gridDim.x * blockDim.x; }
+
+static inline int nblocks(long n, int per_block = NT, int cap = 256 * 16) {
+  long b = (n + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  return static_cast<int>(b > cap ? cap : b);
+}
+
+// ------------------------------------------------------------------ layout
+// x: NCHW fp32 [N][C][H][W] -> y: NHWC bf16 [N][H][W][Cp] (channels >= C zero-filled)
+__global__ void nchw_f32_to_nhwc_bf16(const float *__restrict__ x, bf16_t *__restrict__ y, int N, int C, int H,
+                                      int W, int Cp, float scale) {
+  const long total = static_cast<long>(N) * H * W;
+  for (long pix = grid_stride_start(); pix < total; pix += grid_stride()) {
+    const long n = pix / (static_cast<long>(H) * W);
+    const long hw = pix - n * H * W;
+    const float *src = x + n * C * H * W + hw;
+    bf16_t *dst = y + pix * Cp;
+    for (int c = 0; c < Cp; ++c) dst[c] = c < C ? f2bf(src[static_cast<long>(c) * H * W] * scale) : 0;
+  }
+}
+
+// x: NHWC bf16 [N][H][W][Cp] -> y: NCHW fp32 [N][C][H][W]
+__global__ void nhwc_bf16_to_nchw_f32(const bf16_t *__restrict__ x, float *__restrict__ y, int N, int C, int H,
+                                      int W, int Cp) {
+  const long total = static_cast<long>(N) * C * H * W;
+  for (long i = grid_stride_start(); i < total; i += grid_stride()) {
+    const long w = i % W;
+    long t = i / W;
+    const long h = t % H;
+    t /= H;
+    const long c = t % C;
+    const long n = t / C;
+    y[i] = bf2f(x[((n * H + h) * W + w) * Cp + c]);
+  }
+}
+
+// Batched 2-D transpose x[b][R][Cc] -> y[b][Cc][R] (bf16), tiled through LDS.
+// Flatten of an NHWC activation into the reference's NCHW feature order is
+// transpose(R=HW, Cc=C); its gradient is transpose(R=C, Cc=HW).
+__global__ void batched_transpose(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, int R, int Cc) {
+  __shared__ bf16_t tile[32][34];
+  const long base = static_cast<long>(blockIdx.z) * R * Cc;
+  const int r0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+  for (int r = ty; r < 32; r += 8)
+    if (r0 + r < R && c0 + tx < Cc) tile[r][tx] = x[base + static_cast<long>(r0 + r) * Cc + c0 + tx];
+  __syncthreads();
+  for (int c = ty; c < 32; c += 8)
+    if (c0 + c < Cc && r0 + tx < R) y[base + static_cast<long>(c0 + c) * R + r0 + tx] = tile[tx][c];
+}
+
+// Conv weight transform for data-grad: W[g][co][kh][kw][ci] -> Wt[g][ci][KH-1-kh][KW-1-kw][co]
+__global__ void conv_weight_flip(const bf16_t *__restrict__ w, bf16_t *__restrict__ wt, int G, int Co, int KH,
+                                 int KW, int Ci) {
+  const long total = static_cast<long>(G) * Co * KH * KW * Ci;
+  for (long i = grid_stride_start(); i < total; i += grid_stride()) {
+    long t = i;
+    const int ci = t % Ci; t /= Ci;
+    const int kw = t % KW; t /= KW;
+    const int kh = t % KH; t /= KH;
+    const int co = t % Co;
+    const int g = t / Co;
+    const long o = ((((static_cast<long>(g) * Ci + ci) * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)) * Co) + co;
+    wt[o] = w[i];
+  }
+}
+
+// ------------------------------------------------------------------ pooling
+// mode: 0 max, 1 sum, 2 avg.  relu: apply relu before max (relu_max_pooling).
+// Output size follows the reference ceil rule: min(Hp - k + s - 1, Hp - 1) / s + 1, Hp = H + 2 pad.
+template <int VEC>
+__global__ void pool_fwd(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, bf16_t *__restrict__ y2, int N, int H, int W, int C, int Ho,
+                         int Wo, int KH, int KW, int S, int P, int mode, int relu) {
+  const int CV = C / VEC;
+  const long total = static_cast<long>(N) * Ho * Wo * CV;
+  const float inv = 1.0f / (KH * KW);
+  for (long idx = grid_stride_start(); idx < total; idx += grid_stride()) {
+    const int cv = idx % CV;
+    long t = idx / CV;
+    const int wo = t % Wo; t /= Wo;
+    const int ho = t % Ho;
+    const int n = t / Ho;
+    const int hs = ho * S - P, ws = wo * S - P;
+    const int he = min(hs + KH, H), we = min(ws + KW, W);
+    float acc[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc[e] = mode == 0 ? -INFINITY : 0.f;
+    for (int h = max(hs, 0); h < he; ++h)
+      for (int w = max(ws, 0); w < we; ++w) {
+        const bf16_t *p = x + ((static_cast<long>(n) * H + h) * W + w) * C + cv * VEC;
+        float v[VEC];
+        if constexpr (VEC == 8) unpack8(*reinterpret_cast<const uint4 *>(p), v);
+        else v[0] = bf2f(*p);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          float a = relu ? fmaxf(v[e], 0.f) : v[e];
+          acc[e] = mode == 0 ? fmaxf(acc[e], a) : acc[e] + a;
+        }
+      }
+    if (mode == 2)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) acc[e] *= inv;
+    if constexpr (VEC == 8) {
+      const uint4 o = pack8(acc);
+      *reinterpret_cast<uint4 *>(y + idx * VEC) = o;
+      if (y2) *reinterpret_cast<uint4 *>(y2 + idx * VEC) = o;
+    } else {
+      y[idx] = f2bf(acc[0]);
+      if (y2) y2[idx] = f2bf(acc[0]);
+    }
+  }
+}
+
+// Gather-form backward: each input element sums over the windows that contain it.
+// Max: every input equal to the window maximum receives the gradient (value compare,
+// reference unpool semantics).  relu: multiply by relu'(x).
+template <int VEC>
+__global__ void pool_bwd(const bf16_t *__restrict__ x, const bf16_t *__restrict__ y, const bf16_t *__restrict__ dy,
+                         bf16_t *__restrict__ dx, int N, int H, int W, int C, int Ho, int Wo, int KH, int KW, int S,
+                         int P, int mode, int relu) {
+  const int CV = C / VEC;
+  const long total = static_cast<long>(N) * H * W * CV;
+  const float inv = 1.0f / (KH * KW);
+  for (long idx = grid_stride_start(); idx < total; idx += grid_stride()) {
+    const int cv = idx % CV;
+    long t = idx / CV;
+    const int w = t % W; t /= W;
+    const int h = t % H;
+    const int n = t / H;
+    float xv[VEC], g[VEC];
+    if (mode == 0 || relu) {
+      if constexpr (VEC == 8) unpack8(*reinterpret_cast<const uint4 *>(x + idx * VEC), xv);
+      else xv[0] = bf2f(x[idx]);
+    }
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) g[e] = 0.f;
+    // windows ho with ho*S - P <= h < ho*S - P + KH
+    const int hlo = max(0, (h + P - KH + S) / S), hhi = min(Ho - 1, (h + P) / S);
+    const int wlo = max(0, (w + P - KW + S) / S), whi = min(Wo - 1, (w + P) / S);
+    for (int ho = hlo; ho <= hhi; ++ho)
+      for (int wo = wlo; wo <= whi; ++wo) {
+        const long o = ((static_cast<long>(n) * Ho + ho) * Wo + wo) * C + cv * VEC;
+        float gv[VEC], yv[VEC];
+        if constexpr (VEC == 8) {
+          unpack8(*reinterpret_cast<const uint4 *>(dy + o), gv);
+          if (mode == 0) unpack8(*reinterpret_cast<const uint4 *>(y + o), yv);
+        } else {
+          gv[0] = bf2f(dy[o]);
+          if (mode == 0) yv[0] = bf2f(y[o]);
+        }
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          if (mode == 0) {
+            const float xr = relu ? fmaxf(xv[e], 0.f) : xv[e];
+            // y was rounded to bf16 from the same bf16 inputs, so equality is exact
+            g[e] += (xr == yv[e]) ? gv[e] : 0.f;
+          } else {
+            g[e] += mode == 2 ? gv[e] * inv : gv[e];
+          }
+        }
+      }
+    if (relu)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) g[e] = xv[e] > 0.f ? g[e] : 0.f;
+    if constexpr (VEC == 8) *reinterpret_cast<uint4 *>(dx + idx * VEC) = pack8(g);
+    else dx[idx] = f2bf(g[0]);
+  }
+}
+
+// ------------------------------------------------------------------ LRN
+// norm[c] = knorm + alpha/n * sum_{c' in [c-h, c+h] clipped} x[c']^2 ; y = x * norm^-beta
+// One thread per (pixel, 8 channels); halo of up to 8 channels each side via three 16-B loads.
+__device__ __forceinline__ void load_window(const bf16_t *row, int C, int c0, float *buf /*[24]*/) {
+  // buf[j] = x[c0 - 8 + j], zero outside [0, C)
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const int cs = c0 - 8 + 8 * b;
+    float v[8];
+    if (cs >= 0 && cs + 8 <= C) {
+      unpack8(*reinterpret_cast<const uint4 *>(row + cs), v);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (cs + e >= 0 && cs + e < C) ? bf2f(row[cs + e]) : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) buf[8 * b + e] = v[e];
+  }
+}
+
+__global__ void lrn_fwd(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, long npix, int C, int half,
+                        float salpha, float beta, float knorm) {
+  const int CV = C / 8;
+  const long total = npix * CV;
+  for (long idx = grid_stride_start(); idx < total; idx += grid_stride()) {
+    const long pix = idx / CV;
+    const int c0 = (idx % CV) * 8;
+    const bf16_t *row = x + pix * C;
+    float xb[24];
+    load_window(row, C, c0, xb);
+    float out[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float s = 0.f;
+      for (int d = -half; d <= half; ++d) {
+        const float v = xb[8 + e + d];
+        s += v * v;
+      }
+      const float norm = knorm + salpha * s;
+      out[e] = xb[8 + e] * exp2f(-beta * __log2f(norm));
+    }
+    *reinterpret_cast<uint4 *>(y + pix * C + c0) = pack8(out);
+  }
+}
+
+// g_in[c] = g[c] norm[c]^-b - 2 b salpha x[c] sum_{c' in win(c)} g[c'] x[c'] norm[c']^(-b-1)
+// (norm recomputed from x: no state tensor is stored)
+__global__ void lrn_bwd(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, bf16_t *__restrict__ dx,
+                        long npix, int C, int half, float salpha, float beta, float knorm) {
+  const int CV = C / 8;
+  const long total = npix * CV;
+  for (long idx = grid_stride_start(); idx < total; idx += grid_stride()) {
+    const long pix = idx / CV;
+    const int c0 = (idx % CV) * 8;
+    float xb[24], gb[24];
+    load_window(x + pix * C, C, c0, xb);
+    load_window(dy + pix * C, C, c0, gb);
+    // t[j] = g x norm^(-b-1) for channels c0-8+j, j in [8-half, 16+half)
+    float normv[24], tv[24];
+#pragma unroll
+    for (int j = 0; j < 24; ++j) {
+      normv[j] = 1.f;
+      tv[j] = 0.f;
+    }
+    for (int j = 8 - half; j < 16 + half; ++j) {
+      float s = 0.f;
+      for (int d = -half; d <= half; ++d) {
+        const int q = j + d;
+        const float v = (q >= 0 && q < 24) ? xb[q] : 0.f;
+        s += v * v;
+      }
+      const float norm = knorm + salpha * s;
+      normv[j] = norm;
+      tv[j] = gb[j] * xb[j] * exp2f((-beta - 1.f) * __log2f(norm));
+    }
+    float out[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int j = 8 + e;
+      float s = 0.f;
+      for (int d = -half; d <= half; ++d) s += tv[j + d];
+      out[e] = gb[j] * exp2f(-beta * __log2f(normv[j])) - 2.f * beta * salpha * xb[j] * s;
+    }
+    *reinterpret_cast<uint4 *>(dx + pix * C + c0) = pack8(out);
+  }
+}
+
+// ------------------------------------------------------------------ activations
+// kind: 0 relu, 1 sigmoid, 2 tanh, 3 xelu(b).  Backward is written in terms of the
+// forward OUTPUT y (the reference stores activations in place, src/layer/op.h:32-73).
+__device__ __forceinline__ float act_f(int kind, float x, float b) {
+  switch (kind) {
+    case 0: return fmaxf(x, 0.f);
+    case 1: return 1.f / (1.f + __expf(-x));
+    case 2: return tanhf(x);
+    default: return x > 0.f ? x : x / b;
+  }
+}
+__device__ __forceinline__ float act_g(int kind, float y, float b) {
+  switch (kind) {
+    case 0: return y > 0.f ? 1.f : 0.f;
+    case 1: return y * (1.f - y);
+    case 2: return 1.f - y * y;
+    default: return y > 0.f ? 1.f : 1.f / b;
+  }
+}
+
+// y (and y2 when non-null, the reference's in-place write of the input node) = f(x)
+__global__ void act_fwd(const bf16_t *__restrict__ x, bf16_t *y, bf16_t *y2, long n, int kind, float b) {
+  const long n8 = n / 8;
+  for (long i = grid_stride_start(); i < n8; i += grid_stride()) {
+    float v[8];
+    unpack8(reinterpret_cast<const uint4 *>(x)[i], v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = act_f(kind, v[e], b);
+    const uint4 o = pack8(v);
+    reinterpret_cast<uint4 *>(y)[i] = o;
+    if (y2) reinterpret_cast<uint4 *>(y2)[i] = o;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < n - n8 * 8) {
+    const long i = n8 * 8 + threadIdx.x;
+    const bf16_t o = f2bf(act_f(kind, bf2f(x[i]), b));
+    y[i] = o;
+    if (y2) y2[i] = o;
+  }
+}
+__global__ void act_bwd(const bf16_t *y, const bf16_t *dy, bf16_t *dx, long n, int kind, float b) {
+  const long n8 = n / 8;
+  for (long i = grid_stride_start(); i < n8; i += grid_stride()) {
+    float yv[8], g[8];
+    unpack8(reinterpret_cast<const uint4 *>(y)[i], yv);
+    unpack8(reinterpret_cast<const uint4 *>(dy)[i], g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] *= act_g(kind, yv[e], b);
+    reinterpret_cast<uint4 *>(dx)[i] = pack8(g);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < n - n8 * 8) {
+    const long i = n8 * 8 + threadIdx.x;
+    dx[i] = f2bf(bf2f(dy[i]) * act_g(kind, bf2f(y[i]), b));
+  }
+}
+
+// ------------------------------------------------------------------ dropout
+// keep iff hash(seed, i) < pkeep * 2^32; x *= keep / pkeep.  The same call with the same
+// seed in backward regenerates the mask, so no mask tensor is stored.
+__device__ __forceinline__ uint32_t hash_u32(uint32_t x, uint32_t seed) {
+  x ^= seed * 0x9E3779B9u;
+  x ^= x >> 16; x *= 0x7FEB352Du;
+  x ^= x >> 15; x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+__global__ void dropout_apply(const bf16_t *x, bf16_t *y, long n, uint32_t seed0, const int *counter,
+                              uint32_t thresh, float scale) {
+  // counter (device, nullable) lets a captured HIP graph draw a fresh mask every replay
+  const uint32_t seed = counter ? hash_u32(static_cast<uint32_t>(*counter), seed0) : seed0;
+  const long n8 = n / 8;
+  if (blockIdx.x == 0 && threadIdx.x < n - n8 * 8) {
+    const long i = n8 * 8 + threadIdx.x;
+    y[i] = f2bf(hash_u32(static_cast<uint32_t>(i), seed) < thresh ? bf2f(x[i]) * scale : 0.f);
+  }
+  for (long i = grid_stride_start(); i < n8; i += grid_stride()) {
+    float v[8];
+    unpack8(reinterpret_cast<const uint4 *>(x)[i], v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const uint32_t h = hash_u32(static_cast<uint32_t>(i * 8 + e), seed);
+      v[e] = h < thresh ? v[e] * scale : 0.f;
+    }
+    reinterpret_cast<uint4 *>(y)[i] = pack8(v);
+  }
+}
+
+// ------------------------------------------------------------------ softmax / loss
+// One wave per row.  p = softmax(x) written to y (bf16) and optionally pf (fp32).
+__global__ void softmax_rows(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, float *__restrict__ pf,
+                             int rows, int K) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const bf16_t *xr = x + static_cast<long>(row) * K;
+  float m = -INFINITY;
+  for (int k = lane; k < K; k += 64) m = fmaxf(m, bf2f(xr[k]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  float s = 0.f;
+  for (int k = lane; k < K; k += 64) s += __expf(bf2f(xr[k]) - m);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float inv = 1.f / s;
+  for (int k = lane; k < K; k += 64) {
+    const float p = __expf(bf2f(xr[k]) - m) * inv;
+    y[static_cast<long>(row) * K + k] = f2bf(p);
+    if (pf) pf[static_cast<long>(row) * K + k] = p;
+  }
+}
+
+// grad = (p - onehot(label)) * scale, written in place over the bf16 node.  kind 0 softmax,
+// 1 l2 (x - y), 2 multi-logistic (sigma - y, node already holds sigma).  label: fp32 [rows][lw]
+__global__ void loss_grad(const float *__restrict__ p32, bf16_t *__restrict__ node, const float *__restrict__ label,
+                          int rows, int K, int lw, float scale, int kind) {
+  const long total = static_cast<long>(rows) * K;
+  for (long i = grid_stride_start(); i < total; i += grid_stride()) {
+    const int r = i / K, k = i % K;
+    const float p = p32 ? p32[i] : bf2f(node[i]);
+    float g;
+    if (kind == 0) g = p - (static_cast<int>(label[static_cast<long>(r) * lw]) == k ? 1.f : 0.f);
+    else g = p - label[static_cast<long>(r) * lw + k];
+    node[i] = f2bf(g * scale);
+  }
+}
+
+// ------------------------------------------------------------------ bias gradient
+// db[c] += sum_r dy[r][c]  (dy bf16 [rows][C], C % 8 == 0).  Block = CB column-vectors x RG row
+// groups; per-thread fp32 partials, LDS tree over RG, one atomic per channel per block.
+__global__ void colsum_bf16(const bf16_t *__restrict__ dy, float *__restrict__ db, long rows, int C,
+                            int rows_per_block) {
+  const int CV = C / 8;
+  const int CB = min(CV - static_cast<int>(blockIdx.y) * 64, 64);
+  const int RG = NT / CB;
+  const int t = threadIdx.x;
+  const int cvl = t % CB, rg = t / CB;
+  const int cv = blockIdx.y * 64 + cvl;
+  const long r0 = static_cast<long>(blockIdx.x) * rows_per_block;
+  const long r1 = min(rows, r0 + rows_per_block);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (rg < RG) {
+    for (long r = r0 + rg; r < r1; r += RG) {
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4 *>(dy + r * C + cv * 8), v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+  }
+  __shared__ float red[NT][9];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[t][e] = (rg < RG) ? acc[e] : 0.f;
+  __syncthreads();
+  for (int q = t; q < CB * 8; q += NT) {
+    const int c = q / 8, e = q % 8;
+    float s = 0.f;
+    for (int g = 0; g < RG; ++g) s += red[g * CB + c][e];
+    atomicAdd(db + (blockIdx.y * 64 + c) * 8 + e, s);
+  }
+}
+
+// Small / ragged C: one thread per column.
+__global__ void colsum_scalar(const bf16_t *__restrict__ dy, float *__restrict__ db, long rows, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (long r = 0; r < rows; ++r) s += bf2f(dy[r * C + c]);
+  db[c] += s;
+}
+
+// ------------------------------------------------------------------ elementwise helpers
+__global__ void cast_f32_bf16(const float *__restrict__ x, bf16_t *__restrict__ y, long n) {
+  for (long i = grid_stride_start(); i < n; i += grid_stride()) y[i] = f2bf(x[i]);
+}
+__global__ void add_bf16(const bf16_t *a, const bf16_t *b, bf16_t *y, long n) {
+  const long n8 = n / 8;
+  if (blockIdx.x == 0 && threadIdx.x < n - n8 * 8) {
+    const long i = n8 * 8 + threadIdx.x;
+    y[i] = f2bf(bf2f(a[i]) + bf2f(b[i]));
+  }
+  for (long i = grid_stride_start(); i < n8; i += grid_stride()) {
+    float x[8], z[8];
+    unpack8(reinterpret_cast<const uint4 *>(a)[i], x);
+    unpack8(reinterpret_cast<const uint4 *>(b)[i], z);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] += z[e];
+    reinterpret_cast<uint4 *>(y)[i] = pack8(x);
+  }
+}
+// strided channel copy for ch_concat / slicing: dst[p][doff + c] = src[p][soff + c], c < Cc
+__global__ void channel_copy(const bf16_t *__restrict__ src, int Cs, int soff, bf16_t *__restrict__ dst, int Cd,
+                             int doff, int Cc, long npix, int accumulate) {
+  const long total = npix * Cc;
+  for (long i = grid_stride_start(); i < total; i += grid_stride()) {
+    const long p = i / Cc;
+    const int c = i % Cc;
+    const float v = bf2f(src[p * Cs + soff + c]);
+    bf16_t *d = dst + p * Cd + doff + c;
+    *d = f2bf(accumulate ? bf2f(*d) + v : v);
+  }
+}
+
+}  // namespace
+
+// ================================================================== C ABI
+#define S_ static_cast<hipStream_t>(stream)
+#define RET return hipGetLastError() == hipSuccess ? 0 : -3
+
+CXN_API int cxn_nchw_f32_to_nhwc_bf16(const float *x, void *y, int N, int C, int H, int W, int Cp, float scale,
+                                      void *stream) {
+  nchw_f32_to_nhwc_bf16<<<nblocks(static_cast<long>(N) * H * W), NT, 0, S_>>>(x, (bf16_t *)y, N, C, H, W, Cp, scale);
+  RET;
+}
+CXN_API int cxn_nhwc_bf16_to_nchw_f32(const void *x, float *y, int N, int C, int H, int W, int Cp, void *stream) {
+  nhwc_bf16_to_nchw_f32<<<nblocks(static_cast<long>(N) * C * H * W), NT, 0, S_>>>((const bf16_t *)x, y, N, C, H, W, Cp);
+  RET;
+}
+CXN_API int cxn_transpose(const void *x, void *y, int B, int R, int Cc, void *stream) {
+  dim3 grid(cdiv(R, 32), cdiv(Cc, 32), B);
+  batched_transpose<<<grid, NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, R, Cc);
+  RET;
+}
+CXN_API int cxn_conv_weight_flip(const void *w, void *wt, int G, int Co, int KH, int KW, int Ci, void *stream) {
+  conv_weight_flip<<<nblocks(static_cast<long>(G) * Co * KH * KW * Ci), NT, 0, S_>>>((const bf16_t *)w, (bf16_t *)wt,
+                                                                                     G, Co, KH, KW, Ci);
+  RET;
+}
+CXN_API int cxn_pool_fwd(const void *x, void *y, void *y2, int N, int H, int W, int C, int Ho, int Wo, int KH, int KW, int S,
+                         int P, int mode, int relu, void *stream) {
+  if (C % 8 == 0) {
+    pool_fwd<8><<<nblocks(static_cast<long>(N) * Ho * Wo * C / 8), NT, 0, S_>>>(
+        (const bf16_t *)x, (bf16_t *)y, (bf16_t *)y2, N, H, W, C, Ho, Wo, KH, KW, S, P, mode, relu);
+  } else {
+    pool_fwd<1><<<nblocks(static_cast<long>(N) * Ho * Wo * C), NT, 0, S_>>>(
+        (const bf16_t *)x, (bf16_t *)y, (bf16_t *)y2, N, H, W, C, Ho, Wo, KH, KW, S, P, mode, relu);
+  }
+  RET;
+}
+CXN_API int cxn_pool_bwd(const void *x, const void *y, const void *dy, void *dx, int N, int H, int W, int C, int Ho,
+                         int Wo, int KH, int KW, int S, int P, int mode, int relu, void *stream) {
+  if (C % 8 == 0) {
+    pool_bwd<8><<<nblocks(static_cast<long>(N) * H * W * C / 8), NT, 0, S_>>>(
+        (const bf16_t *)x, (const bf16_t *)y, (const bf16_t *)dy, (bf16_t *)dx, N, H, W, C, Ho, Wo, KH, KW, S, P, mode,
+        relu);
+  } else {
+    pool_bwd<1><<<nblocks(static_cast<long>(N) * H * W * C), NT, 0, S_>>>(
+        (const bf16_t *)x, (const bf16_t *)y, (const bf16_t *)dy, (bf16_t *)dx, N, H, W, C, Ho, Wo, KH, KW, S, P, mode,
+        relu);
+  }
+  RET;
+}
+CXN_API int cxn_lrn_fwd(const void *x, void *y, long npix, int C, int nsize, float alpha, float beta, float knorm,
+                        void *stream) {
+  if (C % 8 != 0 || nsize / 2 > 4) return -1;
+  lrn_fwd<<<nblocks(npix * C / 8), NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, npix, C, nsize / 2, alpha / nsize,
+                                                 beta, knorm);
+  RET;
+}
+CXN_API int cxn_lrn_bwd(const void *x, const void *dy, void *dx, long npix, int C, int nsize, float alpha, float beta,
+                        float knorm, void *stream) {
+  if (C % 8 != 0 || nsize / 2 > 4) return -1;
+  lrn_bwd<<<nblocks(npix * C / 8), NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C,
+                                                 nsize / 2, alpha / nsize, beta, knorm);
+  RET;
+}
+CXN_API int cxn_act_fwd(const void *x, void *y, void *y2, long n, int kind, float b, void *stream) {
+  act_fwd<<<nblocks(n / 8 + 1), NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, (bf16_t *)y2, n, kind, b);
+  RET;
+}
+CXN_API int cxn_act_bwd(const void *y, const void *dy, void *dx, long n, int kind, float b, void *stream) {
+  act_bwd<<<nblocks(n / 8 + 1), NT, 0, S_>>>((const bf16_t *)y, (const bf16_t *)dy, (bf16_t *)dx, n, kind, b);
+  RET;
+}
+CXN_API int cxn_dropout(const void *x, void *y, long n, unsigned seed, const int *counter, float pkeep,
+                        void *stream) {
+  const double t = static_cast<double>(pkeep) * 4294967296.0;
+  const uint32_t thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : static_cast<uint32_t>(t);
+  dropout_apply<<<nblocks(n / 8 + 1), NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, n, seed, counter, thresh, 1.0f / pkeep);
+  RET;
+}
+CXN_API int cxn_softmax(const void *x, void *y, float *pf, int rows, int K, void *stream) {
+  softmax_rows<<<cdiv(rows, 4), 256, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, pf, rows, K);
+  RET;
+}
+CXN_API int cxn_loss_grad(const float *p32, void *node, const float *label, int rows, int K, int lw, float scale,
+                          int kind, void *stream) {
+  loss_grad<<<nblocks(static_cast<long>(rows) * K), NT, 0, S_>>>(p32, (bf16_t *)node, label, rows, K, lw, scale, kind);
+  RET;
+}
+CXN_API int cxn_colsum(const void *dy, float *db, long rows, int C, void *stream) {
+  if (C % 8) {
+    colsum_scalar<<<cdiv(C, NT), NT, 0, S_>>>((const bf16_t *)dy, db, rows, C);
+    RET;
+  }
+  const int CV = C / 8;
+  const int rpb = 512;
+  dim3 grid(cdiv(rows, rpb), cdiv(CV, 64));
+  colsum_bf16<<<grid, NT, 0, S_>>>((const bf16_t *)dy, db, rows, C, rpb);
+  RET;
+}
+CXN_API int cxn_cast_f32_bf16(const float *x, void *y, long n, void *stream) {
+  cast_f32_bf16<<<nblocks(n), NT, 0, S_>>>(x, (bf16_t *)y, n);
+  RET;
+}
+CXN_API int cxn_add_bf16(const void *a, const void *b, void *y, long n, void *stream) {
+  add_bf16<<<nblocks(n / 8 + 1), NT, 0, S_>>>((const bf16_t *)a, (const bf16_t *)b, (bf16_t *)y, n);
+  RET;
+}
+CXN_API int cxn_channel_copy(const void *src, int Cs, int soff, void *dst, int Cd, int doff, int Cc, long npix,
+                             int accumulate, void *stream) {
+  channel_copy<<<nblocks(npix * Cc), NT, 0, S_>>>((const bf16_t *)src, Cs, soff, (bf16_t *)dst, Cd, doff, Cc, npix,
+                                                  accumulate);
+  RET;
+}

@@ -1,0 +1,117 @@
+// Fused multi-tensor optimizer step over the flat parameter arena.
+//
+// One launch updates every parameter segment (weights and biases of every layer):
+// fp32 master weight, fp32 gradient (zeroed after use, the reference's `dw = 0`),
+// fp32 optimizer state, and the bf16 shadow copy the GEMM kernels consume.
+//   SGD  (reference src/updater/sgd_updater-inl.hpp:73-84):
+//        m = mu*m - lr*(clip(g) + wd*w);  w += m
+//   NAG  (reference src/updater/nag_updater-inl.hpp:66-72):
+//        old = m; m = mu*m - lr*(g + wd*w); w += (1+mu)*m - mu*old
+//   Adam (reference src/updater/adam_updater-inl.hpp:74-82, incl. its `grad -= wd*w` sign):
+//        g -= wd*w; m1 += d1*(g-m1); m2 += d2*(g^2-m2); w -= lr_t * m1/(sqrt(m2)+1e-8)
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int MAX_SEG = 48;
+
+struct Seg {
+  long off;
+  long n;
+  float lr, wd, mom, clip;
+};
+struct SegTable {
+  Seg s[MAX_SEG];
+};
+
+__device__ __forceinline__ float clipg(float g, float c) {
+  if (c == 0.f) return g;
+  if (g != g) return 0.f;
+  return fminf(fmaxf(g, -c), c);
+}
+
+// algo: 0 sgd, 1 nag, 2 adam.  st2 used by adam only.  wb may be null.
+__global__ void fused_update(SegTable tab, float *__restrict__ w, float *__restrict__ g, float *__restrict__ st1,
+                             float *__restrict__ st2, bf16_t *__restrict__ wb, int algo, float d1, float d2) {
+  const Seg sg = tab.s[blockIdx.y];
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < sg.n; i += (long)gridDim.x * NT) {
+    const long k = sg.off + i;
+    float wv = w[k];
+    float gv = clipg(g[k], sg.clip);
+    if (algo == 0) {
+      const float m = sg.mom * st1[k] - sg.lr * (gv + sg.wd * wv);
+      st1[k] = m;
+      wv += m;
+    } else if (algo == 1) {
+      const float old = st1[k];
+      const float m = sg.mom * old - sg.lr * (gv + sg.wd * wv);
+      st1[k] = m;
+      wv += (1.f + sg.mom) * m - sg.mom * old;
+    } else {
+      if (sg.wd > 0.f) gv -= sg.wd * wv;
+      float m1 = st1[k], m2 = st2[k];
+      m1 += d1 * (gv - m1);
+      m2 += d2 * (gv * gv - m2);
+      st1[k] = m1;
+      st2[k] = m2;
+      wv -= sg.lr * (m1 / (sqrtf(m2) + 1e-8f));
+    }
+    w[k] = wv;
+    g[k] = 0.f;
+    if (wb) wb[k] = f2bf(wv);
+  }
+}
+
+// Non-finite check over a gradient range (failure detection): flag |= any(!isfinite).
+__global__ void nonfinite_check(const float *__restrict__ g, long n, int *__restrict__ flag) {
+  int bad = 0;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) {
+    const float v = g[i];
+    bad |= !(v - v == 0.f);
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+__global__ void scale_f32(float *__restrict__ x, long n, float s) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) x[i] *= s;
+}
+
+}  // namespace
+
+// segs: packed [nseg][6] doubles-as-floats: off, n, lr, wd, mom, clip
+CXN_API int cxn_fused_update(const long *offs, const long *ns, const float *hyper /*[nseg][4]*/, int nseg, float *w,
+                             float *g, float *st1, float *st2, void *wb, int algo, float d1, float d2, void *stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  for (int base = 0; base < nseg; base += MAX_SEG) {
+    SegTable tab;
+    const int cnt = nseg - base < MAX_SEG ? nseg - base : MAX_SEG;
+    long maxn = 1;
+    for (int i = 0; i < cnt; ++i) {
+      const int j = base + i;
+      tab.s[i] = Seg{offs[j], ns[j], hyper[4 * j + 0], hyper[4 * j + 1], hyper[4 * j + 2], hyper[4 * j + 3]};
+      if (ns[j] > maxn) maxn = ns[j];
+    }
+    long bx = (maxn + NT * 4 - 1) / (NT * 4);
+    if (bx > 2048) bx = 2048;
+    dim3 grid(static_cast<unsigned>(bx), cnt);
+    fused_update<<<grid, NT, 0, s>>>(tab, w, g, st1, st2, static_cast<bf16_t *>(wb), algo, d1, d2);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+CXN_API int cxn_nonfinite_check(const float *g, long n, int *flag, void *stream) {
+  long b = (n + NT * 8 - 1) / (NT * 8);
+  if (b > 1024) b = 1024;
+  if (b < 1) b = 1;
+  nonfinite_check<<<b, NT, 0, static_cast<hipStream_t>(stream)>>>(g, n, flag);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+CXN_API int cxn_scale_f32(float *x, long n, float sc, void *stream) {
+  long b = (n + NT * 8 - 1) / (NT * 8);
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  scale_f32<<<b, NT, 0, static_cast<hipStream_t>(stream)>>>(x, n, sc);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}

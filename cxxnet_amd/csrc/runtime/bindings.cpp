@@ -1,0 +1,166 @@
+// pybind11 bindings of the native runtime (config language, graph config,
+// checkpoint PODs, data IO, metrics). No torch / HIP dependency, so this module
+// builds and runs identically on the CPU container and on the GPU box.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <fstream>
+#include <sstream>
+
+#include "config_reader.h"
+#include "data_io.h"
+#include "layer_param.h"
+#include "layer_types.h"
+#include "metric.h"
+#include "netconfig.h"
+
+namespace py = pybind11;
+using namespace cxxnet_rt;
+
+static KVList ParseConfigFile(const std::string &path) {
+  std::ifstream fi(path, std::ios::binary);
+  if (!fi) throw std::runtime_error("cannot open file " + path);
+  std::stringstream ss;
+  ss << fi.rdbuf();
+  return ConfigTokenizer(ss.str()).ParseAll();
+}
+
+PYBIND11_MODULE(_cxxnet_rt, m) {
+  m.doc() = "cxxnet_amd native runtime: config parser, NetConfig, checkpoint PODs, IO, metrics";
+
+  m.def("parse_config", [](const std::string &text) { return ConfigTokenizer(text).ParseAll(); },
+        "Tokenize .conf text into an ordered list of (name, value) pairs");
+  m.def("parse_config_file", &ParseConfigFile);
+  m.def("get_layer_type", &GetLayerType);
+
+  py::class_<LayerInfo>(m, "LayerInfo")
+      .def(py::init<>())
+      .def_readwrite("type", &LayerInfo::type)
+      .def_readwrite("primary_layer_index", &LayerInfo::primary_layer_index)
+      .def_readwrite("name", &LayerInfo::name)
+      .def_readwrite("nindex_in", &LayerInfo::nindex_in)
+      .def_readwrite("nindex_out", &LayerInfo::nindex_out);
+
+  py::class_<NetConfig>(m, "NetConfig")
+      .def(py::init<>())
+      .def("configure", &NetConfig::Configure)
+      .def("save_net", [](const NetConfig &c) { return py::bytes(c.SaveNet()); })
+      .def("load_net",
+           [](NetConfig &c, py::bytes b) {
+             std::string s = b;
+             return c.LoadNet(s.data(), s.size());
+           },
+           "Load structure from bytes; returns bytes consumed")
+      .def("get_layer_index", &NetConfig::GetLayerIndex)
+      .def_property_readonly("num_nodes", [](const NetConfig &c) { return c.param.num_nodes; })
+      .def_property_readonly("num_layers", [](const NetConfig &c) { return c.param.num_layers; })
+      .def_property_readonly("init_end", [](const NetConfig &c) { return c.param.init_end; })
+      .def_property_readonly("extra_data_num", [](const NetConfig &c) { return c.param.extra_data_num; })
+      .def_property_readonly("input_shape",
+                             [](const NetConfig &c) {
+                               return std::vector<uint32_t>{c.param.input_shape[0], c.param.input_shape[1],
+                                                            c.param.input_shape[2]};
+                             })
+      .def_readonly("layers", &NetConfig::layers)
+      .def_readonly("node_names", &NetConfig::node_names)
+      .def_readonly("node_name_map", &NetConfig::node_name_map)
+      .def_readonly("layer_name_map", &NetConfig::layer_name_map)
+      .def_readonly("updater_type", &NetConfig::updater_type)
+      .def_readonly("sync_type", &NetConfig::sync_type)
+      .def_readonly("label_name_map", &NetConfig::label_name_map)
+      .def_readonly("label_range", &NetConfig::label_range)
+      .def_readonly("defcfg", &NetConfig::defcfg)
+      .def_readonly("layercfg", &NetConfig::layercfg)
+      .def_readonly("extra_shape", &NetConfig::extra_shape);
+
+  py::class_<LayerParam>(m, "LayerParam")
+      .def(py::init<>())
+      .def("set_param", &LayerParam::SetParam)
+      .def("to_bytes",
+           [](const LayerParam &p) { return py::bytes(reinterpret_cast<const char *>(&p), sizeof(LayerParam)); })
+      .def_static("from_bytes",
+                  [](py::bytes b) {
+                    std::string s = b;
+                    if (s.size() < sizeof(LayerParam)) throw std::runtime_error("LayerParam: short buffer");
+                    LayerParam p;
+                    std::memcpy(&p, s.data(), sizeof(LayerParam));
+                    return p;
+                  })
+      .def_property_readonly_static("nbytes", [](py::object) { return sizeof(LayerParam); })
+      .def_readwrite("num_hidden", &LayerParam::num_hidden)
+      .def_readwrite("init_sigma", &LayerParam::init_sigma)
+      .def_readwrite("init_sparse", &LayerParam::init_sparse)
+      .def_readwrite("init_uniform", &LayerParam::init_uniform)
+      .def_readwrite("init_bias", &LayerParam::init_bias)
+      .def_readwrite("num_channel", &LayerParam::num_channel)
+      .def_readwrite("random_type", &LayerParam::random_type)
+      .def_readwrite("num_group", &LayerParam::num_group)
+      .def_readwrite("kernel_height", &LayerParam::kernel_height)
+      .def_readwrite("kernel_width", &LayerParam::kernel_width)
+      .def_readwrite("stride", &LayerParam::stride)
+      .def_readwrite("pad_y", &LayerParam::pad_y)
+      .def_readwrite("pad_x", &LayerParam::pad_x)
+      .def_readwrite("no_bias", &LayerParam::no_bias)
+      .def_readwrite("temp_col_max", &LayerParam::temp_col_max)
+      .def_readwrite("silent", &LayerParam::silent)
+      .def_readwrite("num_input_channel", &LayerParam::num_input_channel)
+      .def_readwrite("num_input_node", &LayerParam::num_input_node);
+
+  m.def("load_mnist", [](const std::string &img, const std::string &lab) {
+    MNISTData d = LoadMNIST(img, lab);
+    py::array_t<float> imgs({d.count, d.rows, d.cols});
+    std::memcpy(imgs.mutable_data(), d.images.data(), d.images.size() * sizeof(float));
+    py::array_t<float> labels(static_cast<py::ssize_t>(d.labels.size()));
+    std::memcpy(labels.mutable_data(), d.labels.data(), d.labels.size() * sizeof(float));
+    return py::make_tuple(imgs, labels);
+  });
+
+  py::class_<BinaryPage>(m, "BinaryPage")
+      .def(py::init<>())
+      .def("size", &BinaryPage::Size)
+      .def("clear", &BinaryPage::Clear)
+      .def("push",
+           [](BinaryPage &p, py::bytes b) {
+             std::string s = b;
+             return p.Push(s.data(), s.size());
+           })
+      .def("get", [](const BinaryPage &p, int r) { return py::bytes(p.Get(r)); })
+      .def("to_bytes", [](const BinaryPage &p) { return py::bytes(p.raw(), BinaryPage::kPageBytes); })
+      .def_property_readonly_static("page_bytes", [](py::object) { return BinaryPage::kPageBytes; });
+  m.def("pack_image_bin", &PackImageBin, "Pack files into 64MB BinaryPages (im2bin)");
+
+  py::class_<ImageBinReader>(m, "ImageBinReader")
+      .def(py::init<std::vector<std::string>, int>(), py::arg("paths"), py::arg("prefetch") = 2)
+      .def("before_first", &ImageBinReader::BeforeFirst, py::call_guard<py::gil_scoped_release>())
+      .def("next", [](ImageBinReader &r) -> py::object {
+        std::string s;
+        bool ok;
+        {
+          py::gil_scoped_release rel;
+          ok = r.Next(&s);
+        }
+        if (!ok) return py::none();
+        return py::bytes(s);
+      });
+
+  py::class_<ImageListEntry>(m, "ImageListEntry")
+      .def_readonly("index", &ImageListEntry::index)
+      .def_readonly("labels", &ImageListEntry::labels)
+      .def_readonly("path", &ImageListEntry::path);
+  m.def("parse_image_list", &ParseImageList);
+
+  py::class_<Metric>(m, "Metric")
+      .def(py::init<const std::string &>())
+      .def("clear", &Metric::Clear)
+      .def("add_eval",
+           [](Metric &mt, py::array_t<float, py::array::c_style | py::array::forcecast> pred,
+              py::array_t<float, py::array::c_style | py::array::forcecast> label) {
+             if (pred.ndim() != 2 || label.ndim() != 2) throw std::runtime_error("add_eval expects 2-D arrays");
+             if (pred.shape(0) != label.shape(0)) throw std::runtime_error("add_eval: batch mismatch");
+             mt.AddEval(pred.data(), static_cast<int>(pred.shape(0)), static_cast<int>(pred.shape(1)),
+                        label.data(), static_cast<int>(label.shape(1)));
+           })
+      .def("get", &Metric::Get)
+      .def_property_readonly("name", &Metric::name);
+}

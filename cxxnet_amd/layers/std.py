@@ -1,0 +1,475 @@
+"""Standard layers: fullc, conv, activations, pooling, lrn, dropout, flatten, losses.
+
+Every layer reproduces the forward/backward semantics of the reference layer cited
+in its docstring; the device work is done by cxxnet_amd.ops (HIP kernels on the GPU).
+Gradients of inputs overwrite the input node (the reference's buffer-sharing scheme:
+the same node holds the activation in forward and its gradient in backward).
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from ..ops.gemm import ConvGeom, conv_out_size
+from .base import BinReader, BinWriter, Layer, Node, ParamSpec
+
+
+def _check(cond, msg):
+    if not cond:
+        raise ValueError(msg)
+
+
+def _bias_init(val):
+    return lambda t: t.fill_(val)
+
+
+# ============================================================================ fullc
+class FullConnectLayer(Layer):
+    """`fullc` -- reference src/layer/fullc_layer-inl.hpp:13-146.
+    out = in . W^T + b;  gW += out_g^T . in;  gb += sum_rows(out_g);  in_g = out_g . W
+    """
+    type_name = "fullc"
+
+    def __init__(self, ctx):
+        super().__init__(ctx)
+        self.fullc_gather = 0
+        self.fuse_relu = False
+
+    def set_param(self, name, val):
+        super().set_param(name, val)
+        if name == "fullc_gather":
+            self.fullc_gather = int(val)
+
+    def init_connection(self, nodes_in, nodes_out):
+        _check(len(nodes_in) == 1 and len(nodes_out) == 1, "FullcLayer: only support 1-1 connection")
+        x = nodes_in[0]
+        _check(x.is_mat(), "FullcLayer: input need to be a matrix")
+        _check(self.lp.num_hidden > 0, "FullcLayer: must set nhidden correctly")
+        nin = x.shape[1] * x.shape[2] * x.shape[3]
+        if self.lp.num_input_node == 0:
+            self.lp.num_input_node = nin
+        else:
+            _check(self.lp.num_input_node == nin, "FullcLayer: input hidden nodes is not consistent")
+        nodes_out[0].set_shape(x.batch, self.lp.num_hidden, 1, 1)
+        nh, ni = self.lp.num_hidden, self.lp.num_input_node
+
+        def init_w(t):
+            self._init_weight(t, ni, nh)
+        self.params = [ParamSpec("wmat", (nh, ni), init_w)]
+        if self.lp.no_bias == 0:
+            self.params.append(ParamSpec("bias", (nh,), _bias_init(self.lp.init_bias)))
+
+    @property
+    def w(self):
+        return self.params[0]
+
+    @property
+    def b(self):
+        return self.params[1] if len(self.params) > 1 else None
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        bias = self.b.w if self.b is not None else None
+        ops.fc_forward(nodes_in[0].mat(), self.w.wb, bias, nodes_out[0].mat(), relu=self.fuse_relu)
+
+    def backprop(self, prop_grad, nodes_in, nodes_out):
+        x, dy = nodes_in[0].mat(), nodes_out[0].mat()
+        if not self.fullc_gather:
+            ops.fc_backward_weight(x, dy, self.w.g)
+        if self.b is not None:
+            ops.bias_grad(dy, self.b.g)
+        if prop_grad:
+            ops.fc_backward_data(dy, self.w.wb, x)
+
+    def save_model(self, fo: BinWriter):
+        fo.write(self.lp.to_bytes())
+        fo.write_tensor(self.w.w.view(self.w.shape))
+        fo.write_tensor(self.b.w if self.b is not None else torch.zeros(self.lp.num_hidden))
+
+    def load_model(self, fi: BinReader):
+        self.lp = fi.read_layer_param()
+        self.loaded = [fi.read_tensor(2), fi.read_tensor(1)]
+
+    def loaded_values(self):
+        w, b = self.loaded
+        out = [w]
+        if self.lp.no_bias == 0:
+            out.append(b)
+        return out
+
+
+# ============================================================================ conv
+class ConvolutionLayer(Layer):
+    """`conv` -- reference src/layer/convolution_layer-inl.hpp:12-228.
+
+    Weights are stored internally as [Cout][KH][KW][Cin/g] (NHWC-friendly); the
+    checkpoint keeps the reference (g, Cout/g, Cin/g*KH*KW) layout in (ci, kh, kw) order.
+    The im2col buffer never exists: the MFMA kernel gathers patches on the fly.
+    """
+    type_name = "conv"
+
+    def __init__(self, ctx):
+        super().__init__(ctx)
+        self.fuse_relu = False
+        self.geo = None
+        self._wt = None
+
+    def init_connection(self, nodes_in, nodes_out):
+        _check(len(nodes_in) == 1 and len(nodes_out) == 1, "ConvolutionLayer: only support 1-1 connection")
+        lp = self.lp
+        x = nodes_in[0]
+        b, c, h, w = x.shape
+        _check(lp.num_channel > 0, "must set nchannel correctly")
+        _check(lp.kernel_height > 0 and lp.kernel_width > 0, "must set kernel_size correctly")
+        _check(lp.kernel_width <= w + 2 * lp.pad_x and lp.kernel_height <= h + 2 * lp.pad_y,
+               "kernel size exceed input")
+        if lp.num_input_channel == 0:
+            lp.num_input_channel = c
+        else:
+            _check(lp.num_input_channel == c, "ConvolutionLayer: number of input channels is not consistent")
+        G = lp.num_group
+        _check(c % G == 0 and lp.num_channel % G == 0, "ConvolutionLayer: channels must divide ngroup")
+        Ho, Wo = conv_out_size(h, w, lp.kernel_height, lp.kernel_width, lp.stride, lp.pad_y, lp.pad_x)
+        nodes_out[0].set_shape(b, lp.num_channel, Ho, Wo)
+        self.cin_phys = x.cp
+        self.geo = ConvGeom(b, h, w, x.cp, Ho, Wo, lp.num_channel, lp.kernel_height, lp.kernel_width, lp.stride,
+                            lp.pad_y, lp.pad_x, G)
+        cg_l, cg_p = c // G, x.cp // G
+        kh, kw, co = lp.kernel_height, lp.kernel_width, lp.num_channel
+
+        def init_w(t):
+            logical = torch.empty(G, co // G, cg_l * kh * kw)
+            self._init_weight(logical, cg_l * kh * kw, co // G)
+            t.copy_(self.from_logical(logical))
+        self.params = [ParamSpec("wmat", (co, kh, kw, cg_p), init_w)]
+        if lp.no_bias == 0:
+            self.params.append(ParamSpec("bias", (co,), _bias_init(lp.init_bias)))
+
+    # logical (G, Cout/G, Cg*KH*KW) in (ci, kh, kw) order  <->  internal [Cout][KH][KW][Cg_phys]
+    def from_logical(self, logical: torch.Tensor) -> torch.Tensor:
+        lp = self.lp
+        G, co, kh, kw = lp.num_group, lp.num_channel, lp.kernel_height, lp.kernel_width
+        cg_l = lp.num_input_channel // G
+        cg_p = self.cin_phys // G
+        t = logical.reshape(co, cg_l, kh, kw).permute(0, 2, 3, 1)
+        out = torch.zeros(co, kh, kw, cg_p, dtype=logical.dtype)
+        out[..., :cg_l] = t
+        return out
+
+    def to_logical(self, internal: torch.Tensor) -> torch.Tensor:
+        lp = self.lp
+        G, co, kh, kw = lp.num_group, lp.num_channel, lp.kernel_height, lp.kernel_width
+        cg_l = lp.num_input_channel // G
+        t = internal.detach().float().cpu()[..., :cg_l].permute(0, 3, 1, 2)  # co, cg, kh, kw
+        return t.reshape(G, co // G, cg_l * kh * kw).contiguous()
+
+    def on_batch_size_changed(self, nodes_in, nodes_out):
+        self.geo.N = nodes_in[0].data.shape[0]
+
+    @property
+    def w(self):
+        return self.params[0]
+
+    @property
+    def b(self):
+        return self.params[1] if len(self.params) > 1 else None
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        self.geo.N = nodes_in[0].data.shape[0]
+        bias = self.b.w if self.b is not None else None
+        ops.conv_forward(nodes_in[0].data, self.w.wb, bias, nodes_out[0].data, self.geo, relu=self.fuse_relu)
+
+    def backprop(self, prop_grad, nodes_in, nodes_out):
+        x, dy = nodes_in[0].data, nodes_out[0].data
+        self.geo.N = x.shape[0]
+        ops.conv_backward_weight(x, dy, self.w.g, self.geo)
+        if self.b is not None:
+            ops.bias_grad(dy.view(-1, dy.shape[-1]), self.b.g)
+        if prop_grad:
+            if self._wt is None or self._wt.shape != self.w.wb.shape:
+                self._wt = torch.empty_like(self.w.wb)
+            ops.conv_backward_data(dy, self.w.wb, x, self.geo, self._wt)
+
+    def save_model(self, fo: BinWriter):
+        fo.write(self.lp.to_bytes())
+        fo.write_tensor(self.to_logical(self.w.w.view(self.w.shape)))
+        fo.write_tensor(self.b.w if self.b is not None else torch.zeros(self.lp.num_channel))
+
+    def load_model(self, fi: BinReader):
+        self.lp = fi.read_layer_param()
+        self.loaded = [fi.read_tensor(3), fi.read_tensor(1)]
+
+    def loaded_values(self):
+        w, b = self.loaded
+        out = [self.from_logical(w)]
+        if self.lp.no_bias == 0:
+            out.append(b)
+        return out
+
+
+# ============================================================================ activations
+class ActivationLayer(Layer):
+    """`relu`/`sigmoid`/`tanh` -- reference src/layer/activation_layer-inl.hpp:11-40;
+    `xelu` -- src/layer/xelu_layer-inl.hpp:15-50.  Applied in place on the input node
+    and copied to the output node; the gradient is expressed through the output."""
+
+    def __init__(self, ctx, kind):
+        super().__init__(ctx)
+        self.kind = kind
+        self.type_name = kind
+        self.b = 5.0
+        self.fused_into_producer = False
+
+    def set_param(self, name, val):
+        super().set_param(name, val)
+        if name == "b":
+            self.b = float(val)
+
+    def init_connection(self, nodes_in, nodes_out):
+        _check(len(nodes_in) == 1 and len(nodes_out) == 1, "ActivationLayer: only support 1-1 connection")
+        nodes_out[0].set_shape(*nodes_in[0].shape, cp=nodes_in[0].cp)
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        x, y = nodes_in[0], nodes_out[0]
+        if self.fused_into_producer:
+            # the producer's epilogue already applied the activation in place on x
+            if x is not y:
+                y.data.copy_(x.data)
+            return
+        if x is y:
+            ops.act_forward(self.kind, x.data, x.data, None, self.b)
+        else:
+            ops.act_forward(self.kind, x.data, y.data, x.data, self.b)
+
+    def backprop(self, prop_grad, nodes_in, nodes_out):
+        x, y = nodes_in[0], nodes_out[0]
+        # x holds f(input) (in-place forward), y holds the incoming gradient
+        ops.act_backward(self.kind, x.data, y.data, x.data, self.b)
+
+
+# ============================================================================ pooling
+class PoolingLayer(Layer):
+    """`max_pooling`/`sum_pooling`/`avg_pooling`/`relu_max_pooling` --
+    reference src/layer/pooling_layer-inl.hpp:11-114 (ceil-mode windows, value-compare
+    unpool).  Extension: `pad` is honoured (the reference parses but ignores it)."""
+
+    def __init__(self, ctx, mode, relu=False):
+        super().__init__(ctx)
+        self.mode = mode
+        self.relu = relu
+        self.type_name = ("relu_" if relu else "") + {"max": "max", "sum": "sum", "avg": "avg"}[mode] + "_pooling"
+        self.state = None
+
+    def init_connection(self, nodes_in, nodes_out):
+        _check(len(nodes_in) == 1 and len(nodes_out) == 1, "PoolingLayer: only support 1-1 connection")
+        lp = self.lp
+        b, c, h, w = nodes_in[0].shape
+        _check(lp.kernel_height > 0 and lp.kernel_width > 0, "must set kernel_size correctly")
+        _check(lp.kernel_width <= w + 2 * lp.pad_x and lp.kernel_height <= h + 2 * lp.pad_y,
+               "kernel size exceed input")
+        ho = ops.pool_out_size(h, lp.kernel_height, lp.stride, lp.pad_y)
+        wo = ops.pool_out_size(w, lp.kernel_width, lp.stride, lp.pad_x)
+        nodes_out[0].set_shape(b, c, ho, wo, cp=nodes_in[0].cp)
+
+    def _state(self, y: Node):
+        if self.state is None or self.state.shape != y.data.shape:
+            self.state = torch.empty_like(y.data)
+        return self.state
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        lp = self.lp
+        st = self._state(nodes_out[0]) if is_train else None
+        ops.pool_forward(nodes_in[0].data, nodes_out[0].data, st, lp.kernel_height, lp.kernel_width, lp.stride,
+                         lp.pad_y, self.mode, self.relu)
+
+    def backprop(self, prop_grad, nodes_in, nodes_out):
+        if not prop_grad:
+            return
+        lp = self.lp
+        x = nodes_in[0].data
+        ops.pool_backward(x, self.state, nodes_out[0].data, x, lp.kernel_height, lp.kernel_width, lp.stride,
+                          lp.pad_y, self.mode, self.relu)
+
+
+# ============================================================================ LRN
+class LRNLayer(Layer):
+    """`lrn` -- reference src/layer/lrn_layer-inl.hpp:12-89 (cross-channel, knorm/alpha/beta)."""
+    type_name = "lrn"
+
+    def __init__(self, ctx):
+        super().__init__(ctx)
+        self.nsize = 3
+        self.alpha = 0.0
+        self.beta = 0.0
+        self.knorm = 1.0
+        self.tmp = None
+
+    def set_param(self, name, val):
+        super().set_param(name, val)
+        if name == "local_size":
+            self.nsize = int(val)
+        elif name == "alpha":
+            self.alpha = float(val)
+        elif name == "beta":
+            self.beta = float(val)
+        elif name == "knorm":
+            self.knorm = float(val)
+
+    def init_connection(self, nodes_in, nodes_out):
+        _check(len(nodes_in) == 1 and len(nodes_out) == 1, "LRNLayer: only support 1-1 connection")
+        _check(nodes_in[0] is not nodes_out[0], "LRNLayer: input and output must be different nodes")
+        nodes_out[0].set_shape(*nodes_in[0].shape, cp=nodes_in[0].cp)
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        ops.lrn_forward(nodes_in[0].data, nodes_out[0].data, self.nsize, self.alpha, self.beta, self.knorm)
+
+    def backprop(self, prop_grad, nodes_in, nodes_out):
+        if not prop_grad:
+            return
+        x = nodes_in[0].data
+        if self.tmp is None or self.tmp.shape != x.shape:
+            self.tmp = torch.empty_like(x)
+        ops.lrn_backward(x, nodes_out[0].data, self.tmp, self.nsize, self.alpha, self.beta, self.knorm)
+        x.copy_(self.tmp)
+
+
+# ============================================================================ dropout
+class DropoutLayer(Layer):
+    """`dropout` -- reference src/layer/dropout_layer-inl.hpp:12-66 (self-loop;
+    mask = (u < pkeep)/pkeep).  The mask is a counter-based hash, regenerated in
+    backward instead of stored."""
+    type_name = "dropout"
+
+    def __init__(self, ctx):
+        super().__init__(ctx)
+        self.threshold = 0.0
+        self.seed = int(torch.randint(0, 2**31 - 1, (1,), generator=ctx.gen).item())
+
+    def set_param(self, name, val):
+        super().set_param(name, val)
+        if name == "threshold":
+            self.threshold = float(val)
+
+    def init_connection(self, nodes_in, nodes_out):
+        _check(len(nodes_in) == 1 and len(nodes_out) == 1, "DropoutLayer: only support 1-1 connection")
+        _check(nodes_in[0] is nodes_out[0], "DropoutLayer is an self-loop Layer")
+        _check(0.0 <= self.threshold < 1.0, "DropoutLayer: invalid dropout threshold")
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        if is_train and self.threshold > 0:
+            x = nodes_in[0].data
+            ops.dropout_apply(x, x, self.seed, 1.0 - self.threshold, self.ctx.step_counter)
+
+    def backprop(self, prop_grad, nodes_in, nodes_out):
+        if self.threshold > 0:
+            x = nodes_in[0].data
+            ops.dropout_apply(x, x, self.seed, 1.0 - self.threshold, self.ctx.step_counter)
+
+
+# ============================================================================ flatten
+class FlattenLayer(Layer):
+    """`flatten` -- reference src/layer/flatten_layer-inl.hpp:11-40: (B,C,H,W) -> (B,1,1,CHW)
+    in NCHW feature order (so fullc weights keep the reference meaning)."""
+    type_name = "flatten"
+
+    def init_connection(self, nodes_in, nodes_out):
+        _check(len(nodes_in) == 1 and len(nodes_out) == 1, "FlattenLayer: only support 1-1 connection")
+        b, c, h, w = nodes_in[0].shape
+        _check(nodes_in[0].cp == c, "FlattenLayer: padded-channel input is not supported")
+        nodes_out[0].set_shape(b, 1, 1, c * h * w)
+        self.dims = (c, h * w)
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        x, y = nodes_in[0].data, nodes_out[0].data
+        c, hw = self.dims
+        if hw == 1 or c == 1:
+            y.view(-1).copy_(x.view(-1))
+        else:
+            ops.transpose(x, y, x.shape[0], hw, c)
+
+    def backprop(self, prop_grad, nodes_in, nodes_out):
+        if not prop_grad:
+            return
+        x, y = nodes_in[0].data, nodes_out[0].data
+        c, hw = self.dims
+        if hw == 1 or c == 1:
+            x.view(-1).copy_(y.view(-1))
+        else:
+            ops.transpose(y, x, x.shape[0], c, hw)
+
+
+# ============================================================================ losses
+class LossLayerBase(Layer):
+    """reference src/layer/loss/loss_layer_base-inl.hpp:11-133.  Self-loop on a matrix
+    node; gradient (pred - target) scaled by grad_scale / (batch_size * update_period)
+    with the GLOBAL batch size.  Computed on device (no host round trip)."""
+    kind = "softmax"
+
+    def __init__(self, ctx):
+        super().__init__(ctx)
+        self.target = "label"
+        self.grad_scale = 1.0
+        self.batch_size = 0
+        self.update_period = 1
+        self.p32 = None
+
+    def set_param(self, name, val):
+        super().set_param(name, val)
+        if name == "target":
+            self.target = val
+        elif name == "grad_scale":
+            self.grad_scale = float(val)
+        elif name == "batch_size":
+            self.batch_size = int(val)
+        elif name == "update_period":
+            self.update_period = int(val)
+
+    def init_connection(self, nodes_in, nodes_out):
+        _check(len(nodes_in) == 1 and len(nodes_out) == 1, "LossLayer: only support 1-1 connection")
+        _check(nodes_in[0] is nodes_out[0], "LossLayer is an self-loop Layer")
+        _check(nodes_in[0].is_mat(), "LossLayer: input need to be a matrix")
+        _check(self.target in self.ctx.label_name_map, f"LossLayer: unknown target={self.target}")
+
+    def _p32(self, node):
+        m = node.mat()
+        if self.p32 is None or self.p32.shape != m.shape:
+            self.p32 = torch.empty(m.shape, dtype=torch.float32, device=m.device)
+        node.fp32_view = self.p32
+        return self.p32
+
+    def backprop(self, prop_grad, nodes_in, nodes_out):
+        label = self.ctx.label_fields[self.target]
+        bs = self.batch_size if self.batch_size > 0 else nodes_in[0].batch
+        scale = self.grad_scale / (bs * self.update_period)
+        node = nodes_in[0].mat()
+        ops.loss_grad(self.kind, node, label[: node.shape[0]], scale, self.p32)
+
+
+class SoftmaxLayer(LossLayerBase):
+    """`softmax` -- reference src/layer/loss/softmax_layer-inl.hpp:12-33."""
+    type_name = "softmax"
+    kind = "softmax"
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        m = nodes_in[0].mat()
+        ops.softmax_forward(m, m, self._p32(nodes_in[0]))
+
+
+class L2LossLayer(LossLayerBase):
+    """`l2_loss` -- reference src/layer/loss/l2_loss_layer-inl.hpp (fwd identity, grad x - y)."""
+    type_name = "l2_loss"
+    kind = "l2"
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        m = nodes_in[0].mat()
+        self._p32(nodes_in[0]).copy_(m)
+
+
+class MultiLogisticLayer(LossLayerBase):
+    """`multi_logistic` -- reference src/layer/loss/multi_logistic_layer-inl.hpp (fwd sigmoid, grad s - y)."""
+    type_name = "multi_logistic"
+    kind = "multi_logistic"
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        m = nodes_in[0].mat()
+        ops.act_forward("sigmoid", m, m)
+        self._p32(nodes_in[0]).copy_(m)

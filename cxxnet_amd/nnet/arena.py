@@ -1,0 +1,79 @@
+"""Flat parameter arena.
+
+Every trainable tensor of the net lives in ONE contiguous fp32 buffer (master
+weights), with same-layout buffers for the gradient and optimizer state, plus a
+bf16 compute shadow on the GPU.  One fused kernel then updates the whole model,
+and data-parallel gradient reduction works on large contiguous ranges (buckets)
+instead of per-tensor messages (contrast the reference's per-key push/pull,
+src/updater/async_updater-inl.hpp:94-127).
+
+Segments are laid out in REVERSE layer order, so the gradients that backward
+produces first (last layers) are at the front of the buffer: a bucket is ready as
+soon as backward has passed its lowest layer.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import torch
+
+ALIGN = 64  # elements; keeps every view 256-B aligned in fp32 and 128-B in bf16
+
+
+class ParamArena:
+    def __init__(self, device: torch.device, shadow_dtype=None):
+        self.device = torch.device(device)
+        self.shadow_dtype = shadow_dtype
+        self.specs = []          # (layer_index, ParamSpec)
+        self.total = 0
+        self.w = self.g = self.m1 = self.m2 = self.wb = None
+
+    def build(self, layer_specs: Sequence[tuple]):
+        """layer_specs: [(layer_index, [ParamSpec, ...]), ...] in forward order."""
+        off = 0
+        self.specs = []
+        for li, specs in sorted(layer_specs, key=lambda t: -t[0]):
+            for s in specs:
+                s.offset = off
+                self.specs.append((li, s))
+                off += (s.numel + ALIGN - 1) // ALIGN * ALIGN
+        self.total = max(off, ALIGN)
+        dev = self.device
+        self.w = torch.zeros(self.total, dtype=torch.float32, device=dev)
+        self.g = torch.zeros(self.total, dtype=torch.float32, device=dev)
+        self.m1 = torch.zeros(self.total, dtype=torch.float32, device=dev)
+        self.m2 = None
+        self.wb = torch.zeros(self.total, dtype=self.shadow_dtype, device=dev) if self.shadow_dtype else None
+        for _, s in self.specs:
+            n = s.numel
+            s.w = self.w[s.offset:s.offset + n].view(s.shape)
+            s.g = self.g[s.offset:s.offset + n].view(s.shape)
+            s.wb = self.wb[s.offset:s.offset + n].view(s.shape) if self.wb is not None else s.w
+
+    def ensure_second_moment(self):
+        if self.m2 is None:
+            self.m2 = torch.zeros_like(self.w)
+
+    def sync_shadow(self):
+        """Refresh the bf16 compute copy from the fp32 masters."""
+        if self.wb is not None:
+            self.wb.copy_(self.w)
+
+    def zero_grad(self):
+        self.g.zero_()
+
+    def reset_state(self):
+        self.m1.zero_()
+        if self.m2 is not None:
+            self.m2.zero_()
+
+    def segments(self):
+        return [(li, s) for li, s in self.specs]
+
+    def used_range(self, li_min: int) -> int:
+        """Arena prefix length covering every segment with layer index >= li_min."""
+        end = 0
+        for li, s in self.specs:
+            if li >= li_min:
+                end = max(end, s.offset + s.numel)
+        return end

@@ -1,0 +1,219 @@
+"""GEMM-shaped ops: convolution (fwd / data-grad / weight-grad) and fully-connected.
+
+Layout contract (both devices):
+  * activations are NHWC: x[N][H][W][C];  a "matrix" node (B,1,1,N) is x[B][N].
+  * conv weights are [Cout][KH][KW][Cin/groups] (channels fastest).
+  * fc weights are [nout][nin] (reference layout, src/layer/fullc_layer-inl.hpp:29).
+On the GPU, activations/weights are bf16 and every op runs the hand-written MFMA
+kernel in csrc/kernels/gemm_mfma.hip.  On the CPU, the same semantics run in fp32
+through torch (the reference's CPU path; also the numerics oracle for tests).
+
+Reference: src/layer/convolution_layer-inl.hpp:70-155 (im2col + GEMM per group),
+src/layer/fullc_layer-inl.hpp:101-130.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from .. import native
+
+DIRECT_K, DIRECT_MN, GATHER_K, GATHER_MN = 0, 1, 2, 3
+EPI_BF16, EPI_F32, EPI_F32_ACC, EPI_F32_ATOMIC = 0, 1, 2, 3
+NUM_CU = 256
+
+
+def _stream():
+    return ctypes_stream(torch.cuda.current_stream())
+
+
+def ctypes_stream(s) -> int:
+    return s.cuda_stream
+
+
+@dataclass
+class ConvGeom:
+    N: int
+    H: int
+    W: int
+    C: int          # physical input channels (>= logical, first layer may be padded)
+    Ho: int
+    Wo: int
+    Cout: int
+    KH: int
+    KW: int
+    stride: int
+    pad_y: int
+    pad_x: int
+    groups: int
+
+    @property
+    def cg_in(self):
+        return self.C // self.groups
+
+    @property
+    def cg_out(self):
+        return self.Cout // self.groups
+
+    @property
+    def kdim(self):
+        return self.KH * self.KW * self.cg_in
+
+
+def _op(ptr=0, gstride=0, ld=0, rows=0, kdim=0, **geo):
+    o = native.CxnOperand()
+    o.ptr = ptr
+    o.gstride = gstride
+    o.ld = ld
+    o.rows = rows
+    o.kdim = kdim
+    o.H = geo.get("H", 0); o.W = geo.get("W", 0); o.C = geo.get("C", 0)
+    o.Ho = geo.get("Ho", 0); o.Wo = geo.get("Wo", 0)
+    o.KH = geo.get("KH", 1); o.KW = geo.get("KW", 1)
+    o.stride = geo.get("stride", 1); o.pad_h = geo.get("pad_h", 0); o.pad_w = geo.get("pad_w", 0)
+    o.dil = geo.get("dil", 1); o.Cg = geo.get("Cg", 1)
+    return o
+
+
+def _pick_tile(rows_i, rows_j, groups):
+    t128 = -(-rows_i // 128) * -(-rows_j // 128) * groups
+    return 128 if t128 >= 2 * NUM_CU else 64
+
+
+def _gemm(a, b, amode, bmode, va, vb, out, out_gstride, ldc, *, alpha=1.0, bias=None, bias_gstride=0,
+          relu=False, epi=EPI_BF16, groups=1, ksplit=1, tile=None):
+    if tile is None:
+        tile = _pick_tile(a.rows, b.rows, groups)
+    rc = native.kernels().cxn_gemm(
+        a, b, amode, bmode, va, vb, out.data_ptr(), out_gstride, ldc, float(alpha),
+        bias.data_ptr() if bias is not None else None, bias_gstride, int(relu), epi, tile, groups, ksplit,
+        _stream())
+    native.check(rc, "gemm")
+
+
+def _auto_split(rows_i, rows_j, groups, kdim, tile=128, target=2 * NUM_CU, min_ktiles=4):
+    tiles = -(-rows_i // tile) * -(-rows_j // tile) * groups
+    ktiles = -(-kdim // 64)
+    split = max(1, min(target // max(tiles, 1), ktiles // min_ktiles))
+    return split
+
+
+# ----------------------------------------------------------------------------- convolution
+def conv_out_size(H, W, KH, KW, stride, pad_y, pad_x):
+    """Reference rule (src/layer/convolution_layer-inl.hpp:174-177)."""
+    return (H + 2 * pad_y - KH) // stride + 1, (W + 2 * pad_x - KW) // stride + 1
+
+
+def _w_nchw(w: torch.Tensor) -> torch.Tensor:
+    # [Cout][KH][KW][Cg] -> [Cout][Cg][KH][KW]
+    return w.permute(0, 3, 1, 2).contiguous()
+
+
+def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
+    """y = conv(x, w) + bias (optionally relu).  x/y NHWC."""
+    if not x.is_cuda:
+        xn = x.permute(0, 3, 1, 2)
+        out = F.conv2d(xn, _w_nchw(w), bias, stride=g.stride, padding=(g.pad_y, g.pad_x), groups=g.groups)
+        if relu:
+            out = out.clamp_min(0)
+        y.copy_(out.permute(0, 2, 3, 1))
+        return
+    cg = g.cg_in
+    va = 8 if cg % 8 == 0 else 4
+    if cg % va:
+        raise ValueError(f"conv: channels per group ({cg}) must be a multiple of 4 on the GPU path")
+    kd = g.kdim
+    A = _op(w.data_ptr(), g.cg_out * kd, kd, g.cg_out, kd)
+    B = _op(x.data_ptr(), cg, 0, g.N * g.Ho * g.Wo, kd, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW,
+            stride=g.stride, pad_h=g.pad_y, pad_w=g.pad_x, dil=1, Cg=cg)
+    _gemm(A, B, DIRECT_K, GATHER_K, va, va, y, g.cg_out, g.Cout, bias=bias, bias_gstride=g.cg_out, relu=relu,
+          epi=EPI_BF16, groups=g.groups)
+
+
+def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None):
+    """dx = conv_transpose(dy, w).  Returns nothing; dx overwritten."""
+    if not dy.is_cuda:
+        dyn = dy.permute(0, 3, 1, 2)
+        out = torch.nn.grad.conv2d_input((g.N, g.C, g.H, g.W), _w_nchw(w), dyn, stride=g.stride,
+                                         padding=(g.pad_y, g.pad_x), groups=g.groups)
+        dx.copy_(out.permute(0, 2, 3, 1))
+        return
+    cg_in, cg_out = g.cg_in, g.cg_out
+    if cg_out % 8:
+        raise ValueError("conv dgrad: output channels per group must be a multiple of 8 on the GPU path")
+    if wt_buf is None:
+        wt_buf = torch.empty_like(w)
+    k = native.kernels()
+    native.check(k.cxn_conv_weight_flip(w.data_ptr(), wt_buf.data_ptr(), g.groups, cg_out, g.KH, g.KW, cg_in,
+                                        _stream()), "conv_weight_flip")
+    kd = g.KH * g.KW * cg_out
+    A = _op(wt_buf.data_ptr(), cg_in * kd, kd, cg_in, kd)
+    B = _op(dy.data_ptr(), cg_out, 0, g.N * g.H * g.W, kd, H=g.Ho, W=g.Wo, C=g.Cout, Ho=g.H, Wo=g.W, KH=g.KH,
+            KW=g.KW, stride=1, pad_h=g.KH - 1 - g.pad_y, pad_w=g.KW - 1 - g.pad_x, dil=g.stride, Cg=cg_out)
+    _gemm(A, B, DIRECT_K, GATHER_K, 8, 8, dx, cg_in, g.C, epi=EPI_BF16, groups=g.groups)
+
+
+def conv_backward_weight(x, dy, dw, g: ConvGeom):
+    """dw += sum over pixels of dy (x) im2col(x).  dw fp32 [Cout][KH][KW][Cg]."""
+    if not x.is_cuda:
+        xn = x.permute(0, 3, 1, 2)
+        dyn = dy.permute(0, 3, 1, 2)
+        gw = torch.nn.grad.conv2d_weight(xn, (g.Cout, g.cg_in, g.KH, g.KW), dyn, stride=g.stride,
+                                         padding=(g.pad_y, g.pad_x), groups=g.groups)
+        dw.add_(gw.permute(0, 2, 3, 1))
+        return
+    cg = g.cg_in
+    va = 8 if cg % 8 == 0 else 4
+    kd = g.kdim
+    P = g.N * g.Ho * g.Wo
+    A = _op(x.data_ptr(), cg, 0, kd, P, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW, stride=g.stride,
+            pad_h=g.pad_y, pad_w=g.pad_x, dil=1, Cg=cg)
+    B = _op(dy.data_ptr(), g.cg_out, g.Cout, g.cg_out, P)
+    split = _auto_split(kd, g.cg_out, g.groups, P)
+    _gemm(A, B, GATHER_MN, DIRECT_MN, va, 8, dw, g.cg_out * kd, kd, epi=EPI_F32_ATOMIC, groups=g.groups,
+          ksplit=split, tile=128)
+
+
+# ----------------------------------------------------------------------------- fully connected
+def fc_forward(x, w, bias, y, relu=False, out_fp32=False):
+    """y[B][nout] = x[B][nin] . w[nout][nin]^T + bias."""
+    if not x.is_cuda:
+        out = x @ w.t()
+        if bias is not None:
+            out = out + bias
+        if relu:
+            out = out.clamp_min(0)
+        y.copy_(out)
+        return
+    Bn, nin = x.shape
+    nout = w.shape[0]
+    A = _op(w.data_ptr(), 0, nin, nout, nin)
+    Bo = _op(x.data_ptr(), 0, nin, Bn, nin)
+    _gemm(A, Bo, DIRECT_K, DIRECT_K, 8, 8, y, 0, nout, bias=bias, relu=relu,
+          epi=EPI_F32 if out_fp32 else EPI_BF16)
+
+
+def fc_backward_data(dy, w, dx):
+    """dx[B][nin] = dy[B][nout] . w[nout][nin]."""
+    if not dy.is_cuda:
+        dx.copy_(dy @ w)
+        return
+    Bn, nout = dy.shape
+    nin = w.shape[1]
+    A = _op(w.data_ptr(), 0, nin, nin, nout)
+    Bo = _op(dy.data_ptr(), 0, nout, Bn, nout)
+    _gemm(A, Bo, DIRECT_MN, DIRECT_K, 8, 8, dx, 0, nin, epi=EPI_BF16)
+
+
+def fc_backward_weight(x, dy, dw):
+    """dw[nout][nin] += dy^T . x  (fp32 accumulate)."""
+    if not x.is_cuda:
+        dw.add_(dy.t() @ x)
+        return
+    Bn, nin = x.shape
+    nout = dy.shape[1]
+    A = _op(x.data_ptr(), 0, nin, nin, Bn)
+    Bo = _op(dy.data_ptr(), 0, nout, nout, Bn)
+    _gemm(A, Bo, DIRECT_MN, DIRECT_MN, 8, 8, dw, 0, nin, epi=EPI_F32_ACC, tile=128)

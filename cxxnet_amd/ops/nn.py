@@ -1,0 +1,317 @@
+"""Memory-bound layer ops (pooling, LRN, activations, dropout, softmax/loss,
+layout conversion, bias gradient).  GPU: csrc/kernels/nn_kernels.hip; CPU: fp32 torch.
+
+All activations are NHWC (see ops/gemm.py for the layout contract).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .. import native
+from .gemm import _stream
+
+ACT_KIND = {"relu": 0, "sigmoid": 1, "tanh": 2, "xelu": 3}
+
+
+def _k():
+    return native.kernels()
+
+
+# ----------------------------------------------------------------------------- layout
+def input_to_nhwc(x_nchw: torch.Tensor, out: torch.Tensor, scale: float = 1.0):
+    """NCHW fp32 batch -> NHWC node (bf16 on GPU), zero-padding extra channels."""
+    N, C, H, W = x_nchw.shape
+    Cp = out.shape[-1]
+    if not out.is_cuda:
+        out.zero_()
+        out[..., :C].copy_(x_nchw.permute(0, 2, 3, 1) * scale)
+        return
+    x = x_nchw.contiguous().float()
+    native.check(_k().cxn_nchw_f32_to_nhwc_bf16(x.data_ptr(), out.data_ptr(), N, C, H, W, Cp, float(scale),
+                                                _stream()), "nchw_to_nhwc")
+
+
+def nhwc_to_nchw(x: torch.Tensor, C: int) -> torch.Tensor:
+    """NHWC node (any dtype) -> NCHW fp32 tensor with C logical channels."""
+    N, H, W, Cp = x.shape
+    if not x.is_cuda:
+        return x[..., :C].permute(0, 3, 1, 2).float().contiguous()
+    out = torch.empty((N, C, H, W), dtype=torch.float32, device=x.device)
+    native.check(_k().cxn_nhwc_bf16_to_nchw_f32(x.data_ptr(), out.data_ptr(), N, C, H, W, Cp, _stream()),
+                 "nhwc_to_nchw")
+    return out
+
+
+def transpose(x: torch.Tensor, y: torch.Tensor, B: int, R: int, Cc: int):
+    """y[b][Cc][R] = x[b][R][Cc]."""
+    if not x.is_cuda:
+        y.view(B, Cc, R).copy_(x.view(B, R, Cc).transpose(1, 2))
+        return
+    native.check(_k().cxn_transpose(x.data_ptr(), y.data_ptr(), B, R, Cc, _stream()), "transpose")
+
+
+# ----------------------------------------------------------------------------- pooling
+POOL_MODE = {"max": 0, "sum": 1, "avg": 2}
+
+
+def pool_out_size(H, k, s, p=0):
+    """Reference ceil rule (src/layer/pooling_layer-inl.hpp:103-106), with optional pad."""
+    Hp = H + 2 * p
+    return min(Hp - k + s - 1, Hp - 1) // s + 1
+
+
+def _pool_ref(x, KH, KW, S, P, mode, relu, Ho, Wo):
+    # x NHWC fp32 -> NHWC, reference semantics (ceil windows, avg = sum/(k*k))
+    xn = x.permute(0, 3, 1, 2)
+    if relu:
+        xn = xn.clamp_min(0)
+    N, C, H, W = xn.shape
+    padv = -math.inf if mode == 0 else 0.0
+    need_h = (Ho - 1) * S + KH - H - P
+    need_w = (Wo - 1) * S + KW - W - P
+    xp = F.pad(xn, (P, max(need_w, 0), P, max(need_h, 0)), value=padv)
+    if mode == 0:
+        out = F.max_pool2d(xp, (KH, KW), S)
+    else:
+        out = F.avg_pool2d(xp, (KH, KW), S) * (KH * KW)
+        if mode == 2:
+            out = out / (KH * KW)
+    return out[:, :, :Ho, :Wo].permute(0, 2, 3, 1)
+
+
+def pool_forward(x, y, state, KH, KW, S, P, mode: str, relu=False):
+    N, H, W, C = x.shape
+    Ho, Wo = y.shape[1], y.shape[2]
+    m = POOL_MODE[mode]
+    if not x.is_cuda:
+        out = _pool_ref(x, KH, KW, S, P, m, relu, Ho, Wo)
+        y.copy_(out)
+        if state is not None:
+            state.copy_(out)
+        return
+    native.check(_k().cxn_pool_fwd(x.data_ptr(), y.data_ptr(), state.data_ptr() if state is not None else None,
+                                   N, H, W, C, Ho, Wo, KH, KW, S, P, m, int(relu), _stream()), "pool_fwd")
+
+
+def pool_backward(x, ypool, dy, dx, KH, KW, S, P, mode: str, relu=False):
+    """dx = unpool(x, ypool, dy); dx may alias x (element-local read-before-write)."""
+    N, H, W, C = x.shape
+    Ho, Wo = dy.shape[1], dy.shape[2]
+    m = POOL_MODE[mode]
+    if not x.is_cuda:
+        xr = x.clamp_min(0) if relu else x
+        g = torch.zeros_like(x)
+        for ho in range(Ho):
+            hs = ho * S - P
+            for wo in range(Wo):
+                ws = wo * S - P
+                h0, h1 = max(hs, 0), min(hs + KH, H)
+                w0, w1 = max(ws, 0), min(ws + KW, W)
+                win = xr[:, h0:h1, w0:w1, :]
+                gv = dy[:, ho:ho + 1, wo:wo + 1, :]
+                if m == 0:
+                    yv = ypool[:, ho:ho + 1, wo:wo + 1, :]
+                    g[:, h0:h1, w0:w1, :] += (win == yv).to(g.dtype) * gv
+                elif m == 1:
+                    g[:, h0:h1, w0:w1, :] += gv
+                else:
+                    g[:, h0:h1, w0:w1, :] += gv / (KH * KW)
+        if relu:
+            g = g * (x > 0).to(g.dtype)
+        dx.copy_(g)
+        return
+    native.check(_k().cxn_pool_bwd(x.data_ptr(), ypool.data_ptr(), dy.data_ptr(), dx.data_ptr(), N, H, W, C, Ho, Wo,
+                                   KH, KW, S, P, m, int(relu), _stream()), "pool_bwd")
+
+
+# ----------------------------------------------------------------------------- LRN
+def _lrn_norm(x, nsize, alpha, knorm):
+    C = x.shape[-1]
+    half = nsize // 2
+    sq = x * x
+    pad = F.pad(sq, (half, half))
+    s = sum(pad[..., i:i + C] for i in range(nsize))
+    return knorm + alpha / nsize * s
+
+
+def lrn_forward(x, y, nsize, alpha, beta, knorm):
+    if not x.is_cuda:
+        y.copy_(x * _lrn_norm(x, nsize, alpha, knorm).pow(-beta))
+        return
+    N, H, W, C = x.shape
+    native.check(_k().cxn_lrn_fwd(x.data_ptr(), y.data_ptr(), N * H * W, C, nsize, float(alpha), float(beta),
+                                  float(knorm), _stream()), "lrn_fwd")
+
+
+def lrn_backward(x, dy, dx, nsize, alpha, beta, knorm):
+    """dx must not alias x or dy."""
+    if not x.is_cuda:
+        norm = _lrn_norm(x, nsize, alpha, knorm)
+        t = dy * x * norm.pow(-beta - 1)
+        C = x.shape[-1]
+        half = nsize // 2
+        tp = F.pad(t, (half, half))
+        s = sum(tp[..., i:i + C] for i in range(nsize))
+        dx.copy_(dy * norm.pow(-beta) - 2 * beta * alpha / nsize * x * s)
+        return
+    N, H, W, C = x.shape
+    native.check(_k().cxn_lrn_bwd(x.data_ptr(), dy.data_ptr(), dx.data_ptr(), N * H * W, C, nsize, float(alpha),
+                                  float(beta), float(knorm), _stream()), "lrn_bwd")
+
+
+# ----------------------------------------------------------------------------- activations
+def _act_ref(kind, x, b):
+    if kind == "relu":
+        return x.clamp_min(0)
+    if kind == "sigmoid":
+        return torch.sigmoid(x)
+    if kind == "tanh":
+        return torch.tanh(x)
+    return torch.where(x > 0, x, x / b)
+
+
+def _act_grad_ref(kind, y, b):
+    if kind == "relu":
+        return (y > 0).to(y.dtype)
+    if kind == "sigmoid":
+        return y * (1 - y)
+    if kind == "tanh":
+        return 1 - y * y
+    return torch.where(y > 0, torch.ones_like(y), torch.full_like(y, 1.0 / b))
+
+
+def act_forward(kind, x, y, y2=None, b=5.0):
+    """y = f(x); when y2 is given it also receives f(x) (in-place write of the input node)."""
+    if not x.is_cuda:
+        out = _act_ref(kind, x, b)
+        y.copy_(out)
+        if y2 is not None:
+            y2.copy_(out)
+        return
+    native.check(_k().cxn_act_fwd(x.data_ptr(), y.data_ptr(), y2.data_ptr() if y2 is not None else None, x.numel(),
+                                  ACT_KIND[kind], float(b), _stream()), "act_fwd")
+
+
+def act_backward(kind, y, dy, dx, b=5.0):
+    """dx = dy * f'(y) (gradient in terms of the forward output)."""
+    if not y.is_cuda:
+        dx.copy_(dy * _act_grad_ref(kind, y, b))
+        return
+    native.check(_k().cxn_act_bwd(y.data_ptr(), dy.data_ptr(), dx.data_ptr(), y.numel(), ACT_KIND[kind], float(b),
+                                  _stream()), "act_bwd")
+
+
+# ----------------------------------------------------------------------------- dropout
+def _hash_u32(idx: torch.Tensor, seed: int) -> torch.Tensor:
+    # identical to hash_u32 in nn_kernels.hip, in int64 arithmetic masked to 32 bits
+    M = 0xFFFFFFFF
+    x = idx ^ ((seed * 0x9E3779B9) & M)
+    x = x ^ (x >> 16); x = (x * 0x7FEB352D) & M
+    x = x ^ (x >> 15); x = (x * 0x846CA68B) & M
+    x = x ^ (x >> 16)
+    return x
+
+
+def effective_seed(seed: int, counter=None) -> int:
+    if counter is None:
+        return seed & 0xFFFFFFFF
+    c = int(counter.item()) & 0xFFFFFFFF
+    return int(_hash_u32(torch.tensor([c], dtype=torch.int64), seed & 0xFFFFFFFF).item())
+
+
+def dropout_mask_ref(n: int, seed: int, pkeep: float, device="cpu") -> torch.Tensor:
+    idx = torch.arange(n, dtype=torch.int64, device=device)
+    t = min(int(pkeep * 4294967296.0), 0xFFFFFFFF)
+    return (_hash_u32(idx, seed & 0xFFFFFFFF) < t).float() / pkeep
+
+
+def dropout_apply(x, y, seed: int, pkeep: float, counter=None):
+    """y = x * mask(seed[, counter]) / pkeep; forward and backward use the same call (x may alias y).
+
+    counter: optional int32 device tensor; the mask seed is hash(counter, seed), read on
+    device, so a captured HIP graph draws a new mask on every replay.
+    """
+    if not x.is_cuda:
+        m = dropout_mask_ref(x.numel(), effective_seed(seed, counter), pkeep).view_as(x).to(x.dtype)
+        y.copy_(x * m)
+        return
+    native.check(_k().cxn_dropout(x.data_ptr(), y.data_ptr(), x.numel(), seed & 0xFFFFFFFF,
+                                  counter.data_ptr() if counter is not None else None, float(pkeep),
+                                  _stream()), "dropout")
+
+
+# ----------------------------------------------------------------------------- softmax / losses
+def softmax_forward(x, y, p32=None):
+    """Row softmax of x[rows][K] into y (and the fp32 copy p32)."""
+    if not x.is_cuda:
+        p = torch.softmax(x.float(), dim=1)
+        y.copy_(p)
+        if p32 is not None:
+            p32.copy_(p)
+        return
+    rows, K = x.shape
+    native.check(_k().cxn_softmax(x.data_ptr(), y.data_ptr(), p32.data_ptr() if p32 is not None else None, rows, K,
+                                  _stream()), "softmax")
+
+
+LOSS_KIND = {"softmax": 0, "l2": 1, "multi_logistic": 2}
+
+
+def loss_grad(kind: str, node, label, scale: float, p32=None):
+    """node <- (pred - target) * scale, pred = p32 if given else node.  label fp32 [rows][lw]."""
+    rows, K = node.shape
+    lw = label.shape[1]
+    if not node.is_cuda:
+        p = p32 if p32 is not None else node
+        if kind == "softmax":
+            oh = torch.zeros_like(p)
+            oh.scatter_(1, label[:, :1].long(), 1.0)
+            node.copy_((p - oh) * scale)
+        else:
+            node.copy_((p - label) * scale)
+        return
+    native.check(_k().cxn_loss_grad(p32.data_ptr() if p32 is not None else None, node.data_ptr(), label.data_ptr(),
+                                    rows, K, lw, float(scale), LOSS_KIND[kind], _stream()), "loss_grad")
+
+
+# ----------------------------------------------------------------------------- reductions / misc
+def bias_grad(dy2d, db):
+    """db[C] += sum over rows of dy2d[rows][C]."""
+    if not dy2d.is_cuda:
+        db.add_(dy2d.sum(0))
+        return
+    rows, C = dy2d.shape
+    native.check(_k().cxn_colsum(dy2d.data_ptr(), db.data_ptr(), rows, C, _stream()), "colsum")
+
+
+def cast_to_bf16(src_f32, dst_bf16):
+    if not src_f32.is_cuda:
+        dst_bf16.copy_(src_f32)
+        return
+    native.check(_k().cxn_cast_f32_bf16(src_f32.data_ptr(), dst_bf16.data_ptr(), src_f32.numel(), _stream()), "cast")
+
+
+def add(a, b, y):
+    if not a.is_cuda:
+        torch.add(a, b, out=y)
+        return
+    native.check(_k().cxn_add_bf16(a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), _stream()), "add")
+
+
+def channel_copy(src, soff, dst, doff, cc, accumulate=False):
+    """dst[..., doff:doff+cc] (+)= src[..., soff:soff+cc] for NHWC tensors with equal pixel counts."""
+    Cs, Cd = src.shape[-1], dst.shape[-1]
+    npix = src.numel() // Cs
+    if not src.is_cuda:
+        d = dst.view(npix, Cd)[:, doff:doff + cc]
+        s = src.view(npix, Cs)[:, soff:soff + cc]
+        if accumulate:
+            d.add_(s)
+        else:
+            d.copy_(s)
+        return
+    native.check(_k().cxn_channel_copy(src.data_ptr(), Cs, soff, dst.data_ptr(), Cd, doff, cc, npix,
+                                       int(accumulate), _stream()), "channel_copy")

@@ -1,0 +1,260 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+Inputs are rounded to bf16 first; the reference then runs in fp32 on the CPU on
+those exact values, so the only differences are bf16 output rounding and fp32
+summation order.  (This is the pairtest idea of reference
+src/layer/pairtest_layer-inl.hpp, with torch as the slave implementation.)
+"""
+import pytest
+import torch
+
+from cxxnet_amd import ops
+from cxxnet_amd.ops.gemm import ConvGeom, conv_out_size
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rnd(*shape, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16).float()
+
+
+def relerr(a, b):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+CONV_CASES = [
+    # N, C(phys), H, W, Cout, K, stride, pad, groups
+    (2, 4, 227, 227, 96, 11, 4, 0, 1),     # AlexNet conv1 (3 channels padded to 4)
+    (2, 96, 27, 27, 256, 5, 1, 2, 2),      # AlexNet conv2 (grouped)
+    (3, 256, 13, 13, 384, 3, 1, 1, 1),     # AlexNet conv3
+    (2, 384, 13, 13, 256, 3, 1, 1, 2),     # AlexNet conv5
+    (2, 64, 17, 19, 40, 1, 1, 0, 1),       # 1x1, ragged spatial / Cout
+    (2, 32, 15, 15, 48, 3, 2, 1, 1),       # strided 3x3 (strided dgrad path)
+    (1, 8, 9, 9, 16, 5, 1, 2, 1),
+]
+
+
+def _geom(N, C, H, W, Cout, K, s, p, g):
+    Ho, Wo = conv_out_size(H, W, K, K, s, p, p)
+    return ConvGeom(N, H, W, C, Ho, Wo, Cout, K, K, s, p, p, g)
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_forward(case):
+    geo = _geom(*case)
+    x = rnd(geo.N, geo.H, geo.W, geo.C, seed=1)
+    w = rnd(geo.Cout, geo.KH, geo.KW, geo.cg_in, scale=0.05, seed=2)
+    b = rnd(geo.Cout, scale=0.1, seed=3)
+    y_ref = torch.empty(geo.N, geo.Ho, geo.Wo, geo.Cout)
+    ops.conv_forward(x, w, b, y_ref, geo, relu=True)
+    y = torch.empty(geo.N, geo.Ho, geo.Wo, geo.Cout, dtype=torch.bfloat16, device=DEV)
+    ops.conv_forward(x.to(DEV, torch.bfloat16), w.to(DEV, torch.bfloat16), b.to(DEV), y, geo, relu=True)
+    torch.cuda.synchronize()
+    assert relerr(y, y_ref) < 2e-2
+
+
+@pytest.mark.parametrize("case", CONV_CASES[1:])
+def test_conv_backward_data(case):
+    geo = _geom(*case)
+    dy = rnd(geo.N, geo.Ho, geo.Wo, geo.Cout, seed=4)
+    w = rnd(geo.Cout, geo.KH, geo.KW, geo.cg_in, scale=0.05, seed=5)
+    dx_ref = torch.empty(geo.N, geo.H, geo.W, geo.C)
+    ops.conv_backward_data(dy, w, dx_ref, geo)
+    dx = torch.empty(geo.N, geo.H, geo.W, geo.C, dtype=torch.bfloat16, device=DEV)
+    ops.conv_backward_data(dy.to(DEV, torch.bfloat16), w.to(DEV, torch.bfloat16), dx, geo)
+    torch.cuda.synchronize()
+    assert relerr(dx, dx_ref) < 2e-2
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_backward_weight(case):
+    geo = _geom(*case)
+    x = rnd(geo.N, geo.H, geo.W, geo.C, seed=6)
+    dy = rnd(geo.N, geo.Ho, geo.Wo, geo.Cout, seed=7)
+    init = rnd(geo.Cout, geo.KH, geo.KW, geo.cg_in, seed=8)
+    dw_ref = init.clone()
+    ops.conv_backward_weight(x, dy, dw_ref, geo)
+    dw = init.to(DEV).clone()
+    ops.conv_backward_weight(x.to(DEV, torch.bfloat16), dy.to(DEV, torch.bfloat16), dw, geo)
+    torch.cuda.synchronize()
+    assert relerr(dw, dw_ref) < 1e-2
+
+
+FC_CASES = [(256, 9216, 4096), (100, 784, 100), (100, 100, 10), (64, 256, 121), (32, 4096, 1000)]
+
+
+@pytest.mark.parametrize("B,nin,nout", FC_CASES)
+def test_fc(B, nin, nout):
+    x = rnd(B, nin, seed=9)
+    w = rnd(nout, nin, scale=0.02, seed=10)
+    b = rnd(nout, scale=0.1, seed=11)
+    dy = rnd(B, nout, seed=12)
+    y_ref = torch.empty(B, nout)
+    ops.fc_forward(x, w, b, y_ref)
+    dx_ref = torch.empty(B, nin)
+    ops.fc_backward_data(dy, w, dx_ref)
+    dw_ref = torch.ones(nout, nin)
+    ops.fc_backward_weight(x, dy, dw_ref)
+
+    xd, wd, dyd = (t.to(DEV, torch.bfloat16) for t in (x, w, dy))
+    y = torch.empty(B, nout, dtype=torch.bfloat16, device=DEV)
+    ops.fc_forward(xd, wd, b.to(DEV), y)
+    dx = torch.empty(B, nin, dtype=torch.bfloat16, device=DEV)
+    ops.fc_backward_data(dyd, wd, dx)
+    dw = torch.ones(nout, nin, device=DEV)
+    ops.fc_backward_weight(xd, dyd, dw)
+    torch.cuda.synchronize()
+    assert relerr(y, y_ref) < 2e-2
+    assert relerr(dx, dx_ref) < 2e-2
+    assert relerr(dw, dw_ref) < 1e-2
+
+
+@pytest.mark.parametrize("mode,relu,k,s,p,C", [("max", False, 3, 2, 0, 96), ("max", True, 3, 2, 0, 256),
+                                               ("avg", False, 3, 1, 1, 64), ("sum", False, 2, 2, 0, 8),
+                                               ("max", False, 3, 2, 0, 3)])
+def test_pool(mode, relu, k, s, p, C):
+    N, H, W = 2, 27, 27
+    Ho = ops.pool_out_size(H, k, s, p)
+    x = rnd(N, H, W, C, seed=13)
+    dy = rnd(N, Ho, Ho, C, seed=14)
+    y_ref = torch.empty(N, Ho, Ho, C)
+    st_ref = torch.empty_like(y_ref)
+    ops.pool_forward(x, y_ref, st_ref, k, k, s, p, mode, relu)
+    y_ref_b = y_ref.to(torch.bfloat16).float()  # the GPU keeps the pooled state in bf16
+    dx_ref = torch.empty_like(x)
+    ops.pool_backward(x, y_ref_b, dy, dx_ref, k, k, s, p, mode, relu)
+
+    xd = x.to(DEV, torch.bfloat16)
+    y = torch.empty(N, Ho, Ho, C, dtype=torch.bfloat16, device=DEV)
+    st = torch.empty_like(y)
+    ops.pool_forward(xd, y, st, k, k, s, p, mode, relu)
+    dx = torch.empty_like(xd)
+    ops.pool_backward(xd, st, dy.to(DEV, torch.bfloat16), dx, k, k, s, p, mode, relu)
+    torch.cuda.synchronize()
+    assert relerr(y, y_ref) < 1e-2
+    assert relerr(st, y_ref) < 1e-2
+    assert relerr(dx, dx_ref) < 2e-2
+
+
+def test_lrn():
+    N, H, W, C = 2, 13, 13, 96
+    x = rnd(N, H, W, C, scale=2.0, seed=15)
+    dy = rnd(N, H, W, C, seed=16)
+    args = (5, 0.001, 0.75, 1.0)
+    y_ref = torch.empty_like(x)
+    ops.lrn_forward(x, y_ref, *args)
+    dx_ref = torch.empty_like(x)
+    ops.lrn_backward(x, dy, dx_ref, *args)
+    xd = x.to(DEV, torch.bfloat16)
+    y = torch.empty_like(xd)
+    ops.lrn_forward(xd, y, *args)
+    dx = torch.empty_like(xd)
+    ops.lrn_backward(xd, dy.to(DEV, torch.bfloat16), dx, *args)
+    torch.cuda.synchronize()
+    assert relerr(y, y_ref) < 1e-2
+    assert relerr(dx, dx_ref) < 2e-2
+
+
+@pytest.mark.parametrize("kind", ["relu", "sigmoid", "tanh", "xelu"])
+def test_activation(kind):
+    x = rnd(1003, seed=17)
+    dy = rnd(1003, seed=18)
+    y_ref = torch.empty_like(x)
+    ops.act_forward(kind, x, y_ref)
+    y_ref_b = y_ref.to(torch.bfloat16).float()
+    dx_ref = torch.empty_like(x)
+    ops.act_backward(kind, y_ref_b, dy, dx_ref)
+    xd = x.to(DEV, torch.bfloat16)
+    y = torch.empty_like(xd)
+    y2 = torch.empty_like(xd)
+    ops.act_forward(kind, xd, y, y2)
+    dx = torch.empty_like(xd)
+    ops.act_backward(kind, y, dy.to(DEV, torch.bfloat16), dx)
+    torch.cuda.synchronize()
+    assert relerr(y, y_ref) < 1e-2 and torch.equal(y, y2)
+    assert relerr(dx, dx_ref) < 1e-2
+
+
+def test_dropout_mask_matches_reference():
+    n = 4099
+    x = rnd(n, seed=19)
+    y_ref = torch.empty_like(x)
+    ops.dropout_apply(x, y_ref, 1234, 0.5)
+    y = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    ops.dropout_apply(x.to(DEV, torch.bfloat16), y, 1234, 0.5)
+    torch.cuda.synchronize()
+    assert relerr(y, y_ref) < 1e-2
+    keep = (y.cpu() != 0).float().mean().item()
+    assert 0.45 < keep < 0.55
+
+
+def test_softmax_and_loss_grad():
+    rows, K = 37, 1000
+    x = rnd(rows, K, scale=3.0, seed=20)
+    label = torch.randint(0, K, (rows, 1)).float()
+    p_ref = torch.empty_like(x)
+    p32_ref = torch.empty_like(x)
+    ops.softmax_forward(x, p_ref, p32_ref)
+    g_ref = p_ref.clone()
+    ops.loss_grad("softmax", g_ref, label, 0.5, p32_ref)
+    xd = x.to(DEV, torch.bfloat16)
+    p = torch.empty_like(xd)
+    p32 = torch.empty(rows, K, device=DEV)
+    ops.softmax_forward(xd, p, p32)
+    ops.loss_grad("softmax", p, label.to(DEV), 0.5, p32)
+    torch.cuda.synchronize()
+    assert relerr(p32, p32_ref) < 1e-2
+    assert relerr(p, g_ref) < 1e-2
+
+
+@pytest.mark.parametrize("rows,C", [(30000, 96), (256, 4096), (100, 10)])
+def test_bias_grad(rows, C):
+    dy = rnd(rows, C, seed=21)
+    db_ref = torch.ones(C)
+    ops.bias_grad(dy, db_ref)
+    db = torch.ones(C, device=DEV)
+    ops.bias_grad(dy.to(DEV, torch.bfloat16), db)
+    torch.cuda.synchronize()
+    assert relerr(db, db_ref) < 1e-3
+
+
+@pytest.mark.parametrize("algo", ["sgd", "nag", "adam"])
+def test_fused_update(algo):
+    n = 10007
+    w = rnd(n, seed=22)
+    g = rnd(n, seed=23)
+    m = rnd(n, scale=0.1, seed=24)
+    m2 = rnd(n, scale=0.1, seed=25).abs()
+    segs = [(0, 5000, 0.01, 0.0005, 0.9, 0.0), (5000, n - 5000, 0.02, 0.0, 0.9, 0.5)]
+    ref = [t.clone() for t in (w, g, m, m2)]
+    wb_ref = torch.empty(n)
+    ops.fused_update(algo, ref[0], ref[1], ref[2], ref[3], wb_ref, segs)
+    dev = [t.to(DEV) for t in (w, g, m, m2)]
+    wb = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    ops.fused_update(algo, dev[0], dev[1], dev[2], dev[3], wb, segs)
+    torch.cuda.synchronize()
+    assert relerr(dev[0], ref[0]) < 1e-5
+    assert relerr(dev[2], ref[2]) < 1e-5
+    assert dev[1].abs().max().item() == 0.0
+    assert relerr(wb, ref[0]) < 1e-2
+
+
+def test_layout_roundtrip():
+    x = torch.randn(2, 3, 11, 13)
+    node = torch.empty(2, 11, 13, 4, dtype=torch.bfloat16, device=DEV)
+    ops.input_to_nhwc(x.to(DEV), node)
+    back = ops.nhwc_to_nchw(node, 3)
+    torch.cuda.synchronize()
+    assert relerr(back, x) < 1e-2
+    assert node[..., 3].abs().max().item() == 0
+    # flatten transpose
+    t = rnd(2, 6 * 6, 256, seed=26)
+    out = torch.empty(2, 256 * 36, dtype=torch.bfloat16, device=DEV)
+    ops.transpose(t.to(DEV, torch.bfloat16), out, 2, 36, 256)
+    ref = t.transpose(1, 2).reshape(2, -1)
+    torch.cuda.synchronize()
+    assert relerr(out, ref) < 1e-2
