@@ -1,0 +1,109 @@
+"""Flagship benchmark: AlexNet (reference example/ImageNet/ImageNet.conf) training
+throughput in images/sec on N MI355X GPUs of one node.
+
+  python bench.py --gpus N --steps K --warmup W
+For N > 1 run under torchrun (one process per GPU, RCCL over xGMI).
+
+Weak scaling: every GPU trains on a fixed per-GPU batch of 256 images (the conf's
+batch size), so the global batch is 256*N.  Data is synthetic 3x227x227 batches
+resident on the device with random-init weights (no dataset / checkpoint on the box).
+A step is the full training step: input layout conversion, forward, loss gradient,
+backward, gradient all-reduce (N > 1) and the fused SGD-momentum update.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_IMG_S = None  # filled from BASELINE.json "measured" when present
+
+
+def _baseline():
+    try:
+        with open(os.path.join(ROOT, "BASELINE.json")) as f:
+            b = json.load(f)
+        m = b.get("measured", {}).get("torch_eager_alexnet_img_s_per_gpu")
+        return float(m) if m else None
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--model", default="alexnet")
+    ap.add_argument("--graph", type=int, default=-1, help="capture the step in a HIP graph (1/0; -1 auto)")
+    a = ap.parse_args()
+
+    from cxxnet_amd.models import load_conf
+    from cxxnet_amd.nnet import NetTrainer
+    from cxxnet_amd.io.data import DataBatch
+    from cxxnet_amd.parallel import init_distributed
+    import torch.distributed as dist
+
+    rank, world = init_distributed()
+    if world != a.gpus and rank == 0:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    torch.cuda.set_device(dev)
+
+    global_batch = a.batch * world
+    pairs = load_conf(a.model, [("batch_size", str(global_batch)), ("eval_train", "0"), ("dev", "gpu"),
+                                ("silent", "1")])
+    pairs = [(k, v) for k, v in pairs if not k.startswith("metric")]
+    tr = NetTrainer()
+    for k, v in pairs:
+        tr.set_param(k, v)
+    tr.init_model()
+    c, h, w = tr.net_cfg.input_shape
+    g = torch.Generator(device="cpu").manual_seed(1234 + rank)
+    data = torch.randn(a.batch, c, h, w, generator=g).to(dev)
+    label = torch.randint(0, 1000, (a.batch, 1), generator=g).float().to(dev)
+    batch = DataBatch(data, label)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        tr.update(batch, local=True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        tr.update(batch, local=True)
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    ms = el / a.steps * 1000.0
+    value = global_batch * a.steps / el
+    base = _baseline()
+    if rank == 0:
+        out = {
+            "metric": "images/sec (whole node) AlexNet ImageNet training at 1/2/4/8 MI355X",
+            "value": round(value, 1), "unit": "images/sec", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": round(value / (base * world), 3) if base else None,
+            "dtype": "bf16", "data": "synthetic (3x227x227 on-device batches, random-init weights)",
+            "config": {"model": a.model, "global_batch": global_batch, "per_gpu_batch": a.batch,
+                       "seq_len": None, "parallelism": f"dp{world}", "input_shape": [c, h, w]},
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -53,6 +53,7 @@ struct Epilogue {
   const float *bias;  // indexed by i (nullable)
   long bias_gstride;
   int relu;
+  int mask_relu;      // bf16 out: keep a value only where the OLD output value is > 0
 };
 
 template <int MODE>
@@ -356,10 +357,21 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
         if (E.relu) f[e] = fmaxf(f[e], 0.f);
       }
       bf16_t *dst = out + static_cast<long>(j) * E.ldc + i;
+      // mask_relu: the destination holds the forward activation relu(z) of a fused
+      // producer->relu pair; the data-grad it is overwritten with is masked by relu'(z).
       if (vec_store) {
+        if (E.mask_relu) {
+          float old[8];
+          unpack8(*reinterpret_cast<const uint4 *>(dst), old);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = old[e] > 0.f ? f[e] : 0.f;
+        }
         *reinterpret_cast<uint4 *>(dst) = pack8(f);
       } else {
-        for (int e = 0; e < 8 && i + e < Mi; ++e) dst[e] = f2bf(f[e]);
+        for (int e = 0; e < 8 && i + e < Mi; ++e) {
+          if (E.mask_relu && !(bf2f(dst[e]) > 0.f)) f[e] = 0.f;
+          dst[e] = f2bf(f[e]);
+        }
       }
     }
   } else {
@@ -464,12 +476,12 @@ static Operand to_operand(const CxnOperand &o, int mode, int vec) {
 
 CXN_API int cxn_gemm(const CxnOperand *a, const CxnOperand *b, int amode, int bmode, int va, int vb,
                      void *out, long out_gstride, int ldc, float alpha, const float *bias, long bias_gstride,
-                     int relu, int epi, int tile, int groups, int ksplit, void *stream) {
+                     int relu, int mask_relu, int epi, int tile, int groups, int ksplit, void *stream) {
   GemmArgs g{amode, bmode, va, vb, epi, tile, groups < 1 ? 1 : groups, ksplit < 1 ? 1 : ksplit};
   Operand A = to_operand(*a, amode, va), B = to_operand(*b, bmode, vb);
   if (A.kdim != B.kdim) return -2;
   if (A.rows <= 0 || B.rows <= 0 || A.kdim <= 0) return 0;
-  Epilogue E{out, out_gstride, ldc, alpha, bias, bias_gstride, relu};
+  Epilogue E{out, out_gstride, ldc, alpha, bias, bias_gstride, relu, mask_relu};
   hipStream_t s = static_cast<hipStream_t>(stream);
   int rc = (tile == 64) ? dispatch_tile<64, 64>(g, A, B, E, s) : dispatch_tile<128, 128>(g, A, B, E, s);
   if (rc != 0) return rc;

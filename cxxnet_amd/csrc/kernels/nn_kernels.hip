@@ -86,9 +86,10 @@ __global__ void conv_weight_flip(const bf16_t *__restrict__ w, bf16_t *__restric
 // ------------------------------------------------------------------ pooling
 // mode: 0 max, 1 sum, 2 avg.  relu: apply relu before max (relu_max_pooling).
 // Output size follows the reference ceil rule: min(Hp - k + s - 1, Hp - 1) / s + 1, Hp = H + 2 pad.
+// Max mode records, per output, the window offset (kh*KW + kw, uint8) of the FIRST maximum.
 template <int VEC>
-__global__ void pool_fwd(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, bf16_t *__restrict__ y2, int N, int H, int W, int C, int Ho,
-                         int Wo, int KH, int KW, int S, int P, int mode, int relu) {
+__global__ void pool_fwd(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, uint8_t *__restrict__ arg, int N,
+                         int H, int W, int C, int Ho, int Wo, int KH, int KW, int S, int P, int mode, int relu) {
   const int CV = C / VEC;
   const long total = static_cast<long>(N) * Ho * Wo * CV;
   const float inv = 1.0f / (KH * KW);
@@ -101,39 +102,53 @@ __global__ void pool_fwd(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, b
     const int hs = ho * S - P, ws = wo * S - P;
     const int he = min(hs + KH, H), we = min(ws + KW, W);
     float acc[VEC];
+    uint32_t am[VEC];
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) acc[e] = mode == 0 ? -INFINITY : 0.f;
+    for (int e = 0; e < VEC; ++e) {
+      acc[e] = mode == 0 ? -INFINITY : 0.f;
+      am[e] = 0;
+    }
     for (int h = max(hs, 0); h < he; ++h)
       for (int w = max(ws, 0); w < we; ++w) {
         const bf16_t *p = x + ((static_cast<long>(n) * H + h) * W + w) * C + cv * VEC;
+        const uint32_t off = static_cast<uint32_t>((h - hs) * KW + (w - ws));
         float v[VEC];
         if constexpr (VEC == 8) unpack8(*reinterpret_cast<const uint4 *>(p), v);
         else v[0] = bf2f(*p);
 #pragma unroll
         for (int e = 0; e < VEC; ++e) {
-          float a = relu ? fmaxf(v[e], 0.f) : v[e];
-          acc[e] = mode == 0 ? fmaxf(acc[e], a) : acc[e] + a;
+          const float a = relu ? fmaxf(v[e], 0.f) : v[e];
+          if (mode == 0) {
+            if (a > acc[e]) {
+              acc[e] = a;
+              am[e] = off;
+            }
+          } else {
+            acc[e] += a;
+          }
         }
       }
     if (mode == 2)
 #pragma unroll
       for (int e = 0; e < VEC; ++e) acc[e] *= inv;
     if constexpr (VEC == 8) {
-      const uint4 o = pack8(acc);
-      *reinterpret_cast<uint4 *>(y + idx * VEC) = o;
-      if (y2) *reinterpret_cast<uint4 *>(y2 + idx * VEC) = o;
+      *reinterpret_cast<uint4 *>(y + idx * VEC) = pack8(acc);
+      if (arg)
+        *reinterpret_cast<uint2 *>(arg + idx * VEC) =
+            make_uint2(am[0] | am[1] << 8 | am[2] << 16 | am[3] << 24, am[4] | am[5] << 8 | am[6] << 16 | am[7] << 24);
     } else {
       y[idx] = f2bf(acc[0]);
-      if (y2) y2[idx] = f2bf(acc[0]);
+      if (arg) arg[idx] = static_cast<uint8_t>(am[0]);
     }
   }
 }
 
-// Gather-form backward: each input element sums over the windows that contain it.
-// Max: every input equal to the window maximum receives the gradient (value compare,
-// reference unpool semantics).  relu: multiply by relu'(x).
+// Gather-form backward: each input element sums the gradients of the windows that contain
+// it.  Max: the window's recorded first-maximum position receives the gradient (the
+// reference compares values, src/layer/pooling_layer-inl.hpp:55-86, which with bf16
+// activations would hand duplicates to rounding ties).  relu: multiply by relu'(x).
 template <int VEC>
-__global__ void pool_bwd(const bf16_t *__restrict__ x, const bf16_t *__restrict__ y, const bf16_t *__restrict__ dy,
+__global__ void pool_bwd(const bf16_t *__restrict__ x, const uint8_t *__restrict__ arg, const bf16_t *__restrict__ dy,
                          bf16_t *__restrict__ dx, int N, int H, int W, int C, int Ho, int Wo, int KH, int KW, int S,
                          int P, int mode, int relu) {
   const int CV = C / VEC;
@@ -146,7 +161,7 @@ __global__ void pool_bwd(const bf16_t *__restrict__ x, const bf16_t *__restrict_
     const int h = t % H;
     const int n = t / H;
     float xv[VEC], g[VEC];
-    if (mode == 0 || relu) {
+    if (relu) {
       if constexpr (VEC == 8) unpack8(*reinterpret_cast<const uint4 *>(x + idx * VEC), xv);
       else xv[0] = bf2f(x[idx]);
     }
@@ -158,23 +173,27 @@ __global__ void pool_bwd(const bf16_t *__restrict__ x, const bf16_t *__restrict_
     for (int ho = hlo; ho <= hhi; ++ho)
       for (int wo = wlo; wo <= whi; ++wo) {
         const long o = ((static_cast<long>(n) * Ho + ho) * Wo + wo) * C + cv * VEC;
-        float gv[VEC], yv[VEC];
+        const uint32_t off = static_cast<uint32_t>((h - (ho * S - P)) * KW + (w - (wo * S - P)));
+        float gv[VEC];
+        uint32_t am[VEC];
         if constexpr (VEC == 8) {
           unpack8(*reinterpret_cast<const uint4 *>(dy + o), gv);
-          if (mode == 0) unpack8(*reinterpret_cast<const uint4 *>(y + o), yv);
+          if (mode == 0) {
+            const uint2 a2 = *reinterpret_cast<const uint2 *>(arg + o);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              am[e] = (a2.x >> (8 * e)) & 0xff;
+              am[e + 4] = (a2.y >> (8 * e)) & 0xff;
+            }
+          }
         } else {
           gv[0] = bf2f(dy[o]);
-          if (mode == 0) yv[0] = bf2f(y[o]);
+          if (mode == 0) am[0] = arg[o];
         }
 #pragma unroll
         for (int e = 0; e < VEC; ++e) {
-          if (mode == 0) {
-            const float xr = relu ? fmaxf(xv[e], 0.f) : xv[e];
-            // y was rounded to bf16 from the same bf16 inputs, so equality is exact
-            g[e] += (xr == yv[e]) ? gv[e] : 0.f;
-          } else {
-            g[e] += mode == 2 ? gv[e] * inv : gv[e];
-          }
+          if (mode == 0) g[e] += (am[e] == off) ? gv[e] : 0.f;
+          else g[e] += mode == 2 ? gv[e] * inv : gv[e];
         }
       }
     if (relu)
@@ -497,26 +516,26 @@ CXN_API int cxn_conv_weight_flip(const void *w, void *wt, int G, int Co, int KH,
                                                                                      G, Co, KH, KW, Ci);
   RET;
 }
-CXN_API int cxn_pool_fwd(const void *x, void *y, void *y2, int N, int H, int W, int C, int Ho, int Wo, int KH, int KW, int S,
+CXN_API int cxn_pool_fwd(const void *x, void *y, void *arg, int N, int H, int W, int C, int Ho, int Wo, int KH, int KW, int S,
                          int P, int mode, int relu, void *stream) {
   if (C % 8 == 0) {
     pool_fwd<8><<<nblocks(static_cast<long>(N) * Ho * Wo * C / 8), NT, 0, S_>>>(
-        (const bf16_t *)x, (bf16_t *)y, (bf16_t *)y2, N, H, W, C, Ho, Wo, KH, KW, S, P, mode, relu);
+        (const bf16_t *)x, (bf16_t *)y, (uint8_t *)arg, N, H, W, C, Ho, Wo, KH, KW, S, P, mode, relu);
   } else {
     pool_fwd<1><<<nblocks(static_cast<long>(N) * Ho * Wo * C), NT, 0, S_>>>(
-        (const bf16_t *)x, (bf16_t *)y, (bf16_t *)y2, N, H, W, C, Ho, Wo, KH, KW, S, P, mode, relu);
+        (const bf16_t *)x, (bf16_t *)y, (uint8_t *)arg, N, H, W, C, Ho, Wo, KH, KW, S, P, mode, relu);
   }
   RET;
 }
-CXN_API int cxn_pool_bwd(const void *x, const void *y, const void *dy, void *dx, int N, int H, int W, int C, int Ho,
+CXN_API int cxn_pool_bwd(const void *x, const void *arg, const void *dy, void *dx, int N, int H, int W, int C, int Ho,
                          int Wo, int KH, int KW, int S, int P, int mode, int relu, void *stream) {
   if (C % 8 == 0) {
     pool_bwd<8><<<nblocks(static_cast<long>(N) * H * W * C / 8), NT, 0, S_>>>(
-        (const bf16_t *)x, (const bf16_t *)y, (const bf16_t *)dy, (bf16_t *)dx, N, H, W, C, Ho, Wo, KH, KW, S, P, mode,
+        (const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, N, H, W, C, Ho, Wo, KH, KW, S, P, mode,
         relu);
   } else {
     pool_bwd<1><<<nblocks(static_cast<long>(N) * H * W * C), NT, 0, S_>>>(
-        (const bf16_t *)x, (const bf16_t *)y, (const bf16_t *)dy, (bf16_t *)dx, N, H, W, C, Ho, Wo, KH, KW, S, P, mode,
+        (const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, N, H, W, C, Ho, Wo, KH, KW, S, P, mode,
         relu);
   }
   RET;

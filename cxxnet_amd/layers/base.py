@@ -37,14 +37,15 @@ class Node:
         return self.shape[0]
 
     def is_mat(self) -> bool:
-        return self.shape[2] == 1 and self.shape[3] == 1
+        """Reference convention: a matrix node is (batch, 1, 1, n)."""
+        return self.shape[1] == 1 and self.shape[2] == 1
 
     def alloc(self, device, dtype):
         b, c, h, w = self.shape
         self.data = torch.zeros((b, h, w, self.cp), device=device, dtype=dtype)
 
     def mat(self) -> torch.Tensor:
-        """(batch, features) view; valid for matrix nodes (c == cp)."""
+        """(batch, c*h*w) view (reference Node::mat); physical order is NHWC."""
         return self.data.view(self.data.shape[0], -1)
 
     def to_nchw(self) -> torch.Tensor:
@@ -97,6 +98,9 @@ class Layer:
         self.lp = native.rt().LayerParam()
         self.params: List[ParamSpec] = []
         self.layer_index = -1
+        # set by the executor's relu fusion: the input node holds relu(z) of a fused
+        # producer, so the gradient this layer writes into it must be masked by relu'(z)
+        self.grad_mask_relu = False
 
     # ---- configuration
     def set_param(self, name: str, val: str):

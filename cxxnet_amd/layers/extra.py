@@ -1,0 +1,523 @@
+"""Remaining reference layers: bias, split, concat, ch_concat, batch_norm, prelu,
+insanity, insanity_max_pooling, fixconn, pairtest.
+
+These are not on the benchmark models' hot path; their device math is written with
+torch tensor ops on the node buffers (fp32 internally) except concat/split/bias,
+which use the HIP channel-copy / add / column-sum kernels on the GPU.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from .base import BinReader, BinWriter, Layer, ParamSpec
+from .std import PoolingLayer, _bias_init, _check
+
+
+def _feat_axis(node):
+    """Per-channel axis of an NHWC node buffer (reference: dim 1 for conv nodes,
+    dim 3 for matrix nodes).  Physical layout is [b][h][w][c]."""
+    return 3 if node.shape[1] != 1 else 2
+
+
+def _num_feat(node):
+    return node.shape[1] if node.shape[1] != 1 else node.shape[3]
+
+
+class BiasLayer(Layer):
+    """`bias` -- reference src/layer/bias_layer-inl.hpp:14-83 (self-loop on a matrix node)."""
+    type_name = "bias"
+
+    def init_connection(self, nodes_in, nodes_out):
+        _check(len(nodes_in) == 1 and len(nodes_out) == 1, "BiasLayer: only support 1-1 connection")
+        _check(nodes_in[0] is nodes_out[0], "BiasLayer is a self-loop Layer")
+        _check(nodes_in[0].is_mat(), "BiasLayer: input need to be a matrix")
+        n = nodes_in[0].shape[3]
+        self.params = [ParamSpec("bias", (n,), _bias_init(self.lp.init_bias))]
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        m = nodes_in[0].mat()
+        m.copy_((m.float() + self.params[0].w).to(m.dtype))
+
+    def backprop(self, prop_grad, nodes_in, nodes_out):
+        ops.bias_grad(nodes_in[0].mat(), self.params[0].g)
+
+    def save_model(self, fo: BinWriter):
+        fo.write(self.lp.to_bytes())
+        fo.write_tensor(self.params[0].w)
+
+    def load_model(self, fi: BinReader):
+        self.lp = fi.read_layer_param()
+        self.loaded = [fi.read_tensor(1)]
+
+    def loaded_values(self):
+        return self.loaded
+
+
+class SplitLayer(Layer):
+    """`split` -- reference src/layer/split_layer-inl.hpp:12-45: 1 -> n copies, grads summed."""
+    type_name = "split"
+
+    def init_connection(self, nodes_in, nodes_out):
+        _check(len(nodes_in) == 1 and len(nodes_out) >= 1, "SplitLayer: only support 1-n connection")
+        for o in nodes_out:
+            o.set_shape(*nodes_in[0].shape, cp=nodes_in[0].cp)
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        for o in nodes_out:
+            o.data.copy_(nodes_in[0].data)
+
+    def backprop(self, prop_grad, nodes_in, nodes_out):
+        if not prop_grad:
+            return
+        x = nodes_in[0].data
+        x.copy_(nodes_out[0].data)
+        for o in nodes_out[1:]:
+            ops.add(x, o.data, x)
+
+
+class ConcatLayer(Layer):
+    """`concat` (dim 3) / `ch_concat` (dim 1) -- reference src/layer/concat_layer-inl.hpp:11-79,
+    2-4 inputs.  On NHWC buffers ch_concat is a strided channel copy per input."""
+
+    def __init__(self, ctx, dim):
+        super().__init__(ctx)
+        self.dim = dim
+        self.type_name = "ch_concat" if dim == 1 else "concat"
+
+    def init_connection(self, nodes_in, nodes_out):
+        _check(len(nodes_in) > 1 and len(nodes_out) == 1, "Concat layer only support n-1 connection")
+        _check(len(nodes_in) <= 4, "More than 4 input node is unspported")
+        s0 = list(nodes_in[0].shape)
+        tot = 0
+        for n in nodes_in:
+            _check(n.cp == n.shape[1], "Concat: padded-channel inputs are not supported")
+            tot += n.shape[self.dim]
+            for j in range(4):
+                if j != self.dim:
+                    _check(n.shape[j] == s0[j], "Concat shape doesn't match")
+        s0[self.dim] = tot
+        nodes_out[0].set_shape(*s0)
+
+    def _pieces(self, nodes_in, nodes_out):
+        out = nodes_out[0]
+        if self.dim == 1:
+            off = 0
+            for n in nodes_in:
+                yield n.data, out.data, off, n.shape[1]
+                off += n.shape[1]
+        else:
+            # width concat: in NHWC this is concat along axis 2 (w); matrix nodes are the common case
+            off = 0
+            for n in nodes_in:
+                yield n, out, off, n.shape[3]
+                off += n.shape[3]
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        if self.dim == 1:
+            for src, dst, off, c in self._pieces(nodes_in, nodes_out):
+                ops.channel_copy(src, 0, dst, off, c)
+        else:
+            torch.cat([n.data for n in nodes_in], dim=2, out=nodes_out[0].data)
+
+    def backprop(self, prop_grad, nodes_in, nodes_out):
+        if not prop_grad:
+            return
+        if self.dim == 1:
+            for src, dst, off, c in self._pieces(nodes_in, nodes_out):
+                ops.channel_copy(dst, off, src, 0, c)
+        else:
+            off = 0
+            for n in nodes_in:
+                w = n.shape[3]
+                n.data.copy_(nodes_out[0].data[:, :, off:off + w, :])
+                off += w
+
+
+class BatchNormLayer(Layer):
+    """`batch_norm` -- reference src/layer/batch_norm_layer-inl.hpp:14-197.  Batch
+    statistics in both train and test (no running mean), eps default 1e-10; slope is
+    visited as "wmat", bias as "bias"; the checkpoint holds slope + bias only."""
+    type_name = "batch_norm"
+
+    def __init__(self, ctx):
+        super().__init__(ctx)
+        self.init_slope = 1.0
+        self.init_bias = 0.0
+        self.eps = 1e-10
+
+    def set_param(self, name, val):
+        super().set_param(name, val)
+        if name == "init_slope":
+            self.init_slope = float(val)
+        elif name == "init_bias":
+            self.init_bias = float(val)
+        elif name == "eps":
+            self.eps = float(val)
+
+    def init_connection(self, nodes_in, nodes_out):
+        _check(len(nodes_in) == 1 and len(nodes_out) == 1, "BNLayer: only support 1-1 connection")
+        nodes_out[0].set_shape(*nodes_in[0].shape, cp=nodes_in[0].cp)
+        self.channel = _num_feat(nodes_in[0])
+        self.params = [ParamSpec("wmat", (self.channel,), _bias_init(self.init_slope)),
+                       ParamSpec("bias", (self.channel,), _bias_init(self.init_bias))]
+
+    def _view(self, node):
+        # -> [rows][channels] fp32 view of the buffer
+        return node.data.view(-1, self.channel)
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        x = self._view(nodes_in[0]).float()
+        mean = x.mean(0)
+        var = ((x - mean) ** 2).mean(0)
+        xhat = (x - mean) / torch.sqrt(var + self.eps)
+        slope, bias = self.params[0].w, self.params[1].w
+        if is_train:
+            self.saved = (x.clone(), mean, var)
+            self._view(nodes_in[0]).copy_(xhat)
+        self._view(nodes_out[0]).copy_(xhat * slope + bias)
+
+    def backprop(self, prop_grad, nodes_in, nodes_out):
+        x, mean, var = self.saved
+        g = self._view(nodes_out[0]).float()
+        xhat = self._view(nodes_in[0]).float()
+        slope = self.params[0].w
+        n = x.shape[0]
+        scale = 1.0 / n
+        inv = 1.0 / torch.sqrt(var + self.eps)
+        gvar = ((g * slope) * (x - mean) * -0.5 * (var + self.eps).pow(-1.5)).sum(0)
+        gexp = (g * slope).sum(0) * -inv
+        gexp = gexp + gvar * (scale * (-2.0 * (x - mean)).sum(0))
+        self.params[0].g.add_((g * xhat).sum(0))
+        self.params[1].g.add_(g.sum(0))
+        if prop_grad:
+            dx = g * slope * inv + gvar * scale * 2.0 * (x - mean) + gexp * scale
+            self._view(nodes_in[0]).copy_(dx)
+
+    def save_model(self, fo: BinWriter):
+        fo.write_tensor(self.params[0].w)
+        fo.write_tensor(self.params[1].w)
+
+    def load_model(self, fi: BinReader):
+        self.loaded = [fi.read_tensor(1), fi.read_tensor(1)]
+
+    def loaded_values(self):
+        return self.loaded
+
+
+class PReluLayer(Layer):
+    """`prelu` -- reference src/layer/prelu_layer-inl.hpp:48-173 (per-channel slope
+    clamped to [0,1], optional multiplicative train-time noise `random`; the slope is
+    visited with tag "bias")."""
+    type_name = "prelu"
+
+    def __init__(self, ctx):
+        super().__init__(ctx)
+        self.init_slope = 0.25
+        self.init_random = 0
+        self.random = 0.0
+
+    def set_param(self, name, val):
+        super().set_param(name, val)
+        if name == "init_slope":
+            self.init_slope = float(val)
+        elif name == "random_slope":
+            self.init_random = int(val)
+        elif name == "random":
+            self.random = float(val)
+
+    def init_connection(self, nodes_in, nodes_out):
+        _check(len(nodes_in) == 1 and len(nodes_out) == 1, "PReluLayer: only support 1-1 connection")
+        nodes_out[0].set_shape(*nodes_in[0].shape, cp=nodes_in[0].cp)
+        self.channel = _num_feat(nodes_in[0])
+
+        def init(t):
+            if self.init_random == 0:
+                t.fill_(self.init_slope)
+            else:
+                t.uniform_(0, 1, generator=self.ctx.gen).mul_(self.init_slope)
+        self.params = [ParamSpec("bias", (self.channel,), init)]
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        x = nodes_in[0].data.view(-1, self.channel).float()
+        slope = self.params[0].w
+        if is_train and self.random > 0:
+            u = torch.rand(x.shape, device=x.device)
+            mask = slope * (1 + u * self.random * 2.0 - self.random)
+        else:
+            mask = slope.expand_as(x)
+        self.mask = mask.clamp(0, 1)
+        nodes_out[0].data.view(-1, self.channel).copy_(torch.where(x > 0, x, x * self.mask))
+
+    def backprop(self, prop_grad, nodes_in, nodes_out):
+        x = nodes_in[0].data.view(-1, self.channel).float()
+        g = nodes_out[0].data.view(-1, self.channel).float()
+        self.params[0].g.add_((torch.clamp(x, max=0) * g).sum(0))
+        if prop_grad:
+            nodes_in[0].data.view(-1, self.channel).copy_(torch.where(x > 0, g, g * self.mask))
+
+    def save_model(self, fo: BinWriter):
+        fo.write_tensor(self.params[0].w)
+
+    def load_model(self, fi: BinReader):
+        self.loaded = [fi.read_tensor(1)]
+
+    def loaded_values(self):
+        return self.loaded
+
+
+class InsanityLayer(Layer):
+    """`insanity` (randomized leaky relu) -- reference src/layer/insanity_layer-inl.hpp:14-102:
+    x / U[lb,ub] for x<=0 in training, x / ((lb+ub)/2) at test; calm_start/calm_end anneal."""
+    type_name = "insanity"
+
+    def __init__(self, ctx):
+        super().__init__(ctx)
+        self.lb, self.ub = 5.0, 10.0
+        self.step = 0
+        self.sat_start = self.sat_end = 0
+        self.delta = 0.0
+        self.inited = False
+
+    def set_param(self, name, val):
+        super().set_param(name, val)
+        if name == "lb":
+            self.lb = float(val)
+        elif name == "ub":
+            self.ub = float(val)
+        elif name == "calm_start":
+            self.sat_start = int(val)
+        elif name == "calm_end":
+            self.sat_end = int(val)
+
+    def init_connection(self, nodes_in, nodes_out):
+        _check(len(nodes_in) == 1 and len(nodes_out) == 1, "InsanityLayer: only support 1-1 connection")
+        nodes_out[0].set_shape(*nodes_in[0].shape, cp=nodes_in[0].cp)
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        if not self.inited:
+            self.inited = True
+            d = (self.ub + self.lb) / 2.0
+            span = (self.sat_end - self.sat_start)
+            self.delta = (self.ub - d) / span if span != 0 else 0.0
+        if self.sat_start < self.step < self.sat_end:
+            self.ub -= self.delta * self.step
+            self.lb += self.delta * self.step
+            self.step += 1
+        x = nodes_in[0].data
+        xf = x.float()
+        if is_train:
+            self.mask = torch.rand(x.shape, device=x.device) * (self.ub - self.lb) + self.lb
+        else:
+            self.mask = torch.full_like(xf, (self.lb + self.ub) / 2.0)
+        y = torch.where(xf > 0, xf, xf / self.mask)
+        x.copy_(y)
+        if nodes_out[0] is not nodes_in[0]:
+            nodes_out[0].data.copy_(y)
+
+    def backprop(self, prop_grad, nodes_in, nodes_out):
+        if prop_grad:
+            y = nodes_in[0].data.float()
+            g = nodes_out[0].data.float()
+            nodes_in[0].data.copy_(torch.where(y > 0, g, g / self.mask))
+
+
+class InsanityPoolingLayer(PoolingLayer):
+    """`insanity_max_pooling` -- reference src/layer/insanity_pooling_layer-inl.hpp:222-286:
+    in training each source pixel is shifted by +-1 in y or x with probability (1-keep)/4."""
+
+    def __init__(self, ctx):
+        super().__init__(ctx, "max")
+        self.type_name = "insanity_max_pooling"
+        self.keep = 1.0
+
+    def set_param(self, name, val):
+        super().set_param(name, val)
+        if name == "keep":
+            self.keep = float(val)
+
+    def _shift_index(self, H, W, device):
+        u = torch.rand(H * W, device=device)
+        d = (1.0 - self.keep) / 4.0
+        ys = torch.arange(H, device=device).repeat_interleave(W)
+        xs = torch.arange(W, device=device).repeat(H)
+        ys = torch.where((u >= self.keep) & (u < self.keep + d), (ys - 1).clamp_min(0), ys)
+        ys = torch.where((u >= self.keep + d) & (u < self.keep + 2 * d), (ys + 1).clamp_max(H - 1), ys)
+        xs = torch.where((u >= self.keep + 2 * d) & (u < self.keep + 3 * d), (xs - 1).clamp_min(0), xs)
+        xs = torch.where(u >= self.keep + 3 * d, (xs + 1).clamp_max(W - 1), xs)
+        return ys * W + xs
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        x = nodes_in[0].data
+        if not is_train or self.keep >= 1.0:
+            return super().forward(is_train, nodes_in, nodes_out)
+        N, H, W, C = x.shape
+        self.idx = self._shift_index(H, W, x.device)
+        self.shifted = x.view(N, H * W, C)[:, self.idx, :].view_as(x).contiguous()
+        lp = self.lp
+        st = self._state(nodes_out[0])
+        ops.pool_forward(self.shifted, nodes_out[0].data, st, lp.kernel_height, lp.kernel_width, lp.stride,
+                         lp.pad_y, "max")
+
+    def backprop(self, prop_grad, nodes_in, nodes_out):
+        if not prop_grad:
+            return
+        if self.keep >= 1.0:
+            return super().backprop(prop_grad, nodes_in, nodes_out)
+        lp = self.lp
+        x = nodes_in[0].data
+        N, H, W, C = x.shape
+        gs = torch.empty_like(self.shifted)
+        ops.pool_backward(self.shifted, self.state, nodes_out[0].data, gs, lp.kernel_height, lp.kernel_width,
+                          lp.stride, lp.pad_y, "max")
+        # each source pixel's gradient comes from its (shifted) slot: gather-form, like the reference
+        x.view(N, H * W, C).copy_(gs.view(N, H * W, C))
+
+
+class FixConnectLayer(Layer):
+    """`fixconn` -- reference src/layer/fixconn_layer-inl.hpp:14-92: fixed sparse weight
+    from a text file (`nrow ncol nnz` then `row col value` triples); no weight gradient."""
+    type_name = "fixconn"
+
+    def __init__(self, ctx):
+        super().__init__(ctx)
+        self.fname = "NULL"
+
+    def set_param(self, name, val):
+        super().set_param(name, val)
+        if name == "fixconn_weight":
+            self.fname = val
+
+    def init_connection(self, nodes_in, nodes_out):
+        _check(len(nodes_in) == 1 and len(nodes_out) == 1, "FixConnLayer: Layer only support 1-1 connection")
+        _check(nodes_in[0].is_mat(), "FixConnLayer: input need to be a matrix")
+        _check(self.lp.num_hidden > 0, "FixConncLayer: must set nhidden correctly")
+        _check(self.fname != "NULL", "FixConnLayer: must specify fixconn_weight")
+        nin = nodes_in[0].shape[3]
+        nodes_out[0].set_shape(nodes_in[0].batch, 1, 1, self.lp.num_hidden)
+        w = torch.zeros(self.lp.num_hidden, nin)
+        with open(self.fname) as f:
+            toks = f.read().split()
+        nrow, ncol, nnz = int(toks[0]), int(toks[1]), int(toks[2])
+        _check(nrow == w.shape[0] and ncol == w.shape[1], "FixConnLayer: fixconn_weight shape do not match architecture")
+        for i in range(nnz):
+            r, c, v = int(toks[3 + 3 * i]), int(toks[4 + 3 * i]), float(toks[5 + 3 * i])
+            _check(r < nrow and c < ncol, "FixConnLayer: fixconn_weight index exceed matrix shape")
+            w[r, c] = v
+        self.w_host = w
+        self.wdev = None
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        x = nodes_in[0].mat()
+        if self.wdev is None:
+            self.wdev = self.w_host.to(x.device, x.dtype)
+        ops.fc_forward(x, self.wdev, None, nodes_out[0].mat())
+
+    def backprop(self, prop_grad, nodes_in, nodes_out):
+        if prop_grad:
+            ops.fc_backward_data(nodes_out[0].mat(), self.wdev, nodes_in[0].mat())
+
+
+class PairTestLayer(Layer):
+    """`pairtest-A-B` -- reference src/layer/pairtest_layer-inl.hpp:14-200: runs master and
+    slave on identical inputs and reports forward/backward discrepancies (relative L1 error
+    > 1e-5, or a bf16-aware bound on the GPU).  `master:`/`slave:` key prefixes configure
+    each side.  The master's results are propagated."""
+    type_name = "pairtest"
+    allow_sharing = False
+
+    def __init__(self, ctx, master, slave):
+        super().__init__(ctx)
+        self.master, self.slave = master, slave
+        self.tol = 1e-5 if not ctx.is_gpu else 2e-2
+        self.reports = []
+
+    def set_param(self, name, val):
+        if name.startswith("master:"):
+            self.master.set_param(name[7:], val)
+        elif name.startswith("slave:"):
+            self.slave.set_param(name[6:], val)
+        else:
+            self.master.set_param(name, val)
+            self.slave.set_param(name, val)
+
+    def init_connection(self, nodes_in, nodes_out):
+        from .base import Node
+        self.master.init_connection(nodes_in, nodes_out)
+        self.s_in = [Node(n.name + "@slave") for n in nodes_in]
+        self.s_out = [Node(n.name + "@slave") for n in nodes_out]
+        for a, b in zip(self.s_in, nodes_in):
+            a.set_shape(*b.shape, cp=b.cp)
+        self.slave.init_connection(self.s_in, self.s_out)
+        self.params = list(self.master.declare_params()) + list(self.slave.declare_params())
+        self.n_master = len(self.master.params)
+
+    def _alloc(self):
+        for n in self.s_in + self.s_out:
+            if n.data is None:
+                n.alloc(self.ctx.device, self.ctx.act_dtype)
+
+    @staticmethod
+    def _relerr(a, b):
+        a, b = a.float(), b.float()
+        return ((a - b).abs().sum() / (b.abs().sum() + 1e-12)).item()
+
+    def _cmp(self, what, a, b):
+        e = self._relerr(a, b)
+        if e > self.tol:
+            msg = f"[pairtest] {self.master.type_name}-{self.slave.type_name} {what}: rel err {e:.3e}"
+            self.reports.append(msg)
+            print(msg)
+
+    def forward(self, is_train, nodes_in, nodes_out):
+        self._alloc()
+        for a, b in zip(self.s_in, nodes_in):
+            a.data.copy_(b.data)
+        for pm, ps in zip(self.master.params, self.slave.params):
+            self._cmp("weight", ps.w, pm.w)
+        self.master.forward(is_train, nodes_in, nodes_out)
+        self.slave.forward(is_train, self.s_in, self.s_out)
+        for i, (a, b) in enumerate(zip(self.s_out, nodes_out)):
+            self._cmp(f"forward out[{i}]", a.data, b.data)
+
+    def backprop(self, prop_grad, nodes_in, nodes_out):
+        for a, b in zip(self.s_out, nodes_out):
+            a.data.copy_(b.data)
+        self.master.backprop(prop_grad, nodes_in, nodes_out)
+        self.slave.backprop(prop_grad, self.s_in, self.s_out)
+        for pm, ps in zip(self.master.params, self.slave.params):
+            self._cmp("grad", ps.g, pm.g)
+        if prop_grad:
+            for i, (a, b) in enumerate(zip(self.s_in, nodes_in)):
+                self._cmp(f"backprop in[{i}]", a.data, b.data)
+
+    def save_model(self, fo):
+        self.master.save_model(fo)
+        self.slave.save_model(fo)
+
+    def load_model(self, fi):
+        self.master.load_model(fi)
+        self.slave.load_model(fi)
+
+    def loaded_values(self):
+        out = []
+        for l in (self.master, self.slave):
+            if hasattr(l, "loaded_values"):
+                out += l.loaded_values()
+        return out
+
+
+def _register():
+    from . import register
+    register(17, BiasLayer)
+    register(23, SplitLayer)
+    register(18, lambda ctx: ConcatLayer(ctx, 3))
+    register(28, lambda ctx: ConcatLayer(ctx, 1))
+    register(30, BatchNormLayer)
+    register(29, PReluLayer)
+    register(24, InsanityLayer)
+    register(25, InsanityPoolingLayer)
+    register(31, FixConnectLayer)
+
+
+_register()

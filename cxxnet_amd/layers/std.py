@@ -50,7 +50,7 @@ class FullConnectLayer(Layer):
             self.lp.num_input_node = nin
         else:
             _check(self.lp.num_input_node == nin, "FullcLayer: input hidden nodes is not consistent")
-        nodes_out[0].set_shape(x.batch, self.lp.num_hidden, 1, 1)
+        nodes_out[0].set_shape(x.batch, 1, 1, self.lp.num_hidden)
         nh, ni = self.lp.num_hidden, self.lp.num_input_node
 
         def init_w(t):
@@ -78,7 +78,7 @@ class FullConnectLayer(Layer):
         if self.b is not None:
             ops.bias_grad(dy, self.b.g)
         if prop_grad:
-            ops.fc_backward_data(dy, self.w.wb, x)
+            ops.fc_backward_data(dy, self.w.wb, x, mask_relu=self.grad_mask_relu)
 
     def save_model(self, fo: BinWriter):
         fo.write(self.lp.to_bytes())
@@ -187,7 +187,7 @@ class ConvolutionLayer(Layer):
         if prop_grad:
             if self._wt is None or self._wt.shape != self.w.wb.shape:
                 self._wt = torch.empty_like(self.w.wb)
-            ops.conv_backward_data(dy, self.w.wb, x, self.geo, self._wt)
+            ops.conv_backward_data(dy, self.w.wb, x, self.geo, self._wt, mask_relu=self.grad_mask_relu)
 
     def save_model(self, fo: BinWriter):
         fo.write(self.lp.to_bytes())
@@ -231,9 +231,7 @@ class ActivationLayer(Layer):
     def forward(self, is_train, nodes_in, nodes_out):
         x, y = nodes_in[0], nodes_out[0]
         if self.fused_into_producer:
-            # the producer's epilogue already applied the activation in place on x
-            if x is not y:
-                y.data.copy_(x.data)
+            # the producer's epilogue applied the activation and y aliases x: nothing to do
             return
         if x is y:
             ops.act_forward(self.kind, x.data, x.data, None, self.b)
@@ -241,6 +239,8 @@ class ActivationLayer(Layer):
             ops.act_forward(self.kind, x.data, y.data, x.data, self.b)
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
+        if self.fused_into_producer:
+            return  # relu' was applied by the layer that wrote this node's gradient
         x, y = nodes_in[0], nodes_out[0]
         # x holds f(input) (in-place forward), y holds the incoming gradient
         ops.act_backward(self.kind, x.data, y.data, x.data, self.b)
@@ -271,8 +271,11 @@ class PoolingLayer(Layer):
         nodes_out[0].set_shape(b, c, ho, wo, cp=nodes_in[0].cp)
 
     def _state(self, y: Node):
+        # max mode: first-max window offsets (uint8); sum/avg need no state
+        if self.mode != "max":
+            return None
         if self.state is None or self.state.shape != y.data.shape:
-            self.state = torch.empty_like(y.data)
+            self.state = torch.empty(y.data.shape, dtype=torch.uint8, device=y.data.device)
         return self.state
 
     def forward(self, is_train, nodes_in, nodes_out):
@@ -287,7 +290,7 @@ class PoolingLayer(Layer):
         lp = self.lp
         x = nodes_in[0].data
         ops.pool_backward(x, self.state, nodes_out[0].data, x, lp.kernel_height, lp.kernel_width, lp.stride,
-                          lp.pad_y, self.mode, self.relu)
+                          lp.pad_y, self.mode, self.relu or self.grad_mask_relu)
 
 
 # ============================================================================ LRN

@@ -1,0 +1,299 @@
+"""Per-device executor: nodes, connections, parameter arena, forward/backprop.
+
+Behavioural parity with reference src/nnet/neural_net-inl.hpp:22-297 (NeuralNet):
+  * layers are created from NetConfig in conf order; `share[tag]` reuses the primary
+    layer object (weight tying);
+  * every layer receives the global config (defcfg) then its own layercfg;
+  * Forward copies the batch into node 0, runs layers in order; Backprop runs them in
+    reverse, with prop_grad=False for layer 0 unless prop_to_input.
+MI355X-first differences:
+  * one stream, no per-layer host sync (the reference waits after every parameterised
+    layer's backprop, :148): gradients stay on device, comm is event/stream ordered;
+  * parameters live in a flat arena updated by one fused kernel (nnet/arena.py);
+  * graph-level fusion on the GPU: conv/fullc -> relu pairs become a relu epilogue with
+    the relu output node aliasing its input (the reference's in-place activation), and
+    relu' is applied by the layer that writes that node's gradient (GEMM data-grad
+    epilogue or pooling backward) -- no separate activation kernels.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from .. import native, ops
+from ..layers import K_SHARED, LayerContext, Node, create_layer
+from ..layers.base import BinReader, BinWriter
+from ..updater import ArenaUpdater
+from .arena import ParamArena
+
+K_CONV, K_FULLC, K_RELU, K_MAXPOOL, K_DROPOUT = 10, 1, 3, 11, 8
+
+
+class Connection:
+    def __init__(self, layer, type_id, nodes_in, nodes_out, shared=False):
+        self.layer = layer
+        self.type = type_id
+        self.nodes_in = nodes_in
+        self.nodes_out = nodes_out
+        self.shared = shared
+
+
+class NeuralNet:
+    def __init__(self, cfg, batch_size: int, device="cpu", seed: int = 0, fuse: Optional[bool] = None):
+        self.cfg = cfg
+        self.max_batch = int(batch_size)
+        self.device = torch.device(device)
+        self.ctx = LayerContext(self.device, seed)
+        self.ctx.label_name_map = dict(cfg.label_name_map)
+        self.ctx.step_counter = torch.zeros(1, dtype=torch.int32, device=self.device)
+        if fuse is None:
+            fuse = self.ctx.is_gpu and os.environ.get("CXXNET_FUSE", "1") != "0"
+        self.fuse = fuse
+        self.nodes: List[Node] = []
+        self.connections: List[Connection] = []
+        self.arena: Optional[ParamArena] = None
+        self.updater: Optional[ArenaUpdater] = None
+        self.cur_batch = self.max_batch
+        self.epoch_counter = 0
+
+    # ------------------------------------------------------------------ construction
+    def _configure_layer(self, i, layer):
+        for k, v in self.cfg.defcfg:
+            layer.set_param(k, v)
+        for k, v in self.cfg.layercfg[i]:
+            layer.set_param(k, v)
+
+    def init_net(self):
+        cfg = self.cfg
+        self.nodes = [Node(n) for n in cfg.node_names]
+        c, h, w = cfg.input_shape
+        self.nodes[0].set_shape(self.max_batch, c, h, w)
+        for i in range(cfg.extra_data_num):
+            es = cfg.extra_shape[3 * i:3 * i + 3]
+            self.nodes[i + 1].set_shape(self.max_batch, *es)
+        self.connections = []
+        for i, info in enumerate(cfg.layers):
+            nin = [self.nodes[j] for j in info.nindex_in]
+            nout = [self.nodes[j] for j in info.nindex_out]
+            if info.type == K_SHARED:
+                prim = self.connections[info.primary_layer_index]
+                if not prim.layer.allow_sharing:
+                    raise ValueError("some layer you set shared do not allow sharing")
+                self.connections.append(Connection(prim.layer, prim.type, nin, nout, shared=True))
+            else:
+                layer = create_layer(info.type, self.ctx)
+                layer.layer_index = i
+                self.connections.append(Connection(layer, info.type, nin, nout))
+        self._pad_input_channels()
+        for i, c_ in enumerate(self.connections):
+            if not c_.shared:
+                self._configure_layer(i, c_.layer)
+
+    def _pad_input_channels(self):
+        """First-layer conv on the GPU: pad input channels to a multiple of 4 so the
+        implicit-GEMM gather can use 8-byte vector loads (weights get zero columns)."""
+        if not self.ctx.is_gpu:
+            return
+        n0 = self.nodes[0]
+        b, c, h, w = n0.shape
+        for conn in self.connections:
+            if conn.type == K_CONV and conn.nodes_in[0] is n0 and c % 8 != 0:
+                n0.cp = (c + 3) // 4 * 4
+                return
+
+    def _connect(self):
+        """Shape inference (InitConnection) in conf order."""
+        for conn in self.connections:
+            conn.layer.init_connection(conn.nodes_in, conn.nodes_out)
+
+    def _fuse(self):
+        if not self.fuse:
+            return
+        producers: Dict[int, list] = {}
+        consumers: Dict[int, list] = {}
+        for i, conn in enumerate(self.connections):
+            self_loop = len(conn.nodes_in) == 1 and conn.nodes_out == conn.nodes_in
+            for n in conn.nodes_out:
+                if not self_loop:
+                    producers.setdefault(id(n), []).append(i)
+            for n in conn.nodes_in:
+                consumers.setdefault(id(n), []).append((i, self_loop))
+        self.aliases = {}
+        for i, conn in enumerate(self.connections):
+            if conn.type != K_RELU or conn.shared or conn.nodes_in[0] is conn.nodes_out[0]:
+                continue
+            a, b = conn.nodes_in[0], conn.nodes_out[0]
+            prod = producers.get(id(a), [])
+            if len(prod) != 1:
+                continue
+            p = self.connections[prod[0]]
+            if p.type not in (K_CONV, K_FULLC) or p.shared:
+                continue
+            if len(consumers.get(id(a), [])) != 1:  # only the relu reads a
+                continue
+            cons = consumers.get(id(b), [])
+            real = [(j, sl) for j, sl in cons if not sl]
+            loops = [j for j, sl in cons if sl]
+            if len(real) != 1 or any(self.connections[j].type != K_DROPOUT for j in loops):
+                continue
+            j = real[0][0]
+            cj = self.connections[j]
+            if j == 0 or cj.shared or cj.type not in (K_CONV, K_FULLC, K_MAXPOOL) or len(cj.nodes_in) != 1:
+                continue
+            # commit: producer epilogue applies relu, b aliases a, consumer masks the gradient
+            p.layer.fuse_relu = True
+            conn.layer.fused_into_producer = True
+            cj.layer.grad_mask_relu = True
+            self.aliases[id(b)] = a
+
+    def _alloc_nodes(self):
+        dt = self.ctx.act_dtype
+        aliases = getattr(self, "aliases", {})
+        for n in self.nodes:
+            if id(n) not in aliases:
+                n.alloc(self.device, dt)
+        for n in self.nodes:
+            if id(n) in aliases:
+                src = aliases[id(n)]
+                if src.data is None:
+                    src.alloc(self.device, dt)
+                n.data = src.data
+
+    def _build_arena(self):
+        specs = []
+        for i, conn in enumerate(self.connections):
+            if not conn.shared:
+                specs.append((i, conn.layer.declare_params()))
+        self.arena = ParamArena(self.device, torch.bfloat16 if self.ctx.is_gpu else None)
+        self.arena.build(specs)
+
+    def _init_updater(self):
+        self.updater = ArenaUpdater(self.cfg.updater_type, self.arena, self.arena.segments(), self.cfg.defcfg,
+                                    self.cfg.layercfg)
+
+    def init_model(self):
+        """Fresh model: build, connect, random-init every parameter (reference InitModel)."""
+        self.init_net()
+        self._connect()
+        self._fuse()
+        self._alloc_nodes()
+        self._build_arena()
+        for li, spec in self.arena.specs:
+            host = torch.zeros(spec.shape, dtype=torch.float32)
+            spec.init(host)
+            spec.w.copy_(host)
+        self.arena.sync_shadow()
+        self._init_updater()
+
+    def load_model(self, fi: BinReader):
+        """Reference LoadModel: per-layer blob in layer order, shared layers skipped."""
+        self.init_net()
+        for conn in self.connections:
+            if not conn.shared:
+                conn.layer.load_model(fi)
+        self._connect()
+        self._fuse()
+        self._alloc_nodes()
+        self._build_arena()
+        for conn in self.connections:
+            if conn.shared or not hasattr(conn.layer, "loaded_values"):
+                continue
+            vals = conn.layer.loaded_values()
+            for spec, v in zip(conn.layer.params, vals):
+                spec.w.copy_(v.reshape(spec.shape))
+        self.arena.sync_shadow()
+        self._init_updater()
+
+    def save_model(self, fo: BinWriter):
+        for conn in self.connections:
+            if not conn.shared:
+                conn.layer.save_model(fo)
+
+    # ------------------------------------------------------------------ execution
+    def adjust_batch_size(self, b: int):
+        if b > self.max_batch:
+            raise ValueError("cannot set batch size larger than max batch")
+        if b == self.cur_batch:
+            return
+        self.cur_batch = b
+        for conn in self.connections:
+            conn.layer.on_batch_size_changed(conn.nodes_in, conn.nodes_out)
+
+    def node_view(self, n: Node) -> torch.Tensor:
+        return n.data[: self.cur_batch]
+
+    def set_input(self, data: torch.Tensor, extra: Sequence[torch.Tensor] = ()):
+        """data: (b, c, h, w) float tensor (any device)."""
+        b = data.shape[0]
+        self.adjust_batch_size(b)
+        n0 = self.nodes[0]
+        src = data.to(self.device, non_blocking=True)
+        ops.input_to_nhwc(src, n0.data[:b])
+        for i, e in enumerate(extra):
+            ops.input_to_nhwc(e.to(self.device, non_blocking=True), self.nodes[i + 1].data[:b])
+
+    def set_labels(self, labels: torch.Tensor):
+        """labels: (b, label_width) float; split into named fields by label_vec ranges."""
+        lab = labels.to(self.device, torch.float32, non_blocking=True)
+        if lab.dim() == 1:
+            lab = lab.view(-1, 1)
+        fields = {}
+        for name, idx in self.cfg.label_name_map.items():
+            a, b = self.cfg.label_range[idx]
+            fields[name] = lab[:, a:b]
+        self.ctx.label_fields = fields
+
+    def _batched(self, conn_nodes):
+        # temporarily narrow node buffers to the current batch
+        return conn_nodes
+
+    def forward(self, is_train: bool):
+        self.ctx.step_counter.add_(1)
+        with _BatchView(self):
+            for conn in self.connections:
+                conn.layer.forward(is_train, conn.nodes_in, conn.nodes_out)
+
+    def backprop(self, prop_to_input: bool = False, hook=None):
+        """Reverse pass.  hook(layer_index) runs after each layer's backprop (used by the
+        data-parallel bucketer to launch reductions as soon as gradients are final)."""
+        with _BatchView(self):
+            for i in range(len(self.connections) - 1, -1, -1):
+                conn = self.connections[i]
+                conn.layer.backprop(i != 0 or prop_to_input, conn.nodes_in, conn.nodes_out)
+                if hook is not None:
+                    hook(i)
+
+    def update(self, epoch: int):
+        self.updater.update(epoch)
+
+    def start_round(self, r: int):
+        if self.updater is not None:
+            self.updater.start_round(r)
+
+
+class _BatchView:
+    """Narrows every node buffer to the current batch for the duration of a pass."""
+
+    def __init__(self, net: NeuralNet):
+        self.net = net
+
+    def __enter__(self):
+        net = self.net
+        if net.cur_batch == net.max_batch:
+            self.saved = None
+            return
+        self.saved = [(n, n.data) for n in net.nodes]
+        seen = {}
+        for n, d in self.saved:
+            key = d.data_ptr()
+            if key not in seen:
+                seen[key] = d[: net.cur_batch]
+            n.data = seen[key]
+
+    def __exit__(self, *exc):
+        if self.saved is not None:
+            for n, d in self.saved:
+                n.data = d
+        return False

@@ -1,0 +1,339 @@
+"""Trainer: the INetTrainer API (reference src/nnet/nnet.h:18-100) over one device
+per process, data-parallel across processes.
+
+Reference: CXXNetThreadTrainer, src/nnet/nnet_impl-inl.hpp:16-455 -- device list,
+batch split step = ceil(batch/ndev), metric[label,node] parsing, Update with
+update_period, Predict (argmax or raw), ExtractFeature (name or top[-k]), Evaluate,
+Set/GetWeight, CopyModelFrom (finetune copy-by-name), and the model file:
+  int32 net_type | NetConfig | int64 epoch_counter | uint64 len + per-layer blob.
+"""
+from __future__ import annotations
+
+import struct
+from typing import List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from .. import native
+from ..layers.base import BinReader, BinWriter
+from ..parallel.dp import GradReducer, world_info
+from ..utils.metric import MetricSet
+from .neural_net import NeuralNet
+
+
+def parse_devices(val: str):
+    """'gpu', 'gpu:0-3', 'gpu:0,1', 'cpu' -> (kind, [ids])."""
+    kind = val.split(":")[0]
+    ids = []
+    if ":" in val:
+        spec = val.split(":", 1)[1]
+        if "-" in spec:
+            a, b = spec.split("-")
+            ids = list(range(int(a), int(b) + 1))
+        else:
+            ids = [int(x) for x in spec.split(",") if x != ""]
+    return kind, ids
+
+
+class NetTrainer:
+    def __init__(self, net_type: int = 0):
+        self.net_type = net_type
+        self.batch_size = 100
+        self.update_period = 1
+        self.sample_counter = 0
+        self.eval_train = 1
+        self.epoch_counter = 0
+        self.seed = 0
+        self.silent = 0
+        self.dev = "cpu"
+        self.device_ids: List[int] = []
+        self.type_pserver = "UNSPECIFIED"
+        self.bucket_mb = 64.0
+        self.comm_dtype = "fp32"
+        self.cfg: List[Tuple[str, str]] = []
+        self.metric = MetricSet()
+        self.train_metric = MetricSet()
+        self.eval_nodes: List[Tuple[str, int]] = []
+        self.net_cfg = native.rt().NetConfig()
+        self.net: Optional[NeuralNet] = None
+        self.reducer: Optional[GradReducer] = None
+        self.rank, self.world = world_info()
+
+    # ------------------------------------------------------------------ configuration
+    def set_param(self, name: str, val: str):
+        if name == "dev":
+            kind, ids = parse_devices(val)
+            self.dev = kind
+            self.device_ids = ids
+        elif name == "batch_size":
+            self.batch_size = int(val)
+        elif name == "update_period":
+            self.update_period = int(val)
+        elif name == "eval_train":
+            self.eval_train = int(val)
+        elif name == "seed":
+            self.seed = int(val)
+        elif name == "silent":
+            self.silent = int(val)
+        elif name == "param_server":
+            self.type_pserver = val
+        elif name == "dp_bucket_mb":
+            self.bucket_mb = float(val)
+        elif name == "dp_comm_dtype":
+            self.comm_dtype = val
+        if name.startswith("metric"):
+            import re
+            m = re.match(r"metric\[([^,\]]+),([^\]]+)\]", name)
+            if m:
+                self.metric.add_metric(val, m.group(1))
+                self.train_metric.add_metric(val, m.group(1))
+                self.eval_nodes.append((m.group(2), 0))
+            else:
+                m1 = re.match(r"metric\[([^\]]+)\]", name)
+                field = m1.group(1) if m1 else "label"
+                self.metric.add_metric(val, field)
+                self.train_metric.add_metric(val, field)
+                self.eval_nodes.append(("", -1))
+        self.cfg.append((name, val))
+
+    def _device(self) -> torch.device:
+        if self.dev == "gpu" and torch.cuda.is_available():
+            if self.world > 1:
+                return torch.device("cuda", torch.cuda.current_device())
+            idx = self.device_ids[0] if self.device_ids else 0
+            return torch.device("cuda", idx)
+        return torch.device("cpu")
+
+    def _local_batch(self) -> int:
+        step = max((self.batch_size + self.world - 1) // self.world, 1)
+        return step
+
+    def _make_net(self) -> NeuralNet:
+        net = NeuralNet(self.net_cfg, self._local_batch(), self._device(), seed=self.seed)
+        return net
+
+    def _forward_global_params(self, net: NeuralNet):
+        # the loss layers need the GLOBAL batch size and the update period
+        for conn in net.connections:
+            if hasattr(conn.layer, "batch_size") and conn.layer.batch_size == 0:
+                conn.layer.batch_size = self.batch_size
+            if hasattr(conn.layer, "update_period"):
+                conn.layer.update_period = self.update_period
+
+    def _init_eval_nodes(self):
+        self.eval_ids = []
+        for name, flag in self.eval_nodes:
+            if flag == -1 or name == "":
+                self.eval_ids.append(len(self.net.nodes) - 1)
+            else:
+                self.eval_ids.append(self.net_cfg.node_name_map[name])
+        if not self.eval_ids:
+            self.eval_ids = []
+
+    def _post_init(self):
+        self._forward_global_params(self.net)
+        self._init_eval_nodes()
+        self.reducer = GradReducer(self.net.arena, self.bucket_mb, True, self.comm_dtype)
+        self.reducer.broadcast_params()
+
+    def init_model(self):
+        self.net_cfg.configure(self.cfg)
+        self.net = self._make_net()
+        self.net.init_model()
+        self._post_init()
+
+    # ------------------------------------------------------------------ model io
+    def save_model(self) -> bytes:
+        fo = BinWriter()
+        self.net.save_model(fo)
+        blob = fo.getvalue()
+        return self.net_cfg.save_net() + struct.pack("<qQ", self.epoch_counter, len(blob)) + blob
+
+    def load_model(self, data: bytes, pos: int = 0):
+        used = self.net_cfg.load_net(data[pos:])
+        pos += used
+        self.epoch_counter, blen = struct.unpack_from("<qQ", data, pos)
+        pos += 16
+        blob = data[pos:pos + blen]
+        self.net_cfg.configure(self.cfg)
+        self.net = self._make_net()
+        self.net.load_model(BinReader(blob))
+        self._post_init()
+
+    def copy_model_from(self, other: "NetTrainer"):
+        """Finetune: copy every layer whose name matches (reference nnet_impl-inl.hpp:101-134)."""
+        src_map = dict(other.net_cfg.layer_name_map)
+        for name, li in self.net_cfg.layer_name_map.items():
+            if name not in src_map:
+                continue
+            sl = other.net.connections[src_map[name]].layer
+            dl = self.net.connections[li].layer
+            if len(sl.params) != len(dl.params):
+                continue
+            ok = all(tuple(a.shape) == tuple(b.shape) for a, b in zip(sl.params, dl.params))
+            if not ok:
+                raise ValueError(f"CopyModelFrom: layer {name} shape mismatch")
+            print(f"Copying layer {name}")
+            for a, b in zip(sl.params, dl.params):
+                b.w.copy_(a.w.to(b.w.device))
+        self.net.arena.sync_shadow()
+
+    # ------------------------------------------------------------------ training
+    def start_round(self, r: int):
+        self.net.start_round(r)
+
+    def _slice(self, t: torch.Tensor, b: int):
+        step = self._local_batch()
+        lo = min(self.rank * step, b)
+        hi = min((self.rank + 1) * step, b)
+        return t[lo:hi]
+
+    def _set_batch(self, batch, local=False):
+        b = batch.batch_size
+        if local:  # batch already holds this rank's rows
+            data, extra, label = batch.data, batch.extra_data, batch.label
+        else:
+            data = self._slice(batch.data, b)
+            extra = [self._slice(e, b) for e in batch.extra_data]
+            label = self._slice(batch.label, b)
+        self.net.set_input(data, extra)
+        self.net.set_labels(label)
+        return data.shape[0]
+
+    def update(self, batch, local=False):
+        """One training step on a global batch (each rank takes its slice), or on this
+        rank's rows directly when local=True."""
+        need_update = (self.sample_counter + 1) % self.update_period == 0
+        self._set_batch(batch, local)
+        net = self.net
+        net.forward(True)
+        evals = self._collect_eval() if self.eval_train else None
+        if need_update:
+            self.reducer.start_step()
+            net.backprop(False, hook=self.reducer.hook)
+            self.reducer.finish()
+            net.update(self.epoch_counter)
+        else:
+            net.backprop(False)
+        if evals is not None:
+            self.train_metric.add_eval(evals, self._label_fields(batch))
+        self.sample_counter += 1
+        if self.sample_counter >= self.update_period:
+            self.sample_counter = 0
+            self.epoch_counter += 1
+
+    # ------------------------------------------------------------------ inference
+    def _node_output(self, nid: int) -> torch.Tensor:
+        node = self.net.nodes[nid]
+        if node.fp32_view is not None:
+            out = node.fp32_view[: self.net.cur_batch]
+            return out.view(out.shape[0], *node.shape[1:])
+        with_data = node.data[: self.net.cur_batch]
+        from ..ops import nhwc_to_nchw
+        return nhwc_to_nchw(with_data, node.shape[1])
+
+    def _gather(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:
+            return t
+        import torch.distributed as dist
+        n = torch.tensor([t.shape[0]], device=t.device)
+        sizes = [torch.zeros_like(n) for _ in range(self.world)]
+        dist.all_gather(sizes, n)
+        mx = int(max(s.item() for s in sizes))
+        pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        pad[: t.shape[0]] = t
+        outs = [torch.empty_like(pad) for _ in range(self.world)]
+        dist.all_gather(outs, pad)
+        return torch.cat([o[: int(s.item())] for o, s in zip(outs, sizes)], 0)
+
+    def _collect_eval(self) -> List[np.ndarray]:
+        out = []
+        for nid in self.eval_ids:
+            t = self._gather(self._node_output(nid).reshape(self.net.cur_batch, -1).float())
+            out.append(t.cpu().numpy())
+        return out
+
+    def _label_fields(self, batch):
+        lab = batch.label.float().cpu().numpy()
+        if lab.ndim == 1:
+            lab = lab.reshape(-1, 1)
+        out = {}
+        for name, idx in self.net_cfg.label_name_map.items():
+            a, b = self.net_cfg.label_range[idx]
+            out[name] = lab[:, a:b]
+        return out
+
+    def forward_to(self, node_ids: List[int], batch) -> List[np.ndarray]:
+        self._set_batch(batch)
+        self.net.forward(False)
+        return [self._gather(self._node_output(n).contiguous().float()).cpu().numpy() for n in node_ids]
+
+    def predict(self, batch) -> np.ndarray:
+        out = self.forward_to([len(self.net.nodes) - 1], batch)[0]
+        out = out.reshape(out.shape[0], -1)
+        if out.shape[1] != 1:
+            return out.argmax(1).astype(np.float32)
+        return out[:, 0].astype(np.float32)
+
+    def extract_feature(self, batch, node_name: str) -> np.ndarray:
+        import re
+        m = re.match(r"top\[-(\d+)\]", node_name)
+        nnode = len(self.net.nodes)
+        if m:
+            off = int(m.group(1))
+            if not (1 <= off <= nnode):
+                raise ValueError("ExtractFeature: offset must be within num_node range")
+            nid = nnode - off
+        else:
+            if node_name not in self.net_cfg.node_name_map:
+                raise ValueError(f"ExtractFeature: Cannot find node name: {node_name}")
+            nid = self.net_cfg.node_name_map[node_name]
+        return self.forward_to([nid], batch)[0]
+
+    def evaluate(self, it, data_name: str) -> str:
+        ret = ""
+        if self.eval_train != 0:
+            ret += self.train_metric.print("train")
+            self.train_metric.clear()
+        if it is None:
+            return ret
+        self.metric.clear()
+        it.before_first()
+        while it.next():
+            batch = it.value()
+            scores = self.forward_to(self.eval_ids, batch)
+            n = batch.batch_size - batch.num_batch_padd
+            scores = [s[:n].reshape(n, -1) for s in scores]
+            fields = {k: v[:n] for k, v in self._label_fields(batch).items()}
+            self.metric.add_eval(scores, fields)
+        ret += self.metric.print(data_name)
+        return ret
+
+    # ------------------------------------------------------------------ weights
+    def _param(self, layer_name: str, tag: str):
+        if tag not in ("bias", "wmat"):
+            raise ValueError("NNet.SetWeight: weight tag can only be bias or wmat")
+        li = self.net_cfg.get_layer_index(layer_name)
+        layer = self.net.connections[li].layer
+        for p in layer.params:
+            if p.tag == tag:
+                return layer, p
+        raise ValueError(f"layer {layer_name} has no {tag}")
+
+    def get_weight(self, layer_name: str, tag: str) -> np.ndarray:
+        layer, p = self._param(layer_name, tag)
+        w = p.w.detach().float().cpu()
+        if hasattr(layer, "to_logical") and tag == "wmat":
+            w = layer.to_logical(w)
+        return w.reshape(w.shape[0], -1).numpy() if w.dim() > 1 else w.reshape(1, -1).numpy()
+
+    def set_weight(self, weight: np.ndarray, layer_name: str, tag: str):
+        layer, p = self._param(layer_name, tag)
+        w = torch.as_tensor(np.asarray(weight, dtype=np.float32))
+        if hasattr(layer, "from_logical") and tag == "wmat":
+            lp = layer.lp
+            G = lp.num_group
+            w = layer.from_logical(w.reshape(G, lp.num_channel // G, -1))
+        p.w.copy_(w.reshape(p.shape))
+        self.net.arena.sync_shadow()

@@ -83,12 +83,13 @@ def _pick_tile(rows_i, rows_j, groups):
 
 
 def _gemm(a, b, amode, bmode, va, vb, out, out_gstride, ldc, *, alpha=1.0, bias=None, bias_gstride=0,
-          relu=False, epi=EPI_BF16, groups=1, ksplit=1, tile=None):
+          relu=False, mask_relu=False, epi=EPI_BF16, groups=1, ksplit=1, tile=None):
     if tile is None:
         tile = _pick_tile(a.rows, b.rows, groups)
     rc = native.kernels().cxn_gemm(
         a, b, amode, bmode, va, vb, out.data_ptr(), out_gstride, ldc, float(alpha),
-        bias.data_ptr() if bias is not None else None, bias_gstride, int(relu), epi, tile, groups, ksplit,
+        bias.data_ptr() if bias is not None else None, bias_gstride, int(relu), int(mask_relu), epi, tile, groups,
+        ksplit,
         _stream())
     native.check(rc, "gemm")
 
@@ -132,13 +133,16 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
           epi=EPI_BF16, groups=g.groups)
 
 
-def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None):
-    """dx = conv_transpose(dy, w).  Returns nothing; dx overwritten."""
+def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False):
+    """dx = conv_transpose(dy, w); dx overwritten.  mask_relu: dx holds relu(z) on entry
+    (fused producer->relu) and the result is multiplied by relu'(z)."""
     if not dy.is_cuda:
         dyn = dy.permute(0, 3, 1, 2)
         out = torch.nn.grad.conv2d_input((g.N, g.C, g.H, g.W), _w_nchw(w), dyn, stride=g.stride,
-                                         padding=(g.pad_y, g.pad_x), groups=g.groups)
-        dx.copy_(out.permute(0, 2, 3, 1))
+                                         padding=(g.pad_y, g.pad_x), groups=g.groups).permute(0, 2, 3, 1)
+        if mask_relu:
+            out = out * (dx > 0).to(out.dtype)
+        dx.copy_(out)
         return
     cg_in, cg_out = g.cg_in, g.cg_out
     if cg_out % 8:
@@ -152,7 +156,7 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None):
     A = _op(wt_buf.data_ptr(), cg_in * kd, kd, cg_in, kd)
     B = _op(dy.data_ptr(), cg_out, 0, g.N * g.H * g.W, kd, H=g.Ho, W=g.Wo, C=g.Cout, Ho=g.H, Wo=g.W, KH=g.KH,
             KW=g.KW, stride=1, pad_h=g.KH - 1 - g.pad_y, pad_w=g.KW - 1 - g.pad_x, dil=g.stride, Cg=cg_out)
-    _gemm(A, B, DIRECT_K, GATHER_K, 8, 8, dx, cg_in, g.C, epi=EPI_BF16, groups=g.groups)
+    _gemm(A, B, DIRECT_K, GATHER_K, 8, 8, dx, cg_in, g.C, epi=EPI_BF16, groups=g.groups, mask_relu=mask_relu)
 
 
 def conv_backward_weight(x, dy, dw, g: ConvGeom):
@@ -195,16 +199,19 @@ def fc_forward(x, w, bias, y, relu=False, out_fp32=False):
           epi=EPI_F32 if out_fp32 else EPI_BF16)
 
 
-def fc_backward_data(dy, w, dx):
-    """dx[B][nin] = dy[B][nout] . w[nout][nin]."""
+def fc_backward_data(dy, w, dx, mask_relu=False):
+    """dx[B][nin] = dy[B][nout] . w[nout][nin]  (mask_relu: see conv_backward_data)."""
     if not dy.is_cuda:
-        dx.copy_(dy @ w)
+        out = dy @ w
+        if mask_relu:
+            out = out * (dx > 0).to(out.dtype)
+        dx.copy_(out)
         return
     Bn, nout = dy.shape
     nin = w.shape[1]
     A = _op(w.data_ptr(), 0, nin, nin, nout)
     Bo = _op(dy.data_ptr(), 0, nout, Bn, nout)
-    _gemm(A, Bo, DIRECT_MN, DIRECT_K, 8, 8, dx, 0, nin, epi=EPI_BF16)
+    _gemm(A, Bo, DIRECT_MN, DIRECT_K, 8, 8, dx, 0, nin, epi=EPI_BF16, mask_relu=mask_relu)
 
 
 def fc_backward_weight(x, dy, dw):

@@ -64,7 +64,8 @@ def pool_out_size(H, k, s, p=0):
 
 
 def _pool_ref(x, KH, KW, S, P, mode, relu, Ho, Wo):
-    # x NHWC fp32 -> NHWC, reference semantics (ceil windows, avg = sum/(k*k))
+    """x NHWC fp32 -> (out NHWC, arg) with reference window semantics (ceil windows,
+    avg = sum/(k*k)); arg = first-max window offset kh*KW+kw (max mode)."""
     xn = x.permute(0, 3, 1, 2)
     if relu:
         xn = xn.clamp_min(0)
@@ -73,58 +74,70 @@ def _pool_ref(x, KH, KW, S, P, mode, relu, Ho, Wo):
     need_h = (Ho - 1) * S + KH - H - P
     need_w = (Wo - 1) * S + KW - W - P
     xp = F.pad(xn, (P, max(need_w, 0), P, max(need_h, 0)), value=padv)
+    arg = None
     if mode == 0:
-        out = F.max_pool2d(xp, (KH, KW), S)
+        out, ind = F.max_pool2d(xp, (KH, KW), S, return_indices=True)
+        out, ind = out[:, :, :Ho, :Wo], ind[:, :, :Ho, :Wo]
+        Wp = xp.shape[3]
+        ih, iw = ind // Wp, ind % Wp
+        ho = torch.arange(Ho).view(1, 1, Ho, 1) * S
+        wo = torch.arange(Wo).view(1, 1, 1, Wo) * S
+        arg = ((ih - ho) * KW + (iw - wo)).to(torch.uint8).permute(0, 2, 3, 1)
     else:
         out = F.avg_pool2d(xp, (KH, KW), S) * (KH * KW)
         if mode == 2:
             out = out / (KH * KW)
-    return out[:, :, :Ho, :Wo].permute(0, 2, 3, 1)
+        out = out[:, :, :Ho, :Wo]
+    return out.permute(0, 2, 3, 1), arg
 
 
 def pool_forward(x, y, state, KH, KW, S, P, mode: str, relu=False):
+    """y = pool(x).  state: uint8 [N][Ho][Wo][C] first-max window offsets (max mode, may be None)."""
     N, H, W, C = x.shape
     Ho, Wo = y.shape[1], y.shape[2]
     m = POOL_MODE[mode]
+    if m == 0 and KH * KW > 255:
+        raise ValueError("max pooling window larger than 255 elements is not supported")
     if not x.is_cuda:
-        out = _pool_ref(x, KH, KW, S, P, m, relu, Ho, Wo)
+        out, arg = _pool_ref(x, KH, KW, S, P, m, relu, Ho, Wo)
         y.copy_(out)
-        if state is not None:
-            state.copy_(out)
+        if state is not None and arg is not None:
+            state.copy_(arg)
         return
-    native.check(_k().cxn_pool_fwd(x.data_ptr(), y.data_ptr(), state.data_ptr() if state is not None else None,
+    native.check(_k().cxn_pool_fwd(x.data_ptr(), y.data_ptr(),
+                                   state.data_ptr() if (state is not None and m == 0) else None,
                                    N, H, W, C, Ho, Wo, KH, KW, S, P, m, int(relu), _stream()), "pool_fwd")
 
 
-def pool_backward(x, ypool, dy, dx, KH, KW, S, P, mode: str, relu=False):
-    """dx = unpool(x, ypool, dy); dx may alias x (element-local read-before-write)."""
+def pool_backward(x, state, dy, dx, KH, KW, S, P, mode: str, relu=False):
+    """dx = unpool(dy) (max: to the recorded first maximum); relu: times relu'(x).
+    dx may alias x (element-local read-before-write)."""
     N, H, W, C = x.shape
     Ho, Wo = dy.shape[1], dy.shape[2]
     m = POOL_MODE[mode]
     if not x.is_cuda:
-        xr = x.clamp_min(0) if relu else x
-        g = torch.zeros_like(x)
+        g = torch.zeros_like(dy.new_empty(N, H + 2 * P + KH + S, W + 2 * P + KW + S, C))
         for ho in range(Ho):
-            hs = ho * S - P
+            hs = ho * S
             for wo in range(Wo):
-                ws = wo * S - P
-                h0, h1 = max(hs, 0), min(hs + KH, H)
-                w0, w1 = max(ws, 0), min(ws + KW, W)
-                win = xr[:, h0:h1, w0:w1, :]
-                gv = dy[:, ho:ho + 1, wo:wo + 1, :]
+                ws = wo * S
+                gv = dy[:, ho, wo, :]
                 if m == 0:
-                    yv = ypool[:, ho:ho + 1, wo:wo + 1, :]
-                    g[:, h0:h1, w0:w1, :] += (win == yv).to(g.dtype) * gv
-                elif m == 1:
-                    g[:, h0:h1, w0:w1, :] += gv
+                    a = state[:, ho, wo, :].long()
+                    for kh in range(KH):
+                        for kw in range(KW):
+                            g[:, hs + kh, ws + kw, :] += (a == kh * KW + kw).to(g.dtype) * gv
                 else:
-                    g[:, h0:h1, w0:w1, :] += gv / (KH * KW)
+                    sc = 1.0 / (KH * KW) if m == 2 else 1.0
+                    g[:, hs:hs + KH, ws:ws + KW, :] += gv[:, None, None, :] * sc
+        g = g[:, P:P + H, P:P + W, :]
         if relu:
             g = g * (x > 0).to(g.dtype)
         dx.copy_(g)
         return
-    native.check(_k().cxn_pool_bwd(x.data_ptr(), ypool.data_ptr(), dy.data_ptr(), dx.data_ptr(), N, H, W, C, Ho, Wo,
-                                   KH, KW, S, P, m, int(relu), _stream()), "pool_bwd")
+    native.check(_k().cxn_pool_bwd(x.data_ptr(), state.data_ptr() if m == 0 else None, dy.data_ptr(),
+                                   dx.data_ptr(), N, H, W, C, Ho, Wo, KH, KW, S, P, m, int(relu), _stream()),
+                 "pool_bwd")
 
 
 # ----------------------------------------------------------------------------- LRN

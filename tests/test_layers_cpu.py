@@ -1,0 +1,271 @@
+"""Executor + layer semantics on the CPU path against independent torch autograd models.
+
+The torch models restate the reference semantics (ceil-mode pooling, cross-channel
+LRN with knorm, in-place activations, loss gradient scaled by 1/batch) directly with
+autograd, so a wiring or formula error in any layer shows up as a gradient mismatch.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from cxxnet_amd import native
+from cxxnet_amd.io.data import DataBatch
+from cxxnet_amd.nnet import NetTrainer
+
+
+def make(conf, batch, extra=()):
+    tr = NetTrainer()
+    for k, v in list(native.rt().parse_config(conf)) + [("batch_size", str(batch)), ("dev", "cpu"),
+                                                        ("eval_train", "0"), ("silent", "1")] + list(extra):
+        tr.set_param(k, v)
+    tr.init_model()
+    return tr
+
+
+def grads_of(tr, x, y):
+    tr.net.set_input(x)
+    tr.net.set_labels(y)
+    tr.net.forward(True)
+    tr.net.backprop(False)
+    return {(li, s.tag): s.g.clone() for li, s in tr.net.arena.specs}
+
+
+def weights(tr, li, tag):
+    for l, s in tr.net.arena.specs:
+        if l == li and s.tag == tag:
+            return s.w.clone()
+    raise KeyError((li, tag))
+
+
+def lrn_ref(x, n, alpha, beta, knorm):
+    sq = (x * x)
+    half = n // 2
+    pad = F.pad(sq, (0, 0, 0, 0, half, half))
+    s = sum(pad[:, i:i + x.shape[1]] for i in range(n))
+    return x * (knorm + alpha / n * s).pow(-beta)
+
+
+CONV_NET = """
+netconfig=start
+layer[0->1] = conv:c1
+  kernel_size = 3
+  stride = 2
+  nchannel = 8
+  pad = 1
+layer[1->2] = relu
+layer[2->3] = max_pooling
+  kernel_size = 3
+  stride = 2
+layer[3->4] = lrn
+  local_size = 5
+  alpha = 0.01
+  beta = 0.75
+  knorm = 2
+layer[4->5] = conv:c2
+  kernel_size = 3
+  nchannel = 6
+  ngroup = 2
+  pad = 1
+layer[5->6] = tanh
+layer[6->7] = avg_pooling
+  kernel_size = 2
+  stride = 2
+layer[7->8] = flatten
+layer[8->9] = fullc:f1
+  nhidden = 12
+layer[9->10] = sigmoid
+layer[10->11] = fullc:f2
+  nhidden = 5
+layer[11->11] = softmax
+netconfig=end
+input_shape = 4,15,15
+random_type = xavier
+init_bias = 0.1
+"""
+
+
+def test_conv_net_gradients_match_autograd():
+    B = 3
+    tr = make(CONV_NET, B)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(B, 4, 15, 15, generator=g)
+    y = torch.randint(0, 5, (B, 1), generator=g).float()
+    ours = grads_of(tr, x, y)
+
+    # independent autograd model with the same weights (logical layouts)
+    def conv_w(li):
+        layer = tr.net.connections[li].layer
+        w = layer.to_logical(weights(tr, li, "wmat"))  # (G, Cout/G, Cg*k*k)
+        lp = layer.lp
+        return w.reshape(lp.num_channel, lp.num_input_channel // lp.num_group, lp.kernel_height,
+                         lp.kernel_width).requires_grad_(True)
+    w1, w2 = conv_w(0), conv_w(4)
+    b1 = weights(tr, 0, "bias").requires_grad_(True)
+    b2 = weights(tr, 4, "bias").requires_grad_(True)
+    wf1 = weights(tr, 8, "wmat").requires_grad_(True)
+    bf1 = weights(tr, 8, "bias").requires_grad_(True)
+    wf2 = weights(tr, 10, "wmat").requires_grad_(True)
+    bf2 = weights(tr, 10, "bias").requires_grad_(True)
+    h = F.relu(F.conv2d(x, w1, b1, stride=2, padding=1))
+    h = F.max_pool2d(h, 3, 2, ceil_mode=True)
+    h = lrn_ref(h, 5, 0.01, 0.75, 2.0)
+    h = torch.tanh(F.conv2d(h, w2, b2, padding=1, groups=2))
+    h = F.avg_pool2d(h, 2, 2, ceil_mode=True)
+    h = h.reshape(B, -1)
+    h = torch.sigmoid(h @ wf1.t() + bf1)
+    logits = h @ wf2.t() + bf2
+    loss = F.cross_entropy(logits, y.long().view(-1), reduction="sum") / B
+    loss.backward()
+
+    def cmp(key, ref):
+        got = ours[key]
+        assert torch.allclose(got.reshape(ref.shape), ref, rtol=1e-3, atol=1e-5), \
+            (key, (got.reshape(ref.shape) - ref).abs().max().item())
+
+    layer0 = tr.net.connections[0].layer
+    layer4 = tr.net.connections[4].layer
+    cmp((0, "wmat"), layer0.from_logical(w1.grad.reshape(1, 8, -1)))
+    cmp((0, "bias"), b1.grad)
+    cmp((4, "wmat"), layer4.from_logical(w2.grad.reshape(2, 3, -1)))
+    cmp((4, "bias"), b2.grad)
+    cmp((8, "wmat"), wf1.grad)
+    cmp((8, "bias"), bf1.grad)
+    cmp((10, "wmat"), wf2.grad)
+    cmp((10, "bias"), bf2.grad)
+
+
+def test_prop_to_input_and_dropout_identity_at_test():
+    conf = """
+netconfig=start
+layer[+1] = fullc:f1
+  nhidden = 7
+layer[+0] = dropout
+  threshold = 0.5
+layer[+1] = fullc:f2
+  nhidden = 3
+layer[+0] = softmax
+netconfig=end
+input_shape = 1,1,5
+"""
+    tr = make(conf, 4)
+    x = torch.randn(4, 1, 1, 5)
+    y = torch.zeros(4, 1)
+    tr.net.set_input(x)
+    tr.net.set_labels(y)
+    tr.net.forward(False)
+    p1 = tr.net.nodes[-1].fp32_view.clone()
+    tr.net.forward(False)
+    assert torch.equal(p1, tr.net.nodes[-1].fp32_view)  # dropout is identity at test time
+    assert torch.allclose(p1.sum(1), torch.ones(4))
+
+
+def test_relu_max_pooling_and_sum_pooling():
+    conf = """
+netconfig=start
+layer[0->1] = relu_max_pooling
+  kernel_size = 3
+  stride = 2
+layer[1->2] = sum_pooling
+  kernel_size = 2
+  stride = 1
+layer[2->3] = flatten
+layer[3->4] = fullc:f
+  nhidden = 4
+layer[4->4] = softmax
+netconfig=end
+input_shape = 2,9,9
+"""
+    B = 2
+    tr = make(conf, B)
+    x = torch.randn(B, 2, 9, 9)
+    y = torch.tensor([[1.0], [3.0]])
+    ours = grads_of(tr, x, y)
+    wf = weights(tr, 3, "wmat").requires_grad_(True)
+    bf = weights(tr, 3, "bias").requires_grad_(True)
+    h = F.max_pool2d(F.relu(x), 3, 2, ceil_mode=True)
+    h = F.avg_pool2d(h, 2, 1, ceil_mode=True) * 4
+    logits = h.reshape(B, -1) @ wf.t() + bf
+    loss = F.cross_entropy(logits, y.long().view(-1), reduction="sum") / B
+    loss.backward()
+    assert torch.allclose(ours[(3, "wmat")], wf.grad, rtol=1e-4, atol=1e-6)
+    assert torch.allclose(ours[(3, "bias")], bf.grad, rtol=1e-4, atol=1e-6)
+
+
+def test_batch_norm_and_prelu_gradients():
+    conf = """
+netconfig=start
+layer[0->1] = conv:c
+  kernel_size = 3
+  nchannel = 4
+layer[1->2] = batch_norm:bn
+layer[2->3] = prelu:pr
+layer[3->4] = flatten
+layer[4->5] = fullc:f
+  nhidden = 3
+layer[5->5] = softmax
+netconfig=end
+input_shape = 2,6,6
+"""
+    B = 4
+    tr = make(conf, B)
+    x = torch.randn(B, 2, 6, 6)
+    y = torch.randint(0, 3, (B, 1)).float()
+    ours = grads_of(tr, x, y)
+    layer0 = tr.net.connections[0].layer
+    w = layer0.to_logical(weights(tr, 0, "wmat")).reshape(4, 2, 3, 3).requires_grad_(True)
+    b = weights(tr, 0, "bias").requires_grad_(True)
+    slope = weights(tr, 1, "wmat").requires_grad_(True)
+    bias = weights(tr, 1, "bias").requires_grad_(True)
+    pr = weights(tr, 2, "bias").requires_grad_(True)
+    wf = weights(tr, 4, "wmat").requires_grad_(True)
+    bf = weights(tr, 4, "bias").requires_grad_(True)
+    h = F.conv2d(x, w, b)
+    mean = h.mean((0, 2, 3), keepdim=True)
+    var = ((h - mean) ** 2).mean((0, 2, 3), keepdim=True)
+    h = (h - mean) / torch.sqrt(var + 1e-10) * slope.view(1, -1, 1, 1) + bias.view(1, -1, 1, 1)
+    h = torch.where(h > 0, h, h * pr.clamp(0, 1).view(1, -1, 1, 1))
+    # the net flattens in NCHW order
+    logits = h.reshape(B, -1) @ wf.t() + bf
+    loss = F.cross_entropy(logits, y.long().view(-1), reduction="sum") / B
+    loss.backward()
+    assert torch.allclose(ours[(1, "wmat")], slope.grad, rtol=1e-3, atol=1e-5)
+    assert torch.allclose(ours[(1, "bias")], bias.grad, rtol=1e-3, atol=1e-5)
+    assert torch.allclose(ours[(2, "bias")], pr.grad, rtol=1e-3, atol=1e-5)
+    assert torch.allclose(ours[(0, "wmat")].reshape(-1).abs().sum(),
+                          layer0.from_logical(w.grad.reshape(1, 4, -1)).abs().sum(), rtol=1e-3)
+
+
+def test_concat_split_bias_graph():
+    conf = """
+netconfig=start
+layer[0->1,2] = split
+layer[1->3] = fullc:a
+  nhidden = 3
+layer[2->4] = fullc:b
+  nhidden = 5
+layer[3,4->5] = concat
+layer[5->5] = bias:bb
+layer[5->6] = fullc:c
+  nhidden = 2
+layer[6->6] = softmax
+netconfig=end
+input_shape = 1,1,6
+"""
+    B = 3
+    tr = make(conf, B)
+    x = torch.randn(B, 1, 1, 6)
+    y = torch.tensor([[0.0], [1.0], [1.0]])
+    ours = grads_of(tr, x.clone(), y)
+    wa, ba = weights(tr, 1, "wmat").requires_grad_(True), weights(tr, 1, "bias").requires_grad_(True)
+    wb, bb = weights(tr, 2, "wmat").requires_grad_(True), weights(tr, 2, "bias").requires_grad_(True)
+    bias = weights(tr, 4, "bias").requires_grad_(True)
+    wc, bc = weights(tr, 5, "wmat").requires_grad_(True), weights(tr, 5, "bias").requires_grad_(True)
+    xi = x.view(B, 6)
+    h = torch.cat([xi @ wa.t() + ba, xi @ wb.t() + bb], 1) + bias
+    logits = h @ wc.t() + bc
+    loss = F.cross_entropy(logits, y.long().view(-1), reduction="sum") / B
+    loss.backward()
+    for key, ref in [((1, "wmat"), wa.grad), ((2, "wmat"), wb.grad), ((4, "bias"), bias.grad),
+                     ((5, "wmat"), wc.grad)]:
+        assert torch.allclose(ours[key], ref, rtol=1e-4, atol=1e-6), key
