@@ -161,6 +161,42 @@ class NetTrainer:
         self.net.load_model(BinReader(blob))
         self._post_init()
 
+    def copy_model_from_bytes(self, data: bytes, pos: int = 0):
+        """Finetune from a model file: parse the old structure and per-layer blobs
+        (no device net is built for it) and copy every layer whose name matches."""
+        from ..layers import LayerContext, create_layer
+        old = native.rt().NetConfig()
+        pos += old.load_net(data[pos:])
+        _, blen = struct.unpack_from("<qQ", data, pos)
+        fi = BinReader(data[pos + 16:pos + 16 + blen])
+        ctx = LayerContext("cpu")
+        loaded = {}
+        for i, info in enumerate(old.layers):
+            if info.type == 0:
+                continue
+            layer = create_layer(info.type, ctx)
+            layer.load_model(fi)
+            if info.name:
+                loaded[info.name] = layer
+        for name, li in self.net_cfg.layer_name_map.items():
+            src = loaded.get(name)
+            if src is None or not hasattr(src, "loaded"):
+                continue
+            dst = self.net.connections[li].layer
+            vals = list(src.loaded)
+            if hasattr(dst, "from_logical") and len(vals) and vals[0].dim() == 3:
+                vals[0] = dst.from_logical(vals[0])
+            if len(dst.params) < 1:
+                continue
+            for spec, v in zip(dst.params, vals):
+                if v.numel() != spec.numel:
+                    raise ValueError(f"CopyModelFrom: layer {name} shape mismatch")
+                spec.w.copy_(v.reshape(spec.shape))
+            print(f"Copying layer {name}")
+        self.net.arena.sync_shadow()
+        if self.reducer is not None:
+            self.reducer.broadcast_params()
+
     def copy_model_from(self, other: "NetTrainer"):
         """Finetune: copy every layer whose name matches (reference nnet_impl-inl.hpp:101-134)."""
         src_map = dict(other.net_cfg.layer_name_map)

@@ -269,3 +269,54 @@ input_shape = 1,1,6
     for key, ref in [((1, "wmat"), wa.grad), ((2, "wmat"), wb.grad), ((4, "bias"), bias.grad),
                      ((5, "wmat"), wc.grad)]:
         assert torch.allclose(ours[key], ref, rtol=1e-4, atol=1e-6), key
+
+
+def test_multi_step_sgd_matches_autograd_sgd():
+    """5 full training steps (SGD momentum, tag-scoped lr/wd) against torch autograd +
+    a hand-written reference update (src/updater/sgd_updater-inl.hpp:73-84)."""
+    conf = CONV_NET + """
+momentum = 0.9
+wmat:lr = 0.05
+wmat:wd = 0.001
+bias:lr = 0.1
+bias:wd = 0.0
+"""
+    B = 4
+    tr = make(conf, B)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(B, 4, 15, 15, generator=g)
+    y = torch.randint(0, 5, (B, 1), generator=g).float()
+
+    l0, l4 = tr.net.connections[0].layer, tr.net.connections[4].layer
+    params = {
+        "w1": l0.to_logical(weights(tr, 0, "wmat")).reshape(8, 4, 3, 3),
+        "b1": weights(tr, 0, "bias"),
+        "w2": l4.to_logical(weights(tr, 4, "wmat")).reshape(6, 4, 3, 3),
+        "b2": weights(tr, 4, "bias"),
+        "wf1": weights(tr, 8, "wmat"), "bf1": weights(tr, 8, "bias"),
+        "wf2": weights(tr, 10, "wmat"), "bf2": weights(tr, 10, "bias"),
+    }
+    mom = {k: torch.zeros_like(v) for k, v in params.items()}
+
+    def loss_fn(p):
+        h = F.relu(F.conv2d(x, p["w1"], p["b1"], stride=2, padding=1))
+        h = F.max_pool2d(h, 3, 2, ceil_mode=True)
+        h = lrn_ref(h, 5, 0.01, 0.75, 2.0)
+        h = torch.tanh(F.conv2d(h, p["w2"], p["b2"], padding=1, groups=2))
+        h = F.avg_pool2d(h, 2, 2, ceil_mode=True).reshape(B, -1)
+        h = torch.sigmoid(h @ p["wf1"].t() + p["bf1"])
+        logits = h @ p["wf2"].t() + p["bf2"]
+        return F.cross_entropy(logits, y.long().view(-1), reduction="sum") / B
+
+    for step in range(5):
+        tr.update(DataBatch(x, y))
+        ps = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+        loss_fn(ps).backward()
+        for k in params:
+            lr, wd = (0.05, 0.001) if k.startswith("w") else (0.1, 0.0)
+            mom[k] = 0.9 * mom[k] - lr * (ps[k].grad + wd * params[k])
+            params[k] = params[k] + mom[k]
+    got = l0.to_logical(weights(tr, 0, "wmat")).reshape(8, 4, 3, 3)
+    assert torch.allclose(got, params["w1"], rtol=1e-3, atol=1e-5)
+    assert torch.allclose(weights(tr, 10, "wmat"), params["wf2"], rtol=1e-3, atol=1e-5)
+    assert torch.allclose(weights(tr, 8, "bias"), params["bf1"], rtol=1e-3, atol=1e-5)

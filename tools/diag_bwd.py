@@ -4,7 +4,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 from cxxnet_amd.models import load_conf
 from cxxnet_amd.nnet import NetTrainer
-batch = 4
+batch = 8
 pairs = [(k, v) for k, v in load_conf("alexnet") if not k.startswith("metric") and k != "dev"]
 pairs += [("batch_size", str(batch)), ("eval_train", "0"), ("silent", "1")]
 pairs = [(k, ("0" if k == "threshold" else v)) for k, v in pairs]
@@ -27,9 +27,9 @@ for tr, xx, yy in ((cpu, x, y), (gpu, x.cuda(), y.cuda())):
     tr.net.set_input(xx); tr.net.set_labels(yy); tr.net.forward(True)
 def rel(a, b):
     a = a.float().cpu().reshape(-1); b = b.float().cpu().reshape(-1)
-    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
 print("label gpu", gpu.net.ctx.label_fields["label"].view(-1).tolist(), "cpu", cpu.net.ctx.label_fields["label"].view(-1).tolist())
-for i in range(len(cpu.net.connections) - 1, 8, -1):
+for i in range(len(cpu.net.connections) - 1, 0, -1):
     cc, gc = cpu.net.connections[i], gpu.net.connections[i]
     cc.layer.backprop(True, cc.nodes_in, cc.nodes_out)
     gc.layer.backprop(True, gc.nodes_in, gc.nodes_out)
