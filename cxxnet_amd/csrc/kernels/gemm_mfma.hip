@@ -218,10 +218,12 @@ constexpr int tile_elems() {
   return KMajorLayout<MODE>::kmajor ? R * (BK + PADK) : BK * (R + PADM);
 }
 
-template <int BM, int BN, int AMODE, int BMODE, int VA, int VB, int EPI>
+template <int BM, int BN, int WAVES_M, int AMODE, int BMODE, int VA, int VB, int EPI>
 __global__ void __launch_bounds__(NT, 2)
 gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int ksplit_tiles, int ktiles_total) {
-  constexpr int WM = BM / 2, WN = BN / 2;  // per-wave tile (2x2 waves)
+  constexpr int WAVES_N = 4 / WAVES_M;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;  // per-wave tile
+  static_assert(WM % 16 == 0 && WN % 16 == 0, "wave tile must be a multiple of 16");
   constexpr int MR = WM / 16, NR = WN / 16;
   constexpr int A_ELEMS = tile_elems<AMODE, BM>();
   constexpr int B_ELEMS = tile_elems<BMODE, BN>();
@@ -272,7 +274,7 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
   if constexpr (BMODE == GATHER_K) init_rows(B, j0, rowB, NVB, VB);
 
   const int wave = threadIdx.x >> 6;
-  const int wi = wave & 1, wj = wave >> 1;
+  const int wi = wave % WAVES_M, wj = wave / WAVES_M;
   f32x4 acc[MR][NR];
 #pragma unroll
   for (int m = 0; m < MR; ++m)
@@ -336,9 +338,10 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
   const float *bias = E.bias ? E.bias + g * E.bias_gstride : nullptr;
   if constexpr (EPI == EPI_BF16) {
     constexpr int LPR = WM / 8;        // lanes per row, 8 elements per lane
-    constexpr int RPI = 64 / LPR;      // rows per instruction
+    constexpr int RPI = 64 / LPR;      // rows per instruction (lanes >= LPR*RPI idle)
     bf16_t *out = reinterpret_cast<bf16_t *>(E.out) + g * E.gstride;
     const int il = (lane % LPR) * 8;
+    const bool lane_on = lane < LPR * RPI;
     const int i = ibase + il;
     float bv[8];
 #pragma unroll
@@ -347,7 +350,7 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
 #pragma unroll 4
     for (int jl = lane / LPR; jl < WN; jl += RPI) {
       const int j = jbase + jl;
-      if (j >= Nj || i >= Mi) continue;
+      if (j >= Nj || i >= Mi || !lane_on) continue;
       const f32x4 x0 = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il);
       const f32x4 x1 = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il + 4);
       float f[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
@@ -380,10 +383,11 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
     constexpr int RPI = 64 / LPR;
     const int il = lane % LPR;
     const int i = ibase + il;
+    const bool lane_on = lane < LPR * RPI;
     const float bv = (bias && i < Mi) ? bias[i] : 0.f;
     for (int jl = lane / LPR; jl < WN; jl += RPI) {
       const int j = jbase + jl;
-      if (j >= Nj || i >= Mi) continue;
+      if (j >= Nj || i >= Mi || !lane_on) continue;
       float v = ep[jl * (WM + 4) + il] * E.alpha + bv;
       float *dst = out + static_cast<long>(j) * E.ldc + i;
       if constexpr (EPI == EPI_F32) {
@@ -400,12 +404,12 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
 // ------------------------------------------------------------------ host side
 struct GemmArgs {
   int amode, bmode, va, vb, epi;
-  int tile;  // 128 or 64
+  int tile;    // tile id, see TILES below
   int groups;
   int ksplit;  // number of K splits (>=1)
 };
 
-template <int BM, int BN, int AM, int BMo, int VA, int VB, int EPI>
+template <int BM, int BN, int WMs, int AM, int BMo, int VA, int VB, int EPI>
 void launch_t(const Operand &A, const Operand &B, const Epilogue &E, int groups, int ksplit, hipStream_t s) {
   const int ti = cdiv(A.rows, BM), tj = cdiv(B.rows, BN);
   const int kdim = A.kdim;
@@ -414,33 +418,57 @@ void launch_t(const Operand &A, const Operand &B, const Epilogue &E, int groups,
   const int per = cdiv(ktiles, ksplit);
   ksplit = cdiv(ktiles, per);
   dim3 grid(ti * tj, ksplit, groups);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, AM, BMo, VA, VB, EPI>), grid, dim3(NT), 0, s, A, B, E, ti, tj, per, ktiles);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, WMs, AM, BMo, VA, VB, EPI>), grid, dim3(NT), 0, s, A, B, E, ti, tj, per,
+                     ktiles);
 }
 
-// Dispatch table over the (modes, vec, epilogue, tile) combinations actually used.
-template <int BM, int BN>
-int dispatch_tile(const GemmArgs &g, const Operand &A, const Operand &B, const Epilogue &E, hipStream_t s) {
-#define CXN_CASE(AM, BMo, VA, VB, EPI)                                                              \
-  if (g.amode == AM && g.bmode == BMo && g.va == VA && g.vb == VB && g.epi == EPI) {                \
-    launch_t<BM, BN, AM, BMo, VA, VB, EPI>(A, B, E, g.groups, g.ksplit, s);                         \
+// Tile ids (BM x BN, waves along M x N):
+//   0: 128x128 (2x2)   1: 64x64 (2x2)   2: 64x128 (1x4)   3: 32x128 (1x4)
+//   4: 96x128 (1x4)    5: 128x64 (2x2)
+#define CXN_T0(AM, BMo, VA, VB, EPI) launch_t<128, 128, 2, AM, BMo, VA, VB, EPI>
+#define CXN_T1(AM, BMo, VA, VB, EPI) launch_t<64, 64, 2, AM, BMo, VA, VB, EPI>
+#define CXN_T2(AM, BMo, VA, VB, EPI) launch_t<64, 128, 1, AM, BMo, VA, VB, EPI>
+#define CXN_T3(AM, BMo, VA, VB, EPI) launch_t<32, 128, 1, AM, BMo, VA, VB, EPI>
+#define CXN_T4(AM, BMo, VA, VB, EPI) launch_t<96, 128, 1, AM, BMo, VA, VB, EPI>
+#define CXN_T5(AM, BMo, VA, VB, EPI) launch_t<128, 64, 2, AM, BMo, VA, VB, EPI>
+
+#define CXN_CASE(AM, BMo, VA, VB, EPI, TID)                                                         \
+  if (g.amode == AM && g.bmode == BMo && g.va == VA && g.vb == VB && g.epi == EPI && g.tile == TID) { \
+    CXN_T##TID(AM, BMo, VA, VB, EPI)(A, B, E, g.groups, g.ksplit, s);                               \
     return 0;                                                                                       \
   }
-  // fully-connected
-  CXN_CASE(DIRECT_K, DIRECT_K, 8, 8, EPI_BF16)          // fc fwd
-  CXN_CASE(DIRECT_K, DIRECT_K, 8, 8, EPI_F32)           // fc fwd fp32 out (loss layers)
-  CXN_CASE(DIRECT_K, DIRECT_K, 8, 8, EPI_F32_ATOMIC)    // split-K
-  CXN_CASE(DIRECT_MN, DIRECT_K, 8, 8, EPI_BF16)         // fc dgrad
-  CXN_CASE(DIRECT_MN, DIRECT_K, 8, 8, EPI_F32_ATOMIC)   // fc dgrad split-K
-  CXN_CASE(DIRECT_MN, DIRECT_MN, 8, 8, EPI_F32_ACC)     // fc wgrad
-  CXN_CASE(DIRECT_MN, DIRECT_MN, 8, 8, EPI_F32_ATOMIC)  // fc wgrad split-K
-  // convolution
-  CXN_CASE(DIRECT_K, GATHER_K, 8, 8, EPI_BF16)          // conv fwd / dgrad, Cg % 8 == 0
-  CXN_CASE(DIRECT_K, GATHER_K, 4, 4, EPI_BF16)          // conv fwd, Cg % 4 == 0 (first layer)
-  CXN_CASE(GATHER_MN, DIRECT_MN, 8, 8, EPI_F32_ATOMIC)  // conv wgrad
-  CXN_CASE(GATHER_MN, DIRECT_MN, 4, 8, EPI_F32_ATOMIC)  // conv wgrad, Cg % 4 == 0
-#undef CXN_CASE
+#define CXN_CASES_FC(AM, BMo, EPI) \
+  CXN_CASE(AM, BMo, 8, 8, EPI, 0) CXN_CASE(AM, BMo, 8, 8, EPI, 1) CXN_CASE(AM, BMo, 8, 8, EPI, 5)
+
+int dispatch(const GemmArgs &g, const Operand &A, const Operand &B, const Epilogue &E, hipStream_t s) {
+  // fully-connected: fwd (K,K), dgrad (MN,K), wgrad (MN,MN)
+  CXN_CASES_FC(DIRECT_K, DIRECT_K, EPI_BF16)
+  CXN_CASES_FC(DIRECT_K, DIRECT_K, EPI_F32)
+  CXN_CASES_FC(DIRECT_K, DIRECT_K, EPI_F32_ATOMIC)
+  CXN_CASES_FC(DIRECT_MN, DIRECT_K, EPI_BF16)
+  CXN_CASES_FC(DIRECT_MN, DIRECT_K, EPI_F32_ATOMIC)
+  CXN_CASES_FC(DIRECT_MN, DIRECT_MN, EPI_F32_ACC)
+  CXN_CASES_FC(DIRECT_MN, DIRECT_MN, EPI_F32)
+  CXN_CASES_FC(DIRECT_MN, DIRECT_MN, EPI_F32_ATOMIC)
+  // convolution forward / data-grad (implicit im2col gather on B)
+  CXN_CASE(DIRECT_K, GATHER_K, 8, 8, EPI_BF16, 0)
+  CXN_CASE(DIRECT_K, GATHER_K, 8, 8, EPI_BF16, 1)
+  CXN_CASE(DIRECT_K, GATHER_K, 8, 8, EPI_BF16, 2)
+  CXN_CASE(DIRECT_K, GATHER_K, 8, 8, EPI_BF16, 3)
+  CXN_CASE(DIRECT_K, GATHER_K, 8, 8, EPI_BF16, 4)
+  CXN_CASE(DIRECT_K, GATHER_K, 4, 4, EPI_BF16, 0)
+  CXN_CASE(DIRECT_K, GATHER_K, 4, 4, EPI_BF16, 2)
+  CXN_CASE(DIRECT_K, GATHER_K, 4, 4, EPI_BF16, 3)
+  CXN_CASE(DIRECT_K, GATHER_K, 4, 4, EPI_BF16, 4)
+  // convolution weight-grad (transposed gather on A), split-K fp32 atomics
+  CXN_CASE(GATHER_MN, DIRECT_MN, 8, 8, EPI_F32_ATOMIC, 0)
+  CXN_CASE(GATHER_MN, DIRECT_MN, 8, 8, EPI_F32_ATOMIC, 5)
+  CXN_CASE(GATHER_MN, DIRECT_MN, 4, 8, EPI_F32_ATOMIC, 0)
+  CXN_CASE(GATHER_MN, DIRECT_MN, 4, 8, EPI_F32_ATOMIC, 5)
   return -1;
 }
+#undef CXN_CASE
+#undef CXN_CASES_FC
 
 }  // namespace
 
@@ -483,7 +511,7 @@ CXN_API int cxn_gemm(const CxnOperand *a, const CxnOperand *b, int amode, int bm
   if (A.rows <= 0 || B.rows <= 0 || A.kdim <= 0) return 0;
   Epilogue E{out, out_gstride, ldc, alpha, bias, bias_gstride, relu, mask_relu};
   hipStream_t s = static_cast<hipStream_t>(stream);
-  int rc = (tile == 64) ? dispatch_tile<64, 64>(g, A, B, E, s) : dispatch_tile<128, 128>(g, A, B, E, s);
+  int rc = dispatch(g, A, B, E, s);
   if (rc != 0) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

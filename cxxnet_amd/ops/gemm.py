@@ -77,9 +77,32 @@ def _op(ptr=0, gstride=0, ld=0, rows=0, kdim=0, **geo):
     return o
 
 
+# tile id -> (BM, BN); must match TILES in gemm_mfma.hip
+TILES = {0: (128, 128), 1: (64, 64), 2: (64, 128), 3: (32, 128), 4: (96, 128), 5: (128, 64)}
+CONV_FWD_TILES = (0, 4, 2, 3, 1)
+CONV_FWD_TILES_V4 = (0, 4, 2, 3)
+WGRAD_TILES = (0, 5)
+FC_TILES = (0, 5, 1)
+
+
+def _cdiv(a, b):
+    return -(-a // b)
+
+
+def _pick(candidates, rows_i, rows_j, groups, min_blocks=2 * NUM_CU):
+    """Least padded work first; among equals the larger tile; then enough blocks to
+    fill the chip (256 CUs x 2 blocks)."""
+    def cost(t):
+        bm, bn = TILES[t]
+        nb = _cdiv(rows_i, bm) * _cdiv(rows_j, bn) * groups
+        padded = _cdiv(rows_i, bm) * bm * _cdiv(rows_j, bn) * bn
+        starve = max(0.0, 1.0 - nb / min_blocks)  # fraction of the chip left idle
+        return (padded * (1.0 + starve), -bm * bn)
+    return min(candidates, key=cost)
+
+
 def _pick_tile(rows_i, rows_j, groups):
-    t128 = -(-rows_i // 128) * -(-rows_j // 128) * groups
-    return 128 if t128 >= 2 * NUM_CU else 64
+    return _pick(FC_TILES, rows_i, rows_j, groups)
 
 
 def _gemm(a, b, amode, bmode, va, vb, out, out_gstride, ldc, *, alpha=1.0, bias=None, bias_gstride=0,
@@ -94,8 +117,9 @@ def _gemm(a, b, amode, bmode, va, vb, out, out_gstride, ldc, *, alpha=1.0, bias=
     native.check(rc, "gemm")
 
 
-def _auto_split(rows_i, rows_j, groups, kdim, tile=128, target=2 * NUM_CU, min_ktiles=4):
-    tiles = -(-rows_i // tile) * -(-rows_j // tile) * groups
+def _auto_split(rows_i, rows_j, groups, kdim, tile=0, target=2 * NUM_CU, min_ktiles=4):
+    bm, bn = TILES[tile]
+    tiles = -(-rows_i // bm) * -(-rows_j // bn) * groups
     ktiles = -(-kdim // 64)
     split = max(1, min(target // max(tiles, 1), ktiles // min_ktiles))
     return split
@@ -129,7 +153,8 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
     A = _op(w.data_ptr(), g.cg_out * kd, kd, g.cg_out, kd)
     B = _op(x.data_ptr(), cg, 0, g.N * g.Ho * g.Wo, kd, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW,
             stride=g.stride, pad_h=g.pad_y, pad_w=g.pad_x, dil=1, Cg=cg)
-    _gemm(A, B, DIRECT_K, GATHER_K, va, va, y, g.cg_out, g.Cout, bias=bias, bias_gstride=g.cg_out, relu=relu,
+    tile = _pick(CONV_FWD_TILES if va == 8 else CONV_FWD_TILES_V4, g.cg_out, g.N * g.Ho * g.Wo, g.groups)
+    _gemm(A, B, DIRECT_K, GATHER_K, va, va, y, g.cg_out, g.Cout, bias=bias, bias_gstride=g.cg_out, relu=relu, tile=tile,
           epi=EPI_BF16, groups=g.groups)
 
 
@@ -156,7 +181,9 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False):
     A = _op(wt_buf.data_ptr(), cg_in * kd, kd, cg_in, kd)
     B = _op(dy.data_ptr(), cg_out, 0, g.N * g.H * g.W, kd, H=g.Ho, W=g.Wo, C=g.Cout, Ho=g.H, Wo=g.W, KH=g.KH,
             KW=g.KW, stride=1, pad_h=g.KH - 1 - g.pad_y, pad_w=g.KW - 1 - g.pad_x, dil=g.stride, Cg=cg_out)
-    _gemm(A, B, DIRECT_K, GATHER_K, 8, 8, dx, cg_in, g.C, epi=EPI_BF16, groups=g.groups, mask_relu=mask_relu)
+    tile = _pick(CONV_FWD_TILES, cg_in, g.N * g.H * g.W, g.groups)
+    _gemm(A, B, DIRECT_K, GATHER_K, 8, 8, dx, cg_in, g.C, epi=EPI_BF16, groups=g.groups, mask_relu=mask_relu,
+          tile=tile)
 
 
 def conv_backward_weight(x, dy, dw, g: ConvGeom):
@@ -175,9 +202,10 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
     A = _op(x.data_ptr(), cg, 0, kd, P, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW, stride=g.stride,
             pad_h=g.pad_y, pad_w=g.pad_x, dil=1, Cg=cg)
     B = _op(dy.data_ptr(), g.cg_out, g.Cout, g.cg_out, P)
-    split = _auto_split(kd, g.cg_out, g.groups, P)
+    tile = _pick(WGRAD_TILES, kd, g.cg_out, g.groups, min_blocks=1)
+    split = _auto_split(kd, g.cg_out, g.groups, P, tile)
     _gemm(A, B, GATHER_MN, DIRECT_MN, va, 8, dw, g.cg_out * kd, kd, epi=EPI_F32_ATOMIC, groups=g.groups,
-          ksplit=split, tile=128)
+          ksplit=split, tile=tile)
 
 
 # ----------------------------------------------------------------------------- fully connected
@@ -223,4 +251,4 @@ def fc_backward_weight(x, dy, dw):
     nout = dy.shape[1]
     A = _op(x.data_ptr(), 0, nin, nin, Bn)
     Bo = _op(dy.data_ptr(), 0, nout, nout, Bn)
-    _gemm(A, Bo, DIRECT_MN, DIRECT_MN, 8, 8, dw, 0, nin, epi=EPI_F32_ACC, tile=128)
+    _gemm(A, Bo, DIRECT_MN, DIRECT_MN, 8, 8, dw, 0, nin, epi=EPI_F32_ACC)

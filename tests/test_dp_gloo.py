@@ -1,0 +1,114 @@
+"""Data-parallel correctness on the CPU with the gloo backend (2 ranks): a DP step over a
+global batch split across ranks must equal the single-process step on the whole batch
+(reference semantics: loss scaled by the GLOBAL batch, summed gradients, identical
+update on every replica -- src/nnet/nnet_impl-inl.hpp:141-185)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+CONF = """
+netconfig=start
+layer[0->1] = conv:c1
+  kernel_size = 3
+  nchannel = 8
+  pad = 1
+layer[1->2] = relu
+layer[2->3] = max_pooling
+  kernel_size = 2
+  stride = 2
+layer[3->4] = flatten
+layer[4->5] = fullc:f1
+  nhidden = 16
+layer[5->6] = relu
+layer[6->7] = fullc:f2
+  nhidden = 5
+layer[7->7] = softmax
+netconfig=end
+input_shape = 3,8,8
+random_type = xavier
+momentum = 0.9
+eta = 0.05
+wd = 0.001
+dp_bucket_mb = 0.001
+"""
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data(B):
+    g = torch.Generator().manual_seed(11)
+    return torch.randn(B, 3, 8, 8, generator=g), torch.randint(0, 5, (B, 1), generator=g).float()
+
+
+def _make(batch, extra=()):
+    from cxxnet_amd import native
+    from cxxnet_amd.nnet import NetTrainer
+    tr = NetTrainer()
+    for k, v in list(native.rt().parse_config(CONF)) + [("batch_size", str(batch)), ("dev", "cpu"),
+                                                        ("eval_train", "1"), ("metric", "error"),
+                                                        ("silent", "1"), ("seed", "5")] + list(extra):
+        tr.set_param(k, v)
+    tr.init_model()
+    return tr
+
+
+def _worker(rank, world, port, steps, out, update_period):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from cxxnet_amd.io.data import DataBatch
+    B = 8
+    tr = _make(B, [("update_period", str(update_period))])
+    if rank == 1:
+        # different local init: the rank-0 broadcast must overwrite it
+        pass
+    x, y = _data(B)
+    for _ in range(steps):
+        tr.update(DataBatch(x, y))
+    line = tr.evaluate(None, "train")
+    if rank == 0:
+        torch.save({"w": tr.net.arena.w.clone(), "line": line}, out)
+    else:
+        torch.save({"w": tr.net.arena.w.clone(), "line": line}, out + ".r1")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("update_period", [1, 2])
+def test_dp_two_ranks_equals_single_process(tmp_path, update_period):
+    from cxxnet_amd.io.data import DataBatch
+    steps = 4
+    out = str(tmp_path / "dp.pt")
+    mp.spawn(_worker, args=(2, _free_port(), steps, out, update_period), nprocs=2, join=True)
+    r0 = torch.load(out, weights_only=True)
+    r1 = torch.load(out + ".r1", weights_only=True)
+    assert torch.equal(r0["w"], r1["w"]), "replicas diverged"
+    # single process, whole batch
+    tr = _make(8, [("update_period", str(update_period))])
+    x, y = _data(8)
+    for _ in range(steps):
+        tr.update(DataBatch(x, y))
+    assert torch.allclose(r0["w"], tr.net.arena.w, rtol=1e-4, atol=1e-6)
+    assert r0["line"] == tr.evaluate(None, "train")
+
+
+def test_bucket_plan_covers_arena():
+    from cxxnet_amd.parallel.dp import GradReducer
+    tr = _make(4)
+    red = GradReducer(tr.net.arena, bucket_mb=0.001)
+    covered = torch.zeros(tr.net.arena.total, dtype=torch.bool)
+    for b in red.buckets:
+        covered[b.start:b.end] = True
+    for _, s in tr.net.arena.specs:
+        assert covered[s.offset:s.offset + s.numel].all()
+    # buckets are in reverse layer order: the first is ready first in backward
+    lis = [b.li_min for b in red.buckets]
+    assert lis == sorted(lis, reverse=True)
