@@ -1,0 +1,40 @@
+"""Run a few GEMM-shaped ops in isolation (for rocprofv3 PMC collection).
+  python benchmarks/kernel_probe.py conv1_wgrad conv3_fwd ..."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cxxnet_amd import ops  # noqa: E402
+from cxxnet_amd.ops.gemm import ConvGeom, conv_out_size  # noqa: E402
+
+N = 256
+CASES = {"conv1": (4, 227, 96, 11, 4, 0, 1), "conv2": (96, 27, 256, 5, 1, 2, 2), "conv3": (256, 13, 384, 3, 1, 1, 1),
+         "conv4": (384, 13, 384, 3, 1, 1, 2), "conv5": (384, 13, 256, 3, 1, 1, 2)}
+
+
+def run(name, iters=5):
+    layer, kind = name.split("_")
+    C, H, Cout, K, s, p, g = CASES[layer]
+    Ho, Wo = conv_out_size(H, H, K, K, s, p, p)
+    geo = ConvGeom(N, H, H, C, Ho, Wo, Cout, K, K, s, p, p, g)
+    bf = torch.bfloat16
+    x = torch.randn(N, H, H, C, device="cuda").to(bf)
+    w = (torch.randn(Cout, K, K, C // g, device="cuda") * 0.05).to(bf)
+    y = torch.randn(N, Ho, Wo, Cout, device="cuda").to(bf)
+    dw = torch.zeros(Cout, K, K, C // g, device="cuda")
+    wt = torch.empty_like(w)
+    for _ in range(iters):
+        if kind == "fwd":
+            ops.conv_forward(x, w, None, y, geo)
+        elif kind == "wgrad":
+            ops.conv_backward_weight(x, y, dw, geo)
+        else:
+            ops.conv_backward_data(y, w, x, geo, wt)
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    for n in sys.argv[1:]:
+        run(n)

@@ -40,6 +40,7 @@ struct Operand {
   int rows;      // valid rows
   int kdim;      // valid k
   int vec_ok;    // 1 when 16-B/8-B vector loads are aligned and legal
+  uint32_t nbytes;  // size of the whole buffer (all groups) for the load descriptor
   // gather geometry (GATHER_*): source NHWC tensor [N][H][W][C]
   int H, W, C, Ho, Wo, KH, KW, stride, pad_h, pad_w, dil, Cg;
   FastDiv fd_cg, fd_kw, fd_hw, fd_wo, fd_dil;
@@ -73,6 +74,20 @@ __device__ __forceinline__ uint2 zero_vec(uint2) { return make_uint2(0, 0); }
 template <typename V>
 __device__ __forceinline__ V load_vec(const bf16_t *p) { return *reinterpret_cast<const V *>(p); }
 
+// Buffer loads: 32-bit byte offsets against a wave-uniform resource descriptor; an
+// offset past num_records returns zeros, so padding / ragged edges need no branches.
+constexpr uint32_t OOB = 0xFFFFFF00u;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void *p, uint32_t nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, static_cast<int>(nbytes), 0x00020000);
+}
+__device__ __forceinline__ uint4 bload(rsrc_t r, uint32_t off, uint4) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ uint2 bload(rsrc_t r, uint32_t off, uint2) {
+  return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+
 // Scalar fallback (unaligned / ragged edges): gather VEC elements one by one.
 template <typename V, int VEC>
 __device__ __forceinline__ V load_scalar(const bf16_t *base, long step, int n) {
@@ -85,40 +100,57 @@ __device__ __forceinline__ V load_scalar(const bf16_t *base, long step, int n) {
 // Load one BK-deep tile of operand `op` starting at k0 into registers.
 // Thread->vector assignment: K-major: v = tid + NT*s -> row = v / (BK/VEC), kv = v % (BK/VEC)
 //                            MN-major: v = tid + NT*s -> k = v / (R/VEC), rv = v % (R/VEC)
+// goff: byte offset of this group's slice within the operand's buffer.
 template <int MODE, int R, int VEC>
-__device__ __forceinline__ void load_tile(const Operand &op, const bf16_t *gptr, int row0, int k0,
-                                          Stage<R, VEC> &st, const int *prow) {
+__device__ __forceinline__ void load_tile(const Operand &op, rsrc_t rs, const bf16_t *gptr, uint32_t goff, int row0,
+                                          int k0, Stage<R, VEC> &st, const int *prow) {
   typedef typename Stage<R, VEC>::vec_t V;
   const int tid = threadIdx.x;
   if constexpr (MODE == DIRECT_K) {
     constexpr int VPR = BK / VEC;
+    if (op.vec_ok) {
 #pragma unroll
-    for (int s = 0; s < Stage<R, VEC>::NV; ++s) {
-      const int v = tid + NT * s;
-      const int row = row0 + v / VPR;
-      const int k = k0 + (v % VPR) * VEC;
-      V val = zero_vec(V());
-      if (row < op.rows && k < op.kdim) {
-        const bf16_t *p = gptr + static_cast<long>(row) * op.ld + k;
-        if (op.vec_ok && k + VEC <= op.kdim) val = load_vec<V>(p);
-        else val = load_scalar<V, VEC>(p, 1, op.kdim - k);
+      for (int s = 0; s < Stage<R, VEC>::NV; ++s) {
+        const int v = tid + NT * s;
+        const int row = row0 + v / VPR;
+        const int k = k0 + (v % VPR) * VEC;
+        const bool ok = row < op.rows && k + VEC <= op.kdim;
+        st.v[s] = bload(rs, ok ? goff + static_cast<uint32_t>(row * op.ld + k) * 2u : OOB, V());
       }
-      st.v[s] = val;
+    } else {
+#pragma unroll
+      for (int s = 0; s < Stage<R, VEC>::NV; ++s) {
+        const int v = tid + NT * s;
+        const int row = row0 + v / VPR;
+        const int k = k0 + (v % VPR) * VEC;
+        V val = zero_vec(V());
+        if (row < op.rows && k < op.kdim) val = load_scalar<V, VEC>(gptr + static_cast<long>(row) * op.ld + k, 1,
+                                                                    op.kdim - k);
+        st.v[s] = val;
+      }
     }
   } else if constexpr (MODE == DIRECT_MN) {
     constexpr int VPK = R / VEC;
+    if (op.vec_ok) {
 #pragma unroll
-    for (int s = 0; s < Stage<R, VEC>::NV; ++s) {
-      const int v = tid + NT * s;
-      const int k = k0 + v / VPK;
-      const int row = row0 + (v % VPK) * VEC;
-      V val = zero_vec(V());
-      if (row < op.rows && k < op.kdim) {
-        const bf16_t *p = gptr + static_cast<long>(k) * op.ld + row;
-        if (op.vec_ok && row + VEC <= op.rows) val = load_vec<V>(p);
-        else val = load_scalar<V, VEC>(p, 1, op.rows - row);
+      for (int s = 0; s < Stage<R, VEC>::NV; ++s) {
+        const int v = tid + NT * s;
+        const int k = k0 + v / VPK;
+        const int row = row0 + (v % VPK) * VEC;
+        const bool ok = row + VEC <= op.rows && k < op.kdim;
+        st.v[s] = bload(rs, ok ? goff + static_cast<uint32_t>(k * op.ld + row) * 2u : OOB, V());
       }
-      st.v[s] = val;
+    } else {
+#pragma unroll
+      for (int s = 0; s < Stage<R, VEC>::NV; ++s) {
+        const int v = tid + NT * s;
+        const int k = k0 + v / VPK;
+        const int row = row0 + (v % VPK) * VEC;
+        V val = zero_vec(V());
+        if (row < op.rows && k < op.kdim) val = load_scalar<V, VEC>(gptr + static_cast<long>(k) * op.ld + row, 1,
+                                                                    op.rows - row);
+        st.v[s] = val;
+      }
     }
   } else if constexpr (MODE == GATHER_K) {
     // rows = output pixels (precomputed in prow: base offset, hi0, wi0 per owned row)
@@ -129,22 +161,22 @@ __device__ __forceinline__ void load_tile(const Operand &op, const bf16_t *gptr,
     const uint32_t kh = fdiv(r, op.fd_kw);
     const int kw = static_cast<int>(r - kh * op.KW);
     const bool kin = k < op.kdim;
+    const uint32_t coff = goff + static_cast<uint32_t>(c) * 2u;
 #pragma unroll
     for (int s = 0; s < Stage<R, VEC>::NV; ++s) {
-      V val = zero_vec(V());
-      const long base = prow[3 * s + 0];
+      const int base = prow[3 * s + 0];
       int hi = prow[3 * s + 1] + static_cast<int>(kh);
       int wi = prow[3 * s + 2] + kw;
       bool ok = kin && base >= 0;
-      if (op.dil > 1) {  // dilated input (strided conv data-grad)
+      if (op.dil > 1) {  // dilated input (strided conv data-grad); uniform branch
         ok = ok && hi >= 0 && wi >= 0 && (hi % op.dil) == 0 && (wi % op.dil) == 0;
         hi /= op.dil;
         wi /= op.dil;
       }
       ok = ok && static_cast<unsigned>(hi) < static_cast<unsigned>(op.H) &&
            static_cast<unsigned>(wi) < static_cast<unsigned>(op.W);
-      if (ok) val = load_vec<V>(gptr + base + (static_cast<long>(hi) * op.W + wi) * op.C + c);
-      st.v[s] = val;
+      const uint32_t off = coff + static_cast<uint32_t>(base + (hi * op.W + wi) * op.C) * 2u;
+      st.v[s] = bload(rs, ok ? off : OOB, V());
     }
   } else {  // GATHER_MN: rows = (kh, kw, c) filter taps, k = pixels
     constexpr int VPK = R / VEC;
@@ -154,22 +186,34 @@ __device__ __forceinline__ void load_tile(const Operand &op, const bf16_t *gptr,
     const uint32_t kh = fdiv(r, op.fd_kw);
     const int kw = static_cast<int>(r - kh * op.KW);
     const bool rin = row < op.rows;
+    const uint32_t coff = goff + static_cast<uint32_t>(c) * 2u;
+    const int hoff = static_cast<int>(kh) - op.pad_h, woff = kw - op.pad_w;
+    // pixel decomposition once, then advance incrementally by NT/VPK pixels per vector
+    constexpr int PSTEP = NT / VPK;
+    int p = k0 + tid / VPK;
+    uint32_t n = fdiv(static_cast<uint32_t>(p), op.fd_hw);
+    const uint32_t rem0 = static_cast<uint32_t>(p) - n * static_cast<uint32_t>(op.Ho * op.Wo);
+    uint32_t ho = fdiv(rem0, op.fd_wo);
+    uint32_t wo = rem0 - ho * op.Wo;
 #pragma unroll
     for (int s = 0; s < Stage<R, VEC>::NV; ++s) {
-      const int p = k0 + tid / VPK + s * (NT / VPK);
-      V val = zero_vec(V());
-      if (rin && p < op.kdim) {
-        const uint32_t n = fdiv(static_cast<uint32_t>(p), op.fd_hw);
-        const uint32_t rem = static_cast<uint32_t>(p) - n * static_cast<uint32_t>(op.Ho * op.Wo);
-        const uint32_t ho = fdiv(rem, op.fd_wo);
-        const uint32_t wo = rem - ho * op.Wo;
-        const int hi = static_cast<int>(ho) * op.stride - op.pad_h + static_cast<int>(kh);
-        const int wi = static_cast<int>(wo) * op.stride - op.pad_w + kw;
-        if (static_cast<unsigned>(hi) < static_cast<unsigned>(op.H) &&
-            static_cast<unsigned>(wi) < static_cast<unsigned>(op.W))
-          val = load_vec<V>(gptr + ((static_cast<long>(n) * op.H + hi) * op.W + wi) * op.C + c);
+      if (s > 0) {
+        p += PSTEP;
+        wo += PSTEP;
+        while (wo >= static_cast<uint32_t>(op.Wo)) {
+          wo -= op.Wo;
+          if (++ho == static_cast<uint32_t>(op.Ho)) {
+            ho = 0;
+            ++n;
+          }
+        }
       }
-      st.v[s] = val;
+      const int hi = static_cast<int>(ho) * op.stride + hoff;
+      const int wi = static_cast<int>(wo) * op.stride + woff;
+      const bool ok = rin && p < op.kdim && static_cast<unsigned>(hi) < static_cast<unsigned>(op.H) &&
+                      static_cast<unsigned>(wi) < static_cast<unsigned>(op.W);
+      const uint32_t off = coff + static_cast<uint32_t>(((static_cast<int>(n) * op.H + hi) * op.W + wi) * op.C) * 2u;
+      st.v[s] = bload(rs, ok ? off : OOB, V());
     }
   }
 }
@@ -246,6 +290,10 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
 
   const bf16_t *gA = A.ptr + g * A.gstride;
   const bf16_t *gB = B.ptr + g * B.gstride;
+  const rsrc_t rA = make_rsrc(A.ptr, A.nbytes);
+  const rsrc_t rB = make_rsrc(B.ptr, B.nbytes);
+  const uint32_t goA = static_cast<uint32_t>(g * A.gstride) * 2u;
+  const uint32_t goB = static_cast<uint32_t>(g * B.gstride) * 2u;
 
   // Per-row gather geometry for GATHER_K operands (rows fixed per thread across K).
   constexpr int NVA = Stage<BM, VA>::NV, NVB = Stage<BN, VB>::NV;
@@ -283,8 +331,8 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
 
   Stage<BM, VA> sa;
   Stage<BN, VB> sb;
-  load_tile<AMODE, BM, VA>(A, gA, i0, kt_beg * BK, sa, rowA);
-  load_tile<BMODE, BN, VB>(B, gB, j0, kt_beg * BK, sb, rowB);
+  load_tile<AMODE, BM, VA>(A, rA, gA, goA, i0, kt_beg * BK, sa, rowA);
+  load_tile<BMODE, BN, VB>(B, rB, gB, goB, j0, kt_beg * BK, sb, rowB);
   store_tile<AMODE, BM, VA>(As0, sa);
   store_tile<BMODE, BN, VB>(Bs0, sb);
   __syncthreads();
@@ -293,8 +341,8 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
   for (int kt = kt_beg; kt < kt_end; ++kt) {
     const bool more = kt + 1 < kt_end;
     if (more) {  // issue next tile's global loads early; they land under this step's MFMAs
-      load_tile<AMODE, BM, VA>(A, gA, i0, (kt + 1) * BK, sa, rowA);
-      load_tile<BMODE, BN, VB>(B, gB, j0, (kt + 1) * BK, sb, rowB);
+      load_tile<AMODE, BM, VA>(A, rA, gA, goA, i0, (kt + 1) * BK, sa, rowA);
+      load_tile<BMODE, BN, VB>(B, rB, gB, goB, j0, (kt + 1) * BK, sb, rowB);
     }
     const bf16_t *as = As0 + cur * A_ELEMS;
     const bf16_t *bs = Bs0 + cur * B_ELEMS;
@@ -476,6 +524,7 @@ int dispatch(const GemmArgs &g, const Operand &A, const Operand &B, const Epilog
 struct CxnOperand {
   const void *ptr;
   long gstride;
+  long nbytes;
   int ld, rows, kdim;
   int H, W, C, Ho, Wo, KH, KW, stride, pad_h, pad_w, dil, Cg;
 };
@@ -487,6 +536,7 @@ static Operand to_operand(const CxnOperand &o, int mode, int vec) {
   r.ld = o.ld;
   r.rows = o.rows;
   r.kdim = o.kdim;
+  r.nbytes = o.nbytes > 0xFFFFFF00L ? 0xFFFFFF00u : static_cast<uint32_t>(o.nbytes);
   r.H = o.H; r.W = o.W; r.C = o.C; r.Ho = o.Ho; r.Wo = o.Wo; r.KH = o.KH; r.KW = o.KW;
   r.stride = o.stride; r.pad_h = o.pad_h; r.pad_w = o.pad_w; r.dil = o.dil < 1 ? 1 : o.dil; r.Cg = o.Cg;
   if (mode == GATHER_K || mode == GATHER_MN) {

@@ -251,6 +251,67 @@ __global__ void lrn_fwd(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, lo
 
 // g_in[c] = g[c] norm[c]^-b - 2 b salpha x[c] sum_{c' in win(c)} g[c'] x[c'] norm[c']^(-b-1)
 // (norm recomputed from x: no state tensor is stored)
+// LDS-staged LRN backward: block = NT/(C/8) pixels, one thread per 8 channels.
+// LDS per pixel: x, g and t = g*x*norm^(-b-1), each with `half` zero pads at both ends.
+__global__ void lrn_bwd_lds(const bf16_t *x, const bf16_t *dy, bf16_t *dx, long npix, int C, int half, float salpha,
+                            float beta, float knorm) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tpp = C / 8;
+  const int ppb = blockDim.x / tpp;
+  const int L = C + 2 * half;
+  const int pl = threadIdx.x / tpp, cv = threadIdx.x % tpp;
+  const long pix = static_cast<long>(blockIdx.x) * ppb + pl;
+  const bool active = pl < ppb && pix < npix;
+  float *xs = sm + pl * 3 * L;
+  float *gs = xs + L;
+  float *ts = gs + L;
+  const int c0 = cv * 8;
+  float xv[8], gv[8];
+  if (active) {
+    unpack8(*reinterpret_cast<const uint4 *>(x + pix * C + c0), xv);
+    unpack8(*reinterpret_cast<const uint4 *>(dy + pix * C + c0), gv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      xs[half + c0 + e] = xv[e];
+      gs[half + c0 + e] = gv[e];
+    }
+    if (cv == 0)
+      for (int h = 0; h < half; ++h) {
+        xs[h] = 0.f; xs[half + C + h] = 0.f;
+        ts[h] = 0.f; ts[half + C + h] = 0.f;
+      }
+  }
+  __syncthreads();
+  float ng[8];
+  if (active) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = half + c0 + e;
+      float s = 0.f;
+      for (int d = -half; d <= half; ++d) {
+        const float v = xs[c + d];
+        s += v * v;
+      }
+      const float lg = __log2f(knorm + salpha * s);
+      const float p = exp2f(-beta * lg);         // norm^-b
+      ng[e] = gv[e] * p;
+      ts[c] = gv[e] * xv[e] * p * exp2f(-lg);    // g x norm^(-b-1)
+    }
+  }
+  __syncthreads();
+  if (active) {
+    float out[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = half + c0 + e;
+      float s = 0.f;
+      for (int d = -half; d <= half; ++d) s += ts[c + d];
+      out[e] = ng[e] - 2.f * beta * salpha * xv[e] * s;
+    }
+    *reinterpret_cast<uint4 *>(dx + pix * C + c0) = pack8(out);
+  }
+}
+
 __global__ void lrn_bwd(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, bf16_t *__restrict__ dx,
                         long npix, int C, int half, float salpha, float beta, float knorm) {
   const int CV = C / 8;
@@ -549,9 +610,22 @@ CXN_API int cxn_lrn_fwd(const void *x, void *y, long npix, int C, int nsize, flo
 }
 CXN_API int cxn_lrn_bwd(const void *x, const void *dy, void *dx, long npix, int C, int nsize, float alpha, float beta,
                         float knorm, void *stream) {
-  if (C % 8 != 0 || nsize / 2 > 4) return -1;
+  if (C % 8 != 0) return -1;
+  const int half = nsize / 2;
+  const int tpp = C / 8;  // threads per pixel
+  if (tpp <= NT && (C + 2 * half) * 3 * 4 * (NT / tpp) <= 48 * 1024) {
+    // LDS-staged form: each pixel row is read once, norm computed once per channel,
+    // and dx may alias x (all reads of a pixel complete before its first write).
+    const int ppb = NT / tpp;
+    const int blocks = static_cast<int>((npix + ppb - 1) / ppb);
+    const size_t smem = static_cast<size_t>(ppb) * (C + 2 * half) * 3 * sizeof(float);
+    lrn_bwd_lds<<<blocks, NT, smem, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, half,
+                                          alpha / nsize, beta, knorm);
+    RET;
+  }
+  if (half > 4 || x == dx) return -1;
   lrn_bwd<<<nblocks(npix * C / 8), NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C,
-                                                 nsize / 2, alpha / nsize, beta, knorm);
+                                                 half, alpha / nsize, beta, knorm);
   RET;
 }
 CXN_API int cxn_act_fwd(const void *x, void *y, void *y2, long n, int kind, float b, void *stream) {

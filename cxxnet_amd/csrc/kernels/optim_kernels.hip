@@ -33,7 +33,11 @@ __device__ __forceinline__ float clipg(float g, float c) {
 
 // algo: 0 sgd, 1 nag, 2 adam.  st2 used by adam only.  wb may be null.
 __global__ void fused_update(SegTable tab, float *__restrict__ w, float *__restrict__ g, float *__restrict__ st1,
-                             float *__restrict__ st2, bf16_t *__restrict__ wb, int algo, float d1, float d2) {
+                             float *__restrict__ st2, bf16_t *__restrict__ wb, int algo_flags, float d1, float d2) {
+  // algo_flags: bits 0-3 algorithm, bit 4 = zero the gradient after use (the reference's
+  // `dw = 0`); without it the next step's first backprop overwrites/zeroes the gradient.
+  const int algo = algo_flags & 15;
+  const bool zero_g = (algo_flags & 16) != 0;
   const Seg sg = tab.s[blockIdx.y];
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < sg.n; i += (long)gridDim.x * NT) {
     const long k = sg.off + i;
@@ -58,7 +62,7 @@ __global__ void fused_update(SegTable tab, float *__restrict__ w, float *__restr
       wv -= sg.lr * (m1 / (sqrtf(m2) + 1e-8f));
     }
     w[k] = wv;
-    g[k] = 0.f;
+    if (zero_g) g[k] = 0.f;
     if (wb) wb[k] = f2bf(wv);
   }
 }

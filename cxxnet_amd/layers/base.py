@@ -64,6 +64,9 @@ class ParamSpec:
     g: Optional[torch.Tensor] = None   # fp32 gradient (accumulated, zeroed by the updater)
     wb: Optional[torch.Tensor] = None  # compute copy (bf16 on GPU, == w on CPU)
     offset: int = 0
+    # True when the layer can WRITE (not accumulate) this gradient on the first
+    # micro-batch of an update cycle, so the arena need not zero it beforehand
+    overwrite: bool = False
 
     @property
     def numel(self):

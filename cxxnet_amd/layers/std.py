@@ -55,7 +55,7 @@ class FullConnectLayer(Layer):
 
         def init_w(t):
             self._init_weight(t, ni, nh)
-        self.params = [ParamSpec("wmat", (nh, ni), init_w)]
+        self.params = [ParamSpec("wmat", (nh, ni), init_w, overwrite=not self.fullc_gather)]
         if self.lp.no_bias == 0:
             self.params.append(ParamSpec("bias", (nh,), _bias_init(self.lp.init_bias)))
 
@@ -74,7 +74,7 @@ class FullConnectLayer(Layer):
     def backprop(self, prop_grad, nodes_in, nodes_out):
         x, dy = nodes_in[0].mat(), nodes_out[0].mat()
         if not self.fullc_gather:
-            ops.fc_backward_weight(x, dy, self.w.g)
+            ops.fc_backward_weight(x, dy, self.w.g, overwrite=getattr(self.ctx, "grad_overwrite", False))
         if self.b is not None:
             ops.bias_grad(dy, self.b.g)
         if prop_grad:
@@ -329,10 +329,8 @@ class LRNLayer(Layer):
         if not prop_grad:
             return
         x = nodes_in[0].data
-        if self.tmp is None or self.tmp.shape != x.shape:
-            self.tmp = torch.empty_like(x)
-        ops.lrn_backward(x, nodes_out[0].data, self.tmp, self.nsize, self.alpha, self.beta, self.knorm)
-        x.copy_(self.tmp)
+        # in place: the LDS-staged kernel reads a pixel's whole channel row before writing it
+        ops.lrn_backward(x, nodes_out[0].data, x, self.nsize, self.alpha, self.beta, self.knorm)
 
 
 # ============================================================================ dropout

@@ -47,7 +47,7 @@ def rt():
 
 class CxnOperand(ctypes.Structure):
     _fields_ = [
-        ("ptr", ctypes.c_void_p), ("gstride", ctypes.c_long),
+        ("ptr", ctypes.c_void_p), ("gstride", ctypes.c_long), ("nbytes", ctypes.c_long),
         ("ld", ctypes.c_int), ("rows", ctypes.c_int), ("kdim", ctypes.c_int),
         ("H", ctypes.c_int), ("W", ctypes.c_int), ("C", ctypes.c_int),
         ("Ho", ctypes.c_int), ("Wo", ctypes.c_int), ("KH", ctypes.c_int), ("KW", ctypes.c_int),

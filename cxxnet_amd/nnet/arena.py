@@ -50,6 +50,25 @@ class ParamArena:
             s.g = self.g[s.offset:s.offset + n].view(s.shape)
             s.wb = self.wb[s.offset:s.offset + n].view(s.shape) if self.wb is not None else s.w
 
+    def accumulate_ranges(self):
+        """Merged [start, end) arena ranges whose gradients are ACCUMULATED (atomics /
+        +=) and so must be zero at the start of an update cycle."""
+        if getattr(self, "_acc_ranges", None) is None:
+            rs = sorted((s.offset, s.offset + s.numel) for _, s in self.specs if not s.overwrite)
+            merged = []
+            for a, b in rs:
+                # segments are ALIGN-padded: bridge gaps between neighbours
+                if merged and a - merged[-1][1] < ALIGN:
+                    merged[-1][1] = max(merged[-1][1], b)
+                else:
+                    merged.append([a, b])
+            self._acc_ranges = [tuple(r) for r in merged]
+        return self._acc_ranges
+
+    def zero_accumulated_grads(self):
+        for a, b in self.accumulate_ranges():
+            self.g[a:b].zero_()
+
     def ensure_second_moment(self):
         if self.m2 is None:
             self.m2 = torch.zeros_like(self.w)

@@ -255,9 +255,17 @@ class NeuralNet:
             for conn in self.connections:
                 conn.layer.forward(is_train, conn.nodes_in, conn.nodes_out)
 
-    def backprop(self, prop_to_input: bool = False, hook=None):
+    def backprop(self, prop_to_input: bool = False, hook=None, first: bool = False):
         """Reverse pass.  hook(layer_index) runs after each layer's backprop (used by the
-        data-parallel bucketer to launch reductions as soon as gradients are final)."""
+        data-parallel bucketer to launch reductions as soon as gradients are final).
+
+        first=True marks the first micro-batch of an update cycle: accumulated gradients
+        are zeroed here and overwrite-capable ones (fullc weights) are stored instead of
+        accumulated -- replacing the reference's `dw = 0` after every update with less
+        memory traffic."""
+        self.ctx.grad_overwrite = bool(first)
+        if first:
+            self.arena.zero_accumulated_grads()
         with _BatchView(self):
             for i in range(len(self.connections) - 1, -1, -1):
                 conn = self.connections[i]

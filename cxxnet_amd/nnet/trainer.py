@@ -241,17 +241,18 @@ class NetTrainer:
         """One training step on a global batch (each rank takes its slice), or on this
         rank's rows directly when local=True."""
         need_update = (self.sample_counter + 1) % self.update_period == 0
+        first = self.sample_counter % self.update_period == 0
         self._set_batch(batch, local)
         net = self.net
         net.forward(True)
         evals = self._collect_eval() if self.eval_train else None
         if need_update:
             self.reducer.start_step()
-            net.backprop(False, hook=self.reducer.hook)
+            net.backprop(False, hook=self.reducer.hook, first=first)
             self.reducer.finish()
             net.update(self.epoch_counter)
         else:
-            net.backprop(False)
+            net.backprop(False, first=first)
         if evals is not None:
             self.train_metric.add_eval(evals, self._label_fields(batch))
         self.sample_counter += 1

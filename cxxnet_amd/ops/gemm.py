@@ -62,9 +62,10 @@ class ConvGeom:
         return self.KH * self.KW * self.cg_in
 
 
-def _op(ptr=0, gstride=0, ld=0, rows=0, kdim=0, **geo):
+def _op(t, gstride=0, ld=0, rows=0, kdim=0, **geo):
     o = native.CxnOperand()
-    o.ptr = ptr
+    o.ptr = t.data_ptr()
+    o.nbytes = t.numel() * t.element_size()  # bound of the kernel's buffer descriptor
     o.gstride = gstride
     o.ld = ld
     o.rows = rows
@@ -150,8 +151,8 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
     if cg % va:
         raise ValueError(f"conv: channels per group ({cg}) must be a multiple of 4 on the GPU path")
     kd = g.kdim
-    A = _op(w.data_ptr(), g.cg_out * kd, kd, g.cg_out, kd)
-    B = _op(x.data_ptr(), cg, 0, g.N * g.Ho * g.Wo, kd, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW,
+    A = _op(w, g.cg_out * kd, kd, g.cg_out, kd)
+    B = _op(x, cg, 0, g.N * g.Ho * g.Wo, kd, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW,
             stride=g.stride, pad_h=g.pad_y, pad_w=g.pad_x, dil=1, Cg=cg)
     tile = _pick(CONV_FWD_TILES if va == 8 else CONV_FWD_TILES_V4, g.cg_out, g.N * g.Ho * g.Wo, g.groups)
     _gemm(A, B, DIRECT_K, GATHER_K, va, va, y, g.cg_out, g.Cout, bias=bias, bias_gstride=g.cg_out, relu=relu, tile=tile,
@@ -178,8 +179,8 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False):
     native.check(k.cxn_conv_weight_flip(w.data_ptr(), wt_buf.data_ptr(), g.groups, cg_out, g.KH, g.KW, cg_in,
                                         _stream()), "conv_weight_flip")
     kd = g.KH * g.KW * cg_out
-    A = _op(wt_buf.data_ptr(), cg_in * kd, kd, cg_in, kd)
-    B = _op(dy.data_ptr(), cg_out, 0, g.N * g.H * g.W, kd, H=g.Ho, W=g.Wo, C=g.Cout, Ho=g.H, Wo=g.W, KH=g.KH,
+    A = _op(wt_buf, cg_in * kd, kd, cg_in, kd)
+    B = _op(dy, cg_out, 0, g.N * g.H * g.W, kd, H=g.Ho, W=g.Wo, C=g.Cout, Ho=g.H, Wo=g.W, KH=g.KH,
             KW=g.KW, stride=1, pad_h=g.KH - 1 - g.pad_y, pad_w=g.KW - 1 - g.pad_x, dil=g.stride, Cg=cg_out)
     tile = _pick(CONV_FWD_TILES, cg_in, g.N * g.H * g.W, g.groups)
     _gemm(A, B, DIRECT_K, GATHER_K, 8, 8, dx, cg_in, g.C, epi=EPI_BF16, groups=g.groups, mask_relu=mask_relu,
@@ -199,9 +200,9 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
     va = 8 if cg % 8 == 0 else 4
     kd = g.kdim
     P = g.N * g.Ho * g.Wo
-    A = _op(x.data_ptr(), cg, 0, kd, P, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW, stride=g.stride,
+    A = _op(x, cg, 0, kd, P, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW, stride=g.stride,
             pad_h=g.pad_y, pad_w=g.pad_x, dil=1, Cg=cg)
-    B = _op(dy.data_ptr(), g.cg_out, g.Cout, g.cg_out, P)
+    B = _op(dy, g.cg_out, g.Cout, g.cg_out, P)
     tile = _pick(WGRAD_TILES, kd, g.cg_out, g.groups, min_blocks=1)
     split = _auto_split(kd, g.cg_out, g.groups, P, tile)
     _gemm(A, B, GATHER_MN, DIRECT_MN, va, 8, dw, g.cg_out * kd, kd, epi=EPI_F32_ATOMIC, groups=g.groups,
@@ -221,8 +222,8 @@ def fc_forward(x, w, bias, y, relu=False, out_fp32=False):
         return
     Bn, nin = x.shape
     nout = w.shape[0]
-    A = _op(w.data_ptr(), 0, nin, nout, nin)
-    Bo = _op(x.data_ptr(), 0, nin, Bn, nin)
+    A = _op(w, 0, nin, nout, nin)
+    Bo = _op(x, 0, nin, Bn, nin)
     _gemm(A, Bo, DIRECT_K, DIRECT_K, 8, 8, y, 0, nout, bias=bias, relu=relu,
           epi=EPI_F32 if out_fp32 else EPI_BF16)
 
@@ -237,18 +238,21 @@ def fc_backward_data(dy, w, dx, mask_relu=False):
         return
     Bn, nout = dy.shape
     nin = w.shape[1]
-    A = _op(w.data_ptr(), 0, nin, nin, nout)
-    Bo = _op(dy.data_ptr(), 0, nout, Bn, nout)
+    A = _op(w, 0, nin, nin, nout)
+    Bo = _op(dy, 0, nout, Bn, nout)
     _gemm(A, Bo, DIRECT_MN, DIRECT_K, 8, 8, dx, 0, nin, epi=EPI_BF16, mask_relu=mask_relu)
 
 
-def fc_backward_weight(x, dy, dw):
-    """dw[nout][nin] += dy^T . x  (fp32 accumulate)."""
+def fc_backward_weight(x, dy, dw, overwrite=False):
+    """dw[nout][nin] += dy^T . x  (fp32 accumulate; overwrite=True stores instead)."""
     if not x.is_cuda:
-        dw.add_(dy.t() @ x)
+        if overwrite:
+            dw.copy_(dy.t() @ x)
+        else:
+            dw.add_(dy.t() @ x)
         return
     Bn, nin = x.shape
     nout = dy.shape[1]
-    A = _op(x.data_ptr(), 0, nin, nin, Bn)
-    Bo = _op(dy.data_ptr(), 0, nout, nout, Bn)
-    _gemm(A, Bo, DIRECT_MN, DIRECT_MN, 8, 8, dw, 0, nin, epi=EPI_F32_ACC)
+    A = _op(x, 0, nin, nin, Bn)
+    Bo = _op(dy, 0, nout, nout, Bn)
+    _gemm(A, Bo, DIRECT_MN, DIRECT_MN, 8, 8, dw, 0, nin, epi=EPI_F32 if overwrite else EPI_F32_ACC)

@@ -160,7 +160,7 @@ def lrn_forward(x, y, nsize, alpha, beta, knorm):
 
 
 def lrn_backward(x, dy, dx, nsize, alpha, beta, knorm):
-    """dx must not alias x or dy."""
+    """dx = d LRN / dx (dx may alias x; it must not alias dy)."""
     if not x.is_cuda:
         norm = _lrn_norm(x, nsize, alpha, knorm)
         t = dy * x * norm.pow(-beta - 1)

@@ -16,7 +16,7 @@ ALGO = {"sgd": 0, "nag": 1, "adam": 2}
 
 
 def fused_update(algo: str, w: torch.Tensor, g: torch.Tensor, st1: torch.Tensor, st2, wb,
-                 segs: Sequence[tuple], d1: float = 0.1, d2: float = 0.001):
+                 segs: Sequence[tuple], d1: float = 0.1, d2: float = 0.001, zero_grad: bool = True):
     """Apply one optimizer step to every segment.
 
     segs: [(offset, n, lr, wd, mom, clip), ...] element ranges of the flat buffers.
@@ -43,7 +43,8 @@ def fused_update(algo: str, w: torch.Tensor, g: torch.Tensor, st1: torch.Tensor,
                 ms.add_(d1 * (gv - ms))
                 m2.add_(d2 * (gv * gv - m2))
                 ws.sub_(lr * (ms / (m2.sqrt() + 1e-8)))
-            gs.zero_()
+            if zero_grad:
+                gs.zero_()
             if wb is not None:
                 wb[off:off + n].copy_(ws)
         return
@@ -54,7 +55,7 @@ def fused_update(algo: str, w: torch.Tensor, g: torch.Tensor, st1: torch.Tensor,
     rc = native.kernels().cxn_fused_update(
         ctypes.cast(offs, ctypes.c_void_p), ctypes.cast(ns, ctypes.c_void_p), ctypes.cast(hyper, ctypes.c_void_p),
         nseg, w.data_ptr(), g.data_ptr(), st1.data_ptr(), st2.data_ptr() if st2 is not None else None,
-        wb.data_ptr() if wb is not None else None, a, float(d1), float(d2), _stream())
+        wb.data_ptr() if wb is not None else None, a | (16 if zero_grad else 0), float(d1), float(d2), _stream())
     native.check(rc, "fused_update")
 
 

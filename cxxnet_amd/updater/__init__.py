@@ -149,4 +149,6 @@ class ArenaUpdater:
 
     def update(self, epoch: int):
         a = self.arena
-        ops.fused_update(self.algo, a.w, a.g, a.m1, a.m2, a.wb, self.segments(epoch), self.beta1, self.beta2)
+        # gradients are reset by the next cycle's first backprop (NeuralNet.backprop(first=True))
+        ops.fused_update(self.algo, a.w, a.g, a.m1, a.m2, a.wb, self.segments(epoch), self.beta1, self.beta2,
+                         zero_grad=False)

@@ -155,9 +155,12 @@ def test_lrn():
     ops.lrn_forward(xd, y, *args)
     dx = torch.empty_like(xd)
     ops.lrn_backward(xd, dy.to(DEV, torch.bfloat16), dx, *args)
+    xi = xd.clone()
+    ops.lrn_backward(xi, dy.to(DEV, torch.bfloat16), xi, *args)  # in place (the layer's usage)
     torch.cuda.synchronize()
     assert relerr(y, y_ref) < 1e-2
     assert relerr(dx, dx_ref) < 2e-2
+    assert torch.equal(xi, dx)
 
 
 @pytest.mark.parametrize("kind", ["relu", "sigmoid", "tanh", "xelu"])

@@ -6,7 +6,9 @@ TAG=${1:-run}; shift
 export TMPDIR=/tmp
 mkdir -p gpurun_out/$TAG
 timeout -k 10 600 python -m pytest tests/ -q -m gpu -x > gpurun_out/$TAG/tests.log 2>&1
-echo "tests rc=$?"; tail -3 gpurun_out/$TAG/tests.log
+rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/$TAG/tests.log
+# 0 = pass, 1 = test failures; anything else (abort/segv/timeout) ends the call
+if [ $rc -gt 1 ]; then exit $rc; fi
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 "$@" > gpurun_out/$TAG/bench.log 2>&1 || { echo bench failed; tail -20 gpurun_out/$TAG/bench.log; exit 1; }
 tail -1 gpurun_out/$TAG/bench.log
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/$TAG/prof -o run -- python bench.py --steps 10 --warmup 3 "$@" > gpurun_out/$TAG/prof.log 2>&1 || { echo prof failed; tail -5 gpurun_out/$TAG/prof.log; exit 1; }
