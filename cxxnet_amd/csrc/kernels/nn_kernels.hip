@@ -37,6 +37,58 @@ __global__ void nchw_f32_to_nhwc_bf16(const float *__restrict__ x, bf16_t *__res
   }
 }
 
+// Decoded image batch -> NHWC bf16 input node, with the reference augmenter's
+// arithmetic fused in (src/io/iter_augment_proc-inl.hpp:98-162).  The host has
+// already cropped and mirrored the uint8 pixels (cheap row copies); mean
+// subtraction, contrast, illumination, scale and the bf16/NHWC/channel-pad
+// conversion run here so only uint8 crosses PCIe.
+//   pix  u8 [B][h][w][C]          prm int [B][4] = {crop_y, crop_x, mirrored, 0}
+//   cm   f32 [B][2] = {contrast, illumination}
+//   mode 0: y = d*scale                      (no mean)
+//        1: y = ((d - mean[c])*ct + il)*scale (mean_value)
+//        2: mean image [C][Hm][Wm] of the uncropped size, read at the crop offset
+//        3: mean image [C][h][w] of the crop size
+__global__ void image_u8_to_nhwc_bf16(const uint8_t *__restrict__ pix, const int *__restrict__ prm,
+                                      const float *__restrict__ cm, const float *__restrict__ mean, int B, int h,
+                                      int w, int C, int Cp, int Hm, int Wm, int mode, float scale,
+                                      bf16_t *__restrict__ y) {
+  const long total = static_cast<long>(B) * h * w;
+  for (long p = grid_stride_start(); p < total; p += grid_stride()) {
+    const int x = static_cast<int>(p % w);
+    const long t = p / w;
+    const int r = static_cast<int>(t % h);
+    const int b = static_cast<int>(t / h);
+    const uint8_t *src = pix + p * C;
+    bf16_t *dst = y + p * Cp;
+    float ct = 1.f, il = 0.f;
+    if (mode != 0) {
+      ct = cm[2 * b];
+      il = cm[2 * b + 1];
+    }
+    for (int c = 0; c < Cp; ++c) {
+      float v = 0.f;
+      if (c < C) {
+        const float d = static_cast<float>(src[c]);
+        if (mode == 0) {
+          v = d * scale;
+        } else {
+          float m;
+          if (mode == 1) {
+            m = mean[c];
+          } else if (mode == 2) {
+            const int xs = prm[4 * b + 2] ? (w - 1 - x) : x;
+            m = mean[(static_cast<long>(c) * Hm + prm[4 * b] + r) * Wm + prm[4 * b + 1] + xs];
+          } else {
+            m = mean[(static_cast<long>(c) * h + r) * w + x];
+          }
+          v = ((d - m) * ct + il) * scale;
+        }
+      }
+      dst[c] = f2bf(v);
+    }
+  }
+}
+
 // x: NHWC bf16 [N][H][W][Cp] -> y: NCHW fp32 [N][C][H][W]
 __global__ void nhwc_bf16_to_nchw_f32(const bf16_t *__restrict__ x, float *__restrict__ y, int N, int C, int H,
                                       int W, int Cp) {
@@ -561,6 +613,15 @@ __global__ void channel_copy(const bf16_t *__restrict__ src, int Cs, int soff, b
 CXN_API int cxn_nchw_f32_to_nhwc_bf16(const float *x, void *y, int N, int C, int H, int W, int Cp, float scale,
                                       void *stream) {
   nchw_f32_to_nhwc_bf16<<<nblocks(static_cast<long>(N) * H * W), NT, 0, S_>>>(x, (bf16_t *)y, N, C, H, W, Cp, scale);
+  RET;
+}
+CXN_API int cxn_image_u8_to_nhwc_bf16(const void *pix, const int *prm, const float *cm, const float *mean, int B,
+                                      int h, int w, int C, int Cp, int Hm, int Wm, int mode, float scale, void *y,
+                                      void *stream) {
+  if (Cp < C || (mode != 0 && cm == nullptr) || (mode >= 1 && mean == nullptr) || (mode == 2 && prm == nullptr))
+    return -2;
+  image_u8_to_nhwc_bf16<<<nblocks(static_cast<long>(B) * h * w), NT, 0, S_>>>(
+      (const uint8_t *)pix, prm, cm, mean, B, h, w, C, Cp, Hm, Wm, mode, scale, (bf16_t *)y);
   RET;
 }
 CXN_API int cxn_nhwc_bf16_to_nchw_f32(const void *x, float *y, int N, int C, int H, int W, int Cp, void *stream) {

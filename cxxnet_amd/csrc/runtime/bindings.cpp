@@ -140,8 +140,28 @@ PYBIND11_MODULE(_cxxnet_rt, m) {
           py::gil_scoped_release rel;
           ok = r.Next(&s);
         }
-        if (!ok) return py::none();
+        if (!ok) {
+          std::string err = r.Error();
+          if (!err.empty()) throw std::runtime_error("ImageBinReader: " + err);
+          return py::none();
+        }
         return py::bytes(s);
+      })
+      .def("next_page", [](ImageBinReader &r) -> py::object {
+        std::vector<std::string> objs;
+        bool ok;
+        {
+          py::gil_scoped_release rel;
+          ok = r.NextPage(&objs);
+        }
+        if (!ok) {
+          std::string err = r.Error();
+          if (!err.empty()) throw std::runtime_error("ImageBinReader: " + err);
+          return py::none();
+        }
+        py::list out;
+        for (auto &o : objs) out.append(py::bytes(o));
+        return out;
       });
 
   py::class_<ImageListEntry>(m, "ImageListEntry")

@@ -167,6 +167,21 @@ class ImageBinReader {
     *out = cur_->Get(cur_idx_++);
     return true;
   }
+  // All remaining objects of the current page (or of the next page when the current
+  // one is exhausted); false at end of all files.  Used by the page-shuffling reader.
+  bool NextPage(std::vector<std::string> *out) {
+    out->clear();
+    std::string s;
+    if (!Next(&s)) return false;
+    out->push_back(std::move(s));
+    while (cur_idx_ < cur_->Size()) out->push_back(cur_->Get(cur_idx_++));
+    return true;
+  }
+  // Non-empty when a file could not be opened by the loader thread.
+  std::string Error() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return error_;
+  }
 
  private:
   void Start() {

@@ -8,6 +8,65 @@ import numpy as np
 import torch
 
 
+class U8Images:
+    """A batch of decoded images still in uint8, with the augmenter's arithmetic
+    pending.  The image iterators emit this instead of a float tensor so that only
+    uint8 pixels cross PCIe; ``ops.image_to_nhwc`` applies mean/contrast/
+    illumination/scale and the NHWC-bf16 conversion in one GPU kernel, and
+    ``to_float`` is the fp32 reference of the same arithmetic (the CPU path).
+
+    pix  uint8 (B, h, w, C): pixels after crop and mirror (RGB order)
+    prm  int32 (B, 4): crop_y, crop_x, mirrored, 0 (for full-size mean images)
+    cm   float32 (B, 2): contrast, illumination
+    mean None | float32 (C,) | (C, Hm, Wm) full-size | (C, h, w) crop-size
+    mode 0 none, 1 per-channel value, 2 full-size mean image, 3 crop-size mean image
+    Reference: src/io/iter_augment_proc-inl.hpp:98-162.
+    """
+
+    def __init__(self, pix, prm, cm, mean=None, mode=0, scale=1.0):
+        self.pix, self.prm, self.cm, self.mean, self.mode, self.scale = pix, prm, cm, mean, mode, float(scale)
+
+    @property
+    def shape(self):
+        B, h, w, C = self.pix.shape
+        return (B, C, h, w)
+
+    def __getitem__(self, sl):
+        if not isinstance(sl, slice):
+            raise TypeError("U8Images supports row slices only")
+        return U8Images(self.pix[sl], self.prm[sl], self.cm[sl], self.mean, self.mode, self.scale)
+
+    def clone(self):
+        return U8Images(self.pix.clone(), self.prm.clone(), self.cm.clone(), self.mean, self.mode, self.scale)
+
+    def to_float(self) -> torch.Tensor:
+        """fp32 NCHW batch (reference arithmetic, CPU)."""
+        d = self.pix.permute(0, 3, 1, 2).float()
+        if self.mode == 0:
+            return d * self.scale
+        B, C, h, w = d.shape
+        ct = self.cm[:, 0].view(B, 1, 1, 1).float()
+        il = self.cm[:, 1].view(B, 1, 1, 1).float()
+        mean = self.mean.float()
+        if self.mode == 1:
+            m = mean.view(1, C, 1, 1)
+        elif self.mode == 3:
+            m = mean.view(1, C, h, w)
+        else:
+            rows = []
+            for b in range(B):
+                y0, x0, mir = (int(v) for v in self.prm[b, :3])
+                mb = mean[:, y0:y0 + h, x0:x0 + w]
+                rows.append(mb.flip(2) if mir else mb)
+            m = torch.stack(rows)
+        return ((d - m) * ct + il) * self.scale
+
+
+def dense(data) -> torch.Tensor:
+    """Float NCHW view of a batch's data whatever its storage."""
+    return data.to_float() if isinstance(data, U8Images) else data
+
+
 @dataclass
 class DataBatch:
     """One mini-batch: data (b,c,h,w) float32, label (b, label_width) float32,

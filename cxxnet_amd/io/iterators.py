@@ -315,6 +315,8 @@ def create_iterator(cfg: List[Tuple[str, str]]) -> DataIterator:
     it: Optional[DataIterator] = None
     for name, val in cfg:
         if name == "iter":
+            if val == "end":
+                break
             if val == "mnist":
                 if it is not None:
                     raise ValueError("mnist can not chain over other iterator")

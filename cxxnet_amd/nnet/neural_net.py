@@ -27,6 +27,7 @@ from ..layers import K_SHARED, LayerContext, Node, create_layer
 from ..layers.base import BinReader, BinWriter
 from ..updater import ArenaUpdater
 from .arena import ParamArena
+from ..io.data import U8Images
 
 K_CONV, K_FULLC, K_RELU, K_MAXPOOL, K_DROPOUT = 10, 1, 3, 11, 8
 
@@ -229,8 +230,11 @@ class NeuralNet:
         b = data.shape[0]
         self.adjust_batch_size(b)
         n0 = self.nodes[0]
-        src = data.to(self.device, non_blocking=True)
-        ops.input_to_nhwc(src, n0.data[:b])
+        if isinstance(data, U8Images):
+            ops.image_to_nhwc(data, n0.data[:b])
+        else:
+            src = data.to(self.device, non_blocking=True)
+            ops.input_to_nhwc(src, n0.data[:b])
         for i, e in enumerate(extra):
             ops.input_to_nhwc(e.to(self.device, non_blocking=True), self.nodes[i + 1].data[:b])
 

@@ -34,6 +34,35 @@ def input_to_nhwc(x_nchw: torch.Tensor, out: torch.Tensor, scale: float = 1.0):
                                                 _stream()), "nchw_to_nhwc")
 
 
+def image_to_nhwc(img, out: torch.Tensor):
+    """U8Images batch -> NHWC input node with the augmenter arithmetic fused
+    (GPU: one kernel over uint8 pixels; CPU: the fp32 reference)."""
+    if not out.is_cuda:
+        input_to_nhwc(img.to_float(), out)
+        return
+    B, C, h, w = img.shape
+    Cp = out.shape[-1]
+    if tuple(out.shape[:3]) != (B, h, w) or Cp < C:
+        raise ValueError(f"image batch {tuple(img.shape)} does not fit input node {tuple(out.shape)}")
+    dev = out.device
+    pix = img.pix.to(dev, non_blocking=True).contiguous()
+    prm = img.prm.to(dev, torch.int32, non_blocking=True).contiguous()
+    cm = img.cm.to(dev, torch.float32, non_blocking=True).contiguous()
+    mean = img.mean.to(dev, torch.float32, non_blocking=True).contiguous() if img.mean is not None else None
+    Hm = Wm = 0
+    if img.mode == 2:
+        Hm, Wm = int(img.mean.shape[1]), int(img.mean.shape[2])
+        if int(img.prm[:, 0].max()) + h > Hm or int(img.prm[:, 1].max()) + w > Wm:
+            raise ValueError("crop offsets fall outside the mean image")
+    elif img.mode == 3 and tuple(img.mean.shape) != (C, h, w):
+        raise ValueError("crop-size mean image has the wrong shape")
+    elif img.mode == 1 and img.mean.numel() < C:
+        raise ValueError("mean_value needs one value per channel")
+    native.check(_k().cxn_image_u8_to_nhwc_bf16(
+        pix.data_ptr(), prm.data_ptr(), cm.data_ptr(), mean.data_ptr() if mean is not None else None,
+        B, h, w, C, Cp, Hm, Wm, int(img.mode), float(img.scale), out.data_ptr(), _stream()), "image_to_nhwc")
+
+
 def nhwc_to_nchw(x: torch.Tensor, C: int) -> torch.Tensor:
     """NHWC node (any dtype) -> NCHW fp32 tensor with C logical channels."""
     N, H, W, Cp = x.shape

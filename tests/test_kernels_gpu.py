@@ -262,3 +262,28 @@ def test_layout_roundtrip():
     ref = t.transpose(1, 2).reshape(2, -1)
     torch.cuda.synchronize()
     assert relerr(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_image_u8_to_nhwc(mode):
+    """Fused augment arithmetic (mean / contrast / illumination / scale / mirror-aware
+    mean lookup) against U8Images.to_float."""
+    from cxxnet_amd.io.data import U8Images
+    g = torch.Generator().manual_seed(mode)
+    B, h, w, C, Cp = 5, 13, 17, 3, 4
+    pix = torch.randint(0, 256, (B, h, w, C), generator=g, dtype=torch.uint8)
+    prm = torch.zeros((B, 4), dtype=torch.int32)
+    prm[:, 0] = torch.randint(0, 4, (B,), generator=g)
+    prm[:, 1] = torch.randint(0, 6, (B,), generator=g)
+    prm[:, 2] = torch.tensor([0, 1, 0, 1, 1])
+    cm = torch.stack([torch.rand(B, generator=g) + 0.5, torch.rand(B, generator=g) * 10 - 5], 1)
+    mean = {0: None, 1: torch.tensor([100.0, 110.0, 120.0]),
+            2: torch.rand((C, h + 3, w + 5), generator=g) * 255,
+            3: torch.rand((C, h, w), generator=g) * 255}[mode]
+    img = U8Images(pix, prm, cm, mean, mode, 1.0 / 64)
+    ref = img.to_float().permute(0, 2, 3, 1)
+    out = torch.empty((B, h, w, Cp), dtype=torch.bfloat16, device=DEV)
+    ops.image_to_nhwc(img, out)
+    got = out.float().cpu()
+    assert relerr(got[..., :C], ref) < 1e-2
+    assert got[..., C:].abs().max().item() == 0
