@@ -112,7 +112,7 @@ class LearnTask:
         self.log("initializing end, start working")
         if self.task in ("train", "finetune"):
             self.task_train()
-        elif self.task == "pred":
+        elif self.task in ("pred", "pred_raw"):
             self.task_predict()
         elif self.task in ("extract", "extract_feature"):
             self.task_extract()
@@ -223,11 +223,11 @@ class LearnTask:
             if name == "iter" and val == "end":
                 if flag == 0:
                     raise RuntimeError("wrong configuration file")
-                if flag == 1 and self.task != "pred":
+                if flag == 1 and self.task not in ("pred", "pred_raw"):
                     if self.itr_train is not None:
                         raise RuntimeError("can only have one data")
                     self.itr_train = create_iterator(itcfg)
-                if flag == 2 and self.task != "pred":
+                if flag == 2 and self.task not in ("pred", "pred_raw"):
                     self.itr_evals.append(create_iterator(itcfg))
                     self.eval_names.append(evname)
                 if flag == 3 and self.task in ("pred", "pred_raw", "extract", "extract_feature"):
@@ -252,17 +252,25 @@ class LearnTask:
         if self.itr_pred is None:
             raise RuntimeError("must specify a predict iterator to generate predictions")
         self.log("start predicting...")
+        raw = self.task == "pred_raw"
         out = []
         self.itr_pred.before_first()
         while self.itr_pred.next():
             b = self.itr_pred.value()
-            pred = self.trainer.predict(b)
+            if raw:  # whole output row per instance (used by the Kaggle bowl submission)
+                top = len(self.trainer.net.nodes) - 1
+                pred = self.trainer.forward_to([top], b)[0].reshape(b.batch_size, -1)
+            else:
+                pred = self.trainer.predict(b)
             sz = len(pred) - b.num_batch_padd
             out.extend(pred[:sz].tolist())
         if self.rank == 0:
             with open(self.name_pred, "w") as f:
                 for v in out:
-                    f.write("%g\n" % v)
+                    if raw:
+                        f.write("".join("%g " % x for x in v) + "\n")
+                    else:
+                        f.write("%g\n" % v)
         self.log(f"finished prediction, write into {self.name_pred}")
 
     def task_extract(self):
