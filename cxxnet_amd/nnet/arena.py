@@ -37,7 +37,11 @@ class ParamArena:
                 s.offset = off
                 self.specs.append((li, s))
                 off += (s.numel + ALIGN - 1) // ALIGN * ALIGN
-        self.total = max(off, ALIGN)
+        # a multiple of world*ALIGN, so that sharded buckets split into equal,
+        # aligned per-rank chunks (parallel/dp.py, update_on_server)
+        from ..parallel.dp import world_info
+        q = ALIGN * world_info()[1]
+        self.total = max((off + q - 1) // q * q, q)
         dev = self.device
         self.w = torch.zeros(self.total, dtype=torch.float32, device=dev)
         self.g = torch.zeros(self.total, dtype=torch.float32, device=dev)

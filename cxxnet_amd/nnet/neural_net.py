@@ -277,8 +277,8 @@ class NeuralNet:
                 if hook is not None:
                     hook(i)
 
-    def update(self, epoch: int):
-        self.updater.update(epoch)
+    def update(self, epoch: int, ranges=None):
+        self.updater.update(epoch, ranges)
 
     def start_round(self, r: int):
         if self.updater is not None:

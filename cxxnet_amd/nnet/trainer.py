@@ -51,6 +51,8 @@ class NetTrainer:
         self.type_pserver = "UNSPECIFIED"
         self.bucket_mb = 64.0
         self.comm_dtype = "fp32"
+        self.shard_update = 0
+        self.test_on_server = 0
         self.cfg: List[Tuple[str, str]] = []
         self.metric = MetricSet()
         self.train_metric = MetricSet()
@@ -82,6 +84,10 @@ class NetTrainer:
             self.bucket_mb = float(val)
         elif name == "dp_comm_dtype":
             self.comm_dtype = val
+        elif name in ("update_on_server", "dp_shard_update"):
+            self.shard_update = int(val)
+        elif name == "test_on_server":
+            self.test_on_server = int(val)
         if name.startswith("metric"):
             import re
             m = re.match(r"metric\[([^,\]]+),([^\]]+)\]", name)
@@ -134,7 +140,8 @@ class NetTrainer:
     def _post_init(self):
         self._forward_global_params(self.net)
         self._init_eval_nodes()
-        self.reducer = GradReducer(self.net.arena, self.bucket_mb, True, self.comm_dtype)
+        self.reducer = GradReducer(self.net.arena, self.bucket_mb, True, self.comm_dtype,
+                                   shard=bool(self.shard_update))
         self.reducer.broadcast_params()
 
     def init_model(self):
@@ -145,6 +152,8 @@ class NetTrainer:
 
     # ------------------------------------------------------------------ model io
     def save_model(self) -> bytes:
+        if self.reducer is not None:
+            self.reducer.sync_master()
         fo = BinWriter()
         self.net.save_model(fo)
         blob = fo.getvalue()
@@ -218,6 +227,8 @@ class NetTrainer:
     # ------------------------------------------------------------------ training
     def start_round(self, r: int):
         self.net.start_round(r)
+        if self.test_on_server and self.reducer is not None:
+            self.reducer.check_consistency()
 
     def _slice(self, t: torch.Tensor, b: int):
         step = self._local_batch()
@@ -250,7 +261,11 @@ class NetTrainer:
             self.reducer.start_step()
             net.backprop(False, hook=self.reducer.hook, first=first)
             self.reducer.finish()
-            net.update(self.epoch_counter)
+            if self.reducer.shard:
+                net.update(self.epoch_counter, self.reducer.owned_ranges())
+                self.reducer.gather_params()
+            else:
+                net.update(self.epoch_counter)
         else:
             net.backprop(False, first=first)
         if evals is not None:
@@ -359,6 +374,8 @@ class NetTrainer:
         raise ValueError(f"layer {layer_name} has no {tag}")
 
     def get_weight(self, layer_name: str, tag: str) -> np.ndarray:
+        if self.reducer is not None:
+            self.reducer.sync_master()
         layer, p = self._param(layer_name, tag)
         w = p.w.detach().float().cpu()
         if hasattr(layer, "to_logical") and tag == "wmat":

@@ -14,6 +14,16 @@ Replaces the reference's mshadow-ps "local"/"dist" parameter server
 Bucket size defaults to 64 MB: AlexNet's 244 MB of gradients become 4-5 messages,
 large enough to run at link rate on 7 xGMI links, small enough that the fc8/fc7
 buckets overlap conv backward.
+
+Sharded mode (``update_on_server = 1``).  This maps the reference's parameter
+server (nnet_ps_server.cpp:54-89: each server owns some keys, workers push
+gradients and pull updated weights) onto collectives.  Every bucket is
+REDUCE-SCATTERED, so rank r holds the summed gradient of its 1/N slice.  The
+fused optimizer updates only that slice (fp32 master and state).  The bf16
+compute weights are then ALL-GATHERED.  Wire bytes per step drop from 8 B/param
+(fp32 all-reduce) to 6 B/param (fp32 reduce-scatter + bf16 all-gather), and each
+GPU runs 1/N of the optimizer.  The fp32 masters of other ranks' slices are
+fetched only when they are needed (save / get_weight).
 """
 from __future__ import annotations
 
@@ -35,18 +45,28 @@ class Bucket:
         self.start, self.end, self.li_min = start, end, li_min
         self.work = None
         self.buf = None
+        self.out = None     # sharded: this rank's reduced chunk
+        self.agin = None    # sharded: all-gather source
+
+    def own(self, rank, world):
+        c = (self.end - self.start) // world
+        return self.start + rank * c, self.start + (rank + 1) * c
 
 
 class GradReducer:
     def __init__(self, arena, bucket_mb: float = 64.0, overlap: bool = True, comm_dtype: str = "fp32",
-                 group=None):
+                 group=None, shard: bool = False):
         self.arena = arena
         self.group = group
         self.rank, self.world = world_info()
         self.overlap = overlap
+        self.shard = bool(shard) and self.world > 1
         self.comm_dtype = torch.bfloat16 if comm_dtype == "bf16" else torch.float32
         limit = max(1, int(bucket_mb * (1 << 20) / 4))
         self.buckets: List[Bucket] = []
+        if self.shard:
+            self._shard_buckets(limit)
+            return
         cur_start, cur_end, cur_li = None, 0, None
         for li, spec in arena.specs:  # arena order = reverse layer order
             s, e = spec.offset, spec.offset + spec.numel
@@ -59,6 +79,36 @@ class GradReducer:
             cur_li = li
         if cur_start is not None and cur_end > cur_start:
             self.buckets.append(Bucket(cur_start, cur_end, cur_li))
+
+    def _shard_buckets(self, limit):
+        """Buckets cut at multiples of world*ALIGN (the arena total is one too), so
+        every bucket splits into equal aligned per-rank chunks.  A cut may fall inside
+        a segment; a bucket is launched once every layer it touches is done."""
+        from ..nnet.arena import ALIGN
+        q = ALIGN * self.world
+        total = self.arena.total
+        assert total % q == 0, "arena must be padded to world*ALIGN"
+        segs = [(spec.offset, spec.offset + spec.numel, li) for li, spec in self.arena.specs]
+        start = 0
+        while start < total:
+            end = min(total, start + max(q, (limit + q - 1) // q * q))
+            # extend to the end of the segment that the cut falls into, rounded up to q
+            for a, b, _ in segs:
+                if a < end < b:
+                    end = min(total, (b + q - 1) // q * q)
+                    break
+            lis = [li for a, b, li in segs if a < end and b > start]
+            self.buckets.append(Bucket(start, end, min(lis) if lis else -1))
+            start = end
+        for b in self.buckets:
+            c = (b.end - b.start) // self.world
+            b.out = torch.empty(c, dtype=self.comm_dtype, device=self.arena.g.device)
+            sh = self.arena.wb if self.arena.wb is not None else self.arena.w
+            b.agin = torch.empty(c, dtype=sh.dtype, device=sh.device)
+
+    def owned_ranges(self):
+        """[start, end) arena ranges this rank updates (sharded mode)."""
+        return [b.own(self.rank, self.world) for b in self.buckets]
 
     @property
     def active(self):
@@ -76,6 +126,12 @@ class GradReducer:
 
     def _launch(self, b: Bucket):
         g = self.arena.g[b.start:b.end]
+        if self.shard:
+            src = g if self.comm_dtype == torch.float32 else g.to(self.comm_dtype)
+            b.buf = src  # keep the (possibly converted) source alive until the op is done
+            b.work = dist.reduce_scatter_tensor(b.out, src, op=dist.ReduceOp.SUM, group=self.group,
+                                                async_op=True)
+            return
         if self.comm_dtype == torch.float32:
             b.buf = None
             b.work = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
@@ -100,10 +156,56 @@ class GradReducer:
                 self._launch(b)
         for b in self.buckets:
             b.work.wait()
-            if b.buf is not None:
+            if self.shard:
+                lo, hi = b.own(self.rank, self.world)
+                self.arena.g[lo:hi].copy_(b.out)
+                b.buf = None
+            elif b.buf is not None:
                 self.arena.g[b.start:b.end].copy_(b.buf)
                 b.buf = None
             b.work = None
+
+    def gather_params(self):
+        """Sharded mode, after the local update: every rank's fresh slice of the
+        compute weights (bf16 shadow on the GPU, fp32 on the CPU) to every rank."""
+        if not self.shard:
+            return
+        a = self.arena
+        sh = a.wb if a.wb is not None else a.w
+        works = []
+        for b in self.buckets:
+            lo, hi = b.own(self.rank, self.world)
+            b.agin.copy_(sh[lo:hi])
+            works.append(dist.all_gather_into_tensor(sh[b.start:b.end], b.agin, group=self.group, async_op=True))
+        for w in works:
+            w.wait()
+
+    def sync_master(self):
+        """Sharded mode: gather the fp32 master weights (for save / get_weight)."""
+        if not self.shard or self.arena.wb is None:
+            return
+        a = self.arena
+        for b in self.buckets:
+            lo, hi = b.own(self.rank, self.world)
+            src = a.w[lo:hi].clone()
+            dist.all_gather_into_tensor(a.w[b.start:b.end], src, group=self.group)
+
+    def check_consistency(self) -> float:
+        """Max |w - w_rank0| over the compute weights of every replica (the
+        reference's test_on_server check, async_updater-inl.hpp:50-52,148-153).
+        Raises if the replicas diverged."""
+        if not self.active:
+            return 0.0
+        a = self.arena
+        sh = a.wb if a.wb is not None else a.w
+        ref = sh.clone()
+        dist.broadcast(ref, src=0, group=self.group)
+        diff = (sh.float() - ref.float()).abs().max().reshape(1)
+        dist.all_reduce(diff, op=dist.ReduceOp.MAX, group=self.group)
+        d = float(diff.item())
+        if d != 0.0:
+            raise RuntimeError(f"data-parallel replicas diverged: max |w - w_rank0| = {d:g}")
+        return d
 
     def allreduce_tensor(self, t: torch.Tensor):
         if self.active:

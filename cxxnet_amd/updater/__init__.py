@@ -147,8 +147,22 @@ class ArenaUpdater:
                 segs.append((spec.offset, spec.numel, p.learning_rate, p.wd, p.momentum, p.clip_gradient))
         return segs
 
-    def update(self, epoch: int):
+    def update(self, epoch: int, ranges=None):
+        """ranges: optional [start, end) arena ranges to update (sharded data
+        parallelism updates only this rank's slice)."""
         a = self.arena
+        segs = self.segments(epoch)
+        if ranges is not None:
+            segs = _clip_segments(segs, ranges)
         # gradients are reset by the next cycle's first backprop (NeuralNet.backprop(first=True))
-        ops.fused_update(self.algo, a.w, a.g, a.m1, a.m2, a.wb, self.segments(epoch), self.beta1, self.beta2,
-                         zero_grad=False)
+        ops.fused_update(self.algo, a.w, a.g, a.m1, a.m2, a.wb, segs, self.beta1, self.beta2, zero_grad=False)
+
+
+def _clip_segments(segs, ranges):
+    out = []
+    for off, n, *hyper in segs:
+        for lo, hi in ranges:
+            a, b = max(off, lo), min(off + n, hi)
+            if a < b:
+                out.append((a, b - a, *hyper))
+    return out
