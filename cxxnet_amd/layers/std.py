@@ -55,7 +55,8 @@ class FullConnectLayer(Layer):
 
         def init_w(t):
             self._init_weight(t, ni, nh)
-        self.params = [ParamSpec("wmat", (nh, ni), init_w, overwrite=not self.fullc_gather)]
+        self.params = [ParamSpec("wmat", (nh, ni), init_w, overwrite=True)]
+        self.params[0].no_reduce = self._gathering()
         if self.lp.no_bias == 0:
             self.params.append(ParamSpec("bias", (nh,), _bias_init(self.lp.init_bias)))
 
@@ -67,14 +68,32 @@ class FullConnectLayer(Layer):
     def b(self):
         return self.params[1] if len(self.params) > 1 else None
 
+    def _gathering(self) -> bool:
+        """fullc_gather (reference fullc_layer-inl.hpp:120-122 + async_updater-inl.hpp:
+        67-93): instead of all-reducing the nout x nin weight gradient, all-gather the
+        B x (nin + nout) activations/gradients of every rank and form the global
+        gradient locally.  Active only under plain (non-sharded) data parallelism."""
+        from ..parallel.dp import world_info
+        return bool(self.fullc_gather) and world_info()[1] > 1 and not getattr(self.ctx, "dp_shard", False)
+
     def forward(self, is_train, nodes_in, nodes_out):
         bias = self.b.w if self.b is not None else None
-        ops.fc_forward(nodes_in[0].mat(), self.w.wb, bias, nodes_out[0].mat(), relu=self.fuse_relu)
+        x = nodes_in[0].mat()
+        if is_train and self._gathering():
+            # backprop overwrites the input node with its gradient: gather it now
+            self._x_all = _all_gather_rows(x)
+        ops.fc_forward(x, self.w.wb, bias, nodes_out[0].mat(), relu=self.fuse_relu)
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
         x, dy = nodes_in[0].mat(), nodes_out[0].mat()
-        if not self.fullc_gather:
-            ops.fc_backward_weight(x, dy, self.w.g, overwrite=getattr(self.ctx, "grad_overwrite", False))
+        overwrite = getattr(self.ctx, "grad_overwrite", False)
+        if self._gathering():
+            dy_all = _all_gather_rows(dy)
+            x_all = self._x_all.wait()
+            ops.fc_backward_weight(x_all, dy_all.wait(), self.w.g, overwrite=overwrite)
+            self._x_all = None
+        else:
+            ops.fc_backward_weight(x, dy, self.w.g, overwrite=overwrite)
         if self.b is not None:
             ops.bias_grad(dy, self.b.g)
         if prop_grad:
@@ -95,6 +114,25 @@ class FullConnectLayer(Layer):
         if self.lp.no_bias == 0:
             out.append(b)
         return out
+
+
+class _Gathered:
+    def __init__(self, out, work):
+        self.out, self.work = out, work
+
+    def wait(self):
+        self.work.wait()
+        return self.out
+
+
+def _all_gather_rows(t: torch.Tensor) -> _Gathered:
+    """Async all-gather of a (rows, cols) matrix over the data-parallel ranks
+    (every rank holds the same number of rows: the trainer's batch split)."""
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    src = t.contiguous()
+    out = torch.empty((world * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+    return _Gathered(out, dist.all_gather_into_tensor(out, src, async_op=True))
 
 
 # ============================================================================ conv

@@ -117,6 +117,7 @@ class NetTrainer:
 
     def _make_net(self) -> NeuralNet:
         net = NeuralNet(self.net_cfg, self._local_batch(), self._device(), seed=self.seed)
+        net.ctx.dp_shard = bool(self.shard_update)
         return net
 
     def _forward_global_params(self, net: NeuralNet):

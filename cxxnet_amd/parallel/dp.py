@@ -70,6 +70,11 @@ class GradReducer:
         cur_start, cur_end, cur_li = None, 0, None
         for li, spec in arena.specs:  # arena order = reverse layer order
             s, e = spec.offset, spec.offset + spec.numel
+            if getattr(spec, "no_reduce", False):  # fullc_gather: gradient is already global
+                if cur_start is not None and cur_end > cur_start:
+                    self.buckets.append(Bucket(cur_start, cur_end, cur_li))
+                cur_start, cur_end, cur_li = None, 0, None
+                continue
             if cur_start is None:
                 cur_start, cur_li = s, li
             if e - cur_start > limit and cur_end > cur_start:

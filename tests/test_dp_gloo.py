@@ -67,7 +67,14 @@ def _worker(rank, world, port, steps, out, update_period, shard=0):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from cxxnet_amd.io.data import DataBatch
     B = 8
-    tr = _make(B, [("update_period", str(update_period)), ("update_on_server", str(shard))])
+    extra = [("update_period", str(update_period))]
+    if shard == 2:  # fullc_gather on both fc layers instead of sharding
+        extra += [("fullc_gather", "1")]
+    else:
+        extra += [("update_on_server", str(shard))]
+    tr = _make(B, extra)
+    if shard == 2:
+        assert sum(getattr(s, "no_reduce", False) for _, s in tr.net.arena.specs) == 2
     if rank == 1:
         # different local init: the rank-0 broadcast must overwrite it
         pass
@@ -84,9 +91,10 @@ def _worker(rank, world, port, steps, out, update_period, shard=0):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("update_period,shard", [(1, 0), (2, 0), (1, 1), (2, 1)])
+@pytest.mark.parametrize("update_period,shard", [(1, 0), (2, 0), (1, 1), (2, 1), (1, 2), (2, 2)])
 def test_dp_two_ranks_equals_single_process(tmp_path, update_period, shard):
-    """shard=1: update_on_server (reduce-scatter, sliced update, all-gather)."""
+    """shard=1: update_on_server (reduce-scatter, sliced update, all-gather);
+    shard=2: fullc_gather (fc weight gradients from all-gathered activations)."""
     from cxxnet_amd.io.data import DataBatch
     steps = 4
     out = str(tmp_path / "dp.pt")
