@@ -55,6 +55,7 @@ struct Epilogue {
   long bias_gstride;
   int relu;
   int mask_relu;      // bf16 out: keep a value only where the OLD output value is > 0
+  long kstride;       // EPI_F32 with split-K: K-slice s writes its own slab at out + s*kstride
 };
 
 template <int MODE>
@@ -427,6 +428,7 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
     }
   } else {
     float *out = reinterpret_cast<float *>(E.out) + g * E.gstride;
+    if constexpr (EPI == EPI_F32) out += blockIdx.y * E.kstride;
     constexpr int LPR = WM;            // one fp32 per lane
     constexpr int RPI = 64 / LPR;
     const int il = lane % LPR;
@@ -494,6 +496,7 @@ int dispatch(const GemmArgs &g, const Operand &A, const Operand &B, const Epilog
   CXN_CASES_FC(DIRECT_K, DIRECT_K, EPI_F32)
   CXN_CASES_FC(DIRECT_K, DIRECT_K, EPI_F32_ATOMIC)
   CXN_CASES_FC(DIRECT_MN, DIRECT_K, EPI_BF16)
+  CXN_CASES_FC(DIRECT_MN, DIRECT_K, EPI_F32)
   CXN_CASES_FC(DIRECT_MN, DIRECT_K, EPI_F32_ATOMIC)
   CXN_CASES_FC(DIRECT_MN, DIRECT_MN, EPI_F32_ACC)
   CXN_CASES_FC(DIRECT_MN, DIRECT_MN, EPI_F32)
@@ -554,12 +557,13 @@ static Operand to_operand(const CxnOperand &o, int mode, int vec) {
 
 CXN_API int cxn_gemm(const CxnOperand *a, const CxnOperand *b, int amode, int bmode, int va, int vb,
                      void *out, long out_gstride, int ldc, float alpha, const float *bias, long bias_gstride,
-                     int relu, int mask_relu, int epi, int tile, int groups, int ksplit, void *stream) {
+                     int relu, int mask_relu, int epi, int tile, int groups, int ksplit, long kstride,
+                     void *stream) {
   GemmArgs g{amode, bmode, va, vb, epi, tile, groups < 1 ? 1 : groups, ksplit < 1 ? 1 : ksplit};
   Operand A = to_operand(*a, amode, va), B = to_operand(*b, bmode, vb);
   if (A.kdim != B.kdim) return -2;
   if (A.rows <= 0 || B.rows <= 0 || A.kdim <= 0) return 0;
-  Epilogue E{out, out_gstride, ldc, alpha, bias, bias_gstride, relu, mask_relu};
+  Epilogue E{out, out_gstride, ldc, alpha, bias, bias_gstride, relu, mask_relu, kstride};
   hipStream_t s = static_cast<hipStream_t>(stream);
   int rc = dispatch(g, A, B, E, s);
   if (rc != 0) return rc;

@@ -136,7 +136,10 @@ __global__ void conv_weight_flip(const bf16_t *__restrict__ w, bf16_t *__restric
 }
 
 // ------------------------------------------------------------------ pooling
-// mode: 0 max, 1 sum, 2 avg.  relu: apply relu before max (relu_max_pooling).
+// mode: 0 max, 1 sum, 2 avg.  relu bit 0: apply relu before max (relu_max_pooling);
+// relu bit 1 (max mode, KH*KW < 128): set bit 7 of the recorded offset when the window
+// maximum is <= 0, so the backward can apply relu' of the argmax element without
+// re-reading the (large) input: relu'(x[argmax]) = (max > 0).
 // Output size follows the reference ceil rule: min(Hp - k + s - 1, Hp - 1) / s + 1, Hp = H + 2 pad.
 // Max mode records, per output, the window offset (kh*KW + kw, uint8) of the FIRST maximum.
 template <int VEC>
@@ -169,7 +172,7 @@ __global__ void pool_fwd(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, u
         else v[0] = bf2f(*p);
 #pragma unroll
         for (int e = 0; e < VEC; ++e) {
-          const float a = relu ? fmaxf(v[e], 0.f) : v[e];
+          const float a = (relu & 1) ? fmaxf(v[e], 0.f) : v[e];
           if (mode == 0) {
             if (a > acc[e]) {
               acc[e] = a;
@@ -183,6 +186,9 @@ __global__ void pool_fwd(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, u
     if (mode == 2)
 #pragma unroll
       for (int e = 0; e < VEC; ++e) acc[e] *= inv;
+    if (mode == 0 && (relu & 2))
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) am[e] |= acc[e] > 0.f ? 0u : 0x80u;
     if constexpr (VEC == 8) {
       *reinterpret_cast<uint4 *>(y + idx * VEC) = pack8(acc);
       if (arg)
@@ -198,7 +204,8 @@ __global__ void pool_fwd(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, u
 // Gather-form backward: each input element sums the gradients of the windows that contain
 // it.  Max: the window's recorded first-maximum position receives the gradient (the
 // reference compares values, src/layer/pooling_layer-inl.hpp:55-86, which with bf16
-// activations would hand duplicates to rounding ties).  relu: multiply by relu'(x).
+// activations would hand duplicates to rounding ties).  relu 1: multiply by relu'(x);
+// relu 2 (max mode): relu' is encoded in the offsets (bit 7, see pool_fwd), x is not read.
 template <int VEC>
 __global__ void pool_bwd(const bf16_t *__restrict__ x, const uint8_t *__restrict__ arg, const bf16_t *__restrict__ dy,
                          bf16_t *__restrict__ dx, int N, int H, int W, int C, int Ho, int Wo, int KH, int KW, int S,
@@ -213,7 +220,7 @@ __global__ void pool_bwd(const bf16_t *__restrict__ x, const uint8_t *__restrict
     const int h = t % H;
     const int n = t / H;
     float xv[VEC], g[VEC];
-    if (relu) {
+    if (relu == 1) {
       if constexpr (VEC == 8) unpack8(*reinterpret_cast<const uint4 *>(x + idx * VEC), xv);
       else xv[0] = bf2f(x[idx]);
     }
@@ -248,7 +255,7 @@ __global__ void pool_bwd(const bf16_t *__restrict__ x, const uint8_t *__restrict
           else g[e] += mode == 2 ? gv[e] * inv : gv[e];
         }
       }
-    if (relu)
+    if (relu == 1)
 #pragma unroll
       for (int e = 0; e < VEC; ++e) g[e] = xv[e] > 0.f ? g[e] : 0.f;
     if constexpr (VEC == 8) *reinterpret_cast<uint4 *>(dx + idx * VEC) = pack8(g);
@@ -544,11 +551,21 @@ __global__ void colsum_bf16(const bf16_t *__restrict__ dy, float *__restrict__ d
   const long r1 = min(rows, r0 + rows_per_block);
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (rg < RG) {
-    for (long r = r0 + rg; r < r1; r += RG) {
-      float v[8];
-      unpack8(*reinterpret_cast<const uint4 *>(dy + r * C + cv * 8), v);
+    constexpr int U = 4;  // independent 16-B loads in flight per thread
+    for (long r = r0 + rg; r < r1; r += RG * U) {
+      uint4 q[U];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+      for (int u = 0; u < U; ++u) {
+        const long rr = r + static_cast<long>(u) * RG;
+        q[u] = rr < r1 ? *reinterpret_cast<const uint4 *>(dy + rr * C + cv * 8) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float v[8];
+        unpack8(q[u], v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += v[e];
+      }
     }
   }
   __shared__ float red[NT][9];
@@ -560,6 +577,39 @@ __global__ void colsum_bf16(const bf16_t *__restrict__ dy, float *__restrict__ d
     float s = 0.f;
     for (int g = 0; g < RG; ++g) s += red[g * CB + c][e];
     atomicAdd(db + (blockIdx.y * 64 + c) * 8 + e, s);
+  }
+}
+
+// Split-K finalisation: out[r][c] = epilogue(sum_s ws[s][r][c]) with optional bias[c],
+// relu, and mask_relu (keep where the OLD out value is > 0).  8 columns per thread.
+__global__ void splitk_finalize(const float *__restrict__ ws, int nsplit, long slab, bf16_t *out, long rows,
+                                int cols, const float *__restrict__ bias, int relu, int mask_relu) {
+  const int cv = cols / 8;
+  const long total = rows * cv;
+  for (long idx = grid_stride_start(); idx < total; idx += grid_stride()) {
+    const long r = idx / cv;
+    const int c0 = static_cast<int>(idx - r * cv) * 8;
+    const float *p = ws + r * cols + c0;
+    float f[8];
+    {
+      const float4 a = *reinterpret_cast<const float4 *>(p), b = *reinterpret_cast<const float4 *>(p + 4);
+      f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+    }
+    for (int sidx = 1; sidx < nsplit; ++sidx) {
+      const float4 a = *reinterpret_cast<const float4 *>(p + sidx * slab);
+      const float4 b = *reinterpret_cast<const float4 *>(p + sidx * slab + 4);
+      f[0] += a.x; f[1] += a.y; f[2] += a.z; f[3] += a.w; f[4] += b.x; f[5] += b.y; f[6] += b.z; f[7] += b.w;
+    }
+    bf16_t *dst = out + r * cols + c0;
+    float old[8];
+    if (mask_relu) unpack8(*reinterpret_cast<const uint4 *>(dst), old);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (bias) f[e] += bias[c0 + e];
+      if (relu) f[e] = fmaxf(f[e], 0.f);
+      if (mask_relu && !(old[e] > 0.f)) f[e] = 0.f;
+    }
+    *reinterpret_cast<uint4 *>(dst) = pack8(f);
   }
 }
 
@@ -722,6 +772,13 @@ CXN_API int cxn_colsum(const void *dy, float *db, long rows, int C, void *stream
   const int rpb = 512;
   dim3 grid(cdiv(rows, rpb), cdiv(CV, 64));
   colsum_bf16<<<grid, NT, 0, S_>>>((const bf16_t *)dy, db, rows, C, rpb);
+  RET;
+}
+CXN_API int cxn_splitk_finalize(const float *ws, int nsplit, long slab, void *out, long rows, int cols,
+                                const float *bias, int relu, int mask_relu, void *stream) {
+  if (cols % 8) return -2;
+  splitk_finalize<<<nblocks(rows * (cols / 8)), NT, 0, S_>>>(ws, nsplit, slab, (bf16_t *)out, rows, cols, bias, relu,
+                                                             mask_relu);
   RET;
 }
 CXN_API int cxn_cast_f32_bf16(const float *x, void *y, long n, void *stream) {

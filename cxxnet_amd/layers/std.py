@@ -320,15 +320,23 @@ class PoolingLayer(Layer):
         lp = self.lp
         st = self._state(nodes_out[0]) if is_train else None
         ops.pool_forward(nodes_in[0].data, nodes_out[0].data, st, lp.kernel_height, lp.kernel_width, lp.stride,
-                         lp.pad_y, self.mode, self.relu)
+                         lp.pad_y, self.mode, self.relu, mark_mask=self._mask_in_state())
+
+    def _mask_in_state(self) -> bool:
+        lp = self.lp
+        return (self.ctx.is_gpu and (self.relu or self.grad_mask_relu)
+                and ops.pool_mask_in_state(self.mode, lp.kernel_height, lp.kernel_width))
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
         if not prop_grad:
             return
         lp = self.lp
         x = nodes_in[0].data
+        relu = self.relu or self.grad_mask_relu
+        if relu and self._mask_in_state():
+            relu = 2  # relu' of the argmax was recorded by the forward: no read of x
         ops.pool_backward(x, self.state, nodes_out[0].data, x, lp.kernel_height, lp.kernel_width, lp.stride,
-                          lp.pad_y, self.mode, self.relu or self.grad_mask_relu)
+                          lp.pad_y, self.mode, relu)
 
 
 # ============================================================================ LRN

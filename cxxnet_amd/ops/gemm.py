@@ -107,15 +107,41 @@ def _pick_tile(rows_i, rows_j, groups):
 
 
 def _gemm(a, b, amode, bmode, va, vb, out, out_gstride, ldc, *, alpha=1.0, bias=None, bias_gstride=0,
-          relu=False, mask_relu=False, epi=EPI_BF16, groups=1, ksplit=1, tile=None):
+          relu=False, mask_relu=False, epi=EPI_BF16, groups=1, ksplit=1, tile=None, kstride=0):
     if tile is None:
         tile = _pick_tile(a.rows, b.rows, groups)
     rc = native.kernels().cxn_gemm(
         a, b, amode, bmode, va, vb, out.data_ptr(), out_gstride, ldc, float(alpha),
         bias.data_ptr() if bias is not None else None, bias_gstride, int(relu), int(mask_relu), epi, tile, groups,
-        ksplit,
-        _stream())
+        ksplit, kstride, _stream())
     native.check(rc, "gemm")
+
+
+def _effective_split(kdim, split):
+    """The kernel's own clamp (launch_t): slices of ceil(ktiles/split) k-tiles."""
+    kt = -(-kdim // 64)
+    split = max(1, min(split, kt))
+    per = -(-kt // split)
+    return -(-kt // per)
+
+
+def _gemm_bf16_out(a, b, amode, bmode, out, ldc, *, bias=None, relu=False, mask_relu=False):
+    """out (bf16, [rows_j][ldc]) = epilogue(A . B) for a single-group GEMM, with split-K
+    through fp32 slabs + one finalize pass when the output tile grid is too small to
+    fill the chip (the FC layers at batch 256: 64 tiles of 128x128 for fc6)."""
+    tile = _pick(FC_TILES, a.rows, b.rows, 1, min_blocks=1)
+    split = _auto_split(a.rows, b.rows, 1, a.kdim, tile, min_ktiles=8)
+    if split > 1 and a.kdim >= 2048 and ldc % 8 == 0 and ldc == a.rows:
+        split = _effective_split(a.kdim, split)
+        slab = b.rows * ldc
+        ws = torch.empty((split, slab), dtype=torch.float32, device=out.device)
+        _gemm(a, b, amode, bmode, 8, 8, ws, 0, ldc, epi=EPI_F32, ksplit=split, tile=tile, kstride=slab)
+        native.check(native.kernels().cxn_splitk_finalize(
+            ws.data_ptr(), split, slab, out.data_ptr(), b.rows, ldc,
+            bias.data_ptr() if bias is not None else None, int(relu), int(mask_relu), _stream()), "splitk_finalize")
+        return
+    _gemm(a, b, amode, bmode, 8, 8, out, 0, ldc, bias=bias, relu=relu, mask_relu=mask_relu, epi=EPI_BF16,
+          tile=tile)
 
 
 def _auto_split(rows_i, rows_j, groups, kdim, tile=0, target=2 * NUM_CU, min_ktiles=4):
@@ -224,8 +250,10 @@ def fc_forward(x, w, bias, y, relu=False, out_fp32=False):
     nout = w.shape[0]
     A = _op(w, 0, nin, nout, nin)
     Bo = _op(x, 0, nin, Bn, nin)
-    _gemm(A, Bo, DIRECT_K, DIRECT_K, 8, 8, y, 0, nout, bias=bias, relu=relu,
-          epi=EPI_F32 if out_fp32 else EPI_BF16)
+    if out_fp32:
+        _gemm(A, Bo, DIRECT_K, DIRECT_K, 8, 8, y, 0, nout, bias=bias, relu=relu, epi=EPI_F32)
+    else:
+        _gemm_bf16_out(A, Bo, DIRECT_K, DIRECT_K, y, nout, bias=bias, relu=relu)
 
 
 def fc_backward_data(dy, w, dx, mask_relu=False):
@@ -240,7 +268,7 @@ def fc_backward_data(dy, w, dx, mask_relu=False):
     nin = w.shape[1]
     A = _op(w, 0, nin, nin, nout)
     Bo = _op(dy, 0, nout, Bn, nout)
-    _gemm(A, Bo, DIRECT_MN, DIRECT_K, 8, 8, dx, 0, nin, epi=EPI_BF16, mask_relu=mask_relu)
+    _gemm_bf16_out(A, Bo, DIRECT_MN, DIRECT_K, dx, nin, mask_relu=mask_relu)
 
 
 def fc_backward_weight(x, dy, dw, overwrite=False):

@@ -120,8 +120,10 @@ def _pool_ref(x, KH, KW, S, P, mode, relu, Ho, Wo):
     return out.permute(0, 2, 3, 1), arg
 
 
-def pool_forward(x, y, state, KH, KW, S, P, mode: str, relu=False):
-    """y = pool(x).  state: uint8 [N][Ho][Wo][C] first-max window offsets (max mode, may be None)."""
+def pool_forward(x, y, state, KH, KW, S, P, mode: str, relu=False, mark_mask=False):
+    """y = pool(x).  state: uint8 [N][Ho][Wo][C] first-max window offsets (max mode, may be None).
+    mark_mask (GPU, max mode, window < 128): also record relu'(max) in bit 7 of the
+    offsets so that pool_backward(relu=2) needs no input read."""
     N, H, W, C = x.shape
     Ho, Wo = y.shape[1], y.shape[2]
     m = POOL_MODE[mode]
@@ -133,13 +135,20 @@ def pool_forward(x, y, state, KH, KW, S, P, mode: str, relu=False):
         if state is not None and arg is not None:
             state.copy_(arg)
         return
+    flags = int(bool(relu)) | (2 if (mark_mask and m == 0 and KH * KW < 128 and state is not None) else 0)
     native.check(_k().cxn_pool_fwd(x.data_ptr(), y.data_ptr(),
                                    state.data_ptr() if (state is not None and m == 0) else None,
-                                   N, H, W, C, Ho, Wo, KH, KW, S, P, m, int(relu), _stream()), "pool_fwd")
+                                   N, H, W, C, Ho, Wo, KH, KW, S, P, m, flags, _stream()), "pool_fwd")
+
+
+def pool_mask_in_state(mode: str, KH: int, KW: int) -> bool:
+    """Whether pool_forward(mark_mask=True) encodes relu' in the max offsets."""
+    return POOL_MODE[mode] == 0 and KH * KW < 128
 
 
 def pool_backward(x, state, dy, dx, KH, KW, S, P, mode: str, relu=False):
-    """dx = unpool(dy) (max: to the recorded first maximum); relu: times relu'(x).
+    """dx = unpool(dy) (max: to the recorded first maximum); relu: times relu'(x)
+    (relu=2 on the GPU: relu' from the offsets written by pool_forward(mark_mask=True)).
     dx may alias x (element-local read-before-write)."""
     N, H, W, C = x.shape
     Ho, Wo = dy.shape[1], dy.shape[2]

@@ -111,6 +111,17 @@ def test_fc(B, nin, nout):
     assert relerr(y, y_ref) < 2e-2
     assert relerr(dx, dx_ref) < 2e-2
     assert relerr(dw, dw_ref) < 1e-2
+    # fused relu: forward with relu epilogue, data-grad masked by the stored activation
+    y_ref.copy_(torch.clamp_min(x @ w.t() + b, 0))
+    ops.fc_forward(xd, wd, b.to(DEV), y, relu=True)
+    assert relerr(y, y_ref) < 2e-2
+    act = rnd(B, nin, seed=15).clamp_min(0)
+    dxm_ref = act.clone()
+    ops.fc_backward_data(dy, w, dxm_ref, mask_relu=True)
+    dxm = act.to(DEV, torch.bfloat16)
+    ops.fc_backward_data(dyd, wd, dxm, mask_relu=True)
+    torch.cuda.synchronize()
+    assert relerr(dxm, dxm_ref) < 2e-2
 
 
 @pytest.mark.parametrize("mode,relu,k,s,p,C", [("max", False, 3, 2, 0, 96), ("max", True, 3, 2, 0, 256),
@@ -138,6 +149,32 @@ def test_pool(mode, relu, k, s, p, C):
     if mode == "max":
         # inputs are exact bf16 values, so the first-max positions must agree exactly
         assert torch.equal(st.cpu(), st_ref)
+    assert relerr(dx, dx_ref) < 2e-2
+
+
+@pytest.mark.parametrize("relu_fwd", [False, True])
+def test_pool_mask_in_state(relu_fwd):
+    """Max pool over relu'd (or relu-in-pool) input: relu' encoded in the offsets
+    (bit 7) gives the same gradient as reading x."""
+    N, H, W, C, k, s = 2, 27, 27, 96, 3, 2
+    Ho = ops.pool_out_size(H, k, s, 0)
+    x = rnd(N, H, W, C, seed=21)
+    if not relu_fwd:
+        x = x.clamp_min(0)  # fused conv->relu producer
+    dy = rnd(N, Ho, Ho, C, seed=22)
+    y_ref = torch.empty(N, Ho, Ho, C)
+    st_ref = torch.empty(N, Ho, Ho, C, dtype=torch.uint8)
+    ops.pool_forward(x, y_ref, st_ref, k, k, s, 0, "max", relu_fwd)
+    dx_ref = torch.empty_like(x)
+    ops.pool_backward(x, st_ref, dy, dx_ref, k, k, s, 0, "max", True)
+    xd = x.to(DEV, torch.bfloat16)
+    y = torch.empty(N, Ho, Ho, C, dtype=torch.bfloat16, device=DEV)
+    st = torch.empty(N, Ho, Ho, C, dtype=torch.uint8, device=DEV)
+    ops.pool_forward(xd, y, st, k, k, s, 0, "max", relu_fwd, mark_mask=True)
+    assert (st.cpu() >= 0x80).any()  # some windows are all <= 0
+    dx = torch.empty_like(xd)
+    ops.pool_backward(xd, st, dy.to(DEV, torch.bfloat16), dx, k, k, s, 0, "max", 2)
+    torch.cuda.synchronize()
     assert relerr(dx, dx_ref) < 2e-2
 
 
