@@ -20,6 +20,7 @@
 // Math: v_mfma_f32_16x16x32_bf16, fp32 accumulate, 4 waves (2x2) per 256-thread block,
 // LDS double buffer with register staging (issue-early / write-late), one barrier per K step.
 // Epilogue is staged through LDS so every global store / atomic is a full contiguous row.
+#include <cstdlib>
 #include <type_traits>
 #include "common.h"
 
@@ -263,7 +264,7 @@ constexpr int tile_elems() {
   return KMajorLayout<MODE>::kmajor ? R * (BK + PADK) : BK * (R + PADM);
 }
 
-template <int BM, int BN, int WAVES_M, int AMODE, int BMODE, int VA, int VB, int EPI>
+template <int BM, int BN, int WAVES_M, int AMODE, int BMODE, int VA, int VB, int EPI, int PF>
 __global__ void __launch_bounds__(NT, 2)
 gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int ksplit_tiles, int ktiles_total) {
   constexpr int WAVES_N = 4 / WAVES_M;
@@ -330,23 +331,10 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
 #pragma unroll
     for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  Stage<BM, VA> sa;
-  Stage<BN, VB> sb;
-  load_tile<AMODE, BM, VA>(A, rA, gA, goA, i0, kt_beg * BK, sa, rowA);
-  load_tile<BMODE, BN, VB>(B, rB, gB, goB, j0, kt_beg * BK, sb, rowB);
-  store_tile<AMODE, BM, VA>(As0, sa);
-  store_tile<BMODE, BN, VB>(Bs0, sb);
-  __syncthreads();
-
-  int cur = 0;
-  for (int kt = kt_beg; kt < kt_end; ++kt) {
-    const bool more = kt + 1 < kt_end;
-    if (more) {  // issue next tile's global loads early; they land under this step's MFMAs
-      load_tile<AMODE, BM, VA>(A, rA, gA, goA, i0, (kt + 1) * BK, sa, rowA);
-      load_tile<BMODE, BN, VB>(B, rB, gB, goB, j0, (kt + 1) * BK, sb, rowB);
-    }
-    const bf16_t *as = As0 + cur * A_ELEMS;
-    const bf16_t *bs = Bs0 + cur * B_ELEMS;
+  const bf16_t *const as0 = As0, *const bs0 = Bs0;
+  auto compute = [&](int cur) {
+    const bf16_t *as = as0 + cur * A_ELEMS;
+    const bf16_t *bs = bs0 + cur * B_ELEMS;
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 32) {
       bf16x8 fa[MR], fb[NR];
@@ -360,12 +348,67 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
         for (int n = 0; n < NR; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
     }
-    if (more) {
-      store_tile<AMODE, BM, VA>(As0 + (cur ^ 1) * A_ELEMS, sa);
-      store_tile<BMODE, BN, VB>(Bs0 + (cur ^ 1) * B_ELEMS, sb);
-    }
+  };
+  // k offset for a tile index; past the slice it is pushed beyond kdim, so the loads
+  // become buffer-OOB (no memory traffic) and the loop body stays straight-line.
+  constexpr int KOFF_NONE = 1 << 30;
+  auto koff = [&](int kt) { return kt < kt_end ? kt * BK : KOFF_NONE; };
+
+  if constexpr (PF == 1) {
+    Stage<BM, VA> sa;
+    Stage<BN, VB> sb;
+    load_tile<AMODE, BM, VA>(A, rA, gA, goA, i0, kt_beg * BK, sa, rowA);
+    load_tile<BMODE, BN, VB>(B, rB, gB, goB, j0, kt_beg * BK, sb, rowB);
+    store_tile<AMODE, BM, VA>(As0, sa);
+    store_tile<BMODE, BN, VB>(Bs0, sb);
     __syncthreads();
-    cur ^= 1;
+    int cur = 0;
+    for (int kt = kt_beg; kt < kt_end; ++kt) {
+      const bool more = kt + 1 < kt_end;
+      if (more) {  // issue next tile's global loads early; they land under this step's MFMAs
+        load_tile<AMODE, BM, VA>(A, rA, gA, goA, i0, (kt + 1) * BK, sa, rowA);
+        load_tile<BMODE, BN, VB>(B, rB, gB, goB, j0, (kt + 1) * BK, sb, rowB);
+      }
+      compute(cur);
+      if (more) {
+        store_tile<AMODE, BM, VA>(As0 + (cur ^ 1) * A_ELEMS, sa);
+        store_tile<BMODE, BN, VB>(Bs0 + (cur ^ 1) * B_ELEMS, sb);
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+  } else {
+    // Two register stages: tile t+2's loads are issued while tile t is computed and
+    // tile t+1 (already in registers) waits to be written to the other LDS buffer, so
+    // every global load has two K-steps of MFMA work to land under.
+    Stage<BM, VA> sa0, sa1;
+    Stage<BN, VB> sb0, sb1;
+    load_tile<AMODE, BM, VA>(A, rA, gA, goA, i0, koff(kt_beg), sa0, rowA);
+    load_tile<BMODE, BN, VB>(B, rB, gB, goB, j0, koff(kt_beg), sb0, rowB);
+    load_tile<AMODE, BM, VA>(A, rA, gA, goA, i0, koff(kt_beg + 1), sa1, rowA);
+    load_tile<BMODE, BN, VB>(B, rB, gB, goB, j0, koff(kt_beg + 1), sb1, rowB);
+    store_tile<AMODE, BM, VA>(As0, sa0);
+    store_tile<BMODE, BN, VB>(Bs0, sb0);
+    __syncthreads();
+    for (int kt = kt_beg; kt < kt_end; kt += 2) {
+      load_tile<AMODE, BM, VA>(A, rA, gA, goA, i0, koff(kt + 2), sa0, rowA);
+      load_tile<BMODE, BN, VB>(B, rB, gB, goB, j0, koff(kt + 2), sb0, rowB);
+      compute(0);
+      if (kt + 1 < kt_end) {
+        store_tile<AMODE, BM, VA>(As0 + A_ELEMS, sa1);
+        store_tile<BMODE, BN, VB>(Bs0 + B_ELEMS, sb1);
+      }
+      __syncthreads();
+      if (kt + 1 >= kt_end) break;
+      load_tile<AMODE, BM, VA>(A, rA, gA, goA, i0, koff(kt + 3), sa1, rowA);
+      load_tile<BMODE, BN, VB>(B, rB, gB, goB, j0, koff(kt + 3), sb1, rowB);
+      compute(1);
+      if (kt + 2 < kt_end) {
+        store_tile<AMODE, BM, VA>(As0, sa0);
+        store_tile<BMODE, BN, VB>(Bs0, sb0);
+      }
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: stage the wave's fp32 tile in LDS as [j][i], then write full rows
@@ -459,6 +502,16 @@ struct GemmArgs {
   int ksplit;  // number of K splits (>=1)
 };
 
+// Global-load prefetch depth of the K loop (1: one tile ahead, 2: two tiles ahead).
+// CXXNET_GEMM_PF overrides the default; read once.
+int gemm_prefetch_depth() {
+  static const int d = [] {
+    const char *e = std::getenv("CXXNET_GEMM_PF");
+    return (e && e[0] == '1') ? 1 : 2;
+  }();
+  return d;
+}
+
 template <int BM, int BN, int WMs, int AM, int BMo, int VA, int VB, int EPI>
 void launch_t(const Operand &A, const Operand &B, const Epilogue &E, int groups, int ksplit, hipStream_t s) {
   const int ti = cdiv(A.rows, BM), tj = cdiv(B.rows, BN);
@@ -468,8 +521,12 @@ void launch_t(const Operand &A, const Operand &B, const Epilogue &E, int groups,
   const int per = cdiv(ktiles, ksplit);
   ksplit = cdiv(ktiles, per);
   dim3 grid(ti * tj, ksplit, groups);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, WMs, AM, BMo, VA, VB, EPI>), grid, dim3(NT), 0, s, A, B, E, ti, tj, per,
-                     ktiles);
+  if (gemm_prefetch_depth() == 1)
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, WMs, AM, BMo, VA, VB, EPI, 1>), grid, dim3(NT), 0, s, A, B, E, ti, tj,
+                       per, ktiles);
+  else
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, WMs, AM, BMo, VA, VB, EPI, 2>), grid, dim3(NT), 0, s, A, B, E, ti, tj,
+                       per, ktiles);
 }
 
 // Tile ids (BM x BN, waves along M x N):
