@@ -7,8 +7,11 @@ For N > 1 run under torchrun (one process per GPU, RCCL over xGMI).
 Weak scaling: every GPU trains on a fixed per-GPU batch of 256 images (the conf's
 batch size), so the global batch is 256*N.  Data is synthetic 3x227x227 batches
 resident on the device with random-init weights (no dataset / checkpoint on the box).
-A step is the full training step: input layout conversion, forward, loss gradient,
-backward, gradient all-reduce (N > 1) and the fused SGD-momentum update.
+By default they are uint8 HWC images -- what the imgbin/img pipeline hands over after
+JPEG decode and crop -- normalised (mean subtraction) and converted to NHWC bf16 by the
+fused augment kernel inside the step; --input f32 feeds float NCHW batches instead.
+A step is the full training step: input normalisation/layout conversion, forward, loss
+gradient, backward, gradient all-reduce (N > 1) and the fused SGD-momentum update.
 """
 import argparse
 import json
@@ -41,7 +44,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     ap.add_argument("--model", default="alexnet")
-    ap.add_argument("--graph", type=int, default=-1, help="capture the step in a HIP graph (1/0; -1 auto)")
+    ap.add_argument("--input", default="u8", choices=["u8", "f32"],
+                    help="u8: decoded-image batches (uint8 HWC) normalised on the GPU by the fused augment kernel, "
+                         "as the imgbin pipeline delivers them; f32: float NCHW batches")
     a = ap.parse_args()
 
     from cxxnet_amd.models import load_conf
@@ -66,7 +71,17 @@ def main():
     tr.init_model()
     c, h, w = tr.net_cfg.input_shape
     g = torch.Generator(device="cpu").manual_seed(1234 + rank)
-    data = torch.randn(a.batch, c, h, w, generator=g).to(dev)
+    if a.input == "u8":
+        from cxxnet_amd.io.data import U8Images
+        pix = torch.randint(0, 256, (a.batch, h, w, c), generator=g, dtype=torch.uint8).to(dev)
+        prm = torch.zeros((a.batch, 4), dtype=torch.int32, device=dev)
+        cm = torch.tensor([[1.0, 0.0]] * a.batch, device=dev)
+        mean = torch.tensor([123.68, 116.78, 103.94][:c], device=dev)  # mean_value subtraction (ImageNet RGB)
+        data = U8Images(pix, prm, cm, mean, 1, 1.0)
+        desc = f"synthetic uint8 {c}x{h}x{w} images on device, mean subtraction fused on GPU; random-init weights"
+    else:
+        data = torch.randn(a.batch, c, h, w, generator=g).to(dev)
+        desc = f"synthetic fp32 {c}x{h}x{w} batches on device; random-init weights"
     label = torch.randint(0, 1000, (a.batch, 1), generator=g).float().to(dev)
     batch = DataBatch(data, label)
 
@@ -96,7 +111,7 @@ def main():
             "value": round(value, 1), "unit": "images/sec", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(value / (base * world), 3) if base else None,
-            "dtype": "bf16", "data": "synthetic (3x227x227 on-device batches, random-init weights)",
+            "dtype": "bf16", "data": desc,
             "config": {"model": a.model, "global_batch": global_batch, "per_gpu_batch": a.batch,
                        "seq_len": None, "parallelism": f"dp{world}", "input_shape": [c, h, w]},
         }

@@ -33,6 +33,14 @@ __global__ void nchw_f32_to_nhwc_bf16(const float *__restrict__ x, bf16_t *__res
     const long hw = pix - n * H * W;
     const float *src = x + n * C * H * W + hw;
     bf16_t *dst = y + pix * Cp;
+    if (Cp == 4) {
+      float v[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = c < C ? src[static_cast<long>(c) * H * W] * scale : 0.f;
+      *reinterpret_cast<uint2 *>(dst) = make_uint2(static_cast<uint32_t>(f2bf(v[0])) | static_cast<uint32_t>(f2bf(v[1])) << 16,
+                                                   static_cast<uint32_t>(f2bf(v[2])) | static_cast<uint32_t>(f2bf(v[3])) << 16);
+      continue;
+    }
     for (int c = 0; c < Cp; ++c) dst[c] = c < C ? f2bf(src[static_cast<long>(c) * H * W] * scale) : 0;
   }
 }
@@ -52,40 +60,73 @@ __global__ void image_u8_to_nhwc_bf16(const uint8_t *__restrict__ pix, const int
                                       const float *__restrict__ cm, const float *__restrict__ mean, int B, int h,
                                       int w, int C, int Cp, int Hm, int Wm, int mode, float scale,
                                       bf16_t *__restrict__ y) {
-  const long total = static_cast<long>(B) * h * w;
-  for (long p = grid_stride_start(); p < total; p += grid_stride()) {
-    const int x = static_cast<int>(p % w);
-    const long t = p / w;
-    const int r = static_cast<int>(t % h);
-    const int b = static_cast<int>(t / h);
-    const uint8_t *src = pix + p * C;
-    bf16_t *dst = y + p * Cp;
-    float ct = 1.f, il = 0.f;
-    if (mode != 0) {
-      ct = cm[2 * b];
-      il = cm[2 * b + 1];
-    }
-    for (int c = 0; c < Cp; ++c) {
-      float v = 0.f;
-      if (c < C) {
-        const float d = static_cast<float>(src[c]);
-        if (mode == 0) {
-          v = d * scale;
-        } else {
-          float m;
-          if (mode == 1) {
-            m = mean[c];
-          } else if (mode == 2) {
-            const int xs = prm[4 * b + 2] ? (w - 1 - x) : x;
-            m = mean[(static_cast<long>(c) * Hm + prm[4 * b] + r) * Wm + prm[4 * b + 1] + xs];
-          } else {
-            m = mean[(static_cast<long>(c) * h + r) * w + x];
-          }
-          v = ((d - m) * ct + il) * scale;
-        }
+  // grid: x over blockIdx.x*NT + tid, one image row (b, r) per blockIdx.y: no per-pixel division
+  const int row = blockIdx.y;
+  const int b = row / h, r = row - b * h;
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= w) return;
+  const long p = static_cast<long>(row) * w + x;
+  const uint8_t *src = pix + p * C;
+  float ct = 1.f, il = 0.f;
+  if (mode != 0) {
+    ct = cm[2 * b];
+    il = cm[2 * b + 1];
+  }
+  const int xs = (mode == 2 && prm[4 * b + 2]) ? (w - 1 - x) : x;
+  float v[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    v[c] = 0.f;
+    if (c < C && c < Cp) {
+      const float d = static_cast<float>(src[c]);
+      if (mode == 0) {
+        v[c] = d * scale;
+      } else {
+        float m;
+        if (mode == 1) m = mean[c];
+        else if (mode == 2) m = mean[(static_cast<long>(c) * Hm + prm[4 * b] + r) * Wm + prm[4 * b + 1] + xs];
+        else m = mean[(static_cast<long>(c) * h + r) * w + x];
+        v[c] = ((d - m) * ct + il) * scale;
       }
-      dst[c] = f2bf(v);
     }
+  }
+  bf16_t *dst = y + p * Cp;
+  if (Cp == 4) {  // one 8-byte store per pixel
+    *reinterpret_cast<uint2 *>(dst) = make_uint2(static_cast<uint32_t>(f2bf(v[0])) | static_cast<uint32_t>(f2bf(v[1])) << 16,
+                                                 static_cast<uint32_t>(f2bf(v[2])) | static_cast<uint32_t>(f2bf(v[3])) << 16);
+  } else {
+    for (int c = 0; c < Cp; ++c) dst[c] = c < 8 ? f2bf(v[c]) : static_cast<bf16_t>(0);
+  }
+}
+
+// Fast path of the above for the common case: C = 3, Cp = 4, mode 0/1, pixel count a
+// multiple of 4.  Four pixels per thread: three aligned 4-byte loads, two 16-byte stores.
+__global__ void image_u8c3_nhwc4(const uint32_t *__restrict__ pix, const float *__restrict__ cm,
+                                 const float *__restrict__ mean, long quads, FastDiv fd_hw, int mode, float scale,
+                                 uint4 *__restrict__ y) {
+  for (long q = grid_stride_start(); q < quads; q += grid_stride()) {
+    const uint32_t w0 = pix[3 * q], w1 = pix[3 * q + 1], w2 = pix[3 * q + 2];
+    const uint32_t bytes[3] = {w0, w1, w2};
+    float out[16];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t p = static_cast<uint32_t>(4 * q + k);
+      float ct = 1.f, il = 0.f;
+      if (mode == 1) {
+        const uint32_t b = fdiv(p, fd_hw);
+        ct = cm[2 * b];
+        il = cm[2 * b + 1];
+      }
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int byte = 3 * k + c;
+        const float d = static_cast<float>((bytes[byte >> 2] >> (8 * (byte & 3))) & 0xffu);
+        out[4 * k + c] = mode == 1 ? ((d - mean[c]) * ct + il) * scale : d * scale;
+      }
+      out[4 * k + 3] = 0.f;
+    }
+    y[2 * q] = pack8(out);
+    y[2 * q + 1] = pack8(out + 8);
   }
 }
 
@@ -206,13 +247,19 @@ __global__ void pool_fwd(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, u
 // reference compares values, src/layer/pooling_layer-inl.hpp:55-86, which with bf16
 // activations would hand duplicates to rounding ties).  relu 1: multiply by relu'(x);
 // relu 2 (max mode): relu' is encoded in the offsets (bit 7, see pool_fwd), x is not read.
+// db (VEC 8 only, nullable): also db[c] += sum over pixels of dx[.][c] -- the bias
+// gradient of the conv that produced x, folded in so that dx is never re-read.  The
+// launch makes gridDim.x*NT a multiple of C/8, so each thread keeps one channel group.
 template <int VEC>
 __global__ void pool_bwd(const bf16_t *__restrict__ x, const uint8_t *__restrict__ arg, const bf16_t *__restrict__ dy,
                          bf16_t *__restrict__ dx, int N, int H, int W, int C, int Ho, int Wo, int KH, int KW, int S,
-                         int P, int mode, int relu) {
+                         int P, int mode, int relu, float *__restrict__ db) {
   const int CV = C / VEC;
   const long total = static_cast<long>(N) * H * W * CV;
   const float inv = 1.0f / (KH * KW);
+  float bsum[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) bsum[e] = 0.f;
   for (long idx = grid_stride_start(); idx < total; idx += grid_stride()) {
     const int cv = idx % CV;
     long t = idx / CV;
@@ -258,10 +305,58 @@ __global__ void pool_bwd(const bf16_t *__restrict__ x, const uint8_t *__restrict
     if (relu == 1)
 #pragma unroll
       for (int e = 0; e < VEC; ++e) g[e] = xv[e] > 0.f ? g[e] : 0.f;
-    if constexpr (VEC == 8) *reinterpret_cast<uint4 *>(dx + idx * VEC) = pack8(g);
-    else dx[idx] = f2bf(g[0]);
+    if constexpr (VEC == 8) {
+      const uint4 packed = pack8(g);
+      *reinterpret_cast<uint4 *>(dx + idx * VEC) = packed;
+      if (db) {  // sum what was stored (bf16-rounded), like a separate pass would
+        float r[8];
+        unpack8(packed, r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bsum[e] += r[e];
+      }
+    } else {
+      dx[idx] = f2bf(g[0]);
+    }
+  }
+  if constexpr (VEC == 8) {
+    if (db) {
+      extern __shared__ float red[];  // [C]
+      for (int c = threadIdx.x; c < C; c += blockDim.x) red[c] = 0.f;
+      __syncthreads();
+      const int cv = static_cast<int>((static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x) % CV);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) atomicAdd(&red[cv * 8 + e], bsum[e]);
+      __syncthreads();
+      // per-block partials (a second kernel sums them): thousands of blocks doing
+      // atomics on the same C addresses serialise in L2
+      for (int c = threadIdx.x; c < C; c += blockDim.x) db[static_cast<long>(blockIdx.x) * C + c] = red[c];
+    }
   }
 }
+
+// db[c] += sum_b part[b][c].  Block = 32 columns x 8 row groups over one chunk of rows
+// (blockIdx.y); one atomic per column per chunk (a few dozen per address).
+__global__ void partials_reduce(const float *__restrict__ part, int nb, int C, float *__restrict__ db) {
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const int rg = threadIdx.x >> 5;
+  const int per = (nb + gridDim.y - 1) / gridDim.y;
+  const int b0 = blockIdx.y * per, b1 = min(nb, b0 + per);
+  float s = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (int b = b0 + rg; b < b1; b += 8) s += part[static_cast<long>(b) * C + c];
+  }
+  __shared__ float red[8][33];
+  red[rg][threadIdx.x & 31] = s;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) t += red[g][threadIdx.x & 31];
+    atomicAdd(db + c, t);
+  }
+}
+static inline dim3 partials_grid(int nb, int C) { return dim3((C + 31) / 32, (nb + 63) / 64); }
 
 // ------------------------------------------------------------------ LRN
 // norm[c] = knorm + alpha/n * sum_{c' in [c-h, c+h] clipped} x[c']^2 ; y = x * norm^-beta
@@ -369,6 +464,104 @@ __global__ void lrn_bwd_lds(const bf16_t *x, const bf16_t *dy, bf16_t *dx, long 
     }
     *reinterpret_cast<uint4 *>(dx + pix * C + c0) = pack8(out);
   }
+}
+
+// Register/shuffle forms: a wave holds floor(64/tpp) whole pixels, tpp = C/8 lanes
+// each with 8 channels; the cross-channel window's halo (<= 4 channels per side)
+// comes from the neighbouring lanes by ds_bpermute (__shfl), so there is no LDS
+// staging and no bank conflicts.  Every lane of the wave executes the shuffles.
+struct LrnLane {
+  long pix;
+  int cv, tpp;
+  bool active;
+};
+__device__ __forceinline__ LrnLane lrn_lane(long npix, int C) {
+  LrnLane r;
+  r.tpp = C / 8;
+  const int ppw = 64 / r.tpp;  // whole pixels per wave
+  const int lane = threadIdx.x & 63;
+  const long wave = (static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int pl = lane / r.tpp;
+  r.cv = lane - pl * r.tpp;
+  r.pix = wave * ppw + pl;
+  r.active = pl < ppw && r.pix < npix;
+  return r;
+}
+// window sum over channels c-h..c+h of v (8 per lane), halo from neighbours
+template <int H>
+__device__ __forceinline__ void lrn_window_sum(const float *v, const LrnLane &L, float *out) {
+  const int lane = threadIdx.x & 63;
+  float lo[4], hi[4];  // lo[j] = channel c0-1-j (left lane), hi[j] = channel c0+8+j (right lane)
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+    const float l = __shfl(v[7 - j], lane - 1);
+    const float r = __shfl(v[j], lane + 1);
+    lo[j] = L.cv > 0 ? l : 0.f;
+    hi[j] = L.cv < L.tpp - 1 ? r : 0.f;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float s = 0.f;
+#pragma unroll
+    for (int d = -H; d <= H; ++d) {
+      const int q = e + d;
+      s += q < 0 ? lo[-q - 1] : (q > 7 ? hi[q - 8] : v[q]);
+    }
+    out[e] = s;
+  }
+}
+
+template <int H>
+__global__ void lrn_fwd_shfl(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, long npix, int C, float salpha,
+                             float beta, float knorm) {
+  const LrnLane L = lrn_lane(npix, C);
+  const long off = L.pix * C + L.cv * 8;
+  float xv[8], sq[8], s[8];
+  if (L.active) unpack8(*reinterpret_cast<const uint4 *>(x + off), xv);
+  else
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xv[e] = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sq[e] = xv[e] * xv[e];
+  lrn_window_sum<H>(sq, L, s);
+  if (!L.active) return;
+  float out[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) out[e] = xv[e] * exp2f(-beta * __log2f(knorm + salpha * s[e]));
+  *reinterpret_cast<uint4 *>(y + off) = pack8(out);
+}
+
+// dx may alias x (each lane reads its x/g before any write; the halo comes by shuffle).
+template <int H>
+__global__ void lrn_bwd_shfl(const bf16_t *x, const bf16_t *__restrict__ dy, bf16_t *dx, long npix, int C,
+                             float salpha, float beta, float knorm) {
+  const LrnLane L = lrn_lane(npix, C);
+  const long off = L.pix * C + L.cv * 8;
+  float xv[8], gv[8], sq[8], s[8];
+  if (L.active) {
+    unpack8(*reinterpret_cast<const uint4 *>(x + off), xv);
+    unpack8(*reinterpret_cast<const uint4 *>(dy + off), gv);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xv[e] = gv[e] = 0.f;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sq[e] = xv[e] * xv[e];
+  lrn_window_sum<H>(sq, L, s);
+  float ng[8], t[8], ts[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float lg = __log2f(knorm + salpha * s[e]);
+    const float p = exp2f(-beta * lg);  // norm^-b
+    ng[e] = gv[e] * p;
+    t[e] = gv[e] * xv[e] * p * exp2f(-lg);  // g x norm^(-b-1)
+  }
+  lrn_window_sum<H>(t, L, ts);
+  if (!L.active) return;
+  float out[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) out[e] = ng[e] - 2.f * beta * salpha * xv[e] * ts[e];
+  *reinterpret_cast<uint4 *>(dx + off) = pack8(out);
 }
 
 __global__ void lrn_bwd(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, bf16_t *__restrict__ dx,
@@ -539,7 +732,7 @@ __global__ void loss_grad(const float *__restrict__ p32, bf16_t *__restrict__ no
 // ------------------------------------------------------------------ bias gradient
 // db[c] += sum_r dy[r][c]  (dy bf16 [rows][C], C % 8 == 0).  Block = CB column-vectors x RG row
 // groups; per-thread fp32 partials, LDS tree over RG, one atomic per channel per block.
-__global__ void colsum_bf16(const bf16_t *__restrict__ dy, float *__restrict__ db, long rows, int C,
+__global__ void colsum_bf16(const bf16_t *__restrict__ dy, float *__restrict__ part, long rows, int C,
                             int rows_per_block) {
   const int CV = C / 8;
   const int CB = min(CV - static_cast<int>(blockIdx.y) * 64, 64);
@@ -576,7 +769,7 @@ __global__ void colsum_bf16(const bf16_t *__restrict__ dy, float *__restrict__ d
     const int c = q / 8, e = q % 8;
     float s = 0.f;
     for (int g = 0; g < RG; ++g) s += red[g * CB + c][e];
-    atomicAdd(db + (blockIdx.y * 64 + c) * 8 + e, s);
+    part[static_cast<long>(blockIdx.x) * C + (blockIdx.y * 64 + c) * 8 + e] = s;  // reduced by partials_reduce
   }
 }
 
@@ -670,8 +863,18 @@ CXN_API int cxn_image_u8_to_nhwc_bf16(const void *pix, const int *prm, const flo
                                       void *stream) {
   if (Cp < C || (mode != 0 && cm == nullptr) || (mode >= 1 && mean == nullptr) || (mode == 2 && prm == nullptr))
     return -2;
-  image_u8_to_nhwc_bf16<<<nblocks(static_cast<long>(B) * h * w), NT, 0, S_>>>(
-      (const uint8_t *)pix, prm, cm, mean, B, h, w, C, Cp, Hm, Wm, mode, scale, (bf16_t *)y);
+  if (C > 8) return -2;
+  const long npix = static_cast<long>(B) * h * w;
+  if (C == 3 && Cp == 4 && mode <= 1 && npix % 4 == 0 && npix < (1L << 32) &&
+      reinterpret_cast<uintptr_t>(pix) % 4 == 0) {
+    image_u8c3_nhwc4<<<nblocks(npix / 4), NT, 0, S_>>>((const uint32_t *)pix, cm, mean, npix / 4,
+                                                        make_fastdiv(static_cast<uint32_t>(h * w)), mode, scale,
+                                                        (uint4 *)y);
+    RET;
+  }
+  dim3 grid(cdiv(w, NT), B * h);
+  image_u8_to_nhwc_bf16<<<grid, NT, 0, S_>>>((const uint8_t *)pix, prm, cm, mean, B, h, w, C, Cp, Hm, Wm, mode, scale,
+                                             (bf16_t *)y);
   RET;
 }
 CXN_API int cxn_nhwc_bf16_to_nchw_f32(const void *x, float *y, int N, int C, int H, int W, int Cp, void *stream) {
@@ -700,21 +903,50 @@ CXN_API int cxn_pool_fwd(const void *x, void *y, void *arg, int N, int H, int W,
   RET;
 }
 CXN_API int cxn_pool_bwd(const void *x, const void *arg, const void *dy, void *dx, int N, int H, int W, int C, int Ho,
-                         int Wo, int KH, int KW, int S, int P, int mode, int relu, void *stream) {
+                         int Wo, int KH, int KW, int S, int P, int mode, int relu, float *db, float *ws,
+                         long ws_elems, void *stream) {
   if (C % 8 == 0) {
-    pool_bwd<8><<<nblocks(static_cast<long>(N) * H * W * C / 8), NT, 0, S_>>>(
-        (const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, N, H, W, C, Ho, Wo, KH, KW, S, P, mode,
-        relu);
+    const long total = static_cast<long>(N) * H * W * C / 8;
+    int nb = nblocks(total);
+    size_t shm = 0;
+    if (db) {  // gridDim*NT must be a multiple of C/8 (fixed channel group per thread)
+      const int cv = C / 8;
+      int gcd = cv, b = NT;
+      while (b) { const int t = gcd % b; gcd = b; b = t; }
+      const int m = cv / gcd;
+      nb = nb / m * m;
+      if (nb < m) nb = m;
+      shm = static_cast<size_t>(C) * sizeof(float);
+    }
+    if (db && (ws == nullptr || ws_elems < static_cast<long>(nb) * C)) return -2;
+    pool_bwd<8><<<nb, NT, shm, S_>>>((const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, N, H,
+                                     W, C, Ho, Wo, KH, KW, S, P, mode, relu, db ? ws : nullptr);
+    if (db) partials_reduce<<<partials_grid(nb, C), NT, 0, S_>>>(ws, nb, C, db);
   } else {
+    if (db) return -2;
     pool_bwd<1><<<nblocks(static_cast<long>(N) * H * W * C), NT, 0, S_>>>(
-        (const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, N, H, W, C, Ho, Wo, KH, KW, S, P, mode,
-        relu);
+        (const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, N, H, W, C, Ho, Wo, KH, KW, S, P,
+        mode, relu, nullptr);
   }
   RET;
 }
 CXN_API int cxn_lrn_fwd(const void *x, void *y, long npix, int C, int nsize, float alpha, float beta, float knorm,
                         void *stream) {
   if (C % 8 != 0 || nsize / 2 > 4) return -1;
+  const int tpp = C / 8;
+  if (tpp <= 64) {  // shuffle form
+    const long waves = (npix + 64 / tpp - 1) / (64 / tpp);
+    const int blocks = static_cast<int>((waves + NT / 64 - 1) / (NT / 64));
+    const float sa = alpha / nsize;
+    switch (nsize / 2) {
+      case 0: lrn_fwd_shfl<0><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, npix, C, sa, beta, knorm); break;
+      case 1: lrn_fwd_shfl<1><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, npix, C, sa, beta, knorm); break;
+      case 2: lrn_fwd_shfl<2><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, npix, C, sa, beta, knorm); break;
+      case 3: lrn_fwd_shfl<3><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, npix, C, sa, beta, knorm); break;
+      default: lrn_fwd_shfl<4><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, npix, C, sa, beta, knorm); break;
+    }
+    RET;
+  }
   lrn_fwd<<<nblocks(npix * C / 8), NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, npix, C, nsize / 2, alpha / nsize,
                                                  beta, knorm);
   RET;
@@ -724,6 +956,19 @@ CXN_API int cxn_lrn_bwd(const void *x, const void *dy, void *dx, long npix, int 
   if (C % 8 != 0) return -1;
   const int half = nsize / 2;
   const int tpp = C / 8;  // threads per pixel
+  if (tpp <= 64 && half <= 4) {  // shuffle form: whole pixels per wave
+    const long waves = (npix + 64 / tpp - 1) / (64 / tpp);
+    const int blocks = static_cast<int>((waves + NT / 64 - 1) / (NT / 64));
+    const float sa = alpha / nsize;
+    switch (half) {
+      case 0: lrn_bwd_shfl<0><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm); break;
+      case 1: lrn_bwd_shfl<1><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm); break;
+      case 2: lrn_bwd_shfl<2><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm); break;
+      case 3: lrn_bwd_shfl<3><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm); break;
+      default: lrn_bwd_shfl<4><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm); break;
+    }
+    RET;
+  }
   if (tpp <= NT && (C + 2 * half) * 3 * 4 * (NT / tpp) <= 48 * 1024) {
     // LDS-staged form: each pixel row is read once, norm computed once per channel,
     // and dx may alias x (all reads of a pixel complete before its first write).
@@ -763,15 +1008,19 @@ CXN_API int cxn_loss_grad(const float *p32, void *node, const float *label, int 
   loss_grad<<<nblocks(static_cast<long>(rows) * K), NT, 0, S_>>>(p32, (bf16_t *)node, label, rows, K, lw, scale, kind);
   RET;
 }
-CXN_API int cxn_colsum(const void *dy, float *db, long rows, int C, void *stream) {
+CXN_API int cxn_colsum(const void *dy, float *db, long rows, int C, float *ws, long ws_elems, void *stream) {
   if (C % 8) {
     colsum_scalar<<<cdiv(C, NT), NT, 0, S_>>>((const bf16_t *)dy, db, rows, C);
     RET;
   }
   const int CV = C / 8;
-  const int rpb = 512;
+  int rpb = 512;
+  // keep the partials within the caller's workspace
+  while (static_cast<long>(cdiv(rows, rpb)) * C > ws_elems && rpb < (1 << 24)) rpb *= 2;
+  if (static_cast<long>(cdiv(rows, rpb)) * C > ws_elems) return -2;
   dim3 grid(cdiv(rows, rpb), cdiv(CV, 64));
-  colsum_bf16<<<grid, NT, 0, S_>>>((const bf16_t *)dy, db, rows, C, rpb);
+  colsum_bf16<<<grid, NT, 0, S_>>>((const bf16_t *)dy, ws, rows, C, rpb);
+  partials_reduce<<<partials_grid(static_cast<int>(grid.x), C), NT, 0, S_>>>(ws, static_cast<int>(grid.x), C, db);
   RET;
 }
 CXN_API int cxn_splitk_finalize(const float *ws, int nsplit, long slab, void *out, long rows, int cols,

@@ -108,7 +108,8 @@ class SyntheticIterator(DataIterator):
     """`iter = synthetic` -- fixed random batches resident on the target device.
 
     Keys: input_shape=c,h,w, batch_size, num_class (labels uniform in [0,num_class)),
-    num_batch (batches per round, default 100), synthetic_device=gpu|cpu, label_width.
+    num_batch (batches per round, default 100), synthetic_device=gpu|cpu, label_width,
+    synthetic_dtype=float32|uint8 (uint8: decoded-image batches normalised on the device).
     """
 
     def __init__(self):
@@ -135,10 +136,25 @@ class SyntheticIterator(DataIterator):
             self.label_width = int(val)
         elif name == "seed_data":
             self.seed = int(val)
+        elif name == "synthetic_dtype":
+            self.dtype = val
 
     def init(self):
         dev = torch.device("cuda") if (self.device == "gpu" and torch.cuda.is_available()) else torch.device("cpu")
         g = torch.Generator(device="cpu").manual_seed(self.seed)
+        if getattr(self, "dtype", "float32") in ("uint8", "u8"):
+            # decoded-image form: uint8 HWC, normalised on the device by the augment kernel
+            from .data import U8Images
+            c, h, w = self.shape
+            B = self.batch_size
+            pix = torch.randint(0, 256, (B, h, w, c), generator=g, dtype=torch.uint8)
+            data = U8Images(pix.to(dev), torch.zeros((B, 4), dtype=torch.int32, device=dev),
+                            torch.tensor([[1.0, 0.0]] * B, device=dev), torch.full((c,), 127.5, device=dev), 1,
+                            1.0 / 64)
+            label = torch.randint(0, self.num_class, (B, self.label_width), generator=g).float()
+            self.batch = DataBatch(data, label.to(dev), np.arange(B, dtype=np.uint32))
+            self.i = 0
+            return
         data = torch.randn((self.batch_size,) + tuple(self.shape), generator=g)
         label = torch.randint(0, self.num_class, (self.batch_size, self.label_width), generator=g).float()
         self.batch = DataBatch(data.to(dev), label.to(dev), np.arange(self.batch_size, dtype=np.uint32))

@@ -72,7 +72,7 @@ _SIGS = {
     "cxn_transpose": [_P, _P, _I, _I, _I, _P],
     "cxn_conv_weight_flip": [_P, _P, _I, _I, _I, _I, _I, _P],
     "cxn_pool_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
-    "cxn_pool_bwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "cxn_pool_bwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _L, _P],
     "cxn_lrn_fwd": [_P, _P, _L, _I, _I, _F, _F, _F, _P],
     "cxn_lrn_bwd": [_P, _P, _P, _L, _I, _I, _F, _F, _F, _P],
     "cxn_act_fwd": [_P, _P, _P, _L, _I, _F, _P],
@@ -80,7 +80,7 @@ _SIGS = {
     "cxn_dropout": [_P, _P, _L, _U, _P, _F, _P],
     "cxn_softmax": [_P, _P, _P, _I, _I, _P],
     "cxn_loss_grad": [_P, _P, _P, _I, _I, _I, _F, _I, _P],
-    "cxn_colsum": [_P, _P, _L, _I, _P],
+    "cxn_colsum": [_P, _P, _L, _I, _P, _L, _P],
     "cxn_cast_f32_bf16": [_P, _P, _L, _P],
     "cxn_add_bf16": [_P, _P, _P, _L, _P],
     "cxn_channel_copy": [_P, _I, _I, _P, _I, _I, _I, _L, _I, _P],

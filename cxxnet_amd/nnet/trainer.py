@@ -9,6 +9,7 @@ Set/GetWeight, CopyModelFrom (finetune copy-by-name), and the model file:
 """
 from __future__ import annotations
 
+import os
 import struct
 from typing import List, Optional, Tuple
 
@@ -53,6 +54,10 @@ class NetTrainer:
         self.comm_dtype = "fp32"
         self.shard_update = 0
         self.test_on_server = 0
+        # overlapped per-bucket optimizer: on by default only under data parallelism
+        # (1 GPU: the memory-bound update just competes with the memory-bound
+        # pool/LRN backward, measured -1.7%)
+        self.overlap_update = int(os.environ.get("CXXNET_OVERLAP_UPDATE", "-1"))
         self.cfg: List[Tuple[str, str]] = []
         self.metric = MetricSet()
         self.train_metric = MetricSet()
@@ -88,6 +93,8 @@ class NetTrainer:
             self.shard_update = int(val)
         elif name == "test_on_server":
             self.test_on_server = int(val)
+        elif name == "overlap_update":
+            self.overlap_update = int(val)
         if name.startswith("metric"):
             import re
             m = re.match(r"metric\[([^,\]]+),([^\]]+)\]", name)
@@ -143,6 +150,9 @@ class NetTrainer:
         self._init_eval_nodes()
         self.reducer = GradReducer(self.net.arena, self.bucket_mb, True, self.comm_dtype,
                                    shard=bool(self.shard_update))
+        if self.overlap_update == 1 or (self.overlap_update == -1 and self.world > 1):
+            net = self.net
+            self.reducer.enable_overlapped_update(lambda ranges: net.update(self.epoch_counter, ranges))
         self.reducer.broadcast_params()
 
     def init_model(self):
@@ -265,7 +275,7 @@ class NetTrainer:
             if self.reducer.shard:
                 net.update(self.epoch_counter, self.reducer.owned_ranges())
                 self.reducer.gather_params()
-            else:
+            elif self.reducer.update_fn is None:
                 net.update(self.epoch_counter)
         else:
             net.backprop(False, first=first)

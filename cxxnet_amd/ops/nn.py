@@ -146,10 +146,12 @@ def pool_mask_in_state(mode: str, KH: int, KW: int) -> bool:
     return POOL_MODE[mode] == 0 and KH * KW < 128
 
 
-def pool_backward(x, state, dy, dx, KH, KW, S, P, mode: str, relu=False):
+def pool_backward(x, state, dy, dx, KH, KW, S, P, mode: str, relu=False, dbias=None):
     """dx = unpool(dy) (max: to the recorded first maximum); relu: times relu'(x)
     (relu=2 on the GPU: relu' from the offsets written by pool_forward(mark_mask=True)).
-    dx may alias x (element-local read-before-write)."""
+    dx may alias x (element-local read-before-write).
+    dbias (fp32 [C], optional): += per-channel sum of dx (the producing conv's bias
+    gradient, computed here instead of in a separate pass over dx)."""
     N, H, W, C = x.shape
     Ho, Wo = dy.shape[1], dy.shape[2]
     m = POOL_MODE[mode]
@@ -172,10 +174,21 @@ def pool_backward(x, state, dy, dx, KH, KW, S, P, mode: str, relu=False):
         if relu:
             g = g * (x > 0).to(g.dtype)
         dx.copy_(g)
+        if dbias is not None:
+            dbias.add_(g.reshape(-1, C).sum(0))
         return
+    if dbias is not None and C % 8:
+        native.check(_k().cxn_pool_bwd(x.data_ptr(), state.data_ptr() if m == 0 else None, dy.data_ptr(),
+                                       dx.data_ptr(), N, H, W, C, Ho, Wo, KH, KW, S, P, m, int(relu), None, None, 0,
+                                       _stream()), "pool_bwd")
+        bias_grad(dx.reshape(-1, C), dbias)
+        return
+    ws = _workspace(4096 * C, x.device) if dbias is not None else None
     native.check(_k().cxn_pool_bwd(x.data_ptr(), state.data_ptr() if m == 0 else None, dy.data_ptr(),
-                                   dx.data_ptr(), N, H, W, C, Ho, Wo, KH, KW, S, P, m, int(relu), _stream()),
-                 "pool_bwd")
+                                   dx.data_ptr(), N, H, W, C, Ho, Wo, KH, KW, S, P, m, int(relu),
+                                   dbias.data_ptr() if dbias is not None else None,
+                                   ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0,
+                                   _stream()), "pool_bwd")
 
 
 # ----------------------------------------------------------------------------- LRN
@@ -329,13 +342,30 @@ def loss_grad(kind: str, node, label, scale: float, p32=None):
 
 
 # ----------------------------------------------------------------------------- reductions / misc
+_WS = {}
+
+
+def _workspace(n: int, device) -> torch.Tensor:
+    """Reusable fp32 scratch (per device) for per-block partial sums; used in stream
+    order on the compute stream only."""
+    key = str(device)
+    t = _WS.get(key)
+    if t is None or t.numel() < n:
+        t = torch.empty(max(n, 1 << 16), dtype=torch.float32, device=device)
+        _WS[key] = t
+    return t
+
+
 def bias_grad(dy2d, db):
     """db[C] += sum over rows of dy2d[rows][C]."""
     if not dy2d.is_cuda:
         db.add_(dy2d.sum(0))
         return
     rows, C = dy2d.shape
-    native.check(_k().cxn_colsum(dy2d.data_ptr(), db.data_ptr(), rows, C, _stream()), "colsum")
+    n = max(4096, -(-rows // 512)) * C
+    ws = _workspace(n, dy2d.device)
+    native.check(_k().cxn_colsum(dy2d.data_ptr(), db.data_ptr(), rows, C, ws.data_ptr(), ws.numel(), _stream()),
+                 "colsum")
 
 
 def cast_to_bf16(src_f32, dst_bf16):

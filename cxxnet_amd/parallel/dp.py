@@ -64,6 +64,9 @@ class GradReducer:
         self.comm_dtype = torch.bfloat16 if comm_dtype == "bf16" else torch.float32
         limit = max(1, int(bucket_mb * (1 << 20) / 4))
         self.buckets: List[Bucket] = []
+        self.update_fn = None      # overlapped per-bucket optimizer (enable_overlapped_update)
+        self.side = None
+        self.extra_ranges = []     # fullc_gather segments: updated after backward
         if self.shard:
             self._shard_buckets(limit)
             return
@@ -71,6 +74,7 @@ class GradReducer:
         for li, spec in arena.specs:  # arena order = reverse layer order
             s, e = spec.offset, spec.offset + spec.numel
             if getattr(spec, "no_reduce", False):  # fullc_gather: gradient is already global
+                self.extra_ranges.append((s, e))
                 if cur_start is not None and cur_end > cur_start:
                     self.buckets.append(Bucket(cur_start, cur_end, cur_li))
                 cur_start, cur_end, cur_li = None, 0, None
@@ -125,9 +129,23 @@ class GradReducer:
         dist.broadcast(self.arena.w, src=src, group=self.group)
         self.arena.sync_shadow()
 
+    def enable_overlapped_update(self, update_fn):
+        """Run the optimizer per bucket on a side stream as soon as the bucket's
+        gradients are final (and, under data parallelism, reduced), so the update of
+        the large fc layers overlaps the conv backward.  The per-bucket optimizer
+        runs after its all-reduce, as the survey's P5 plan puts it: the reference's
+        pull-callback update (async_updater-inl.hpp:200-221).  GPU only, not with
+        the sharded update."""
+        if self.shard or not self.arena.g.is_cuda:
+            return False
+        self.update_fn = update_fn
+        self.side = torch.cuda.Stream(device=self.arena.g.device)
+        return True
+
     def start_step(self):
         for b in self.buckets:
             b.work = None
+            b.ready = False
 
     def _launch(self, b: Bucket):
         g = self.arena.g[b.start:b.end]
@@ -144,21 +162,50 @@ class GradReducer:
             b.buf = g.to(self.comm_dtype)
             b.work = dist.all_reduce(b.buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
+    def _ready(self, b: Bucket):
+        """Bucket b's gradients are final on the compute stream."""
+        b.ready = True
+        if self.active:
+            self._launch(b)
+        if self.update_fn is None:
+            return
+        ev = torch.cuda.current_stream().record_event()
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(ev)
+            if self.active:
+                b.work.wait()  # the side stream waits for the collective
+                if b.buf is not None:
+                    self.arena.g[b.start:b.end].copy_(b.buf)
+                    b.buf.record_stream(self.side)
+                    b.buf = None
+                b.work = None
+            self.update_fn([(b.start, b.end)])
+
     def hook(self, layer_index: int):
         """Called after each layer's backprop (reverse order)."""
-        if not self.active or not self.overlap:
+        if not self.overlap or not (self.active or self.update_fn is not None):
             return
         for b in self.buckets:
-            if b.work is None and layer_index <= b.li_min:
-                self._launch(b)
+            if not getattr(b, "ready", False) and layer_index <= b.li_min:
+                self._ready(b)
 
     def finish(self):
-        """Launch what is left and make the compute stream wait for every reduction."""
+        """Launch what is left and make the compute stream wait for every reduction
+        (and, with the overlapped update, for every bucket's optimizer step)."""
+        if self.update_fn is not None:
+            for b in self.buckets:
+                if not getattr(b, "ready", False):
+                    self._ready(b)
+            torch.cuda.current_stream().wait_stream(self.side)
+            if self.extra_ranges:
+                self.update_fn(self.extra_ranges)
+            return
         if not self.active:
             return
         for b in self.buckets:
             if b.work is None:
                 self._launch(b)
+                b.ready = True
         for b in self.buckets:
             b.work.wait()
             if self.shard:

@@ -173,16 +173,22 @@ def test_pool_mask_in_state(relu_fwd):
     ops.pool_forward(xd, y, st, k, k, s, 0, "max", relu_fwd, mark_mask=True)
     assert (st.cpu() >= 0x80).any()  # some windows are all <= 0
     dx = torch.empty_like(xd)
-    ops.pool_backward(xd, st, dy.to(DEV, torch.bfloat16), dx, k, k, s, 0, "max", 2)
+    db = torch.full((C,), 0.5, device=DEV)
+    ops.pool_backward(xd, st, dy.to(DEV, torch.bfloat16), dx, k, k, s, 0, "max", 2, dbias=db)
     torch.cuda.synchronize()
     assert relerr(dx, dx_ref) < 2e-2
+    # folded bias gradient of the producing conv: 0.5 + column sums of dx
+    assert relerr(db, 0.5 + dx_ref.reshape(-1, C).sum(0)) < 2e-2
 
 
-def test_lrn():
-    N, H, W, C = 2, 13, 13, 96
+@pytest.mark.parametrize("C,nsize", [(96, 5), (256, 5), (40, 3), (64, 9), (1024, 5)])
+def test_lrn(C, nsize):
+    """Shuffle kernels (C <= 512: whole pixels per wave, halo by ds_bpermute; odd pixel
+    count leaves a partial last wave) and the LDS fallback (C = 1024)."""
+    N, H, W = 2, 13, 13
     x = rnd(N, H, W, C, scale=2.0, seed=15)
     dy = rnd(N, H, W, C, seed=16)
-    args = (5, 0.001, 0.75, 1.0)
+    args = (nsize, 0.001, 0.75, 1.0)
     y_ref = torch.empty_like(x)
     ops.lrn_forward(x, y_ref, *args)
     dx_ref = torch.empty_like(x)
@@ -324,3 +330,20 @@ def test_image_u8_to_nhwc(mode):
     got = out.float().cpu()
     assert relerr(got[..., :C], ref) < 1e-2
     assert got[..., C:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_image_u8_fast_path(mode):
+    """C=3 -> Cp=4, 4 pixels per thread (pixel count % 4 == 0), batches straddled by quads."""
+    from cxxnet_amd.io.data import U8Images
+    g = torch.Generator().manual_seed(7 + mode)
+    B, h, w = 4, 9, 7  # 63 pixels per image: quads cross image boundaries
+    pix = torch.randint(0, 256, (B, h, w, 3), generator=g, dtype=torch.uint8)
+    cm = torch.stack([torch.rand(B, generator=g) + 0.5, torch.rand(B, generator=g) * 10 - 5], 1)
+    img = U8Images(pix, torch.zeros((B, 4), dtype=torch.int32), cm, torch.tensor([120.0, 110.0, 100.0]), mode, 0.02)
+    ref = img.to_float().permute(0, 2, 3, 1)
+    out = torch.empty((B, h, w, 4), dtype=torch.bfloat16, device=DEV)
+    ops.image_to_nhwc(img, out)
+    got = out.float().cpu()
+    assert relerr(got[..., :3], ref) < 1e-2
+    assert got[..., 3].abs().max().item() == 0
