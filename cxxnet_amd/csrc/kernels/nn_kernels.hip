@@ -358,6 +358,109 @@ __global__ void partials_reduce(const float *__restrict__ part, int nb, int C, f
 }
 static inline dim3 partials_grid(int nb, int C) { return dim3((C + 31) / 32, (nb + 63) / 64); }
 
+// One-element-per-thread forms of pool_fwd / pool_bwd for C % 8 == 0 and < 2^32
+// elements: the index split is three 32-bit fast divisions (the grid-stride forms above
+// spend most of their issue slots on 64-bit divisions).  Same semantics, including the
+// relu' bit.
+__global__ void pool_fwd_rows(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, uint8_t *__restrict__ arg, int H,
+                              int W, int C, int Ho, int Wo, int KH, int KW, int S, int P, int mode, int relu,
+                              FastDiv fd_cv, FastDiv fd_row, FastDiv fd_h, uint32_t total) {
+  const int CV = C / 8;
+  const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int row = static_cast<int>(fdiv(idx, fd_row));           // n * Ho + ho
+  const int e = static_cast<int>(idx) - row * (Wo * CV);
+  const int n = static_cast<int>(fdiv(static_cast<uint32_t>(row), fd_h)), ho = row - n * Ho;
+  const int wo = static_cast<int>(fdiv(static_cast<uint32_t>(e), fd_cv));
+  const int cv = e - wo * CV;
+  const int hs = ho * S - P, ws = wo * S - P;
+  const int he = min(hs + KH, H), we = min(ws + KW, W);
+  float acc[8];
+  uint32_t am[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    acc[q] = mode == 0 ? -INFINITY : 0.f;
+    am[q] = 0;
+  }
+  const bf16_t *xb = x + static_cast<long>(n) * H * W * C + cv * 8;
+  for (int h = max(hs, 0); h < he; ++h)
+    for (int w = max(ws, 0); w < we; ++w) {
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4 *>(xb + (static_cast<long>(h) * W + w) * C), v);
+      const uint32_t off = static_cast<uint32_t>((h - hs) * KW + (w - ws));
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float a = (relu & 1) ? fmaxf(v[q], 0.f) : v[q];
+        if (mode == 0) {
+          if (a > acc[q]) {
+            acc[q] = a;
+            am[q] = off;
+          }
+        } else {
+          acc[q] += a;
+        }
+      }
+    }
+  if (mode == 2) {
+    const float inv = 1.0f / (KH * KW);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] *= inv;
+  }
+  if (mode == 0 && (relu & 2))
+#pragma unroll
+    for (int q = 0; q < 8; ++q) am[q] |= acc[q] > 0.f ? 0u : 0x80u;
+  const long o = (static_cast<long>(row) * Wo + wo) * C + cv * 8;
+  *reinterpret_cast<uint4 *>(y + o) = pack8(acc);
+  if (arg)
+    *reinterpret_cast<uint2 *>(arg + o) =
+        make_uint2(am[0] | am[1] << 8 | am[2] << 16 | am[3] << 24, am[4] | am[5] << 8 | am[6] << 16 | am[7] << 24);
+}
+
+__global__ void pool_bwd_rows(const bf16_t *__restrict__ x, const uint8_t *__restrict__ arg,
+                              const bf16_t *__restrict__ dy, bf16_t *__restrict__ dx, int H, int W, int C, int Ho,
+                              int Wo, int KH, int KW, int S, int P, int mode, int relu, FastDiv fd_cv,
+                              FastDiv fd_row, FastDiv fd_h, uint32_t total) {
+  const int CV = C / 8;
+  const uint32_t gidx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gidx >= total) return;
+  const int row = static_cast<int>(fdiv(gidx, fd_row));          // n * H + h
+  const int e = static_cast<int>(gidx) - row * (W * CV);
+  const int n = static_cast<int>(fdiv(static_cast<uint32_t>(row), fd_h)), h = row - n * H;
+  const int w = static_cast<int>(fdiv(static_cast<uint32_t>(e), fd_cv));
+  const int cv = e - w * CV;
+  const long idx = (static_cast<long>(row) * W + w) * C + cv * 8;
+  float xv[8], g[8];
+  if (relu == 1) unpack8(*reinterpret_cast<const uint4 *>(x + idx), xv);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) g[q] = 0.f;
+  const int hlo = max(0, (h + P - KH + S) / S), hhi = min(Ho - 1, (h + P) / S);
+  const int wlo = max(0, (w + P - KW + S) / S), whi = min(Wo - 1, (w + P) / S);
+  const float inv = 1.0f / (KH * KW);
+  const long nb = static_cast<long>(n) * Ho;
+  for (int ho = hlo; ho <= hhi; ++ho)
+    for (int wo = wlo; wo <= whi; ++wo) {
+      const long o = ((nb + ho) * Wo + wo) * C + cv * 8;
+      const uint32_t off = static_cast<uint32_t>((h - (ho * S - P)) * KW + (w - (wo * S - P)));
+      float gv[8];
+      unpack8(*reinterpret_cast<const uint4 *>(dy + o), gv);
+      if (mode == 0) {
+        const uint2 a2 = *reinterpret_cast<const uint2 *>(arg + o);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          g[q] += (((a2.x >> (8 * q)) & 0xff) == off) ? gv[q] : 0.f;
+          g[q + 4] += (((a2.y >> (8 * q)) & 0xff) == off) ? gv[q + 4] : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) g[q] += mode == 2 ? gv[q] * inv : gv[q];
+      }
+    }
+  if (relu == 1)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) g[q] = xv[q] > 0.f ? g[q] : 0.f;
+  *reinterpret_cast<uint4 *>(dx + idx) = pack8(g);
+}
+
 // ------------------------------------------------------------------ LRN
 // norm[c] = knorm + alpha/n * sum_{c' in [c-h, c+h] clipped} x[c']^2 ; y = x * norm^-beta
 // One thread per (pixel, 8 channels); halo of up to 8 channels each side via three 16-B loads.
@@ -777,11 +880,11 @@ __global__ void colsum_bf16(const bf16_t *__restrict__ dy, float *__restrict__ p
 // relu, and mask_relu (keep where the OLD out value is > 0).  8 columns per thread.
 __global__ void splitk_finalize(const float *__restrict__ ws, int nsplit, long slab, bf16_t *out, long rows,
                                 int cols, const float *__restrict__ bias, int relu, int mask_relu) {
-  const int cv = cols / 8;
-  const long total = rows * cv;
-  for (long idx = grid_stride_start(); idx < total; idx += grid_stride()) {
-    const long r = idx / cv;
-    const int c0 = static_cast<int>(idx - r * cv) * 8;
+  // grid: blockIdx.y = row, x over 8-column groups (no 64-bit division per element)
+  {
+    const long r = blockIdx.y;
+    const int c0 = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+    if (c0 >= cols) return;
     const float *p = ws + r * cols + c0;
     float f[8];
     {
@@ -894,8 +997,12 @@ CXN_API int cxn_conv_weight_flip(const void *w, void *wt, int G, int Co, int KH,
 CXN_API int cxn_pool_fwd(const void *x, void *y, void *arg, int N, int H, int W, int C, int Ho, int Wo, int KH, int KW, int S,
                          int P, int mode, int relu, void *stream) {
   if (C % 8 == 0) {
-    pool_fwd<8><<<nblocks(static_cast<long>(N) * Ho * Wo * C / 8), NT, 0, S_>>>(
-        (const bf16_t *)x, (bf16_t *)y, (uint8_t *)arg, N, H, W, C, Ho, Wo, KH, KW, S, P, mode, relu);
+    const long total = static_cast<long>(N) * Ho * Wo * (C / 8);
+    if (total >= (1L << 31)) return -2;  // fdiv (mulhi + n) stays exact below 2^31
+    pool_fwd_rows<<<cdiv(total, NT), NT, 0, S_>>>(
+        (const bf16_t *)x, (bf16_t *)y, (uint8_t *)arg, H, W, C, Ho, Wo, KH, KW, S, P, mode, relu,
+        make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(Wo * (C / 8))),
+        make_fastdiv(static_cast<uint32_t>(Ho)), static_cast<uint32_t>(total));
   } else {
     pool_fwd<1><<<nblocks(static_cast<long>(N) * Ho * Wo * C), NT, 0, S_>>>(
         (const bf16_t *)x, (bf16_t *)y, (uint8_t *)arg, N, H, W, C, Ho, Wo, KH, KW, S, P, mode, relu);
@@ -905,6 +1012,15 @@ CXN_API int cxn_pool_fwd(const void *x, void *y, void *arg, int N, int H, int W,
 CXN_API int cxn_pool_bwd(const void *x, const void *arg, const void *dy, void *dx, int N, int H, int W, int C, int Ho,
                          int Wo, int KH, int KW, int S, int P, int mode, int relu, float *db, float *ws,
                          long ws_elems, void *stream) {
+  if (C % 8 == 0 && db == nullptr) {
+    const long total = static_cast<long>(N) * H * W * (C / 8);
+    if (total >= (1L << 31)) return -2;  // fdiv (mulhi + n) stays exact below 2^31
+    pool_bwd_rows<<<cdiv(total, NT), NT, 0, S_>>>(
+        (const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, H, W, C, Ho, Wo, KH, KW, S, P, mode,
+        relu, make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(W * (C / 8))),
+        make_fastdiv(static_cast<uint32_t>(H)), static_cast<uint32_t>(total));
+    RET;
+  }
   if (C % 8 == 0) {
     const long total = static_cast<long>(N) * H * W * C / 8;
     int nb = nblocks(total);
@@ -1026,8 +1142,8 @@ CXN_API int cxn_colsum(const void *dy, float *db, long rows, int C, float *ws, l
 CXN_API int cxn_splitk_finalize(const float *ws, int nsplit, long slab, void *out, long rows, int cols,
                                 const float *bias, int relu, int mask_relu, void *stream) {
   if (cols % 8) return -2;
-  splitk_finalize<<<nblocks(rows * (cols / 8)), NT, 0, S_>>>(ws, nsplit, slab, (bf16_t *)out, rows, cols, bias, relu,
-                                                             mask_relu);
+  dim3 grid(cdiv(cols / 8, NT), static_cast<unsigned>(rows));
+  splitk_finalize<<<grid, NT, 0, S_>>>(ws, nsplit, slab, (bf16_t *)out, rows, cols, bias, relu, mask_relu);
   RET;
 }
 CXN_API int cxn_cast_f32_bf16(const float *x, void *y, long n, void *stream) {
