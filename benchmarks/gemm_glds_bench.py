@@ -1,0 +1,95 @@
+"""A/B the LDS-DMA GEMM (csrc/kernels/gemm_glds.hip) against the register-staged kernel
+(csrc/kernels/gemm_mfma.hip) on every AlexNet (batch 256) GEMM it serves, per tile
+variant, and check that the outputs agree.
+
+  python benchmarks/gemm_glds_bench.py [--iters 20] [--ops conv2_fwd,fc6_fwd] > out.jsonl
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cxxnet_amd import ops  # noqa: E402
+from cxxnet_amd.ops import gemm as G  # noqa: E402
+
+N = 256
+BF = torch.bfloat16
+CONV = {"conv1": (4, 227, 96, 11, 4, 0, 1), "conv2": (96, 27, 256, 5, 1, 2, 2), "conv3": (256, 13, 384, 3, 1, 1, 1),
+        "conv4": (384, 13, 384, 3, 1, 1, 2), "conv5": (384, 13, 256, 3, 1, 1, 2)}
+FC = {"fc6": (9216, 4096), "fc7": (4096, 4096), "fc8": (4096, 1000)}
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1000.0
+
+
+def make(name):
+    layer, kind = name.split("_")
+    g = torch.Generator(device="cuda").manual_seed(0)
+    if layer in FC:
+        nin, nout = FC[layer]
+        x = torch.randn(N, nin, device="cuda", generator=g).to(BF)
+        w = (torch.randn(nout, nin, device="cuda", generator=g) * 0.02).to(BF)
+        b = torch.randn(nout, device="cuda", generator=g) * 0.1
+        y = torch.empty(N, nout, device="cuda", dtype=BF)
+        return (lambda: ops.fc_forward(x, w, b, y, relu=True)), y, 2.0 * N * nin * nout
+    C, H, Cout, K, s, p, grp = CONV[layer]
+    Ho, Wo = G.conv_out_size(H, H, K, K, s, p, p)
+    geo = G.ConvGeom(N, H, H, C, Ho, Wo, Cout, K, K, s, p, p, grp)
+    w = (torch.randn(Cout, K, K, C // grp, device="cuda", generator=g) * 0.05).to(BF)
+    flops = 2.0 * N * Ho * Wo * Cout * (C // grp) * K * K
+    if kind == "fwd":
+        x = torch.randn(N, H, H, C, device="cuda", generator=g).to(BF)
+        b = torch.randn(Cout, device="cuda", generator=g) * 0.1
+        y = torch.empty(N, Ho, Wo, Cout, device="cuda", dtype=BF)
+        return (lambda: ops.conv_forward(x, w, b, y, geo, relu=True)), y, flops
+    dy = torch.randn(N, Ho, Wo, Cout, device="cuda", generator=g).to(BF)
+    dx = torch.empty(N, H, H, C, device="cuda", dtype=BF)
+    wt = torch.empty_like(w)
+    return (lambda: ops.conv_backward_data(dy, w, dx, geo, wt)), dx, flops
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--ops", default="conv2_fwd,conv2_dgrad,conv3_fwd,conv3_dgrad,conv4_fwd,conv4_dgrad,conv5_fwd,"
+                                     "conv5_dgrad,fc6_fwd,fc7_fwd,fc8_fwd")
+    ap.add_argument("--tiles", default="0,1,2,4,5,6")
+    a = ap.parse_args()
+    for name in a.ops.split(","):
+        run, out, flops = make(name)
+        G.set_glds(False)
+        run()
+        torch.cuda.synchronize()
+        ref = out.float().clone()
+        t_old = timeit(run, a.iters)
+        rec = {"op": name, "old_us": round(t_old, 1), "old_tflops": round(flops / t_old / 1e6, 1)}
+        for t in [int(v) for v in a.tiles.split(",")]:
+            G.set_glds(True, t)
+            out.zero_()
+            run()
+            torch.cuda.synchronize()
+            err = ((out.float() - ref).abs().max() / ref.abs().max().clamp_min(1e-6)).item()
+            us = timeit(run, a.iters)
+            rec[f"t{t}_us"] = round(us, 1)
+            rec[f"t{t}_err"] = round(err, 4)
+        G.set_glds(True, -1)
+        rec["auto_us"] = round(timeit(run, a.iters), 1)
+        rec["auto_tflops"] = round(flops / rec["auto_us"] / 1e6, 1)
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

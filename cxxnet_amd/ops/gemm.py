@@ -13,6 +13,7 @@ src/layer/fullc_layer-inl.hpp:101-130.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -102,6 +103,86 @@ def _pick(candidates, rows_i, rows_j, groups, min_blocks=2 * NUM_CU):
     return min(candidates, key=cost)
 
 
+# ----------------------------------------------------------------------------- LDS-DMA kernel
+# gemm_glds.hip: both operands K-major (conv fwd / dgrad, fc fwd), 4 waves, one block per CU.
+GLDS_TILES = {0: (128, 256), 1: (128, 128), 2: (128, 128), 4: (192, 256), 5: (64, 256), 6: (256, 128),
+              7: (64, 128), 8: (192, 128), 9: (96, 128), 10: (128, 64), 11: (64, 128), 12: (64, 128),
+              13: (128, 128), 14: (128, 64), 15: (64, 64), 16: (192, 64)}
+B_DIRECT, B_GATHER = 0, 1
+_glds_cfg = {"on": os.environ.get("CXXNET_GEMM_GLDS", "1") != "0",
+             "tile": int(os.environ.get("CXXNET_GLDS_TILE", "-1")),
+             "tune": os.environ.get("CXXNET_GEMM_TUNE", "1") != "0"}
+# Autotuning candidates: the 2-stage tiles that run 2-5 blocks per CU measured best on every
+# AlexNet shape (profiles/r14_glds_tiles.jsonl); 2 and 0 cover wide-i GEMMs (fc).
+GLDS_CANDS = (1, 7, 10, 15, 2, 0)
+_TUNE = {}
+
+
+def set_glds(on: bool = True, tile: int = -1, tune: bool = True):
+    """Enable/disable the LDS-DMA GEMM path, force its tile, or turn autotuning off."""
+    _glds_cfg.update(on=bool(on), tile=int(tile), tune=bool(tune))
+
+
+def _tuned_tile(key, run, out, default):
+    """Tile for a GEMM signature: the fastest candidate, timed once per process on a
+    scratch output (the first call of each shape pays a few extra launches and one host
+    sync); the heuristic pick when tuning is off or a graph is being captured."""
+    if _glds_cfg["tile"] >= 0:
+        return _glds_cfg["tile"]
+    t = _TUNE.get(key)
+    if t is not None:
+        return t
+    if not _glds_cfg["tune"] or torch.cuda.is_current_stream_capturing():
+        return default()
+    scratch = torch.empty_like(out)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best, best_ms = None, float("inf")
+    for tile in GLDS_CANDS:
+        if not run(tile, scratch):
+            continue
+        ts = []
+        for _ in range(3):
+            s.record()
+            run(tile, scratch)
+            e.record()
+            e.synchronize()
+            ts.append(s.elapsed_time(e))
+        ms = sorted(ts)[1]
+        if ms < best_ms:
+            best, best_ms = tile, ms
+    _TUNE[key] = best if best is not None else default()
+    return _TUNE[key]
+
+
+def _pick_glds(rows_i, rows_j, groups, nblocks_target=NUM_CU):
+    """Padded MFMA work divided by the fraction of the last dispatch wave that is busy
+    (one 4-wave block per CU), then the larger tile."""
+    def cost(t):
+        bm, bn = GLDS_TILES[t]
+        nb = _cdiv(rows_i, bm) * _cdiv(rows_j, bn) * groups
+        padded = _cdiv(rows_i, bm) * bm * _cdiv(rows_j, bn) * bn * groups
+        waves = _cdiv(nb, nblocks_target)
+        return (padded * waves * nblocks_target / nb, -bm * bn, t)
+    return min((1, 7, 10, 15), key=cost)
+
+
+def _glds(a, b, bmode, out, out_gstride, ldc, *, alpha=1.0, bias=None, bias_gstride=0, relu=False,
+          mask_relu=False, epi=EPI_BF16, groups=1, ksplit=1, kstride=0, tile=None) -> bool:
+    """Run the LDS-DMA kernel; False when it does not support the operands (caller falls back)."""
+    if not _glds_cfg["on"]:
+        return False
+    if tile is None:
+        tile = _glds_cfg["tile"] if _glds_cfg["tile"] >= 0 else _pick_glds(a.rows, b.rows, groups)
+    rc = native.kernels().cxn_gemm_glds(
+        a, b, bmode, out.data_ptr(), out_gstride, ldc, float(alpha),
+        bias.data_ptr() if bias is not None else None, bias_gstride, int(relu), int(mask_relu), epi, tile, groups,
+        ksplit, kstride, _stream())
+    if rc == -1:
+        return False
+    native.check(rc, "gemm_glds")
+    return True
+
+
 def _pick_tile(rows_i, rows_j, groups):
     return _pick(FC_TILES, rows_i, rows_j, groups)
 
@@ -129,6 +210,8 @@ def _gemm_bf16_out(a, b, amode, bmode, out, ldc, *, bias=None, relu=False, mask_
     """out (bf16, [rows_j][ldc]) = epilogue(A . B) for a single-group GEMM, with split-K
     through fp32 slabs + one finalize pass when the output tile grid is too small to
     fill the chip (the FC layers at batch 256: 64 tiles of 128x128 for fc6)."""
+    if amode == DIRECT_K and bmode == DIRECT_K and _glds_cfg["on"] and _fc_glds(a, b, out, ldc, bias, relu, mask_relu):
+        return
     tile = _pick(FC_TILES, a.rows, b.rows, 1, min_blocks=1)
     split = _auto_split(a.rows, b.rows, 1, a.kdim, tile, min_ktiles=8)
     if split > 1 and a.kdim >= 2048 and ldc % 8 == 0 and ldc == a.rows:
@@ -142,6 +225,34 @@ def _gemm_bf16_out(a, b, amode, bmode, out, ldc, *, bias=None, relu=False, mask_
         return
     _gemm(a, b, amode, bmode, 8, 8, out, 0, ldc, bias=bias, relu=relu, mask_relu=mask_relu, epi=EPI_BF16,
           tile=tile)
+
+
+def _fc_glds(a, b, out, ldc, bias, relu, mask_relu) -> bool:
+    """fc forward on the LDS-DMA kernel (autotuned tile)."""
+    key = ("fc", a.rows, b.rows, a.kdim, ldc)
+    run = lambda t, o: _fc_glds_tile(a, b, o, ldc, bias, relu, mask_relu, t)  # noqa: E731
+    tile = _tuned_tile(key, run, out, lambda: _pick_glds(a.rows, b.rows, 1))
+    return run(tile, out)
+
+
+def _fc_glds_tile(a, b, out, ldc, bias, relu, mask_relu, tile) -> bool:
+    """split-K through fp32 slabs when the output tile grid cannot fill the chip (fc6 at
+    batch 256: 32 tiles of 128x256)."""
+    bm, bn = GLDS_TILES[tile]
+    tiles = _cdiv(a.rows, bm) * _cdiv(b.rows, bn)
+    ktiles = _cdiv(a.kdim, 64)
+    split = max(1, min(NUM_CU // max(tiles, 1), ktiles // 8))
+    if split > 1 and ldc % 8 == 0 and ldc == a.rows:
+        split = _effective_split(a.kdim, split)
+        slab = b.rows * ldc
+        ws = torch.empty((split, slab), dtype=torch.float32, device=out.device)
+        if not _glds(a, b, B_DIRECT, ws, 0, ldc, epi=EPI_F32, ksplit=split, kstride=slab, tile=tile):
+            return False
+        native.check(native.kernels().cxn_splitk_finalize(
+            ws.data_ptr(), split, slab, out.data_ptr(), b.rows, ldc,
+            bias.data_ptr() if bias is not None else None, int(relu), int(mask_relu), _stream()), "splitk_finalize")
+        return True
+    return _glds(a, b, B_DIRECT, out, 0, ldc, bias=bias, relu=relu, mask_relu=mask_relu, tile=tile)
 
 
 def _auto_split(rows_i, rows_j, groups, kdim, tile=0, target=2 * NUM_CU, min_ktiles=4):
@@ -180,6 +291,12 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
     A = _op(w, g.cg_out * kd, kd, g.cg_out, kd)
     B = _op(x, cg, 0, g.N * g.Ho * g.Wo, kd, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW,
             stride=g.stride, pad_h=g.pad_y, pad_w=g.pad_x, dil=1, Cg=cg)
+    if va == 8 and _glds_cfg["on"]:
+        run = lambda t, o: _glds(A, B, B_GATHER, o, g.cg_out, g.Cout, bias=bias, bias_gstride=g.cg_out,  # noqa: E731
+                                 relu=relu, groups=g.groups, tile=t)
+        key = ("cf", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
+        if run(_tuned_tile(key, run, y, lambda: _pick_glds(A.rows, B.rows, g.groups)), y):
+            return
     tile = _pick(CONV_FWD_TILES if va == 8 else CONV_FWD_TILES_V4, g.cg_out, g.N * g.Ho * g.Wo, g.groups)
     _gemm(A, B, DIRECT_K, GATHER_K, va, va, y, g.cg_out, g.Cout, bias=bias, bias_gstride=g.cg_out, relu=relu, tile=tile,
           epi=EPI_BF16, groups=g.groups)
@@ -208,6 +325,12 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False):
     A = _op(wt_buf, cg_in * kd, kd, cg_in, kd)
     B = _op(dy, cg_out, 0, g.N * g.H * g.W, kd, H=g.Ho, W=g.Wo, C=g.Cout, Ho=g.H, Wo=g.W, KH=g.KH,
             KW=g.KW, stride=1, pad_h=g.KH - 1 - g.pad_y, pad_w=g.KW - 1 - g.pad_x, dil=g.stride, Cg=cg_out)
+    if g.stride == 1 and _glds_cfg["on"]:
+        run = lambda t, o: _glds(A, B, B_GATHER, o, cg_in, g.C, groups=g.groups, mask_relu=mask_relu,  # noqa: E731
+                                 tile=t)
+        key = ("cd", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
+        if run(_tuned_tile(key, run, dx, lambda: _pick_glds(A.rows, B.rows, g.groups)), dx):
+            return
     tile = _pick(CONV_FWD_TILES, cg_in, g.N * g.H * g.W, g.groups)
     _gemm(A, B, DIRECT_K, GATHER_K, 8, 8, dx, cg_in, g.C, epi=EPI_BF16, groups=g.groups, mask_relu=mask_relu,
           tile=tile)
