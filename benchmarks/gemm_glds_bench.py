@@ -44,6 +44,14 @@ def make(name):
         w = (torch.randn(nout, nin, device="cuda", generator=g) * 0.02).to(BF)
         b = torch.randn(nout, device="cuda", generator=g) * 0.1
         y = torch.empty(N, nout, device="cuda", dtype=BF)
+        if kind == "dgrad":
+            dy = torch.randn(N, nout, device="cuda", generator=g).to(BF)
+            dx = torch.empty(N, nin, device="cuda", dtype=BF)
+            return (lambda: ops.fc_backward_data(dy, w, dx)), dx, 2.0 * N * nin * nout
+        if kind == "wgrad":
+            dy = torch.randn(N, nout, device="cuda", generator=g).to(BF)
+            dw = torch.empty(nout, nin, device="cuda")
+            return (lambda: ops.fc_backward_weight(x, dy, dw, overwrite=True)), dw, 2.0 * N * nin * nout
         return (lambda: ops.fc_forward(x, w, b, y, relu=True)), y, 2.0 * N * nin * nout
     C, H, Cout, K, s, p, grp = CONV[layer]
     Ho, Wo = G.conv_out_size(H, H, K, K, s, p, p)
@@ -56,6 +64,10 @@ def make(name):
         y = torch.empty(N, Ho, Wo, Cout, device="cuda", dtype=BF)
         return (lambda: ops.conv_forward(x, w, b, y, geo, relu=True)), y, flops
     dy = torch.randn(N, Ho, Wo, Cout, device="cuda", generator=g).to(BF)
+    if kind == "wgrad":
+        x = torch.randn(N, H, H, C, device="cuda", generator=g).to(BF)
+        dw = torch.zeros(Cout, K, K, C // grp, device="cuda")
+        return (lambda: (dw.zero_(), ops.conv_backward_weight(x, dy, dw, geo))), dw, flops
     dx = torch.empty(N, H, H, C, device="cuda", dtype=BF)
     wt = torch.empty_like(w)
     return (lambda: ops.conv_backward_data(dy, w, dx, geo, wt)), dx, flops
@@ -64,9 +76,10 @@ def make(name):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--ops", default="conv2_fwd,conv2_dgrad,conv3_fwd,conv3_dgrad,conv4_fwd,conv4_dgrad,conv5_fwd,"
-                                     "conv5_dgrad,fc6_fwd,fc7_fwd,fc8_fwd")
-    ap.add_argument("--tiles", default="0,1,2,4,5,6")
+    ap.add_argument("--ops", default="conv2_fwd,conv2_dgrad,conv2_wgrad,conv3_fwd,conv3_dgrad,conv3_wgrad,conv4_fwd,"
+                                     "conv4_dgrad,conv4_wgrad,conv5_fwd,conv5_dgrad,conv5_wgrad,fc6_fwd,fc6_dgrad,"
+                                     "fc6_wgrad,fc7_fwd,fc7_dgrad,fc7_wgrad,fc8_fwd,fc8_dgrad,fc8_wgrad")
+    ap.add_argument("--tiles", default="0,1,2,7,10,13,15,17")
     a = ap.parse_args()
     for name in a.ops.split(","):
         run, out, flops = make(name)

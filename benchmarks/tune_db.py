@@ -1,0 +1,50 @@
+"""Build the gfx950 GEMM tile database (cxxnet_amd/ops/glds_tune_gfx950.json): run a few
+training steps of each model at its benchmark batch so every GEMM signature is timed once,
+then write the table.
+
+  python benchmarks/tune_db.py [--models alexnet:256,inception_v1:64] [--out path]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--models", default="alexnet:256,alexnet:32,alexnet:128,inception_v1:64,vgg16:32,mnist_conv:100,"
+                                        "bowl:64")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    from cxxnet_amd.io.data import DataBatch
+    from cxxnet_amd.models import load_conf
+    from cxxnet_amd.nnet import NetTrainer
+    from cxxnet_amd.ops import gemm as G
+    G._TUNE.clear()
+    for spec in a.models.split(","):
+        name, b = spec.split(":")
+        b = int(b)
+        pairs = load_conf(name, [("batch_size", str(b)), ("eval_train", "0"), ("dev", "gpu"), ("silent", "1")])
+        tr = NetTrainer()
+        for k, v in pairs:
+            if not k.startswith("metric"):
+                tr.set_param(k, v)
+        tr.init_model()
+        c, h, w = tr.net_cfg.input_shape
+        x = torch.randn(b, c, h, w, device="cuda")
+        y = torch.zeros(b, 1, device="cuda")
+        for _ in range(2):
+            tr.update(DataBatch(x, y))
+        torch.cuda.synchronize()
+        print(name, b, len(G._TUNE), flush=True)
+        del tr
+        torch.cuda.empty_cache()
+    G.save_tune_db(a.out or None)
+    print("wrote", a.out or G.TUNE_DB, len(G._TUNE), "entries")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,27 +1,39 @@
-// LDS-DMA pipelined bf16 MFMA GEMM for gfx950 (K-major operands).
+// LDS-DMA pipelined bf16 MFMA GEMM for gfx950.
 //
-// Serves the GEMMs whose two operands are both K-contiguous:
-//   conv forward    A = weights [Cout][KH][KW][Cg],  B = implicit im2col of NHWC x   (reference K1-K4)
-//   conv data-grad  A = flipped weights,             B = implicit im2col of NHWC dy  (reference K7+K8)
-//   fc forward      A = weights [nout][nin],         B = activations [batch][nin]     (reference K9)
-// (reference: src/layer/convolution_layer-inl.hpp:70-155, src/layer/fullc_layer-inl.hpp:101-112).
+// Computes, per group g = blockIdx.z:   C[j][i] (+)= alpha * sum_k A(i, k) * B(j, k)
+// with each operand loaded by one of four loaders:
+//   K_DIRECT  : elem(row,k) = p[row*ld + k]          (k contiguous)
+//   K_GATHER  : rows = output pixels, k = (kh,kw,c)   implicit im2col of an NHWC tensor
+//   MN_DIRECT : elem(row,k) = p[k*ld + row]          (row contiguous)
+//   MN_GATHER : rows = (kh,kw,c), k = output pixels   transposed implicit im2col
+// It serves every GEMM-shaped op of AlexNet-class nets except conv1 (3 input channels):
+//   conv forward     A K_DIRECT (weights)        B K_GATHER (x)          bf16 out   (reference K1-K4)
+//   conv data-grad   A K_DIRECT (flipped w)      B K_GATHER (dy)         bf16 out   (reference K7+K8)
+//   conv weight-grad A MN_GATHER (x)             B MN_DIRECT (dy)        fp32 atomics, split-K (K5/K6)
+//   fc forward       A K_DIRECT (W)              B K_DIRECT (x)          bf16 / split-K slabs (K9)
+//   fc data-grad     A MN_DIRECT (W)             B K_DIRECT (dy)         bf16 / split-K slabs (K12)
+//   fc weight-grad   A MN_DIRECT (x)             B MN_DIRECT (dy)        fp32 store / += (K10)
+// (reference: src/layer/convolution_layer-inl.hpp:70-155, src/layer/fullc_layer-inl.hpp:101-130,
+//  which do these as im2col + cuBLAS sgemm).
 //
-// Design (MI355X-first; see gemm_mfma.hip for the register-staged generic kernel):
+// Design (MI355X-first):
 //   * both tiles go global -> LDS with `buffer_load_dwordx4 ... lds` (LDS-DMA): no VGPR
-//     staging, no ds_write pass, out-of-range rows / padding taps become buffer-OOB loads
-//     that land as zeros;
-//   * LDS image is lane-linear per wave-instruction (8 rows x 128 B) with an XOR swizzle
-//     on the 16-byte chunk (chunk ^ ((row >> 1) & 7)) applied on the SOURCE address, so the
-//     16x16x32 fragment reads (ds_read_b128) are bank-conflict free;
-//   * STAGES-deep ring of LDS buffers; each wave waits only for its own loads of the tile
-//     about to be read (counted `s_waitcnt vmcnt(N)`), then a raw s_barrier -- the DMAs of
-//     the next tiles stay in flight across it;
-//   * 4 waves, wave grid WGM x WGN, v_mfma_f32_16x16x32_bf16 with fp32 accumulators;
-//   * implicit-GEMM gather: per tile each lane decodes ONE k offset (its 16-byte chunk is
-//     fixed by the swizzle), the per-row pixel geometry is precomputed once;
-//   * epilogue: bias / relu / relu'-mask / alpha, staged per wave through LDS so every
-//     global store is a full 16-byte vector of a contiguous output row; or fp32 split-K
-//     slabs (EPI_F32) reduced by splitk_finalize.
+//     staging, no ds_write pass; out-of-range rows, K tails and padding taps are buffer-OOB
+//     loads that land as zeros;
+//   * the LDS image is lane-linear per DMA instruction (1 KiB) with an XOR swizzle of the
+//     16-byte chunks applied on the SOURCE address, so the fragment reads are bank-conflict
+//     free: K-major tiles [rows][64] are read with ds_read_b128 (chunk ^ ((row>>1)&7)),
+//     MN-major tiles [64][128] with ds_read_b64_tr_b16 (chunk ^ 2*((k&3) | ((k>>3)&1)<<2));
+//   * each lane's 16-byte chunk is fixed by the swizzle, so per K-tile a lane decodes one k
+//     (K-major) or one pixel per DMA (MN-major); row geometry is precomputed once;
+//   * STAGES-deep LDS ring; every iteration issues one tile of DMAs (all-OOB dummies past the
+//     K slice) so each wave waits with one constant `s_waitcnt vmcnt(N)` for its own loads of
+//     the tile to read, then a raw s_barrier: DMAs of later tiles stay in flight across it;
+//   * 4 waves (wave grid WGM x WGN) of v_mfma_f32_16x16x32_bf16; small-LDS 2-stage tiles run
+//     2-5 blocks per CU, which is what hides the DMA latency best (profiles/r14_glds_tiles.jsonl);
+//   * epilogues staged per wave through LDS so every global access is a contiguous row
+//     segment: bf16 (+bias, relu, relu'-mask of the old value), fp32 split-K slab, fp32 +=,
+//     fp32 atomics.
 #include <utility>
 #include "common.h"
 
@@ -33,8 +45,8 @@ constexpr uint32_t OOB = 0x80000000u;  // >= num_records: the load returns zeros
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef __attribute__((address_space(3))) void lds_void;
 
-enum { B_DIRECT = 0, B_GATHER = 1 };
-enum { EPI_BF16 = 0, EPI_F32 = 1 };
+enum { K_DIRECT = 0, K_GATHER = 1, MN_DIRECT = 2, MN_GATHER = 3 };
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_ACC = 2, EPI_F32_ATOMIC = 3 };
 
 struct GOperand {
   const bf16_t *ptr;
@@ -81,7 +93,156 @@ __device__ __forceinline__ void block_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int BM, int BN, int WGM, int WGN, int STAGES, int BMODE, int EPI>
+constexpr bool kmajor(int mode) { return mode == K_DIRECT || mode == K_GATHER; }
+
+// ---------------------------------------------------------------------------------- operands
+// One operand tile: R rows (i or j) x BK k, R*128 bytes, R/32 DMA instructions per wave
+// (instruction q = wave + 4s writes LDS bytes [1024q, 1024q + 1024) of the tile).
+template <int MODE, int R>
+struct Op {
+  static constexpr int NI = R / 32;
+  static_assert(kmajor(MODE) || R == 128, "MN-major tiles are 128 columns wide");
+  // K-major: per-instruction row state (byte offset or base/hi/wi); MN-major: column state
+  int s0[NI], s1[NI], s2[NI];
+  int lchunk;            // this lane's logical 16-byte chunk (fixed for every DMA of the wave)
+  uint32_t coff;         // MN: byte offset of the lane's column (+ group), or OOB
+  int hoff, woff;        // MN gather: tap offsets of the lane's column
+
+  __device__ __forceinline__ void init(const GOperand &op, int row0, uint32_t goff, int wave, int lane) {
+    if constexpr (kmajor(MODE)) {
+      // rows 8q + lane/8; chunk ^ ((row >> 1) & 7) with (row >> 1) & 7 == 4(wave&1) + lane/16
+      lchunk = (lane & 7) ^ (((wave & 1) << 2) + (lane >> 4));
+#pragma unroll
+      for (int s = 0; s < NI; ++s) {
+        const int r = row0 + 8 * (wave + 4 * s) + (lane >> 3);
+        if constexpr (MODE == K_DIRECT) {
+          s0[s] = r < op.rows ? static_cast<int>(goff + static_cast<uint32_t>(r * op.ld) * 2u) : -1;
+          s1[s] = s2[s] = 0;
+        } else {
+          if (r < op.rows) {
+            const uint32_t n = fdiv(static_cast<uint32_t>(r), op.fd_hw);
+            const uint32_t rem = static_cast<uint32_t>(r) - n * static_cast<uint32_t>(op.Ho * op.Wo);
+            const uint32_t ho = fdiv(rem, op.fd_wo);
+            const uint32_t wo = rem - ho * op.Wo;
+            s0[s] = static_cast<int>(n) * op.H * op.W * op.C;
+            s1[s] = static_cast<int>(ho) * op.stride - op.pad_h;
+            s2[s] = static_cast<int>(wo) * op.stride - op.pad_w;
+          } else {
+            s0[s] = -1;
+            s1[s] = s2[s] = 0;
+          }
+        }
+      }
+    } else {
+      // k-rows 4q + lane/16 (256-byte rows of 16 chunks); swizzle 2*((k&3) | ((k>>3)&1) << 2)
+      lchunk = (lane & 15) ^ (2 * ((lane >> 4) | (((wave >> 1) & 1) << 2)));
+      const int col = row0 + lchunk * 8;  // first of the lane's 8 columns (rows % 8 == 0)
+      const bool ok = col < op.rows;
+      if constexpr (MODE == MN_DIRECT) {
+        coff = ok ? goff + static_cast<uint32_t>(col) * 2u : OOB;
+        hoff = woff = 0;
+      } else {
+        int c = 0, kh = 0, kw = 0;
+        if (ok) {
+          const uint32_t r = fdiv(static_cast<uint32_t>(col), op.fd_cg);
+          c = col - static_cast<int>(r) * op.Cg;
+          const uint32_t q = fdiv(r, op.fd_kw);
+          kh = static_cast<int>(q);
+          kw = static_cast<int>(r - q * op.KW);
+        }
+        coff = ok ? goff + static_cast<uint32_t>(c) * 2u : OOB;
+        hoff = kh - op.pad_h;
+        woff = kw - op.pad_w;
+      }
+    }
+  }
+
+  // per K-tile, per lane: K-major -> the lane's k decode; MN-major -> the k-tile base
+  struct Prep {
+    int k;            // K-major: this lane's k; MN-major: first k of the tile
+    int kh, kw;       // K gather
+    uint32_t cb;      // K gather: channel byte offset (+ group)
+    bool kin;
+  };
+  __device__ __forceinline__ Prep prep(const GOperand &op, int kt, int kt_end, uint32_t goff) const {
+    Prep p;
+    if constexpr (kmajor(MODE)) {
+      p.k = kt * BK + lchunk * 8;
+      p.kin = kt < kt_end && p.k < op.kdim;
+      if constexpr (MODE == K_GATHER) {
+        const uint32_t r = fdiv(static_cast<uint32_t>(p.k), op.fd_cg);
+        const int c = p.k - static_cast<int>(r) * op.Cg;
+        const uint32_t q = fdiv(r, op.fd_kw);
+        p.kh = p.kin ? static_cast<int>(q) : -(1 << 20);  // past the slice: every row OOB
+        p.kw = static_cast<int>(r - q * op.KW);
+        p.cb = goff + static_cast<uint32_t>(c) * 2u;
+      } else {
+        p.kh = p.kw = 0;
+        p.cb = 0;
+      }
+    } else {
+      p.k = kt * BK;
+      p.kin = kt < kt_end;
+      p.kh = p.kw = 0;
+      p.cb = 0;
+    }
+    return p;
+  }
+
+  template <int S>
+  __device__ __forceinline__ uint32_t offset(const GOperand &op, const Prep &p, int wave, int lane) const {
+    uint32_t off;
+    if constexpr (MODE == K_DIRECT) {
+      off = (p.kin && s0[S] >= 0) ? static_cast<uint32_t>(s0[S]) + static_cast<uint32_t>(p.k) * 2u : OOB;
+    } else if constexpr (MODE == K_GATHER) {
+      const int hi = s1[S] + p.kh, wi = s2[S] + p.kw;
+      const bool ok = s0[S] >= 0 && static_cast<unsigned>(hi) < static_cast<unsigned>(op.H) &&
+                      static_cast<unsigned>(wi) < static_cast<unsigned>(op.W);
+      off = ok ? p.cb + static_cast<uint32_t>(s0[S] + (hi * op.W + wi) * op.C) * 2u : OOB;
+    } else {
+      const int kp = p.k + 4 * (wave + 4 * S) + (lane >> 4);  // this DMA's k (pixel / batch row)
+      const bool kin = p.kin && kp < op.kdim && coff != OOB;
+      if constexpr (MODE == MN_DIRECT) {
+        off = kin ? coff + static_cast<uint32_t>(kp * op.ld) * 2u : OOB;
+      } else {
+        const uint32_t n = fdiv(static_cast<uint32_t>(kp), op.fd_hw);
+        const uint32_t rem = static_cast<uint32_t>(kp) - n * static_cast<uint32_t>(op.Ho * op.Wo);
+        const uint32_t ho = fdiv(rem, op.fd_wo);
+        const int wo = static_cast<int>(rem - ho * op.Wo);
+        const int hi = static_cast<int>(ho) * op.stride + hoff, wi = wo * op.stride + woff;
+        const bool ok = kin && static_cast<unsigned>(hi) < static_cast<unsigned>(op.H) &&
+                        static_cast<unsigned>(wi) < static_cast<unsigned>(op.W);
+        off = ok ? coff + static_cast<uint32_t>((static_cast<int>(n) * op.H + hi) * op.W + wi) * op.C * 2u : OOB;
+      }
+    }
+    asm volatile("" : "+v"(off));  // keep the select: no per-lane branch around the DMA
+    return off;
+  }
+};
+
+// 16x16x32 fragment of rows [base, base+16) at k-step kk (0 or 32) from a staged tile.
+template <int MODE>
+__device__ __forceinline__ bf16x8 frag(const char *tile, int base, int kk, int lane) {
+  if constexpr (kmajor(MODE)) {
+    const int row = base + (lane & 15);
+    const int ch = ((kk >> 3) + (lane >> 4)) ^ ((lane & 15) >> 1);
+    return *reinterpret_cast<const bf16x8 *>(tile + row * 128 + ch * 16);
+  } else {
+    // ds_read_b64_tr_b16 pair: lane (i, gq) reads k-rows kk + 8gq + i/4 (+4), columns base + 4(i&3)
+    const int i = lane & 15, gq = lane >> 4;
+    const int f = (i >> 2) | ((gq & 1) << 2);              // swizzle/2 of both k-rows
+    const int ch = ((base >> 4) ^ f) * 2 + ((i & 3) >> 1);  // (2*(base/16) + h) ^ 2f
+    const char *p0 = tile + (kk + 8 * gq + (i >> 2)) * 256 + ch * 16 + (i & 1) * 8;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p0));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p0 + 4 * 256));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, r);
+  }
+}
+
+// ---------------------------------------------------------------------------------- kernel
+template <int BM, int BN, int WGM, int WGN, int STAGES, int AMODE, int BMODE, int EPI>
 __global__ void __launch_bounds__(NT, 1)
 gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_tiles, int ktiles_total) {
   static_assert(WGM * WGN == 4, "4 waves");
@@ -89,8 +250,9 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
   constexpr int WM = BM / WGM, WN = BN / WGN;
   static_assert(WM % 16 == 0 && WN % 16 == 0, "wave tile must be a multiple of 16");
   constexpr int MR = WM / 16, NR = WN / 16;
-  constexpr int NIA = BM / 32, NIB = BN / 32;  // DMA instructions per wave per tile
-  constexpr int NPT = NIA + NIB;
+  using OA = Op<AMODE, BM>;
+  using OB = Op<BMODE, BN>;
+  constexpr int NPT = OA::NI + OB::NI;  // DMA instructions per wave per tile
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
   constexpr int EPI_BYTES = 4 * 16 * (WM + 4) * 4;
@@ -113,96 +275,26 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
   const rsrc_t rB = make_rsrc(B.ptr, B.nbytes);
   const uint32_t goA = static_cast<uint32_t>(g * A.gstride) * 2u;
   const uint32_t goB = static_cast<uint32_t>(g * B.gstride) * 2u;
+  OA oa;
+  OB ob;
+  oa.init(A, i0, goA, wave, lane);
+  ob.init(B, j0, goB, wave, lane);
 
-  // This lane's logical 16-byte chunk inside its 128-byte row, identical for every DMA
-  // the wave issues (rows 8q + lane/8 with q = wave + 4s): chunk ^ ((row >> 1) & 7).
-  const int lchunk = (lane & 7) ^ (((wave & 1) << 2) + (lane >> 4));
-  const int lrow = lane >> 3;
-
-  // ---- per-row source geometry, fixed across K
-  uint32_t rowA[NIA];
-#pragma unroll
-  for (int s = 0; s < NIA; ++s) {
-    const int r = i0 + 8 * (wave + 4 * s) + lrow;
-    rowA[s] = r < A.rows ? goA + static_cast<uint32_t>(r * A.ld) * 2u : OOB;
-  }
-  int bbase[NIB], bh[NIB], bw[NIB];
-#pragma unroll
-  for (int s = 0; s < NIB; ++s) {
-    const int p = j0 + 8 * (wave + 4 * s) + lrow;
-    if constexpr (BMODE == B_GATHER) {
-      if (p < B.rows) {
-        const uint32_t n = fdiv(static_cast<uint32_t>(p), B.fd_hw);
-        const uint32_t rem = static_cast<uint32_t>(p) - n * static_cast<uint32_t>(B.Ho * B.Wo);
-        const uint32_t ho = fdiv(rem, B.fd_wo);
-        const uint32_t wo = rem - ho * B.Wo;
-        bbase[s] = static_cast<int>(n) * B.H * B.W * B.C;
-        bh[s] = static_cast<int>(ho) * B.stride - B.pad_h;
-        bw[s] = static_cast<int>(wo) * B.stride - B.pad_w;
-      } else {
-        bbase[s] = -1;
-        bh[s] = 0;
-        bw[s] = 0;
-      }
-    } else {
-      bbase[s] = p < B.rows ? static_cast<int>(goB) + p * B.ld * 2 : -1;
-      bh[s] = bw[s] = 0;
-    }
-  }
-
-  // ---- DMAs of one K-tile: prep() decodes this lane's k once, issue_one<q>() sends
-  // DMA instruction q (A rows for q < NIA, then B rows) into stage buffer `st`.  The
-  // pieces are interleaved with the previous tile's MFMAs by compute().
-  struct Prep {
-    uint32_t ka;   // byte offset of k in an A row, or OOB
-    uint32_t kb;   // direct B: byte offset of k; gather B: channel byte offset (+ group)
-    int kh, kw;
-    bool kin;
-  };
-  auto prep = [&](int kt) {
-    Prep p;
-    const int k = kt * BK + lchunk * 8;
-    p.kin = kt < kt_end && k < A.kdim;
-    p.ka = p.kin ? static_cast<uint32_t>(k) * 2u : OOB;
-    if constexpr (BMODE == B_GATHER) {
-      const uint32_t r = fdiv(static_cast<uint32_t>(k), B.fd_cg);
-      const int c = k - static_cast<int>(r) * B.Cg;
-      const uint32_t kh = fdiv(r, B.fd_kw);
-      p.kh = p.kin ? static_cast<int>(kh) : -(1 << 20);  // out of range -> every row OOB
-      p.kw = static_cast<int>(r - kh * B.KW);
-      p.kb = goB + static_cast<uint32_t>(c) * 2u;
-    } else {
-      p.kb = p.ka;
-      p.kh = p.kw = 0;
-    }
-    return p;
-  };
-  auto issue_one = [&](const Prep &p, int st, auto qc) {
-    constexpr int q = decltype(qc)::value;
+  // issue every DMA of K-tile kt into stage buffer st (dummies past the slice)
+  auto issue = [&](int kt, int st) {
+    const typename OA::Prep pa = oa.prep(A, kt, kt_end, goA);
+    const typename OB::Prep pb = ob.prep(B, kt, kt_end, goB);
     char *sa = smem + st * STAGE_BYTES;
-    uint32_t off;
-    if constexpr (q < NIA) {
-      off = (p.ka != OOB && rowA[q] != OOB) ? rowA[q] + p.ka : OOB;
-      asm volatile("" : "+v"(off));  // keep the select: no per-lane branch around the DMA
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void *)(sa + (wave + 4 * q) * 1024), 16, off, 0, 0, 0);
-    } else {
-      constexpr int s = q - NIA;
-      if constexpr (BMODE == B_GATHER) {
-        const int hi = bh[s] + p.kh, wi = bw[s] + p.kw;
-        const bool ok = bbase[s] >= 0 && static_cast<unsigned>(hi) < static_cast<unsigned>(B.H) &&
-                        static_cast<unsigned>(wi) < static_cast<unsigned>(B.W);
-        off = ok ? p.kb + static_cast<uint32_t>(bbase[s] + (hi * B.W + wi) * B.C) * 2u : OOB;
-      } else {
-        off = (p.kin && bbase[s] >= 0) ? static_cast<uint32_t>(bbase[s]) + p.kb : OOB;
-      }
-      asm volatile("" : "+v"(off));
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void *)(sa + A_BYTES + (wave + 4 * s) * 1024), 16, off, 0,
-                                               0, 0);
-    }
-  };
-  auto issue_all = [&](int kt, int st) {
-    const Prep p = prep(kt);
-    static_for<NPT>([&](auto qc) { issue_one(p, st, qc); });
+    static_for<OA::NI>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void *)(sa + (wave + 4 * s) * 1024), 16,
+                                               oa.template offset<s>(A, pa, wave, lane), 0, 0, 0);
+    });
+    static_for<OB::NI>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void *)(sa + A_BYTES + (wave + 4 * s) * 1024), 16,
+                                               ob.template offset<s>(B, pb, wave, lane), 0, 0, 0);
+    });
   };
 
   const int wi_ = wave % WGM, wj_ = wave / WGM;
@@ -212,93 +304,62 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
 #pragma unroll
     for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // fragment addressing: rows base16 + (lane & 15); (row >> 1) & 7 == (lane & 15) >> 1
-  const int frow = (lane & 15) * 128;
-  const int fx0 = ((0 + (lane >> 4)) ^ ((lane & 15) >> 1)) << 4;
-  const int fx1 = ((4 + (lane >> 4)) ^ ((lane & 15) >> 1)) << 4;
-  // compute one staged tile; the DMAs of the tile STAGES-1 ahead are issued first, ahead
-  // of the fragment reads (issue-before-read: their latency hides under this tile's MFMAs).
-  // Interleaving them between MFMA rows measured worse codegen: the live ranges pushed the
-  // loop past 256 VGPRs and hipcc copied the accumulators AGPR<->VGPR every iteration.
-  auto compute = [&](int st, const Prep &p, int st_w) {
-    const char *sa = smem + st * STAGE_BYTES + wi_ * WM * 128 + frow;
-    const char *sb = smem + st * STAGE_BYTES + A_BYTES + wj_ * WN * 128 + frow;
+  // One staged tile: the DMAs of the tile STAGES-1 ahead are issued first, ahead of the
+  // fragment reads (their latency hides under this tile's MFMAs).  Interleaving them between
+  // MFMA rows measured worse: the live ranges pushed the loop past 256 VGPRs and hipcc copied
+  // the accumulators AGPR<->VGPR every iteration.
+  auto compute = [&](int st) {
+    const char *sa = smem + st * STAGE_BYTES;
+    const char *sb = sa + A_BYTES;
     static_for<2>([&](auto kkc) {
-      constexpr int kk = decltype(kkc)::value;
-      const int fx = kk ? fx1 : fx0;
-      if constexpr (kk == 0) static_for<NPT>([&](auto qc) { issue_one(p, st_w, qc); });
+      constexpr int kk = decltype(kkc)::value * 32;
       bf16x8 fa[MR], fb[NR];
 #pragma unroll
-      for (int m = 0; m < MR; ++m) fa[m] = *reinterpret_cast<const bf16x8 *>(sa + m * 16 * 128 + fx);
+      for (int m = 0; m < MR; ++m) fa[m] = frag<AMODE>(sa, wi_ * WM + m * 16, kk, lane);
 #pragma unroll
-      for (int n = 0; n < NR; ++n) fb[n] = *reinterpret_cast<const bf16x8 *>(sb + n * 16 * 128 + fx);
-      static_for<MR>([&](auto mc) {
-        constexpr int m = decltype(mc)::value;
+      for (int n = 0; n < NR; ++n) fb[n] = frag<BMODE>(sb, wj_ * WN + n * 16, kk, lane);
+#pragma unroll
+      for (int m = 0; m < MR; ++m)
 #pragma unroll
         for (int n = 0; n < NR; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
-
-      });
     });
   };
 
   // ---- main loop: STAGES-deep DMA ring
 #pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s) issue_all(kt_beg + s, s);  // (all-OOB dummies past the slice)
+  for (int s = 0; s < STAGES - 1; ++s) issue(kt_beg + s, s);
   int st_read = 0, st_write = STAGES - 1;
   for (int t = 0; t < nt; ++t) {
-    // Every iteration issues one tile's DMAs (past the slice: all-OOB dummies that write
-    // zeros into the buffer of the already-consumed tile t-1), so exactly STAGES-2 tiles
-    // of this wave's DMAs may stay in flight beyond tile t -- a branch-free loop body.
+    // exactly STAGES-2 tiles of this wave's DMAs may stay in flight beyond tile t
     wait_vmcnt<NPT * (STAGES - 2)>();
     block_barrier();  // every wave's DMAs of tile t have landed; every wave is done reading tile t-1
-    const Prep p = prep(kt_beg + t + STAGES - 1);
-    compute(st_read, p, st_write);
+    issue(kt_beg + t + STAGES - 1, st_write);
+    compute(st_read);
     st_read = st_read + 1 == STAGES ? 0 : st_read + 1;
     st_write = st_write + 1 == STAGES ? 0 : st_write + 1;
   }
   wait_vmcnt<0>();
   __syncthreads();  // stage buffers are reused by the epilogue
 
-  // ---- epilogue
+  // ---- epilogue: each wave stages 16 output rows (j) x WM columns (i) in LDS, then writes rows
   const int Mi = A.rows, Nj = B.rows;
   const int ibase = i0 + wi_ * WM, jbase = j0 + wj_ * WN;
-  if constexpr (EPI == EPI_F32) {
-    float *out = reinterpret_cast<float *>(E.out) + g * E.gstride + blockIdx.y * E.kstride;
+  float *ep = reinterpret_cast<float *>(smem) + wave * 16 * (WM + 4);
+  const float *bias = E.bias ? E.bias + g * E.bias_gstride : nullptr;
+#pragma unroll
+  for (int n = 0; n < NR; ++n) {
 #pragma unroll
     for (int m = 0; m < MR; ++m)
-#pragma unroll
-      for (int n = 0; n < NR; ++n) {
-        const int i = ibase + m * 16 + (lane >> 4) * 4;
-        const int j = jbase + n * 16 + (lane & 15);
-        if (j < Nj && i < Mi) {
-          f32x4 v = acc[m][n] * E.alpha;
-          float *dst = out + static_cast<long>(j) * E.ldc + i;
-          if (i + 4 <= Mi && (E.ldc & 3) == 0) {
-            *reinterpret_cast<f32x4 *>(dst) = v;
-          } else {
-            for (int e = 0; e < 4 && i + e < Mi; ++e) dst[e] = v[e];
-          }
-        }
-      }
-  } else {
-    float *ep = reinterpret_cast<float *>(smem) + wave * 16 * (WM + 4);
-    bf16_t *out = reinterpret_cast<bf16_t *>(E.out) + g * E.gstride;
-    const float *bias = E.bias ? E.bias + g * E.bias_gstride : nullptr;
-    constexpr int LPR = WM / 8;   // lanes per output row (8 bf16 per lane)
-    constexpr int RPI = 64 / LPR; // rows per pass
-    const int il = (lane % LPR) * 8;
-    const int i = ibase + il;
-    float bv[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) bv[e] = (bias && i + e < Mi) ? bias[i + e] : 0.f;
-    const bool vec_store = ((E.ldc & 7) == 0) && (i + 8 <= Mi);
-#pragma unroll
-    for (int n = 0; n < NR; ++n) {
-#pragma unroll
-      for (int m = 0; m < MR; ++m)
-        *reinterpret_cast<f32x4 *>(ep + (lane & 15) * (WM + 4) + m * 16 + (lane >> 4) * 4) = acc[m][n];
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes are visible to its reads
+      *reinterpret_cast<f32x4 *>(ep + (lane & 15) * (WM + 4) + m * 16 + (lane >> 4) * 4) = acc[m][n];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    if constexpr (EPI == EPI_BF16) {
+      bf16_t *out = reinterpret_cast<bf16_t *>(E.out) + g * E.gstride;
+      constexpr int LPR = WM / 8;    // lanes per output row (8 bf16 per lane)
+      constexpr int RPI = 64 / LPR;  // rows per pass
+      const int il = (lane % LPR) * 8;
+      const int i = ibase + il;
+      const bool vec_store = ((E.ldc & 7) == 0) && (i + 8 <= Mi);
 #pragma unroll
       for (int jl = lane / LPR; jl < 16; jl += RPI) {
         const int j = jbase + n * 16 + jl;
@@ -308,7 +369,7 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
           float f[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            f[e] = f[e] * E.alpha + bv[e];
+            f[e] = f[e] * E.alpha + ((bias && i + e < Mi) ? bias[i + e] : 0.f);
             if (E.relu) f[e] = fmaxf(f[e], 0.f);
           }
           bf16_t *dst = out + static_cast<long>(j) * E.ldc + i;
@@ -328,12 +389,48 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
           }
         }
       }
-      __builtin_amdgcn_s_waitcnt(0xc07f);
+    } else if constexpr (EPI == EPI_F32_ATOMIC) {
+      // one float per lane: every atomic instruction covers 64 consecutive floats of a row
+      float *out = reinterpret_cast<float *>(E.out) + g * E.gstride;
+#pragma unroll 4
+      for (int jl = 0; jl < 16; ++jl) {
+        const int j = jbase + n * 16 + jl;
+#pragma unroll
+        for (int u = 0; u < (WM + 63) / 64; ++u) {
+          const int il = u * 64 + lane;
+          const int i = ibase + il;
+          if (j < Nj && il < WM && i < Mi)
+            atomicAdd(out + static_cast<long>(j) * E.ldc + i, ep[jl * (WM + 4) + il] * E.alpha);
+        }
+      }
+    } else {
+      float *out = reinterpret_cast<float *>(E.out) + g * E.gstride;
+      if constexpr (EPI == EPI_F32) out += blockIdx.y * E.kstride;
+      constexpr int LPR = WM / 4;    // lanes per row, 4 floats per lane (16-byte accesses)
+      constexpr int RPI = 64 / LPR;
+      const int il = (lane % LPR) * 4;
+      const int i = ibase + il;
+      const bool vec = ((E.ldc & 3) == 0) && (i + 4 <= Mi);
+#pragma unroll
+      for (int jl = lane / LPR; jl < 16; jl += RPI) {
+        const int j = jbase + n * 16 + jl;
+        if (j < Nj && i < Mi) {
+          f32x4 v = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il) * E.alpha;
+          float *dst = out + static_cast<long>(j) * E.ldc + i;
+          if (vec) {
+            if constexpr (EPI == EPI_F32_ACC) v += *reinterpret_cast<const f32x4 *>(dst);
+            *reinterpret_cast<f32x4 *>(dst) = v;
+          } else {
+            for (int e = 0; e < 4 && i + e < Mi; ++e) dst[e] = (EPI == EPI_F32_ACC ? dst[e] : 0.f) + v[e];
+          }
+        }
+      }
     }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, int STAGES, int BMODE, int EPI>
+template <int BM, int BN, int WGM, int WGN, int STAGES, int AMODE, int BMODE, int EPI>
 void launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int ksplit, hipStream_t s) {
   const int ti = cdiv(A.rows, BM), tj = cdiv(B.rows, BN);
   const int ktiles = cdiv(A.kdim, BK);
@@ -341,46 +438,56 @@ void launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int
   const int per = cdiv(ktiles, ksplit);
   ksplit = cdiv(ktiles, per);
   dim3 grid(ti * tj, ksplit, groups);
-  hipLaunchKernelGGL((gemm_glds<BM, BN, WGM, WGN, STAGES, BMODE, EPI>), grid, dim3(NT), 0, s, A, B, E, ti, tj, per,
-                     ktiles);
+  hipLaunchKernelGGL((gemm_glds<BM, BN, WGM, WGN, STAGES, AMODE, BMODE, EPI>), grid, dim3(NT), 0, s, A, B, E, ti,
+                     tj, per, ktiles);
 }
 
-// Tile ids (BM x BN, wave grid, stages):
-//   0: 128x256 (1x4) 3 stages   1: 128x128 (1x4) 2 stages   2: 128x128 (2x2) 3 stages
-//   4: 192x256 (1x4) 2 stages   5: 64x256 (1x4) 3 stages
-//   6: 256x128 (4x1) 3 stages   7: 64x128 (1x4) 2 stages    8: 192x128 (1x4) 2 stages
-//   9: 96x128 (1x4) 2 stages    10: 128x64 (2x2) 2 stages   11: 64x128 (1x4) 3 stages
-//  12: 64x128 (1x4) 4 stages   13: 128x128 (1x4) 3 stages  14: 128x64 (2x2) 3 stages
-//  15: 64x64 (2x2) 3 stages    16: 192x64 (2x2) 3 stages
-#define CXG_TILES(BMODE, EPI)                                                               \
-  switch (tile) {                                                                           \
-    case 0: launch<128, 256, 1, 4, 3, BMODE, EPI>(A, B, E, groups, ksplit, s); return 0;    \
-    case 1: launch<128, 128, 1, 4, 2, BMODE, EPI>(A, B, E, groups, ksplit, s); return 0;    \
-    case 2: launch<128, 128, 2, 2, 3, BMODE, EPI>(A, B, E, groups, ksplit, s); return 0;    \
-    case 4: launch<192, 256, 1, 4, 2, BMODE, EPI>(A, B, E, groups, ksplit, s); return 0;    \
-    case 5: launch<64, 256, 1, 4, 3, BMODE, EPI>(A, B, E, groups, ksplit, s); return 0;     \
-    case 6: launch<256, 128, 4, 1, 3, BMODE, EPI>(A, B, E, groups, ksplit, s); return 0;    \
-    case 7: launch<64, 128, 1, 4, 2, BMODE, EPI>(A, B, E, groups, ksplit, s); return 0;     \
-    case 8: launch<192, 128, 1, 4, 2, BMODE, EPI>(A, B, E, groups, ksplit, s); return 0;    \
-    case 9: launch<96, 128, 1, 4, 2, BMODE, EPI>(A, B, E, groups, ksplit, s); return 0;     \
-    case 10: launch<128, 64, 2, 2, 2, BMODE, EPI>(A, B, E, groups, ksplit, s); return 0;    \
-    case 11: launch<64, 128, 1, 4, 3, BMODE, EPI>(A, B, E, groups, ksplit, s); return 0;    \
-    case 12: launch<64, 128, 1, 4, 4, BMODE, EPI>(A, B, E, groups, ksplit, s); return 0;    \
-    case 13: launch<128, 128, 1, 4, 3, BMODE, EPI>(A, B, E, groups, ksplit, s); return 0;   \
-    case 14: launch<128, 64, 2, 2, 3, BMODE, EPI>(A, B, E, groups, ksplit, s); return 0;    \
-    case 15: launch<64, 64, 2, 2, 3, BMODE, EPI>(A, B, E, groups, ksplit, s); return 0;     \
-    case 16: launch<192, 64, 2, 2, 3, BMODE, EPI>(A, B, E, groups, ksplit, s); return 0;    \
-    default: return -1;                                                                     \
+// Tile ids (BM x BN, wave grid, stages); MN-major operands need a 128-wide tile side:
+//   0: 128x256 (1x4) 3      1: 128x128 (1x4) 2      2: 128x128 (2x2) 3      7: 64x128 (1x4) 2
+//  10: 128x64 (2x2) 2      13: 128x128 (1x4) 3     15: 64x64 (2x2) 3       17: 128x128 (2x2) 2
+#define CXG_T(ID, BM, BN, WGM, WGN, ST) \
+  case ID: launch<BM, BN, WGM, WGN, ST, AM, BMo, EP>(A, B, E, groups, ksplit, s); return 0;
+#define CXG_KK_TILES                                                                                      \
+  switch (tile) {                                                                                         \
+    CXG_T(0, 128, 256, 1, 4, 3) CXG_T(1, 128, 128, 1, 4, 2) CXG_T(2, 128, 128, 2, 2, 3)                   \
+    CXG_T(7, 64, 128, 1, 4, 2) CXG_T(10, 128, 64, 2, 2, 2) CXG_T(15, 64, 64, 2, 2, 3)                     \
+    default: return -1;                                                                                   \
+  }
+#define CXG_MK_TILES  /* A MN-major (BM = 128), B K-major */                                              \
+  switch (tile) {                                                                                         \
+    CXG_T(0, 128, 256, 1, 4, 3) CXG_T(1, 128, 128, 1, 4, 2) CXG_T(2, 128, 128, 2, 2, 3)                   \
+    CXG_T(10, 128, 64, 2, 2, 2) CXG_T(13, 128, 128, 1, 4, 3) CXG_T(17, 128, 128, 2, 2, 2)                 \
+    default: return -1;                                                                                   \
+  }
+#define CXG_MM_TILES  /* both MN-major (128 x 128) */                                                     \
+  switch (tile) {                                                                                         \
+    CXG_T(1, 128, 128, 1, 4, 2) CXG_T(2, 128, 128, 2, 2, 3) CXG_T(13, 128, 128, 1, 4, 3)                  \
+    CXG_T(17, 128, 128, 2, 2, 2)                                                                          \
+    default: return -1;                                                                                   \
+  }
+#define CXG_CASE(AMV, BMV, EPV, TILES)                       \
+  if (amode == AMV && bmode == BMV && epi == EPV) {          \
+    constexpr int AM = AMV, BMo = BMV, EP = EPV;             \
+    TILES                                                    \
   }
 
-int dispatch(int bmode, int epi, int tile, const GOperand &A, const GOperand &B, const GEpi &E, int groups, int ksplit,
-             hipStream_t s) {
-  if (bmode == B_GATHER && epi == EPI_BF16) { CXG_TILES(B_GATHER, EPI_BF16) }
-  if (bmode == B_DIRECT && epi == EPI_BF16) { CXG_TILES(B_DIRECT, EPI_BF16) }
-  if (bmode == B_DIRECT && epi == EPI_F32) { CXG_TILES(B_DIRECT, EPI_F32) }
+int dispatch(int amode, int bmode, int epi, int tile, const GOperand &A, const GOperand &B, const GEpi &E,
+             int groups, int ksplit, hipStream_t s) {
+  CXG_CASE(K_DIRECT, K_GATHER, EPI_BF16, CXG_KK_TILES)    // conv fwd / dgrad
+  CXG_CASE(K_DIRECT, K_DIRECT, EPI_BF16, CXG_KK_TILES)    // fc fwd
+  CXG_CASE(K_DIRECT, K_DIRECT, EPI_F32, CXG_KK_TILES)     // fc fwd split-K
+  CXG_CASE(MN_GATHER, MN_DIRECT, EPI_F32_ATOMIC, CXG_MM_TILES)  // conv wgrad
+  CXG_CASE(MN_DIRECT, K_DIRECT, EPI_BF16, CXG_MK_TILES)   // fc dgrad
+  CXG_CASE(MN_DIRECT, K_DIRECT, EPI_F32, CXG_MK_TILES)    // fc dgrad split-K
+  CXG_CASE(MN_DIRECT, MN_DIRECT, EPI_F32, CXG_MM_TILES)   // fc wgrad (store)
+  CXG_CASE(MN_DIRECT, MN_DIRECT, EPI_F32_ACC, CXG_MM_TILES)  // fc wgrad (+=)
   return -1;
 }
-#undef CXG_TILES
+#undef CXG_CASE
+#undef CXG_MM_TILES
+#undef CXG_MK_TILES
+#undef CXG_KK_TILES
+#undef CXG_T
 
 }  // namespace
 
@@ -393,39 +500,45 @@ struct CxnOperandG {
   int H, W, C, Ho, Wo, KH, KW, stride, pad_h, pad_w, dil, Cg;
 };
 
+namespace {
+bool supported(const CxnOperandG *o, int mode) {
+  if (o->nbytes >= (1L << 31) || (reinterpret_cast<uintptr_t>(o->ptr) & 15) || o->gstride % 8 != 0) return false;
+  if (mode == K_DIRECT || mode == MN_DIRECT) return o->ld % 8 == 0 && (mode == K_DIRECT || o->rows % 8 == 0);
+  if (o->Cg % 8 != 0 || o->C % 8 != 0 || o->dil > 1) return false;
+  return mode == K_GATHER || o->rows % 8 == 0;
+}
+void fill(GOperand &r, const CxnOperandG *o, int mode) {
+  r.ptr = static_cast<const bf16_t *>(o->ptr);
+  r.gstride = o->gstride;
+  r.nbytes = static_cast<uint32_t>(o->nbytes);
+  r.ld = o->ld; r.rows = o->rows; r.kdim = o->kdim;
+  if (mode == K_GATHER || mode == MN_GATHER) {
+    r.H = o->H; r.W = o->W; r.C = o->C; r.Ho = o->Ho; r.Wo = o->Wo; r.KW = o->KW;
+    r.stride = o->stride; r.pad_h = o->pad_h; r.pad_w = o->pad_w; r.Cg = o->Cg;
+    r.fd_cg = make_fastdiv(o->Cg);
+    r.fd_kw = make_fastdiv(o->KW > 0 ? o->KW : 1);
+    r.fd_hw = make_fastdiv(o->Ho * o->Wo > 0 ? o->Ho * o->Wo : 1);
+    r.fd_wo = make_fastdiv(o->Wo > 0 ? o->Wo : 1);
+  }
+}
+}  // namespace
+
 // Returns 0 on success, -1 unsupported configuration (the caller falls back), -3 launch error.
-// Requirements: kdim % 8 == 0, 16-byte aligned rows (ld % 8 == 0), gather: Cg % 8 == 0 and
-// dil == 1, every buffer < 2 GiB.
-CXN_API int cxn_gemm_glds(const CxnOperandG *a, const CxnOperandG *b, int bmode, void *out, long out_gstride, int ldc,
-                          float alpha, const float *bias, long bias_gstride, int relu, int mask_relu, int epi,
-                          int tile, int groups, int ksplit, long kstride, void *stream) {
-  if (a->kdim != b->kdim || a->kdim % 8 != 0) return -1;
-  if (a->nbytes >= (1L << 31) || b->nbytes >= (1L << 31)) return -1;
-  if (a->ld % 8 != 0 || a->gstride % 8 != 0 || (reinterpret_cast<uintptr_t>(a->ptr) & 15)) return -1;
-  if (reinterpret_cast<uintptr_t>(b->ptr) & 15) return -1;
-  if (bmode == B_GATHER && (b->Cg % 8 != 0 || b->C % 8 != 0 || b->dil > 1 || b->gstride % 8 != 0)) return -1;
-  if (bmode == B_DIRECT && (b->ld % 8 != 0 || b->gstride % 8 != 0)) return -1;
+// Requirements: kdim % 8 == 0; 16-byte aligned rows; MN-major operands: rows % 8 == 0;
+// gathers: Cg % 8 == 0 and dil == 1; every buffer < 2 GiB.
+CXN_API int cxn_gemm_glds(const CxnOperandG *a, const CxnOperandG *b, int amode, int bmode, void *out,
+                          long out_gstride, int ldc, float alpha, const float *bias, long bias_gstride, int relu,
+                          int mask_relu, int epi, int tile, int groups, int ksplit, long kstride, void *stream) {
+  if (a->kdim != b->kdim) return -1;
+  if ((kmajor(amode) || kmajor(bmode)) && a->kdim % 8 != 0) return -1;
+  if (!supported(a, amode) || !supported(b, bmode)) return -1;
   if (a->rows <= 0 || b->rows <= 0 || a->kdim <= 0) return 0;
   GOperand A{}, B{};
-  A.ptr = static_cast<const bf16_t *>(a->ptr);
-  A.gstride = a->gstride;
-  A.nbytes = static_cast<uint32_t>(a->nbytes);
-  A.ld = a->ld; A.rows = a->rows; A.kdim = a->kdim;
-  B.ptr = static_cast<const bf16_t *>(b->ptr);
-  B.gstride = b->gstride;
-  B.nbytes = static_cast<uint32_t>(b->nbytes);
-  B.ld = b->ld; B.rows = b->rows; B.kdim = b->kdim;
-  if (bmode == B_GATHER) {
-    B.H = b->H; B.W = b->W; B.C = b->C; B.Ho = b->Ho; B.Wo = b->Wo; B.KW = b->KW;
-    B.stride = b->stride; B.pad_h = b->pad_h; B.pad_w = b->pad_w; B.Cg = b->Cg;
-    B.fd_cg = make_fastdiv(b->Cg);
-    B.fd_kw = make_fastdiv(b->KW > 0 ? b->KW : 1);
-    B.fd_hw = make_fastdiv(b->Ho * b->Wo > 0 ? b->Ho * b->Wo : 1);
-    B.fd_wo = make_fastdiv(b->Wo > 0 ? b->Wo : 1);
-  }
+  fill(A, a, amode);
+  fill(B, b, bmode);
   GEpi E{out, out_gstride, ldc, alpha, bias, bias_gstride, relu, mask_relu, kstride};
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int rc = dispatch(bmode, epi, tile, A, B, E, groups < 1 ? 1 : groups, ksplit < 1 ? 1 : ksplit, s);
+  const int rc = dispatch(amode, bmode, epi, tile, A, B, E, groups < 1 ? 1 : groups, ksplit < 1 ? 1 : ksplit, s);
   if (rc != 0) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -107,20 +107,56 @@ def _pick(candidates, rows_i, rows_j, groups, min_blocks=2 * NUM_CU):
 # gemm_glds.hip: both operands K-major (conv fwd / dgrad, fc fwd), 4 waves, one block per CU.
 GLDS_TILES = {0: (128, 256), 1: (128, 128), 2: (128, 128), 4: (192, 256), 5: (64, 256), 6: (256, 128),
               7: (64, 128), 8: (192, 128), 9: (96, 128), 10: (128, 64), 11: (64, 128), 12: (64, 128),
-              13: (128, 128), 14: (128, 64), 15: (64, 64), 16: (192, 64)}
-B_DIRECT, B_GATHER = 0, 1
+              13: (128, 128), 14: (128, 64), 15: (64, 64), 16: (192, 64), 17: (128, 128)}
+# operand loaders of gemm_glds.hip
+GL_K, GL_KG, GL_MN, GL_MNG = 0, 1, 2, 3  # K_DIRECT, K_GATHER, MN_DIRECT, MN_GATHER
+EPI_F32_ACC_G, EPI_F32_ATOMIC_G = 2, 3
 _glds_cfg = {"on": os.environ.get("CXXNET_GEMM_GLDS", "1") != "0",
              "tile": int(os.environ.get("CXXNET_GLDS_TILE", "-1")),
-             "tune": os.environ.get("CXXNET_GEMM_TUNE", "1") != "0"}
+             "tune": os.environ.get("CXXNET_GEMM_TUNE", "1") != "0",
+             # op classes routed to it: conv fwd, conv dgrad, conv wgrad, fc fwd, fc wgrad
+             "ops": set(os.environ.get("CXXNET_GLDS_OPS", "cf,cd,fc,fw").split(","))}
+# conv weight-grad ("cw") has an LDS-DMA form too, but whole-step A/B measured it 0.6% slower
+# than the register-staged split-K kernel on AlexNet (profiles/r14_ab_glds_ops.jsonl)
 # Autotuning candidates: the 2-stage tiles that run 2-5 blocks per CU measured best on every
 # AlexNet shape (profiles/r14_glds_tiles.jsonl); 2 and 0 cover wide-i GEMMs (fc).
-GLDS_CANDS = (1, 7, 10, 15, 2, 0)
-_TUNE = {}
+GLDS_CANDS = (1, 7, 10, 15, 2, 0, 13, 17)
+# Tuning database: {signature: tile}.  A shipped table for gfx950 (written by
+# benchmarks/tune_db.py on an MI355X) makes tile choice deterministic across runs and
+# data-parallel ranks; shapes it does not hold are timed on first use.
+TUNE_DB = os.environ.get("CXXNET_GEMM_TUNE_DB", os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                               "glds_tune_gfx950.json"))
 
 
-def set_glds(on: bool = True, tile: int = -1, tune: bool = True):
-    """Enable/disable the LDS-DMA GEMM path, force its tile, or turn autotuning off."""
+def _load_tune_db(path):
+    import json
+    try:
+        with open(path) as f:
+            return {str(k): int(v) for k, v in json.load(f).items()}
+    except (OSError, ValueError):
+        return {}
+
+
+_TUNE = _load_tune_db(TUNE_DB)
+
+
+def save_tune_db(path=None):
+    """Write every tile choice made so far (shipped + newly timed) as JSON."""
+    import json
+    with open(path or TUNE_DB, "w") as f:
+        json.dump(dict(sorted(_TUNE.items())), f, indent=0)
+
+
+def set_glds(on: bool = True, tile: int = -1, tune: bool = True, ops=None):
+    """Enable/disable the LDS-DMA GEMM path, force its tile, turn autotuning off, or pick
+    the op classes it serves (subset of cf, cd, cw, fc, fw)."""
     _glds_cfg.update(on=bool(on), tile=int(tile), tune=bool(tune))
+    if ops is not None:
+        _glds_cfg["ops"] = set(ops)
+
+
+def _use(op: str) -> bool:
+    return _glds_cfg["on"] and op in _glds_cfg["ops"]
 
 
 def _tuned_tile(key, run, out, default):
@@ -129,6 +165,7 @@ def _tuned_tile(key, run, out, default):
     sync); the heuristic pick when tuning is off or a graph is being captured."""
     if _glds_cfg["tile"] >= 0:
         return _glds_cfg["tile"]
+    key = "|".join(str(k) for k in key)
     t = _TUNE.get(key)
     if t is not None:
         return t
@@ -166,7 +203,7 @@ def _pick_glds(rows_i, rows_j, groups, nblocks_target=NUM_CU):
     return min((1, 7, 10, 15), key=cost)
 
 
-def _glds(a, b, bmode, out, out_gstride, ldc, *, alpha=1.0, bias=None, bias_gstride=0, relu=False,
+def _glds(a, b, amode, bmode, out, out_gstride, ldc, *, alpha=1.0, bias=None, bias_gstride=0, relu=False,
           mask_relu=False, epi=EPI_BF16, groups=1, ksplit=1, kstride=0, tile=None) -> bool:
     """Run the LDS-DMA kernel; False when it does not support the operands (caller falls back)."""
     if not _glds_cfg["on"]:
@@ -174,7 +211,7 @@ def _glds(a, b, bmode, out, out_gstride, ldc, *, alpha=1.0, bias=None, bias_gstr
     if tile is None:
         tile = _glds_cfg["tile"] if _glds_cfg["tile"] >= 0 else _pick_glds(a.rows, b.rows, groups)
     rc = native.kernels().cxn_gemm_glds(
-        a, b, bmode, out.data_ptr(), out_gstride, ldc, float(alpha),
+        a, b, amode, bmode, out.data_ptr(), out_gstride, ldc, float(alpha),
         bias.data_ptr() if bias is not None else None, bias_gstride, int(relu), int(mask_relu), epi, tile, groups,
         ksplit, kstride, _stream())
     if rc == -1:
@@ -210,7 +247,10 @@ def _gemm_bf16_out(a, b, amode, bmode, out, ldc, *, bias=None, relu=False, mask_
     """out (bf16, [rows_j][ldc]) = epilogue(A . B) for a single-group GEMM, with split-K
     through fp32 slabs + one finalize pass when the output tile grid is too small to
     fill the chip (the FC layers at batch 256: 64 tiles of 128x128 for fc6)."""
-    if amode == DIRECT_K and bmode == DIRECT_K and _glds_cfg["on"] and _fc_glds(a, b, out, ldc, bias, relu, mask_relu):
+    # fc data-grad (A MN-major) stays on the register-staged kernel: its LDS-DMA form measured
+    # slower on AlexNet's fc6-8 (profiles/r14_glds_tiles.jsonl)
+    if bmode == DIRECT_K and amode == DIRECT_K and _use("fc") and \
+            _fc_glds(a, b, GL_K, out, ldc, bias, relu, mask_relu):
         return
     tile = _pick(FC_TILES, a.rows, b.rows, 1, min_blocks=1)
     split = _auto_split(a.rows, b.rows, 1, a.kdim, tile, min_ktiles=8)
@@ -227,15 +267,15 @@ def _gemm_bf16_out(a, b, amode, bmode, out, ldc, *, bias=None, relu=False, mask_
           tile=tile)
 
 
-def _fc_glds(a, b, out, ldc, bias, relu, mask_relu) -> bool:
-    """fc forward on the LDS-DMA kernel (autotuned tile)."""
-    key = ("fc", a.rows, b.rows, a.kdim, ldc)
-    run = lambda t, o: _fc_glds_tile(a, b, o, ldc, bias, relu, mask_relu, t)  # noqa: E731
-    tile = _tuned_tile(key, run, out, lambda: _pick_glds(a.rows, b.rows, 1))
+def _fc_glds(a, b, amode, out, ldc, bias, relu, mask_relu) -> bool:
+    """fc forward (A = W, K-major) / data-grad (A = W, MN-major) on the LDS-DMA kernel."""
+    key = ("fc", amode, a.rows, b.rows, a.kdim, ldc)
+    run = lambda t, o: _fc_glds_tile(a, b, amode, o, ldc, bias, relu, mask_relu, t)  # noqa: E731
+    tile = _tuned_tile(key, run, out, lambda: 1 if amode == GL_MN else _pick_glds(a.rows, b.rows, 1))
     return run(tile, out)
 
 
-def _fc_glds_tile(a, b, out, ldc, bias, relu, mask_relu, tile) -> bool:
+def _fc_glds_tile(a, b, amode, out, ldc, bias, relu, mask_relu, tile) -> bool:
     """split-K through fp32 slabs when the output tile grid cannot fill the chip (fc6 at
     batch 256: 32 tiles of 128x256)."""
     bm, bn = GLDS_TILES[tile]
@@ -246,13 +286,13 @@ def _fc_glds_tile(a, b, out, ldc, bias, relu, mask_relu, tile) -> bool:
         split = _effective_split(a.kdim, split)
         slab = b.rows * ldc
         ws = torch.empty((split, slab), dtype=torch.float32, device=out.device)
-        if not _glds(a, b, B_DIRECT, ws, 0, ldc, epi=EPI_F32, ksplit=split, kstride=slab, tile=tile):
+        if not _glds(a, b, amode, GL_K, ws, 0, ldc, epi=EPI_F32, ksplit=split, kstride=slab, tile=tile):
             return False
         native.check(native.kernels().cxn_splitk_finalize(
             ws.data_ptr(), split, slab, out.data_ptr(), b.rows, ldc,
             bias.data_ptr() if bias is not None else None, int(relu), int(mask_relu), _stream()), "splitk_finalize")
         return True
-    return _glds(a, b, B_DIRECT, out, 0, ldc, bias=bias, relu=relu, mask_relu=mask_relu, tile=tile)
+    return _glds(a, b, amode, GL_K, out, 0, ldc, bias=bias, relu=relu, mask_relu=mask_relu, tile=tile)
 
 
 def _auto_split(rows_i, rows_j, groups, kdim, tile=0, target=2 * NUM_CU, min_ktiles=4):
@@ -291,8 +331,8 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
     A = _op(w, g.cg_out * kd, kd, g.cg_out, kd)
     B = _op(x, cg, 0, g.N * g.Ho * g.Wo, kd, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW,
             stride=g.stride, pad_h=g.pad_y, pad_w=g.pad_x, dil=1, Cg=cg)
-    if va == 8 and _glds_cfg["on"]:
-        run = lambda t, o: _glds(A, B, B_GATHER, o, g.cg_out, g.Cout, bias=bias, bias_gstride=g.cg_out,  # noqa: E731
+    if va == 8 and _use("cf"):
+        run = lambda t, o: _glds(A, B, GL_K, GL_KG, o, g.cg_out, g.Cout, bias=bias, bias_gstride=g.cg_out,  # noqa: E731
                                  relu=relu, groups=g.groups, tile=t)
         key = ("cf", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
         if run(_tuned_tile(key, run, y, lambda: _pick_glds(A.rows, B.rows, g.groups)), y):
@@ -325,8 +365,8 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False):
     A = _op(wt_buf, cg_in * kd, kd, cg_in, kd)
     B = _op(dy, cg_out, 0, g.N * g.H * g.W, kd, H=g.Ho, W=g.Wo, C=g.Cout, Ho=g.H, Wo=g.W, KH=g.KH,
             KW=g.KW, stride=1, pad_h=g.KH - 1 - g.pad_y, pad_w=g.KW - 1 - g.pad_x, dil=g.stride, Cg=cg_out)
-    if g.stride == 1 and _glds_cfg["on"]:
-        run = lambda t, o: _glds(A, B, B_GATHER, o, cg_in, g.C, groups=g.groups, mask_relu=mask_relu,  # noqa: E731
+    if g.stride == 1 and _use("cd"):
+        run = lambda t, o: _glds(A, B, GL_K, GL_KG, o, cg_in, g.C, groups=g.groups, mask_relu=mask_relu,  # noqa: E731
                                  tile=t)
         key = ("cd", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
         if run(_tuned_tile(key, run, dx, lambda: _pick_glds(A.rows, B.rows, g.groups)), dx):
@@ -352,6 +392,16 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
     A = _op(x, cg, 0, kd, P, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW, stride=g.stride,
             pad_h=g.pad_y, pad_w=g.pad_x, dil=1, Cg=cg)
     B = _op(dy, g.cg_out, g.Cout, g.cg_out, P)
+    if _use("cw") and va == 8:
+        def run(t, o):
+            bm, bn = GLDS_TILES[t]
+            tiles = _cdiv(kd, bm) * _cdiv(g.cg_out, bn) * g.groups
+            split = max(1, min(2 * NUM_CU // max(tiles, 1), _cdiv(P, 64) // 16))
+            return _glds(A, B, GL_MNG, GL_MN, o, g.cg_out * kd, kd, epi=EPI_F32_ATOMIC_G, groups=g.groups,
+                         ksplit=split, tile=t)
+        key = ("cw", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
+        if run(_tuned_tile(key, run, dw, lambda: 1), dw):
+            return
     tile = _pick(WGRAD_TILES, kd, g.cg_out, g.groups, min_blocks=1)
     split = _auto_split(kd, g.cg_out, g.groups, P, tile)
     _gemm(A, B, GATHER_MN, DIRECT_MN, va, 8, dw, g.cg_out * kd, kd, epi=EPI_F32_ATOMIC, groups=g.groups,
@@ -406,4 +456,13 @@ def fc_backward_weight(x, dy, dw, overwrite=False):
     nout = dy.shape[1]
     A = _op(x, 0, nin, nin, Bn)
     Bo = _op(dy, 0, nout, nout, Bn)
+    if _use("fw"):
+        epi = EPI_F32 if overwrite else EPI_F32_ACC_G
+        run = lambda t, o: _glds(A, Bo, GL_MN, GL_MN, o, 0, nin, epi=epi, tile=t)  # noqa: E731
+        if overwrite:
+            tile = _tuned_tile(("fw", nin, nout, Bn), run, dw, lambda: 1)
+        else:  # += epilogue: never time it on the live buffer
+            tile = _TUNE.get(f"fw|{nin}|{nout}|{Bn}", 1) if _glds_cfg["tile"] < 0 else _glds_cfg["tile"]
+        if run(tile, dw):
+            return
     _gemm(A, Bo, DIRECT_MN, DIRECT_MN, 8, 8, dw, 0, nin, epi=EPI_F32 if overwrite else EPI_F32_ACC)
