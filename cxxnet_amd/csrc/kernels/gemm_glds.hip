@@ -4,10 +4,13 @@
 // with each operand loaded by one of four loaders:
 //   K_DIRECT  : elem(row,k) = p[row*ld + k]          (k contiguous)
 //   K_GATHER  : rows = output pixels, k = (kh,kw,c)   implicit im2col of an NHWC tensor
+//   K_ROWGATHER: rows = output pixels, k = (kh, j)   j over a kernel row's KW*C contiguous
+//               elements, zero-padded to 8 (few-channel convs: conv1's 11x11x4 runs of 44)
 //   MN_DIRECT : elem(row,k) = p[k*ld + row]          (row contiguous)
 //   MN_GATHER : rows = (kh,kw,c), k = output pixels   transposed implicit im2col
-// It serves every GEMM-shaped op of AlexNet-class nets except conv1 (3 input channels):
+// It serves the GEMM-shaped ops of AlexNet-class nets:
 //   conv forward     A K_DIRECT (weights)        B K_GATHER (x)          bf16 out   (reference K1-K4)
+//   conv1 forward    A K_DIRECT (row-padded w)   B K_ROWGATHER (x)       bf16 out
 //   conv data-grad   A K_DIRECT (flipped w)      B K_GATHER (dy)         bf16 out   (reference K7+K8)
 //   conv weight-grad A MN_GATHER (x)             B MN_DIRECT (dy)        fp32 atomics, split-K (K5/K6)
 //   fc forward       A K_DIRECT (W)              B K_DIRECT (x)          bf16 / split-K slabs (K9)
@@ -45,7 +48,7 @@ constexpr uint32_t OOB = 0x80000000u;  // >= num_records: the load returns zeros
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef __attribute__((address_space(3))) void lds_void;
 
-enum { K_DIRECT = 0, K_GATHER = 1, MN_DIRECT = 2, MN_GATHER = 3 };
+enum { K_DIRECT = 0, K_GATHER = 1, MN_DIRECT = 2, MN_GATHER = 3, K_ROWGATHER = 4 };
 enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_ACC = 2, EPI_F32_ATOMIC = 3 };
 
 struct GOperand {
@@ -54,7 +57,8 @@ struct GOperand {
   uint32_t nbytes;  // descriptor range (all groups)
   int ld, rows, kdim;
   int H, W, C, Ho, Wo, KW, stride, pad_h, pad_w, Cg;  // gather geometry (NHWC source)
-  FastDiv fd_cg, fd_kw, fd_hw, fd_wo;
+  int KH, rlc;  // row gather: kernel rows, 16-byte chunks per (zero-padded) kernel-row run
+  FastDiv fd_cg, fd_kw, fd_hw, fd_wo, fd_rlc;
 };
 
 struct GEpi {
@@ -93,7 +97,7 @@ __device__ __forceinline__ void block_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-constexpr bool kmajor(int mode) { return mode == K_DIRECT || mode == K_GATHER; }
+constexpr bool kmajor(int mode) { return mode == K_DIRECT || mode == K_GATHER || mode == K_ROWGATHER; }
 
 // ---------------------------------------------------------------------------------- operands
 // One operand tile: R rows (i or j) x BK k, R*128 bytes, R/32 DMA instructions per wave
@@ -117,6 +121,20 @@ struct Op {
         const int r = row0 + 8 * (wave + 4 * s) + (lane >> 3);
         if constexpr (MODE == K_DIRECT) {
           s0[s] = r < op.rows ? static_cast<int>(goff + static_cast<uint32_t>(r * op.ld) * 2u) : -1;
+          s1[s] = s2[s] = 0;
+        } else if constexpr (MODE == K_ROWGATHER) {
+          // byte offset of the pixel's first kernel-row run (pad 0: every run is in bounds)
+          if (r < op.rows) {
+            const uint32_t n = fdiv(static_cast<uint32_t>(r), op.fd_hw);
+            const uint32_t rem = static_cast<uint32_t>(r) - n * static_cast<uint32_t>(op.Ho * op.Wo);
+            const uint32_t ho = fdiv(rem, op.fd_wo);
+            const uint32_t wo = rem - ho * op.Wo;
+            s0[s] = static_cast<int>(goff) +
+                    ((static_cast<int>(n) * op.H + static_cast<int>(ho) * op.stride) * op.W +
+                     static_cast<int>(wo) * op.stride) * op.C * 2;
+          } else {
+            s0[s] = -1;
+          }
           s1[s] = s2[s] = 0;
         } else {
           if (r < op.rows) {
@@ -169,7 +187,14 @@ struct Op {
     if constexpr (kmajor(MODE)) {
       p.k = kt * BK + lchunk * 8;
       p.kin = kt < kt_end && p.k < op.kdim;
-      if constexpr (MODE == K_GATHER) {
+      if constexpr (MODE == K_ROWGATHER) {
+        // k = (kernel row kh, position j in the row's KW*C-element run padded to rlc chunks)
+        const int kc = kt * (BK / 8) + lchunk;
+        const int kh = static_cast<int>(fdiv(static_cast<uint32_t>(kc), op.fd_rlc));
+        p.kin = p.kin && kh < op.KH;
+        p.kh = p.kw = 0;
+        p.cb = static_cast<uint32_t>(kh * op.W * op.C + (kc - kh * op.rlc) * 8) * 2u;
+      } else if constexpr (MODE == K_GATHER) {
         const uint32_t r = fdiv(static_cast<uint32_t>(p.k), op.fd_cg);
         const int c = p.k - static_cast<int>(r) * op.Cg;
         const uint32_t q = fdiv(r, op.fd_kw);
@@ -194,6 +219,8 @@ struct Op {
     uint32_t off;
     if constexpr (MODE == K_DIRECT) {
       off = (p.kin && s0[S] >= 0) ? static_cast<uint32_t>(s0[S]) + static_cast<uint32_t>(p.k) * 2u : OOB;
+    } else if constexpr (MODE == K_ROWGATHER) {
+      off = (p.kin && s0[S] >= 0) ? static_cast<uint32_t>(s0[S]) + p.cb : OOB;
     } else if constexpr (MODE == K_GATHER) {
       const int hi = s1[S] + p.kh, wi = s2[S] + p.kw;
       const bool ok = s0[S] >= 0 && static_cast<unsigned>(hi) < static_cast<unsigned>(op.H) &&
@@ -474,6 +501,7 @@ void launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int
 int dispatch(int amode, int bmode, int epi, int tile, const GOperand &A, const GOperand &B, const GEpi &E,
              int groups, int ksplit, hipStream_t s) {
   CXG_CASE(K_DIRECT, K_GATHER, EPI_BF16, CXG_KK_TILES)    // conv fwd / dgrad
+  CXG_CASE(K_DIRECT, K_ROWGATHER, EPI_BF16, CXG_KK_TILES)  // conv fwd, few input channels (conv1)
   CXG_CASE(K_DIRECT, K_DIRECT, EPI_BF16, CXG_KK_TILES)    // fc fwd
   CXG_CASE(K_DIRECT, K_DIRECT, EPI_F32, CXG_KK_TILES)     // fc fwd split-K
   CXG_CASE(MN_GATHER, MN_DIRECT, EPI_F32_ATOMIC, CXG_MM_TILES)  // conv wgrad
@@ -504,6 +532,9 @@ namespace {
 bool supported(const CxnOperandG *o, int mode) {
   if (o->nbytes >= (1L << 31) || (reinterpret_cast<uintptr_t>(o->ptr) & 15) || o->gstride % 8 != 0) return false;
   if (mode == K_DIRECT || mode == MN_DIRECT) return o->ld % 8 == 0 && (mode == K_DIRECT || o->rows % 8 == 0);
+  if (mode == K_ROWGATHER)  // whole kernel rows read as runs: no padding, one group, 8-byte aligned pixels
+    return o->pad_h == 0 && o->pad_w == 0 && o->Cg == o->C && o->C % 4 == 0 && o->dil <= 1 &&
+           o->kdim == o->KH * ((o->KW * o->C + 7) / 8) * 8;
   if (o->Cg % 8 != 0 || o->C % 8 != 0 || o->dil > 1) return false;
   return mode == K_GATHER || o->rows % 8 == 0;
 }
@@ -517,6 +548,14 @@ void fill(GOperand &r, const CxnOperandG *o, int mode) {
     r.stride = o->stride; r.pad_h = o->pad_h; r.pad_w = o->pad_w; r.Cg = o->Cg;
     r.fd_cg = make_fastdiv(o->Cg);
     r.fd_kw = make_fastdiv(o->KW > 0 ? o->KW : 1);
+    r.fd_hw = make_fastdiv(o->Ho * o->Wo > 0 ? o->Ho * o->Wo : 1);
+    r.fd_wo = make_fastdiv(o->Wo > 0 ? o->Wo : 1);
+  }
+  if (mode == K_ROWGATHER) {
+    r.H = o->H; r.W = o->W; r.C = o->C; r.Ho = o->Ho; r.Wo = o->Wo; r.KW = o->KW; r.KH = o->KH;
+    r.stride = o->stride; r.pad_h = r.pad_w = 0; r.Cg = o->Cg;
+    r.rlc = (o->KW * o->C + 7) / 8;
+    r.fd_rlc = make_fastdiv(r.rlc);
     r.fd_hw = make_fastdiv(o->Ho * o->Wo > 0 ? o->Ho * o->Wo : 1);
     r.fd_wo = make_fastdiv(o->Wo > 0 ? o->Wo : 1);
   }

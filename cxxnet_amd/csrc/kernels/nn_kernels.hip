@@ -950,6 +950,17 @@ __global__ void channel_copy(const bf16_t *__restrict__ src, int Cs, int soff, b
   }
 }
 
+// dst[r][0:L] = src[r][0:L], dst[r][L:Lp] = 0 (row-padded copy, e.g. conv1 weights for the
+// row-gather GEMM: [Cout][KH][KW*C] -> [Cout][KH][roundup(KW*C, 8)])
+__global__ void pad_rows(const bf16_t *__restrict__ src, bf16_t *__restrict__ dst, long rows, int L, int Lp) {
+  const long total = rows * Lp;
+  for (long i = grid_stride_start(); i < total; i += grid_stride()) {
+    const long r = i / Lp;
+    const int c = static_cast<int>(i - r * Lp);
+    dst[i] = c < L ? src[r * L + c] : static_cast<bf16_t>(0);
+  }
+}
+
 }  // namespace
 
 // ================================================================== C ABI
@@ -1158,5 +1169,10 @@ CXN_API int cxn_channel_copy(const void *src, int Cs, int soff, void *dst, int C
                              int accumulate, void *stream) {
   channel_copy<<<nblocks(npix * Cc), NT, 0, S_>>>((const bf16_t *)src, Cs, soff, (bf16_t *)dst, Cd, doff, Cc, npix,
                                                   accumulate);
+  RET;
+}
+
+CXN_API int cxn_pad_rows(const void *src, void *dst, long rows, int L, int Lp, void *stream) {
+  pad_rows<<<nblocks(rows * Lp), NT, 0, S_>>>((const bf16_t *)src, (bf16_t *)dst, rows, L, Lp);
   RET;
 }

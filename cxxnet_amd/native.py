@@ -67,6 +67,7 @@ _SIGS = {
                  _P, _L, _I, _F, _P, _L, _I, _I, _I, _I, _I, _I, _L, _P],
     "cxn_gemm_glds": [ctypes.POINTER(CxnOperand), ctypes.POINTER(CxnOperand), _I, _I, _P, _L, _I, _F, _P, _L, _I,
                       _I, _I, _I, _I, _I, _L, _P],
+    "cxn_pad_rows": [_P, _P, _L, _I, _I, _P],
     "cxn_splitk_finalize": [_P, _I, _L, _P, _L, _I, _P, _I, _I, _P],
     "cxn_nchw_f32_to_nhwc_bf16": [_P, _P, _I, _I, _I, _I, _I, _F, _P],
     "cxn_image_u8_to_nhwc_bf16": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _P, _P],

@@ -109,13 +109,13 @@ GLDS_TILES = {0: (128, 256), 1: (128, 128), 2: (128, 128), 4: (192, 256), 5: (64
               7: (64, 128), 8: (192, 128), 9: (96, 128), 10: (128, 64), 11: (64, 128), 12: (64, 128),
               13: (128, 128), 14: (128, 64), 15: (64, 64), 16: (192, 64), 17: (128, 128)}
 # operand loaders of gemm_glds.hip
-GL_K, GL_KG, GL_MN, GL_MNG = 0, 1, 2, 3  # K_DIRECT, K_GATHER, MN_DIRECT, MN_GATHER
+GL_K, GL_KG, GL_MN, GL_MNG, GL_KR = 0, 1, 2, 3, 4  # K_DIRECT, K_GATHER, MN_DIRECT, MN_GATHER, K_ROWGATHER
 EPI_F32_ACC_G, EPI_F32_ATOMIC_G = 2, 3
 _glds_cfg = {"on": os.environ.get("CXXNET_GEMM_GLDS", "1") != "0",
              "tile": int(os.environ.get("CXXNET_GLDS_TILE", "-1")),
              "tune": os.environ.get("CXXNET_GEMM_TUNE", "1") != "0",
-             # op classes routed to it: conv fwd, conv dgrad, conv wgrad, fc fwd, fc wgrad
-             "ops": set(os.environ.get("CXXNET_GLDS_OPS", "cf,cd,fc,fw").split(","))}
+             # op classes routed to it: conv fwd, conv1-style row-gather fwd, conv dgrad, conv wgrad, fc fwd, fc wgrad
+             "ops": set(os.environ.get("CXXNET_GLDS_OPS", "cf,cr,cd,fc,fw").split(","))}
 # conv weight-grad ("cw") has an LDS-DMA form too, but whole-step A/B measured it 0.6% slower
 # than the register-staged split-K kernel on AlexNet (profiles/r14_ab_glds_ops.jsonl)
 # Autotuning candidates: the 2-stage tiles that run 2-5 blocks per CU measured best on every
@@ -314,6 +314,23 @@ def _w_nchw(w: torch.Tensor) -> torch.Tensor:
     return w.permute(0, 3, 1, 2).contiguous()
 
 
+_wpad = {}
+
+
+def _row_padded_weights(w, g: ConvGeom):
+    """[Cout][KH][KW][C] -> [Cout][KH][roundup(KW*C, 8)] with zero tails (refreshed every call:
+    the optimizer rewrites w each step).  The buffer is cached per weight tensor."""
+    L = g.KW * g.C
+    lp = (L + 7) // 8 * 8
+    key = (w.data_ptr(), tuple(w.shape))
+    buf = _wpad.get(key)
+    if buf is None:
+        buf = _wpad[key] = torch.empty((g.Cout, g.KH, lp), dtype=w.dtype, device=w.device)
+    native.check(native.kernels().cxn_pad_rows(w.data_ptr(), buf.data_ptr(), g.Cout * g.KH, L, lp, _stream()),
+                 "pad_rows")
+    return buf, lp
+
+
 def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
     """y = conv(x, w) + bias (optionally relu).  x/y NHWC."""
     if not x.is_cuda:
@@ -336,6 +353,18 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
                                  relu=relu, groups=g.groups, tile=t)
         key = ("cf", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
         if run(_tuned_tile(key, run, y, lambda: _pick_glds(A.rows, B.rows, g.groups)), y):
+            return
+    if va != 8 and g.groups == 1 and g.pad_y == 0 and g.pad_x == 0 and g.C % 4 == 0 and _use("cr"):
+        # few input channels (conv1: 11x11 taps of 4 channels): each kernel row's KW*C
+        # elements are contiguous in NHWC; the GEMM reads them as zero-padded runs
+        wp, lp = _row_padded_weights(w, g)
+        kr = g.KH * lp
+        Ar = _op(wp, 0, kr, g.Cout, kr)
+        Br = _op(x, 0, 0, g.N * g.Ho * g.Wo, kr, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW,
+                 stride=g.stride, pad_h=0, pad_w=0, dil=1, Cg=g.C)
+        run = lambda t, o: _glds(Ar, Br, GL_K, GL_KR, o, 0, g.Cout, bias=bias, relu=relu, tile=t)  # noqa: E731
+        key = ("cr", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride)
+        if run(_tuned_tile(key, run, y, lambda: 1), y):
             return
     tile = _pick(CONV_FWD_TILES if va == 8 else CONV_FWD_TILES_V4, g.cg_out, g.N * g.Ho * g.Wo, g.groups)
     _gemm(A, B, DIRECT_K, GATHER_K, va, va, y, g.cg_out, g.Cout, bias=bias, bias_gstride=g.cg_out, relu=relu, tile=tile,
