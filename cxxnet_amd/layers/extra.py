@@ -1,15 +1,17 @@
 """Remaining reference layers: bias, split, concat, ch_concat, batch_norm, prelu,
 insanity, insanity_max_pooling, fixconn, pairtest.
 
-These are not on the benchmark models' hot path; their device math is written with
-torch tensor ops on the node buffers (fp32 internally) except concat/split/bias,
-which use the HIP channel-copy / add / column-sum kernels on the GPU.
+On the GPU every one of them runs hand-written HIP kernels: batch_norm / prelu / insanity /
+insanity_max_pooling in csrc/kernels/layer_kernels.hip (ops/layer_ops.py), concat / split /
+bias on the channel-copy / add / column-sum kernels, fixconn on the MFMA GEMM.  The CPU
+executor runs the same formulas in fp32 torch with the same counter-hash random draws.
 """
 from __future__ import annotations
 
 import torch
 
 from .. import ops
+from ..ops import layer_ops as L
 from .base import BinReader, BinWriter, Layer, ParamSpec
 from .std import PoolingLayer, _bias_init, _check
 
@@ -37,7 +39,18 @@ class BiasLayer(Layer):
 
     def forward(self, is_train, nodes_in, nodes_out):
         m = nodes_in[0].mat()
-        m.copy_((m.float() + self.params[0].w).to(m.dtype))
+        if m.is_cuda:  # y = 1*x + b on the BN affine kernel: mean 0, inv 1, slope 1
+            st = self._affine(m.shape[1], m.device)
+            L.affine_forward(m, m, st.mean, st.inv, self._ones, self.params[0].w)
+        else:
+            m.copy_((m.float() + self.params[0].w).to(m.dtype))
+
+    def _affine(self, C, device):
+        if getattr(self, "_st", None) is None:
+            self._st = L.BNState(C, device)
+            self._st.inv.fill_(1.0)
+            self._ones = torch.ones(C, dtype=torch.float32, device=device)
+        return self._st
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
         ops.bias_grad(nodes_in[0].mat(), self.params[0].g)
@@ -64,14 +77,16 @@ class SplitLayer(Layer):
             o.set_shape(*nodes_in[0].shape, cp=nodes_in[0].cp)
 
     def forward(self, is_train, nodes_in, nodes_out):
+        x = nodes_in[0].data
         for o in nodes_out:
-            o.data.copy_(nodes_in[0].data)
+            C = x.shape[-1]
+            ops.channel_copy(x, 0, o.data, 0, C)
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
         if not prop_grad:
             return
         x = nodes_in[0].data
-        x.copy_(nodes_out[0].data)
+        ops.channel_copy(nodes_out[0].data, 0, x, 0, x.shape[-1])
         for o in nodes_out[1:]:
             ops.add(x, o.data, x)
 
@@ -118,7 +133,14 @@ class ConcatLayer(Layer):
             for src, dst, off, c in self._pieces(nodes_in, nodes_out):
                 ops.channel_copy(src, 0, dst, off, c)
         else:
-            torch.cat([n.data for n in nodes_in], dim=2, out=nodes_out[0].data)
+            # width concat: rows of [B*H][W_i*C] into [B*H][W*C] at a column offset
+            out = nodes_out[0].data
+            B, H, W, C = out.shape
+            off = 0
+            for n in nodes_in:
+                wi = n.data.shape[2]
+                ops.channel_copy(n.data.reshape(B * H, wi * C), 0, out.view(B * H, W * C), off * C, wi * C)
+                off += wi
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
         if not prop_grad:
@@ -127,11 +149,13 @@ class ConcatLayer(Layer):
             for src, dst, off, c in self._pieces(nodes_in, nodes_out):
                 ops.channel_copy(dst, off, src, 0, c)
         else:
+            out = nodes_out[0].data
+            B, H, W, C = out.shape
             off = 0
             for n in nodes_in:
-                w = n.shape[3]
-                n.data.copy_(nodes_out[0].data[:, :, off:off + w, :])
-                off += w
+                wi = n.data.shape[2]
+                ops.channel_copy(out.view(B * H, W * C), off * C, n.data.view(B * H, wi * C), 0, wi * C)
+                off += wi
 
 
 class BatchNormLayer(Layer):
@@ -163,36 +187,23 @@ class BatchNormLayer(Layer):
                        ParamSpec("bias", (self.channel,), _bias_init(self.init_bias))]
 
     def _view(self, node):
-        # -> [rows][channels] fp32 view of the buffer
+        # -> [rows][channels] view of the NHWC / matrix buffer
         return node.data.view(-1, self.channel)
 
+    def _state(self, device):
+        if getattr(self, "_st", None) is None:
+            self._st = L.BNState(self.channel, device)
+        return self._st
+
     def forward(self, is_train, nodes_in, nodes_out):
-        x = self._view(nodes_in[0]).float()
-        mean = x.mean(0)
-        var = ((x - mean) ** 2).mean(0)
-        xhat = (x - mean) / torch.sqrt(var + self.eps)
-        slope, bias = self.params[0].w, self.params[1].w
-        if is_train:
-            self.saved = (x.clone(), mean, var)
-            self._view(nodes_in[0]).copy_(xhat)
-        self._view(nodes_out[0]).copy_(xhat * slope + bias)
+        x = self._view(nodes_in[0])
+        L.bn_forward(x, self._view(nodes_out[0]), self.params[0].w, self.params[1].w, self.eps,
+                     self._state(x.device), is_train)
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
-        x, mean, var = self.saved
-        g = self._view(nodes_out[0]).float()
-        xhat = self._view(nodes_in[0]).float()
-        slope = self.params[0].w
-        n = x.shape[0]
-        scale = 1.0 / n
-        inv = 1.0 / torch.sqrt(var + self.eps)
-        gvar = ((g * slope) * (x - mean) * -0.5 * (var + self.eps).pow(-1.5)).sum(0)
-        gexp = (g * slope).sum(0) * -inv
-        gexp = gexp + gvar * (scale * (-2.0 * (x - mean)).sum(0))
-        self.params[0].g.add_((g * xhat).sum(0))
-        self.params[1].g.add_(g.sum(0))
-        if prop_grad:
-            dx = g * slope * inv + gvar * scale * 2.0 * (x - mean) + gexp * scale
-            self._view(nodes_in[0]).copy_(dx)
+        g = self._view(nodes_out[0])
+        L.bn_backward(g, self._view(nodes_in[0]), self.params[0].w, self.params[0].g, self.params[1].g,
+                      self._state(g.device), prop_grad)
 
     def save_model(self, fo: BinWriter):
         fo.write_tensor(self.params[0].w)
@@ -216,6 +227,7 @@ class PReluLayer(Layer):
         self.init_slope = 0.25
         self.init_random = 0
         self.random = 0.0
+        self.seed = int(torch.randint(0, 2**31 - 1, (1,), generator=ctx.gen).item())
 
     def set_param(self, name, val):
         super().set_param(name, val)
@@ -238,23 +250,18 @@ class PReluLayer(Layer):
                 t.uniform_(0, 1, generator=self.ctx.gen).mul_(self.init_slope)
         self.params = [ParamSpec("bias", (self.channel,), init)]
 
+    def _noise(self, is_train):
+        return self.random if is_train else 0.0
+
     def forward(self, is_train, nodes_in, nodes_out):
-        x = nodes_in[0].data.view(-1, self.channel).float()
-        slope = self.params[0].w
-        if is_train and self.random > 0:
-            u = torch.rand(x.shape, device=x.device)
-            mask = slope * (1 + u * self.random * 2.0 - self.random)
-        else:
-            mask = slope.expand_as(x)
-        self.mask = mask.clamp(0, 1)
-        nodes_out[0].data.view(-1, self.channel).copy_(torch.where(x > 0, x, x * self.mask))
+        self._train = is_train
+        L.prelu_forward(nodes_in[0].data.view(-1, self.channel), nodes_out[0].data.view(-1, self.channel),
+                        self.params[0].w, self.seed, self.ctx.step_counter, self._noise(is_train))
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
-        x = nodes_in[0].data.view(-1, self.channel).float()
-        g = nodes_out[0].data.view(-1, self.channel).float()
-        self.params[0].g.add_((torch.clamp(x, max=0) * g).sum(0))
-        if prop_grad:
-            nodes_in[0].data.view(-1, self.channel).copy_(torch.where(x > 0, g, g * self.mask))
+        x = nodes_in[0].data.view(-1, self.channel)
+        L.prelu_backward(x, nodes_out[0].data.view(-1, self.channel), x, self.params[0].w, self.params[0].g,
+                         self.seed, self.ctx.step_counter, self._noise(getattr(self, "_train", True)), prop_grad)
 
     def save_model(self, fo: BinWriter):
         fo.write_tensor(self.params[0].w)
@@ -278,6 +285,7 @@ class InsanityLayer(Layer):
         self.sat_start = self.sat_end = 0
         self.delta = 0.0
         self.inited = False
+        self.seed = int(torch.randint(0, 2**31 - 1, (1,), generator=ctx.gen).item())
 
     def set_param(self, name, val):
         super().set_param(name, val)
@@ -305,21 +313,15 @@ class InsanityLayer(Layer):
             self.lb += self.delta * self.step
             self.step += 1
         x = nodes_in[0].data
-        xf = x.float()
-        if is_train:
-            self.mask = torch.rand(x.shape, device=x.device) * (self.ub - self.lb) + self.lb
-        else:
-            self.mask = torch.full_like(xf, (self.lb + self.ub) / 2.0)
-        y = torch.where(xf > 0, xf, xf / self.mask)
-        x.copy_(y)
-        if nodes_out[0] is not nodes_in[0]:
-            nodes_out[0].data.copy_(y)
+        self._train = is_train
+        y2 = nodes_out[0].data if nodes_out[0] is not nodes_in[0] else None
+        L.insanity_forward(x, x, y2, self.lb, self.ub, is_train, self.seed, self.ctx.step_counter)
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
         if prop_grad:
-            y = nodes_in[0].data.float()
-            g = nodes_out[0].data.float()
-            nodes_in[0].data.copy_(torch.where(y > 0, g, g / self.mask))
+            y = nodes_in[0].data
+            L.insanity_backward(y, nodes_out[0].data, y, self.lb, self.ub, getattr(self, "_train", True), self.seed,
+                                self.ctx.step_counter)
 
 
 class InsanityPoolingLayer(PoolingLayer):
@@ -330,48 +332,35 @@ class InsanityPoolingLayer(PoolingLayer):
         super().__init__(ctx, "max")
         self.type_name = "insanity_max_pooling"
         self.keep = 1.0
+        self.seed = int(torch.randint(0, 2**31 - 1, (1,), generator=ctx.gen).item())
 
     def set_param(self, name, val):
         super().set_param(name, val)
         if name == "keep":
             self.keep = float(val)
 
-    def _shift_index(self, H, W, device):
-        u = torch.rand(H * W, device=device)
-        d = (1.0 - self.keep) / 4.0
-        ys = torch.arange(H, device=device).repeat_interleave(W)
-        xs = torch.arange(W, device=device).repeat(H)
-        ys = torch.where((u >= self.keep) & (u < self.keep + d), (ys - 1).clamp_min(0), ys)
-        ys = torch.where((u >= self.keep + d) & (u < self.keep + 2 * d), (ys + 1).clamp_max(H - 1), ys)
-        xs = torch.where((u >= self.keep + 2 * d) & (u < self.keep + 3 * d), (xs - 1).clamp_min(0), xs)
-        xs = torch.where(u >= self.keep + 3 * d, (xs + 1).clamp_max(W - 1), xs)
-        return ys * W + xs
-
     def forward(self, is_train, nodes_in, nodes_out):
-        x = nodes_in[0].data
-        if not is_train or self.keep >= 1.0:
+        self._shifted = is_train and self.keep < 1.0
+        if not self._shifted:
             return super().forward(is_train, nodes_in, nodes_out)
-        N, H, W, C = x.shape
-        self.idx = self._shift_index(H, W, x.device)
-        self.shifted = x.view(N, H * W, C)[:, self.idx, :].view_as(x).contiguous()
-        lp = self.lp
-        st = self._state(nodes_out[0])
-        ops.pool_forward(self.shifted, nodes_out[0].data, st, lp.kernel_height, lp.kernel_width, lp.stride,
-                         lp.pad_y, "max")
+        y = nodes_out[0].data
+        if getattr(self, "ysave", None) is None or self.ysave.shape != y.shape:
+            self.ysave = torch.empty_like(y)
+        L.ins_pool_forward(nodes_in[0].data, y, self.ysave, self.lp.kernel_height, self.lp.stride, self.keep,
+                           self.seed, self.ctx.step_counter)
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
         if not prop_grad:
             return
-        if self.keep >= 1.0:
+        if not getattr(self, "_shifted", False):
             return super().backprop(prop_grad, nodes_in, nodes_out)
-        lp = self.lp
         x = nodes_in[0].data
-        N, H, W, C = x.shape
-        gs = torch.empty_like(self.shifted)
-        ops.pool_backward(self.shifted, self.state, nodes_out[0].data, gs, lp.kernel_height, lp.kernel_width,
-                          lp.stride, lp.pad_y, "max")
-        # each source pixel's gradient comes from its (shifted) slot: gather-form, like the reference
-        x.view(N, H * W, C).copy_(gs.view(N, H * W, C))
+        if getattr(self, "gscratch", None) is None or self.gscratch.shape != x.shape:
+            self.gscratch = torch.empty_like(x)
+        # gather-form unpool reads shifted neighbours of x: write to scratch, then copy back
+        L.ins_pool_backward(x, self.ysave, nodes_out[0].data, self.gscratch, self.lp.kernel_height, self.lp.stride,
+                            self.keep, self.seed, self.ctx.step_counter)
+        ops.channel_copy(self.gscratch, 0, x, 0, x.shape[-1])
 
 
 class FixConnectLayer(Layer):

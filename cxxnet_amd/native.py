@@ -68,6 +68,14 @@ _SIGS = {
     "cxn_gemm_glds": [ctypes.POINTER(CxnOperand), ctypes.POINTER(CxnOperand), _I, _I, _P, _L, _I, _F, _P, _L, _I,
                       _I, _I, _I, _I, _I, _L, _P],
     "cxn_pad_rows": [_P, _P, _L, _I, _I, _P],
+    "cxn_chan_reduce": [_P, _P, _P, _P, _L, _I, _I, _P],
+    "cxn_bn_stats": [_P, _P, _P, _P, _L, _I, _F, _P],
+    "cxn_bn_fwd": [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
+    "cxn_bn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
+    "cxn_prelu": [_P, _P, _P, _P, _L, _I, _U, _P, _F, _I, _P],
+    "cxn_insanity": [_P, _P, _P, _P, _L, _F, _F, _I, _U, _P, _I, _P],
+    "cxn_ins_pool_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _U, _P, _P],
+    "cxn_ins_pool_bwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _U, _P, _P],
     "cxn_splitk_finalize": [_P, _I, _L, _P, _L, _I, _P, _I, _I, _P],
     "cxn_nchw_f32_to_nhwc_bf16": [_P, _P, _I, _I, _I, _I, _I, _F, _P],
     "cxn_image_u8_to_nhwc_bf16": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _P, _P],

@@ -320,3 +320,26 @@ bias:wd = 0.0
     assert torch.allclose(got, params["w1"], rtol=1e-3, atol=1e-5)
     assert torch.allclose(weights(tr, 10, "wmat"), params["wf2"], rtol=1e-3, atol=1e-5)
     assert torch.allclose(weights(tr, 8, "bias"), params["bf1"], rtol=1e-3, atol=1e-5)
+
+
+def test_exotic_layers_train_cpu():
+    """batch_norm / prelu (noisy) / split / ch_concat / bias / insanity in one net: two CPU
+    training steps stay finite and move every parameter."""
+    import torch
+    from cxxnet_amd import native
+    from cxxnet_amd.io.data import DataBatch
+    from cxxnet_amd.nnet import NetTrainer
+    from test_layer_kernels_gpu import EXOTIC
+    tr = NetTrainer()
+    for k, v in list(native.rt().parse_config(EXOTIC)) + [("batch_size", "4"), ("dev", "cpu"), ("seed", "2"),
+                                                          ("silent", "1"), ("eval_train", "0")]:
+        tr.set_param(k, v)
+    tr.init_model()
+    before = tr.net.arena.w.clone()
+    g = torch.Generator().manual_seed(0)
+    x, y = torch.randn(4, 8, 8, 8, generator=g), torch.randint(0, 10, (4, 1), generator=g).float()
+    for _ in range(2):
+        tr.update(DataBatch(x, y))
+    assert torch.isfinite(tr.net.nodes[-1].fp32_view).all()
+    for _, s in tr.net.arena.specs:
+        assert not torch.equal(before[s.offset:s.offset + s.numel], tr.net.arena.w[s.offset:s.offset + s.numel]), s.tag
