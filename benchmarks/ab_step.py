@@ -2,7 +2,8 @@
 configurations (per guide rule: perf deltas come from interleaved rounds in ONE process).
 
   python benchmarks/ab_step.py --configs "all:cf,cd,cw,fc,fw" "no_cw:cf,cd,fc,fw" --rounds 5
-Each config is `name:glds-op-classes` ("none" = register-staged kernel everywhere).
+Each config is `name:glds-op-classes[:ov]` ("none" = register-staged kernel everywhere; ":ov" runs
+the optimizer per gradient bucket on a side stream, overlapped with the rest of backward).
 Prints one JSON line per config: median / min ms per step over the rounds.
 """
 import argparse
@@ -48,12 +49,18 @@ def main():
 
     cfgs = []
     for spec in a.configs:
-        name, ops = spec.split(":")
-        cfgs.append((name, [] if ops == "none" else ops.split(",")))
-    times = {n: [] for n, _ in cfgs}
+        name, ops, *flags = spec.split(":")
+        cfgs.append((name, [] if ops == "none" else ops.split(","), "ov" in flags))
+    net = tr.net
+    ov_fn = lambda ranges: net.update(tr.epoch_counter, ranges)  # noqa: E731
+    times = {n: [] for n, _, _ in cfgs}
     for r in range(a.rounds):
-        for name, ops in cfgs:
+        for name, ops, ov in cfgs:
             G.set_glds(on=bool(ops), ops=ops)
+            if ov:
+                tr.reducer.enable_overlapped_update(ov_fn)
+            else:
+                tr.reducer.update_fn = None
             for _ in range(3):
                 tr.update(batch, local=True)
             torch.cuda.synchronize()
@@ -62,7 +69,7 @@ def main():
                 tr.update(batch, local=True)
             torch.cuda.synchronize()
             times[name].append((time.perf_counter() - t0) / a.steps * 1000.0)
-    for name, _ in cfgs:
+    for name, _, _ in cfgs:
         ts = times[name]
         print(json.dumps({"config": name, "median_ms": round(statistics.median(ts), 4), "min_ms": round(min(ts), 4),
                           "img_s_median": round(a.batch / statistics.median(ts) * 1000.0, 1)}), flush=True)

@@ -76,7 +76,7 @@ def make(name):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--ops", default="conv1_fwd,conv2_fwd,conv2_dgrad,conv2_wgrad,conv3_fwd,conv3_dgrad,conv3_wgrad,conv4_fwd,"
+    ap.add_argument("--ops", default="conv1_fwd,conv1_wgrad,conv2_fwd,conv2_dgrad,conv2_wgrad,conv3_fwd,conv3_dgrad,conv3_wgrad,conv4_fwd,"
                                      "conv4_dgrad,conv4_wgrad,conv5_fwd,conv5_dgrad,conv5_wgrad,fc6_fwd,fc6_dgrad,"
                                      "fc6_wgrad,fc7_fwd,fc7_dgrad,fc7_wgrad,fc8_fwd,fc8_dgrad,fc8_wgrad")
     ap.add_argument("--tiles", default="0,1,2,7,10,13,15,17")

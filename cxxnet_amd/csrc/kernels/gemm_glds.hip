@@ -43,7 +43,6 @@
 namespace {
 
 constexpr int BK = 64;
-constexpr int NT = 256;
 constexpr uint32_t OOB = 0x80000000u;  // >= num_records: the load returns zeros
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef __attribute__((address_space(3))) void lds_void;
@@ -102,9 +101,9 @@ constexpr bool kmajor(int mode) { return mode == K_DIRECT || mode == K_GATHER ||
 // ---------------------------------------------------------------------------------- operands
 // One operand tile: R rows (i or j) x BK k, R*128 bytes, R/32 DMA instructions per wave
 // (instruction q = wave + 4s writes LDS bytes [1024q, 1024q + 1024) of the tile).
-template <int MODE, int R>
+template <int MODE, int R, int NW>
 struct Op {
-  static constexpr int NI = R / 32;
+  static constexpr int NI = R / (8 * NW);
   static_assert(kmajor(MODE) || R == 128, "MN-major tiles are 128 columns wide");
   // K-major: per-instruction row state (byte offset or base/hi/wi); MN-major: column state
   int s0[NI], s1[NI], s2[NI];
@@ -118,7 +117,7 @@ struct Op {
       lchunk = (lane & 7) ^ (((wave & 1) << 2) + (lane >> 4));
 #pragma unroll
       for (int s = 0; s < NI; ++s) {
-        const int r = row0 + 8 * (wave + 4 * s) + (lane >> 3);
+        const int r = row0 + 8 * (wave + NW * s) + (lane >> 3);
         if constexpr (MODE == K_DIRECT) {
           s0[s] = r < op.rows ? static_cast<int>(goff + static_cast<uint32_t>(r * op.ld) * 2u) : -1;
           s1[s] = s2[s] = 0;
@@ -227,7 +226,7 @@ struct Op {
                       static_cast<unsigned>(wi) < static_cast<unsigned>(op.W);
       off = ok ? p.cb + static_cast<uint32_t>(s0[S] + (hi * op.W + wi) * op.C) * 2u : OOB;
     } else {
-      const int kp = p.k + 4 * (wave + 4 * S) + (lane >> 4);  // this DMA's k (pixel / batch row)
+      const int kp = p.k + 4 * (wave + NW * S) + (lane >> 4);  // this DMA's k (pixel / batch row)
       const bool kin = p.kin && kp < op.kdim && coff != OOB;
       if constexpr (MODE == MN_DIRECT) {
         off = kin ? coff + static_cast<uint32_t>(kp * op.ld) * 2u : OOB;
@@ -270,19 +269,20 @@ __device__ __forceinline__ bf16x8 frag(const char *tile, int base, int kk, int l
 
 // ---------------------------------------------------------------------------------- kernel
 template <int BM, int BN, int WGM, int WGN, int STAGES, int AMODE, int BMODE, int EPI>
-__global__ void __launch_bounds__(NT, 1)
+__global__ void __launch_bounds__(64 * WGM * WGN, 1)
 gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_tiles, int ktiles_total) {
-  static_assert(WGM * WGN == 4, "4 waves");
-  static_assert(BM % 32 == 0 && BN % 32 == 0, "tile rows must be a multiple of 32 (8 rows per DMA x 4 waves)");
+  constexpr int NW = WGM * WGN;  // 4 waves, or 8 (two per SIMD) for the large tiles
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows: a multiple of 8 rows per DMA x waves");
   constexpr int WM = BM / WGM, WN = BN / WGN;
   static_assert(WM % 16 == 0 && WN % 16 == 0, "wave tile must be a multiple of 16");
   constexpr int MR = WM / 16, NR = WN / 16;
-  using OA = Op<AMODE, BM>;
-  using OB = Op<BMODE, BN>;
+  using OA = Op<AMODE, BM, NW>;
+  using OB = Op<BMODE, BN, NW>;
   constexpr int NPT = OA::NI + OB::NI;  // DMA instructions per wave per tile
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
-  constexpr int EPI_BYTES = 4 * 16 * (WM + 4) * 4;
+  constexpr int EPI_BYTES = NW * 16 * (WM + 4) * 4;
   constexpr int SMEM = STAGES * STAGE_BYTES > EPI_BYTES ? STAGES * STAGE_BYTES : EPI_BYTES;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
@@ -314,12 +314,12 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
     char *sa = smem + st * STAGE_BYTES;
     static_for<OA::NI>([&](auto sc) {
       constexpr int s = decltype(sc)::value;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void *)(sa + (wave + 4 * s) * 1024), 16,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void *)(sa + (wave + NW * s) * 1024), 16,
                                                oa.template offset<s>(A, pa, wave, lane), 0, 0, 0);
     });
     static_for<OB::NI>([&](auto sc) {
       constexpr int s = decltype(sc)::value;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void *)(sa + A_BYTES + (wave + 4 * s) * 1024), 16,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void *)(sa + A_BYTES + (wave + NW * s) * 1024), 16,
                                                ob.template offset<s>(B, pb, wave, lane), 0, 0, 0);
     });
   };
@@ -388,7 +388,7 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
       const int i = ibase + il;
       const bool vec_store = ((E.ldc & 7) == 0) && (i + 8 <= Mi);
 #pragma unroll
-      for (int jl = lane / LPR; jl < 16; jl += RPI) {
+      for (int jl = lane < LPR * RPI ? lane / LPR : 16; jl < 16; jl += RPI) {  // WM = 96: 4 lanes idle
         const int j = jbase + n * 16 + jl;
         if (j < Nj && i < Mi) {
           const f32x4 x0 = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il);
@@ -439,7 +439,7 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
       const int i = ibase + il;
       const bool vec = ((E.ldc & 3) == 0) && (i + 4 <= Mi);
 #pragma unroll
-      for (int jl = lane / LPR; jl < 16; jl += RPI) {
+      for (int jl = lane < LPR * RPI ? lane / LPR : 16; jl < 16; jl += RPI) {
         const int j = jbase + n * 16 + jl;
         if (j < Nj && i < Mi) {
           f32x4 v = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il) * E.alpha;
@@ -465,31 +465,36 @@ void launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int
   const int per = cdiv(ktiles, ksplit);
   ksplit = cdiv(ktiles, per);
   dim3 grid(ti * tj, ksplit, groups);
-  hipLaunchKernelGGL((gemm_glds<BM, BN, WGM, WGN, STAGES, AMODE, BMODE, EPI>), grid, dim3(NT), 0, s, A, B, E, ti,
+  hipLaunchKernelGGL((gemm_glds<BM, BN, WGM, WGN, STAGES, AMODE, BMODE, EPI>), grid, dim3(64 * WGM * WGN), 0, s, A, B, E, ti,
                      tj, per, ktiles);
 }
 
 // Tile ids (BM x BN, wave grid, stages); MN-major operands need a 128-wide tile side:
 //   0: 128x256 (1x4) 3      1: 128x128 (1x4) 2      2: 128x128 (2x2) 3      7: 64x128 (1x4) 2
 //  10: 128x64 (2x2) 2      13: 128x128 (1x4) 3     15: 64x64 (2x2) 3       17: 128x128 (2x2) 2
+// 8 waves, two per SIMD (half the DMA bytes per MFMA of a 128x128 tile):
+//  20: 128x512 (1x8) 2     21: 256x256 (2x4) 2     23: 128x128 (2x4) 3     25: 64x512 (1x8) 2
+// (as plain 2-stage loops they tie the 4-wave tiles on AlexNet shapes: profiles/r15_glds_8wave.jsonl)
 #define CXG_T(ID, BM, BN, WGM, WGN, ST) \
   case ID: launch<BM, BN, WGM, WGN, ST, AM, BMo, EP>(A, B, E, groups, ksplit, s); return 0;
 #define CXG_KK_TILES                                                                                      \
   switch (tile) {                                                                                         \
     CXG_T(0, 128, 256, 1, 4, 3) CXG_T(1, 128, 128, 1, 4, 2) CXG_T(2, 128, 128, 2, 2, 3)                   \
     CXG_T(7, 64, 128, 1, 4, 2) CXG_T(10, 128, 64, 2, 2, 2) CXG_T(15, 64, 64, 2, 2, 3)                     \
+    CXG_T(20, 128, 512, 1, 8, 2) CXG_T(21, 256, 256, 2, 4, 2) CXG_T(25, 64, 512, 1, 8, 2)                 \
     default: return -1;                                                                                   \
   }
 #define CXG_MK_TILES  /* A MN-major (BM = 128), B K-major */                                              \
   switch (tile) {                                                                                         \
     CXG_T(0, 128, 256, 1, 4, 3) CXG_T(1, 128, 128, 1, 4, 2) CXG_T(2, 128, 128, 2, 2, 3)                   \
     CXG_T(10, 128, 64, 2, 2, 2) CXG_T(13, 128, 128, 1, 4, 3) CXG_T(17, 128, 128, 2, 2, 2)                 \
+    CXG_T(20, 128, 512, 1, 8, 2)                                                                          \
     default: return -1;                                                                                   \
   }
 #define CXG_MM_TILES  /* both MN-major (128 x 128) */                                                     \
   switch (tile) {                                                                                         \
     CXG_T(1, 128, 128, 1, 4, 2) CXG_T(2, 128, 128, 2, 2, 3) CXG_T(13, 128, 128, 1, 4, 3)                  \
-    CXG_T(17, 128, 128, 2, 2, 2)                                                                          \
+    CXG_T(17, 128, 128, 2, 2, 2) CXG_T(23, 128, 128, 2, 4, 3)                                             \
     default: return -1;                                                                                   \
   }
 #define CXG_CASE(AMV, BMV, EPV, TILES)                       \
@@ -535,7 +540,11 @@ bool supported(const CxnOperandG *o, int mode) {
   if (mode == K_ROWGATHER)  // whole kernel rows read as runs: no padding, one group, 8-byte aligned pixels
     return o->pad_h == 0 && o->pad_w == 0 && o->Cg == o->C && o->C % 4 == 0 && o->dil <= 1 &&
            o->kdim == o->KH * ((o->KW * o->C + 7) / 8) * 8;
-  if (o->Cg % 8 != 0 || o->C % 8 != 0 || o->dil > 1) return false;
+  if (o->Cg % 8 != 0 || o->dil > 1) return false;
+  // MN gather over whole kernel rows (few-channel weight-grad, conv1): KW = 1 and Cg = a kernel row's
+  // KW*C elements padded to 8, so a 16-byte chunk runs across pixels; with C % 8 == 4 it is 8-byte aligned
+  const bool row_runs = mode == MN_GATHER && o->KW == 1 && o->pad_h == 0 && o->pad_w == 0 && o->C % 4 == 0;
+  if (o->C % 8 != 0 && !row_runs) return false;
   return mode == K_GATHER || o->rows % 8 == 0;
 }
 void fill(GOperand &r, const CxnOperandG *o, int mode) {

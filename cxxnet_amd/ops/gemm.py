@@ -107,7 +107,8 @@ def _pick(candidates, rows_i, rows_j, groups, min_blocks=2 * NUM_CU):
 # gemm_glds.hip: both operands K-major (conv fwd / dgrad, fc fwd), 4 waves, one block per CU.
 GLDS_TILES = {0: (128, 256), 1: (128, 128), 2: (128, 128), 4: (192, 256), 5: (64, 256), 6: (256, 128),
               7: (64, 128), 8: (192, 128), 9: (96, 128), 10: (128, 64), 11: (64, 128), 12: (64, 128),
-              13: (128, 128), 14: (128, 64), 15: (64, 64), 16: (192, 64), 17: (128, 128)}
+              13: (128, 128), 14: (128, 64), 15: (64, 64), 16: (192, 64), 17: (128, 128),
+              20: (128, 512), 21: (256, 256), 23: (128, 128), 25: (64, 512)}
 # operand loaders of gemm_glds.hip
 GL_K, GL_KG, GL_MN, GL_MNG, GL_KR = 0, 1, 2, 3, 4  # K_DIRECT, K_GATHER, MN_DIRECT, MN_GATHER, K_ROWGATHER
 EPI_F32_ACC_G, EPI_F32_ATOMIC_G = 2, 3
@@ -117,10 +118,12 @@ _glds_cfg = {"on": os.environ.get("CXXNET_GEMM_GLDS", "1") != "0",
              # op classes routed to it: conv fwd, conv1-style row-gather fwd, conv dgrad, conv wgrad, fc fwd, fc wgrad
              "ops": set(os.environ.get("CXXNET_GLDS_OPS", "cf,cr,cd,fc,fw").split(","))}
 # conv weight-grad ("cw") has an LDS-DMA form too, but whole-step A/B measured it 0.6% slower
-# than the register-staged split-K kernel on AlexNet (profiles/r14_ab_glds_ops.jsonl)
+# than the register-staged split-K kernel on AlexNet (profiles/r14_ab_glds_ops.jsonl).  The
+# row-run weight-grad for few-channel convs ("cwr", conv1) is 3% faster as a kernel but its
+# padded-buffer zero + fold-back pass makes the whole step 1.1% slower (profiles/r15_ab_cwr.jsonl)
 # Autotuning candidates: the 2-stage tiles that run 2-5 blocks per CU measured best on every
 # AlexNet shape (profiles/r14_glds_tiles.jsonl); 2 and 0 cover wide-i GEMMs (fc).
-GLDS_CANDS = (1, 7, 10, 15, 2, 0, 13, 17)
+GLDS_CANDS = (1, 7, 10, 15, 2, 0, 13, 17, 21, 25)
 # Tuning database: {signature: tile}.  A shipped table for gfx950 (written by
 # benchmarks/tune_db.py on an MI355X) makes tile choice deterministic across runs and
 # data-parallel ranks; shapes it does not hold are timed on first use.
@@ -331,6 +334,18 @@ def _row_padded_weights(w, g: ConvGeom):
     return buf, lp
 
 
+_wgpad = {}
+
+
+def _wgrad_pad_buf(cout, kr, device):
+    """fp32 [Cout][KH * roundup(KW*C, 8)] accumulation buffer of the row-run weight-grad."""
+    key = (cout, kr, str(device))
+    buf = _wgpad.get(key)
+    if buf is None:
+        buf = _wgpad[key] = torch.empty((cout, kr), dtype=torch.float32, device=device)
+    return buf
+
+
 def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
     """y = conv(x, w) + bias (optionally relu).  x/y NHWC."""
     if not x.is_cuda:
@@ -430,6 +445,26 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
                          ksplit=split, tile=t)
         key = ("cw", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
         if run(_tuned_tile(key, run, dw, lambda: 1), dw):
+            return
+    if va != 8 and g.groups == 1 and g.pad_y == 0 and g.pad_x == 0 and g.C % 4 == 0 and _use("cwr"):
+        # few input channels (conv1): the KW*C im2col rows of one kernel row are one contiguous run
+        # of x, so the transposed gather reads each run as Cg = roundup(KW*C, 8) "channels" of a
+        # 1-wide kernel; the result lands in a row-padded fp32 buffer whose pad columns are dropped
+        lp = (g.KW * g.C + 7) // 8 * 8
+        kr = g.KH * lp
+        Ar = _op(x, lp, 0, kr, P, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=1, stride=g.stride,
+                 pad_h=0, pad_w=0, dil=1, Cg=lp)
+        ws = _wgrad_pad_buf(g.Cout, kr, dw.device)
+
+        def run(t, o):
+            bm, bn = GLDS_TILES[t]
+            split = max(1, min(2 * NUM_CU // max(_cdiv(kr, bm) * _cdiv(g.Cout, bn), 1), _cdiv(P, 64) // 16))
+            return _glds(Ar, B, GL_MNG, GL_MN, o, 0, kr, epi=EPI_F32_ATOMIC_G, ksplit=split, tile=t)
+        key = ("cwr", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride)
+        ws.zero_()
+        if run(_tuned_tile(key, run, ws, lambda: 1), ws):
+            L = g.KW * g.C
+            dw.view(g.Cout, g.KH, L).add_(ws.view(g.Cout, g.KH, lp)[:, :, :L])
             return
     tile = _pick(WGRAD_TILES, kd, g.cg_out, g.groups, min_blocks=1)
     split = _auto_split(kd, g.cg_out, g.groups, P, tile)

@@ -273,9 +273,11 @@ def init_distributed(backend: Optional[str] = None):
     if ws <= 1:
         return 0, 1
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = os.environ.get("CXXNET_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    if backend == "nccl":
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    if torch.cuda.is_available():
+        # one process per GPU; with fewer GPUs than ranks (rehearsing N ranks on one card with
+        # the gloo backend) ranks share devices round-robin
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
     dist.init_process_group(backend=backend)
     return world_info()

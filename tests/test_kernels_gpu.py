@@ -276,7 +276,9 @@ def test_fused_update(algo):
     g = rnd(n, seed=23)
     m = rnd(n, scale=0.1, seed=24)
     m2 = rnd(n, scale=0.1, seed=25).abs()
-    segs = [(0, 5000, 0.01, 0.0005, 0.9, 0.0), (5000, n - 5000, 0.02, 0.0, 0.9, 0.5)]
+    # 4-aligned segments with and without a < 4 tail, and an unaligned slice (element-wise path)
+    segs = [(0, 5000, 0.01, 0.0005, 0.9, 0.0), (5000, 3001, 0.02, 0.0, 0.9, 0.5),
+            (8001, n - 8001, 0.03, 0.001, 0.8, 0.0)]
     ref = [t.clone() for t in (w, g, m, m2)]
     wb_ref = torch.empty(n)
     ops.fused_update(algo, ref[0], ref[1], ref[2], ref[3], wb_ref, segs)
@@ -286,6 +288,8 @@ def test_fused_update(algo):
     torch.cuda.synchronize()
     assert relerr(dev[0], ref[0]) < 1e-5
     assert relerr(dev[2], ref[2]) < 1e-5
+    if algo == "adam":
+        assert relerr(dev[3], ref[3]) < 1e-5
     assert dev[1].abs().max().item() == 0.0
     assert relerr(wb, ref[0]) < 1e-2
 
