@@ -2,8 +2,9 @@
 configurations (per guide rule: perf deltas come from interleaved rounds in ONE process).
 
   python benchmarks/ab_step.py --configs "all:cf,cd,cw,fc,fw" "no_cw:cf,cd,fc,fw" --rounds 5
-Each config is `name:glds-op-classes[:ov]` ("none" = register-staged kernel everywhere; ":ov" runs
-the optimizer per gradient bucket on a side stream, overlapped with the rest of backward).
+Each config is `name:glds-op-classes[:ov][:db=path]` ("none" = register-staged kernel everywhere;
+":ov" runs the optimizer per gradient bucket on a side stream, overlapped with the rest of backward;
+":db=path" lays a tile table written by benchmarks/tune_db.py over the shipped one).
 Prints one JSON line per config: median / min ms per step over the rounds.
 """
 import argparse
@@ -50,13 +51,22 @@ def main():
     cfgs = []
     for spec in a.configs:
         name, ops, *flags = spec.split(":")
-        cfgs.append((name, [] if ops == "none" else ops.split(","), "ov" in flags))
+        db = {}
+        for f in flags:
+            if f.startswith("db="):
+                db = G._load_tune_db(f[3:])
+                assert db, f"empty or unreadable tile table {f[3:]}"
+        cfgs.append((name, [] if ops == "none" else ops.split(","), "ov" in flags, db))
+    shipped = dict(G._TUNE)
     net = tr.net
     ov_fn = lambda ranges: net.update(tr.epoch_counter, ranges)  # noqa: E731
-    times = {n: [] for n, _, _ in cfgs}
+    times = {n: [] for n, *_ in cfgs}
     for r in range(a.rounds):
-        for name, ops, ov in cfgs:
+        for name, ops, ov, db in cfgs:
             G.set_glds(on=bool(ops), ops=ops)
+            G._TUNE.clear()
+            G._TUNE.update(shipped)
+            G._TUNE.update(db)
             if ov:
                 tr.reducer.enable_overlapped_update(ov_fn)
             else:
@@ -69,7 +79,7 @@ def main():
                 tr.update(batch, local=True)
             torch.cuda.synchronize()
             times[name].append((time.perf_counter() - t0) / a.steps * 1000.0)
-    for name, _, _ in cfgs:
+    for name, *_ in cfgs:
         ts = times[name]
         print(json.dumps({"config": name, "median_ms": round(statistics.median(ts), 4), "min_ms": round(min(ts), 4),
                           "img_s_median": round(a.batch / statistics.median(ts) * 1000.0, 1)}), flush=True)

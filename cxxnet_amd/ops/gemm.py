@@ -124,6 +124,10 @@ _glds_cfg = {"on": os.environ.get("CXXNET_GEMM_GLDS", "1") != "0",
 # Autotuning candidates: the 2-stage tiles that run 2-5 blocks per CU measured best on every
 # AlexNet shape (profiles/r14_glds_tiles.jsonl); 2 and 0 cover wide-i GEMMs (fc).
 GLDS_CANDS = (1, 7, 10, 15, 2, 0, 13, 17, 21, 25)
+# Pseudo-tile: the register-staged kernel (gemm_mfma.hip) with its heuristic tile.  A candidate
+# for conv forward / data-grad, where it still wins a few shapes (conv2 forward on AlexNet:
+# 172 vs 186 us, profiles/r15_glds_8wave.jsonl "old_us").
+REG = 99
 # Tuning database: {signature: tile}.  A shipped table for gfx950 (written by
 # benchmarks/tune_db.py on an MI355X) makes tile choice deterministic across runs and
 # data-parallel ranks; shapes it does not hold are timed on first use.
@@ -162,7 +166,7 @@ def _use(op: str) -> bool:
     return _glds_cfg["on"] and op in _glds_cfg["ops"]
 
 
-def _tuned_tile(key, run, out, default):
+def _tuned_tile(key, run, out, default, extra=()):
     """Tile for a GEMM signature: the fastest candidate, timed once per process on a
     scratch output (the first call of each shape pays a few extra launches and one host
     sync); the heuristic pick when tuning is off or a graph is being captured."""
@@ -177,7 +181,7 @@ def _tuned_tile(key, run, out, default):
     scratch = torch.empty_like(out)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     best, best_ms = None, float("inf")
-    for tile in GLDS_CANDS:
+    for tile in GLDS_CANDS + tuple(extra):
         if not run(tile, scratch):
             continue
         ts = []
@@ -363,11 +367,19 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
     A = _op(w, g.cg_out * kd, kd, g.cg_out, kd)
     B = _op(x, cg, 0, g.N * g.Ho * g.Wo, kd, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW,
             stride=g.stride, pad_h=g.pad_y, pad_w=g.pad_x, dil=1, Cg=cg)
+    def reg(o):
+        tile = _pick(CONV_FWD_TILES if va == 8 else CONV_FWD_TILES_V4, g.cg_out, g.N * g.Ho * g.Wo, g.groups)
+        _gemm(A, B, DIRECT_K, GATHER_K, va, va, o, g.cg_out, g.Cout, bias=bias, bias_gstride=g.cg_out, relu=relu,
+              tile=tile, epi=EPI_BF16, groups=g.groups)
+        return True
     if va == 8 and _use("cf"):
-        run = lambda t, o: _glds(A, B, GL_K, GL_KG, o, g.cg_out, g.Cout, bias=bias, bias_gstride=g.cg_out,  # noqa: E731
-                                 relu=relu, groups=g.groups, tile=t)
+        def run(t, o):
+            if t == REG:
+                return reg(o)
+            return _glds(A, B, GL_K, GL_KG, o, g.cg_out, g.Cout, bias=bias, bias_gstride=g.cg_out, relu=relu,
+                         groups=g.groups, tile=t)
         key = ("cf", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
-        if run(_tuned_tile(key, run, y, lambda: _pick_glds(A.rows, B.rows, g.groups)), y):
+        if run(_tuned_tile(key, run, y, lambda: _pick_glds(A.rows, B.rows, g.groups), extra=(REG,)), y):
             return
     if va != 8 and g.groups == 1 and g.pad_y == 0 and g.pad_x == 0 and g.C % 4 == 0 and _use("cr"):
         # few input channels (conv1: 11x11 taps of 4 channels): each kernel row's KW*C
@@ -381,9 +393,7 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
         key = ("cr", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride)
         if run(_tuned_tile(key, run, y, lambda: 1), y):
             return
-    tile = _pick(CONV_FWD_TILES if va == 8 else CONV_FWD_TILES_V4, g.cg_out, g.N * g.Ho * g.Wo, g.groups)
-    _gemm(A, B, DIRECT_K, GATHER_K, va, va, y, g.cg_out, g.Cout, bias=bias, bias_gstride=g.cg_out, relu=relu, tile=tile,
-          epi=EPI_BF16, groups=g.groups)
+    reg(y)
 
 
 def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False):
@@ -409,15 +419,20 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False):
     A = _op(wt_buf, cg_in * kd, kd, cg_in, kd)
     B = _op(dy, cg_out, 0, g.N * g.H * g.W, kd, H=g.Ho, W=g.Wo, C=g.Cout, Ho=g.H, Wo=g.W, KH=g.KH,
             KW=g.KW, stride=1, pad_h=g.KH - 1 - g.pad_y, pad_w=g.KW - 1 - g.pad_x, dil=g.stride, Cg=cg_out)
+    def reg(o):
+        tile = _pick(CONV_FWD_TILES, cg_in, g.N * g.H * g.W, g.groups)
+        _gemm(A, B, DIRECT_K, GATHER_K, 8, 8, o, cg_in, g.C, epi=EPI_BF16, groups=g.groups, mask_relu=mask_relu,
+              tile=tile)
+        return True
     if g.stride == 1 and _use("cd"):
-        run = lambda t, o: _glds(A, B, GL_K, GL_KG, o, cg_in, g.C, groups=g.groups, mask_relu=mask_relu,  # noqa: E731
-                                 tile=t)
+        def run(t, o):
+            if t == REG:
+                return reg(o)
+            return _glds(A, B, GL_K, GL_KG, o, cg_in, g.C, groups=g.groups, mask_relu=mask_relu, tile=t)
         key = ("cd", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
-        if run(_tuned_tile(key, run, dx, lambda: _pick_glds(A.rows, B.rows, g.groups)), dx):
+        if run(_tuned_tile(key, run, dx, lambda: _pick_glds(A.rows, B.rows, g.groups), extra=(REG,)), dx):
             return
-    tile = _pick(CONV_FWD_TILES, cg_in, g.N * g.H * g.W, g.groups)
-    _gemm(A, B, DIRECT_K, GATHER_K, 8, 8, dx, cg_in, g.C, epi=EPI_BF16, groups=g.groups, mask_relu=mask_relu,
-          tile=tile)
+    reg(dx)
 
 
 def conv_backward_weight(x, dy, dw, g: ConvGeom):
