@@ -116,17 +116,19 @@ _glds_cfg = {"on": os.environ.get("CXXNET_GEMM_GLDS", "1") != "0",
              "tile": int(os.environ.get("CXXNET_GLDS_TILE", "-1")),
              "tune": os.environ.get("CXXNET_GEMM_TUNE", "1") != "0",
              # op classes routed to it: conv fwd, conv1-style row-gather fwd, conv dgrad, conv wgrad, fc fwd, fc wgrad
-             "ops": set(os.environ.get("CXXNET_GLDS_OPS", "cf,cr,cd,fc,fw").split(","))}
-# conv weight-grad ("cw") has an LDS-DMA form too, but whole-step A/B measured it 0.6% slower
-# than the register-staged split-K kernel on AlexNet (profiles/r14_ab_glds_ops.jsonl).  The
+             "ops": set(os.environ.get("CXXNET_GLDS_OPS", "cf,cr,cd,cw,fc,fw").split(","))}
+# conv weight-grad ("cw"): on every AlexNet layer together the LDS-DMA form is 0.6% slower than the
+# register-staged split-K kernel (profiles/r14_ab_glds_ops.jsonl), but per layer it wins conv4
+# (0.3% of the step, profiles/r15_ab_cw_layers.jsonl, r15_ab_cw_tiles.jsonl), so the register
+# kernel is a tuning candidate (REG) and the shipped table keeps it for conv2/3/5.  The
 # row-run weight-grad for few-channel convs ("cwr", conv1) is 3% faster as a kernel but its
 # padded-buffer zero + fold-back pass makes the whole step 1.1% slower (profiles/r15_ab_cwr.jsonl)
 # Autotuning candidates: the 2-stage tiles that run 2-5 blocks per CU measured best on every
 # AlexNet shape (profiles/r14_glds_tiles.jsonl); 2 and 0 cover wide-i GEMMs (fc).
 GLDS_CANDS = (1, 7, 10, 15, 2, 0, 13, 17, 21, 25)
 # Pseudo-tile: the register-staged kernel (gemm_mfma.hip) with its heuristic tile.  A candidate
-# for conv forward / data-grad, where it still wins a few shapes (conv2 forward on AlexNet:
-# 172 vs 186 us, profiles/r15_glds_8wave.jsonl "old_us").
+# for conv forward / data-grad / weight-grad, where it still wins some shapes (conv2 forward on
+# AlexNet timed alone: 172 vs 186 us, profiles/r15_glds_8wave.jsonl "old_us").
 REG = 99
 # Tuning database: {signature: tile}.  A shipped table for gfx950 (written by
 # benchmarks/tune_db.py on an MI355X) makes tile choice deterministic across runs and
@@ -166,7 +168,7 @@ def _use(op: str) -> bool:
     return _glds_cfg["on"] and op in _glds_cfg["ops"]
 
 
-def _tuned_tile(key, run, out, default, extra=()):
+def _tuned_tile(key, run, out, default, extra=(), tune=True):
     """Tile for a GEMM signature: the fastest candidate, timed once per process on a
     scratch output (the first call of each shape pays a few extra launches and one host
     sync); the heuristic pick when tuning is off or a graph is being captured."""
@@ -176,7 +178,7 @@ def _tuned_tile(key, run, out, default, extra=()):
     t = _TUNE.get(key)
     if t is not None:
         return t
-    if not _glds_cfg["tune"] or torch.cuda.is_current_stream_capturing():
+    if not (tune and _glds_cfg["tune"]) or torch.cuda.is_current_stream_capturing():
         return default()
     scratch = torch.empty_like(out)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -451,15 +453,26 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
     A = _op(x, cg, 0, kd, P, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW, stride=g.stride,
             pad_h=g.pad_y, pad_w=g.pad_x, dil=1, Cg=cg)
     B = _op(dy, g.cg_out, g.Cout, g.cg_out, P)
+
+    def reg(o):
+        tile = _pick(WGRAD_TILES, kd, g.cg_out, g.groups, min_blocks=1)
+        split = _auto_split(kd, g.cg_out, g.groups, P, tile)
+        _gemm(A, B, GATHER_MN, DIRECT_MN, va, 8, o, g.cg_out * kd, kd, epi=EPI_F32_ATOMIC, groups=g.groups,
+              ksplit=split, tile=tile)
+        return True
     if _use("cw") and va == 8:
         def run(t, o):
+            if t == REG:
+                return reg(o)
             bm, bn = GLDS_TILES[t]
             tiles = _cdiv(kd, bm) * _cdiv(g.cg_out, bn) * g.groups
             split = max(1, min(2 * NUM_CU // max(tiles, 1), _cdiv(P, 64) // 16))
             return _glds(A, B, GL_MNG, GL_MN, o, g.cg_out * kd, kd, epi=EPI_F32_ATOMIC_G, groups=g.groups,
                          ksplit=split, tile=t)
         key = ("cw", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
-        if run(_tuned_tile(key, run, dw, lambda: 1), dw):
+        # shapes missing from the table keep the register kernel: timed alone, the LDS-DMA form
+        # wins shapes where it loses inside the step (conv2/conv3 above)
+        if run(_tuned_tile(key, run, dw, lambda: REG, extra=(REG,), tune=False), dw):
             return
     if va != 8 and g.groups == 1 and g.pad_y == 0 and g.pad_x == 0 and g.C % 4 == 0 and _use("cwr"):
         # few input channels (conv1): the KW*C im2col rows of one kernel row are one contiguous run
@@ -481,10 +494,7 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
             L = g.KW * g.C
             dw.view(g.Cout, g.KH, L).add_(ws.view(g.Cout, g.KH, lp)[:, :, :L])
             return
-    tile = _pick(WGRAD_TILES, kd, g.cg_out, g.groups, min_blocks=1)
-    split = _auto_split(kd, g.cg_out, g.groups, P, tile)
-    _gemm(A, B, GATHER_MN, DIRECT_MN, va, 8, dw, g.cg_out * kd, kd, epi=EPI_F32_ATOMIC, groups=g.groups,
-          ksplit=split, tile=tile)
+    reg(dw)
 
 
 # ----------------------------------------------------------------------------- fully connected
