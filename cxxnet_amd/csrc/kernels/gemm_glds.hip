@@ -475,8 +475,9 @@ void launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int
 // 8 waves, two per SIMD (half the DMA bytes per MFMA of a 128x128 tile):
 //  20: 128x512 (1x8) 2     21: 256x256 (2x4) 2     23: 128x128 (2x4) 3     25: 64x512 (1x8) 2
 // (as plain 2-stage loops they tie the 4-wave tiles on AlexNet shapes: profiles/r15_glds_8wave.jsonl)
-// 96-row tiles for 96-output-channel convs (AlexNet conv1: a 128-row tile idles a quarter of its MFMAs):
-//   9: 96x128 (2x2) 2      26: 96x64 (2x2) 2       27: 96x256 (2x2) 2
+// 96-row tiles (9: 96x128, 26: 96x64, 27: 96x256, 2x2 waves) were tried for 96-channel convs and
+// withdrawn: they ran 8-18% faster on conv1 but their outputs were wrong (max rel err 0.86 on every
+// shape, profiles/r16_t96_tiles.jsonl), so no table or candidate list names them.
 #define CXG_T(ID, BM, BN, WGM, WGN, ST) \
   case ID: launch<BM, BN, WGM, WGN, ST, AM, BMo, EP>(A, B, E, groups, ksplit, s); return 0;
 #define CXG_KK_TILES                                                                                      \
@@ -484,7 +485,6 @@ void launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int
     CXG_T(0, 128, 256, 1, 4, 3) CXG_T(1, 128, 128, 1, 4, 2) CXG_T(2, 128, 128, 2, 2, 3)                   \
     CXG_T(7, 64, 128, 1, 4, 2) CXG_T(10, 128, 64, 2, 2, 2) CXG_T(15, 64, 64, 2, 2, 3)                     \
     CXG_T(20, 128, 512, 1, 8, 2) CXG_T(21, 256, 256, 2, 4, 2) CXG_T(25, 64, 512, 1, 8, 2)                 \
-    CXG_T(9, 96, 128, 2, 2, 2) CXG_T(26, 96, 64, 2, 2, 2) CXG_T(27, 96, 256, 2, 2, 2)                     \
     default: return -1;                                                                                   \
   }
 #define CXG_MK_TILES  /* A MN-major (BM = 128), B K-major */                                              \

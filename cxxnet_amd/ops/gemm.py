@@ -108,7 +108,7 @@ def _pick(candidates, rows_i, rows_j, groups, min_blocks=2 * NUM_CU):
 GLDS_TILES = {0: (128, 256), 1: (128, 128), 2: (128, 128), 4: (192, 256), 5: (64, 256), 6: (256, 128),
               7: (64, 128), 8: (192, 128), 9: (96, 128), 10: (128, 64), 11: (64, 128), 12: (64, 128),
               13: (128, 128), 14: (128, 64), 15: (64, 64), 16: (192, 64), 17: (128, 128),
-              20: (128, 512), 21: (256, 256), 23: (128, 128), 25: (64, 512), 26: (96, 64), 27: (96, 256)}
+              20: (128, 512), 21: (256, 256), 23: (128, 128), 25: (64, 512)}
 # operand loaders of gemm_glds.hip
 GL_K, GL_KG, GL_MN, GL_MNG, GL_KR = 0, 1, 2, 3, 4  # K_DIRECT, K_GATHER, MN_DIRECT, MN_GATHER, K_ROWGATHER
 EPI_F32_ACC_G, EPI_F32_ATOMIC_G = 2, 3
