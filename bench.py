@@ -47,6 +47,10 @@ def main():
     ap.add_argument("--input", default="u8", choices=["u8", "f32"],
                     help="u8: decoded-image batches (uint8 HWC) normalised on the GPU by the fused augment kernel, "
                          "as the imgbin pipeline delivers them; f32: float NCHW batches")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="replay forward/backward as HIP graphs (1 GPU; the optimizer stays eager). Off by default: "
+                         "the AlexNet and GoogLeNet steps are GPU-bound, graph replay measured -0.4%/+0.5%% "
+                         "(profiles/r16_graph_ab.jsonl)")
     a = ap.parse_args()
 
     from cxxnet_amd.models import load_conf
@@ -63,7 +67,7 @@ def main():
 
     global_batch = a.batch * world
     pairs = load_conf(a.model, [("batch_size", str(global_batch)), ("eval_train", "0"), ("dev", "gpu"),
-                                ("silent", "1")])
+                                ("silent", "1"), ("cuda_graph", str(a.graph))])
     pairs = [(k, v) for k, v in pairs if not k.startswith("metric")]
     tr = NetTrainer()
     for k, v in pairs:

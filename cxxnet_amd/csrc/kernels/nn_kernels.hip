@@ -950,6 +950,27 @@ __global__ void channel_copy(const bf16_t *__restrict__ src, int Cs, int soff, b
   }
 }
 
+// 8-channel (16-byte) form of channel_copy when every stride/offset/count is a multiple of 8
+// (all GoogLeNet concat branches): one uint4 per lane, 32-bit index math (total8 < 2^31).
+__global__ void channel_copy8(const uint4 *__restrict__ src, int Cs8, int soff8, uint4 *__restrict__ dst, int Cd8,
+                              int doff8, int Cc8, uint32_t total8, int accumulate) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total8; i += gridDim.x * blockDim.x) {
+    const uint32_t p = i / static_cast<uint32_t>(Cc8);
+    const uint32_t c = i - p * static_cast<uint32_t>(Cc8);
+    uint4 v = src[static_cast<size_t>(p) * Cs8 + soff8 + c];
+    uint4 *d = dst + static_cast<size_t>(p) * Cd8 + doff8 + c;
+    if (accumulate) {
+      float a[8], b[8];
+      unpack8(v, a);
+      unpack8(*d, b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += b[e];
+      v = pack8(a);
+    }
+    *d = v;
+  }
+}
+
 // dst[r][0:L] = src[r][0:L], dst[r][L:Lp] = 0 (row-padded copy, e.g. conv1 weights for the
 // row-gather GEMM: [Cout][KH][KW*C] -> [Cout][KH][roundup(KW*C, 8)])
 __global__ void pad_rows(const bf16_t *__restrict__ src, bf16_t *__restrict__ dst, long rows, int L, int Lp) {
@@ -1167,6 +1188,13 @@ CXN_API int cxn_add_bf16(const void *a, const void *b, void *y, long n, void *st
 }
 CXN_API int cxn_channel_copy(const void *src, int Cs, int soff, void *dst, int Cd, int doff, int Cc, long npix,
                              int accumulate, void *stream) {
+  const long total8 = npix * (Cc / 8);
+  if (((Cs | soff | Cd | doff | Cc) & 7) == 0 && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0 &&
+      total8 > 0 && total8 < (1L << 31)) {
+    channel_copy8<<<nblocks(total8), NT, 0, S_>>>((const uint4 *)src, Cs / 8, soff / 8, (uint4 *)dst, Cd / 8, doff / 8,
+                                                  Cc / 8, static_cast<uint32_t>(total8), accumulate);
+    RET;
+  }
   channel_copy<<<nblocks(npix * Cc), NT, 0, S_>>>((const bf16_t *)src, Cs, soff, (bf16_t *)dst, Cd, doff, Cc, npix,
                                                   accumulate);
   RET;

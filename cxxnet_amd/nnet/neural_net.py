@@ -243,6 +243,14 @@ class NeuralNet:
         lab = labels.to(self.device, torch.float32, non_blocking=True)
         if lab.dim() == 1:
             lab = lab.view(-1, 1)
+        # staged in one persistent buffer: loss layers (and captured HIP graphs) read the
+        # labels from a fixed address
+        buf = getattr(self, "_label_buf", None)
+        if buf is None or buf.shape[0] < lab.shape[0] or buf.shape[1] != lab.shape[1]:
+            buf = self._label_buf = torch.empty((max(self.max_batch, lab.shape[0]), lab.shape[1]),
+                                                dtype=torch.float32, device=self.device)
+        buf[: lab.shape[0]].copy_(lab, non_blocking=True)
+        lab = buf[: lab.shape[0]]
         fields = {}
         for name, idx in self.cfg.label_name_map.items():
             a, b = self.cfg.label_range[idx]

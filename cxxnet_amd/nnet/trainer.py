@@ -58,6 +58,12 @@ class NetTrainer:
         # (1 GPU: the memory-bound update just competes with the memory-bound
         # pool/LRN backward, measured -1.7%)
         self.overlap_update = int(os.environ.get("CXXNET_OVERLAP_UPDATE", "-1"))
+        # HIP-graph replay of the forward and backward passes (1 GPU, update_period 1):
+        # every layer kernel of a step is launched by two graph replays instead of one
+        # host call each; the optimizer stays an eager launch so lr schedules still apply
+        self.cuda_graph = int(os.environ.get("CXXNET_CUDA_GRAPH", "0"))
+        self._graphs = {}
+        self._graph_warm = {}
         self.cfg: List[Tuple[str, str]] = []
         self.metric = MetricSet()
         self.train_metric = MetricSet()
@@ -95,6 +101,8 @@ class NetTrainer:
             self.test_on_server = int(val)
         elif name == "overlap_update":
             self.overlap_update = int(val)
+        elif name == "cuda_graph":
+            self.cuda_graph = int(val)
         if name.startswith("metric"):
             import re
             m = re.match(r"metric\[([^,\]]+),([^\]]+)\]", name)
@@ -266,6 +274,9 @@ class NetTrainer:
         first = self.sample_counter % self.update_period == 0
         self._set_batch(batch, local)
         net = self.net
+        self._cur_batch = batch
+        if self._graph_step():
+            return
         net.forward(True)
         evals = self._collect_eval() if self.eval_train else None
         if need_update:
@@ -285,6 +296,50 @@ class NetTrainer:
         if self.sample_counter >= self.update_period:
             self.sample_counter = 0
             self.epoch_counter += 1
+
+    def _graph_eligible(self) -> bool:
+        net = self.net
+        return (self.cuda_graph > 0 and net.device.type == "cuda" and self.world == 1 and self.update_period == 1
+                and self.reducer is not None and self.reducer.update_fn is None and not self.reducer.shard)
+
+    def _graph_step(self) -> bool:
+        """One training step as two HIP-graph replays (forward, backward) plus the eager
+        fused optimizer.  The first step of each batch size runs eagerly (it autotunes the
+        GEMM tiles and allocates the layers' persistent buffers); the second captures.
+        Inputs and labels live in static node / label buffers, so a replay reads the batch
+        that _set_batch just staged.  Returns False to take the eager path."""
+        if not self._graph_eligible():
+            return False
+        net = self.net
+        key = net.cur_batch
+        gr = self._graphs.get(key)
+        if gr is None:
+            if self._graph_warm.get(key, 0) < 1:
+                self._graph_warm[key] = 1
+                return False
+            try:
+                torch.cuda.synchronize()
+                gf, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gf):
+                    net.forward(True)
+                with torch.cuda.graph(gb, pool=gf.pool()):
+                    net.backprop(False, first=True)
+            except Exception as e:  # a layer that syncs with the host (e.g. pairtest): stay eager
+                if not self.silent:
+                    print(f"cuda_graph: capture failed ({type(e).__name__}: {e}); running eagerly")
+                self.cuda_graph = 0
+                torch.cuda.synchronize()
+                return False
+            gr = self._graphs[key] = (gf, gb)
+        gf, gb = gr
+        gf.replay()
+        evals = self._collect_eval() if self.eval_train else None
+        gb.replay()
+        net.update(self.epoch_counter)
+        if evals is not None:
+            self.train_metric.add_eval(evals, self._label_fields(self._cur_batch))
+        self.epoch_counter += 1
+        return True
 
     # ------------------------------------------------------------------ inference
     def _node_output(self, nid: int) -> torch.Tensor:

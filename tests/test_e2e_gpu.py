@@ -97,3 +97,30 @@ def test_dropout_step_counter_changes_mask_on_gpu():
     b = tr.net.nodes[18].data.clone()
     za, zb = (a == 0), (b == 0)
     assert (za != zb).float().mean().item() > 0.1  # a fresh mask each step
+
+
+@pytest.mark.parametrize("model,batch", [("alexnet", 16), ("inception_v1", 8)])
+def test_cuda_graph_step_matches_eager(model, batch):
+    """cuda_graph=1 (forward and backward as HIP-graph replays, eager optimizer) trains
+    the same weights as the eager step: fresh batches each step (input staging), dropout
+    masks that change per step (device step counter), an lr schedule that moves every
+    update (expdecay: the optimizer must stay outside the graph)."""
+    over = {"eval_train": "1", "metric": "error", "lr:schedule": "expdecay", "lr:gamma": "0.5", "lr:step": "2"}
+    eager = _trainer(_pairs(model, batch, **over), "gpu")
+    graph = _trainer(_pairs(model, batch, cuda_graph="1", **over), "gpu")
+    graph.net.arena.w.copy_(eager.net.arena.w)
+    graph.net.arena.sync_shadow()
+    c, h, w = eager.net_cfg.input_shape
+    g = torch.Generator().manual_seed(3)
+    for _ in range(4):
+        x = torch.randn(batch, c, h, w, generator=g).cuda()
+        y = torch.randint(0, 1000, (batch, 1), generator=g).float().cuda()
+        eager.update(DataBatch(x, y))
+        graph.update(DataBatch(x, y))
+    torch.cuda.synchronize()
+    assert len(graph._graphs) == 1, "the graph path did not capture"
+    assert int(graph.net.ctx.step_counter.item()) == int(eager.net.ctx.step_counter.item()) == 4
+    # the whole optimizer state after 4 steps (atomic weight-grad epilogues: not bitwise)
+    assert _rel(graph.net.arena.m1, eager.net.arena.m1) < 0.05
+    assert _rel(graph.net.arena.w, eager.net.arena.w) < 1e-3
+    assert "train-error" in graph.train_metric.print("train")
