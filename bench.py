@@ -49,7 +49,7 @@ def main():
                          "as the imgbin pipeline delivers them; f32: float NCHW batches")
     ap.add_argument("--graph", type=int, default=0,
                     help="replay forward/backward as HIP graphs (1 GPU; the optimizer stays eager). Off by default: "
-                         "the AlexNet and GoogLeNet steps are GPU-bound, graph replay measured -0.4%/+0.5%% "
+                         "the AlexNet and GoogLeNet steps are GPU-bound, graph replay measured -0.4%%/+0.5%% "
                          "(profiles/r16_graph_ab.jsonl)")
     a = ap.parse_args()
 
