@@ -937,6 +937,40 @@ __global__ void add_bf16(const bf16_t *a, const bf16_t *b, bf16_t *y, long n) {
     reinterpret_cast<uint4 *>(y)[i] = pack8(x);
   }
 }
+// split forward: one read of the source, up to 4 copies written (n8 16-byte vectors)
+__global__ void fanout_bf16(const uint4 *__restrict__ src, uint4 *d0, uint4 *d1, uint4 *d2, uint4 *d3, int nd,
+                            long n8) {
+  for (long i = grid_stride_start(); i < n8; i += grid_stride()) {
+    const uint4 v = src[i];
+    d0[i] = v;
+    if (nd > 1) d1[i] = v;
+    if (nd > 2) d2[i] = v;
+    if (nd > 3) d3[i] = v;
+  }
+}
+// split backward: y = s0 + s1 (+ s2 + s3) in fp32, rounded once (y may alias s0)
+__global__ void sum_bf16(const uint4 *s0, const uint4 *s1, const uint4 *s2, const uint4 *s3, int ns, uint4 *y,
+                         long n8) {
+  for (long i = grid_stride_start(); i < n8; i += grid_stride()) {
+    float a[8], b[8];
+    unpack8(s0[i], a);
+    unpack8(s1[i], b);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] += b[e];
+    if (ns > 2) {
+      unpack8(s2[i], b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += b[e];
+    }
+    if (ns > 3) {
+      unpack8(s3[i], b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += b[e];
+    }
+    y[i] = pack8(a);
+  }
+}
+
 // strided channel copy for ch_concat / slicing: dst[p][doff + c] = src[p][soff + c], c < Cc
 __global__ void channel_copy(const bf16_t *__restrict__ src, int Cs, int soff, bf16_t *__restrict__ dst, int Cd,
                              int doff, int Cc, long npix, int accumulate) {
@@ -1184,6 +1218,21 @@ CXN_API int cxn_cast_f32_bf16(const float *x, void *y, long n, void *stream) {
 }
 CXN_API int cxn_add_bf16(const void *a, const void *b, void *y, long n, void *stream) {
   add_bf16<<<nblocks(n / 8 + 1), NT, 0, S_>>>((const bf16_t *)a, (const bf16_t *)b, (bf16_t *)y, n);
+  RET;
+}
+CXN_API int cxn_fanout_bf16(const void *src, void *d0, void *d1, void *d2, void *d3, int nd, long n, void *stream) {
+  if (nd < 1 || nd > 4 || (n & 7) != 0) return -2;
+  const long n8 = n / 8;
+  fanout_bf16<<<nblocks(n8), NT, 0, S_>>>((const uint4 *)src, (uint4 *)d0, (uint4 *)d1, (uint4 *)d2, (uint4 *)d3, nd,
+                                          n8);
+  RET;
+}
+CXN_API int cxn_sum_bf16(const void *s0, const void *s1, const void *s2, const void *s3, int ns, void *y, long n,
+                         void *stream) {
+  if (ns < 2 || ns > 4 || (n & 7) != 0) return -2;
+  const long n8 = n / 8;
+  sum_bf16<<<nblocks(n8), NT, 0, S_>>>((const uint4 *)s0, (const uint4 *)s1, (const uint4 *)s2, (const uint4 *)s3, ns,
+                                       (uint4 *)y, n8);
   RET;
 }
 CXN_API int cxn_channel_copy(const void *src, int Cs, int soff, void *dst, int Cd, int doff, int Cc, long npix,

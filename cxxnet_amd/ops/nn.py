@@ -382,6 +382,45 @@ def add(a, b, y):
     native.check(_k().cxn_add_bf16(a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), _stream()), "add")
 
 
+def _vec8(*ts):
+    return all(t.is_contiguous() and t.dtype == torch.bfloat16 and t.data_ptr() % 16 == 0 and t.numel() % 8 == 0
+               for t in ts)
+
+
+def fanout_copy(src, dsts):
+    """dst[k] = src for every dst (split forward): the source is read once per 4 copies."""
+    if not src.is_cuda or not _vec8(src, *dsts):
+        for d in dsts:
+            d.copy_(src)
+        return
+    for k in range(0, len(dsts), 4):
+        ds = list(dsts[k:k + 4])
+        ptr = [d.data_ptr() for d in ds] + [None] * (4 - len(ds))
+        native.check(_k().cxn_fanout_bf16(src.data_ptr(), *ptr, len(ds), src.numel(), _stream()), "fanout")
+
+
+def sum_into(y, srcs):
+    """y = sum(srcs) (split backward), accumulated in fp32 and rounded once per 4 terms;
+    y may alias srcs[0]."""
+    if len(srcs) == 1:
+        if y.data_ptr() != srcs[0].data_ptr():
+            y.copy_(srcs[0])
+        return
+    if not y.is_cuda or not _vec8(y, *srcs):
+        acc = srcs[0].float()
+        for t in srcs[1:]:
+            acc = acc + t.float()
+        y.copy_(acc)
+        return
+    first, rest = srcs[0], list(srcs[1:])
+    while rest:
+        part = [first] + rest[:3]
+        rest = rest[3:]
+        ptr = [t.data_ptr() for t in part] + [None] * (4 - len(part))
+        native.check(_k().cxn_sum_bf16(*ptr, len(part), y.data_ptr(), y.numel(), _stream()), "sum")
+        first = y
+
+
 def channel_copy(src, soff, dst, doff, cc, accumulate=False):
     """dst[..., doff:doff+cc] (+)= src[..., soff:soff+cc] for NHWC tensors with equal pixel counts."""
     Cs, Cd = src.shape[-1], dst.shape[-1]

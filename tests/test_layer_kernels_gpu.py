@@ -178,3 +178,21 @@ def test_exotic_net_gpu_vs_cpu():
         mg = gpu.net.arena.m1[sg.offset:sg.offset + sg.numel]
         errs[(li, cpu.net.connections[li].layer.type_name, sc.tag)] = round(relerr(mg, mc), 4)
     assert max(errs.values()) < 0.1, errs
+
+
+@pytest.mark.parametrize("nd", [1, 2, 3, 4, 5, 7])
+def test_split_fanout_and_sum_kernels(nd):
+    """split forward (one read, up to 4 writes per launch) and backward (fp32 sum of up
+    to 4 gradients per launch) against torch."""
+    from cxxnet_amd import ops
+    g = torch.Generator().manual_seed(nd)
+    x = torch.randn(3, 7, 5, 24, generator=g).to(torch.bfloat16).cuda()
+    outs = [torch.empty_like(x) for _ in range(nd)]
+    ops.fanout_copy(x, outs)
+    for o in outs:
+        assert torch.equal(o, x)
+    grads = [torch.randn(x.shape, generator=g).to(torch.bfloat16).cuda() for _ in range(nd)]
+    y = torch.empty_like(x)
+    ops.sum_into(y, grads)
+    ref = torch.stack([t.float() for t in grads]).sum(0)
+    assert (y.float() - ref).abs().max().item() <= 0.02 * ref.abs().max().item() + 1e-6
