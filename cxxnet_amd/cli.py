@@ -46,6 +46,11 @@ class LearnTask:
         self.itr_pred = None
         self.itr_evals = []
         self.eval_names = []
+        # checkpoint sidecar with momentum / second moment (<model>.state), restored on continue
+        self.save_opt_state = 0
+        # failure detection: abort the process if one update takes longer than this (seconds)
+        self.step_timeout = 0.0
+        self._last_progress = 0.0
 
     # ------------------------------------------------------------------ config
     def set_param(self, name: str, val: str):
@@ -83,6 +88,10 @@ class LearnTask:
             self.extract_node_name = val
         elif name == "output_format":
             self.output_format = 1 if val == "txt" else 0
+        elif name == "save_optimizer_state":
+            self.save_opt_state = int(val)
+        elif name == "step_timeout":
+            self.step_timeout = float(val)
         self.cfg.append((name, val))
 
     @property
@@ -144,8 +153,14 @@ class LearnTask:
         self.net_type = struct.unpack_from("<i", data, 0)[0]
         self.trainer = self._create_net()
         self.trainer.load_model(data, 4)
+        self._load_state_sidecar(last)
         self.start_counter = s - 1
         return True
+
+    def _load_state_sidecar(self, model_path: str):
+        if self.save_opt_state and os.path.exists(model_path + ".state"):
+            self.trainer.load_optimizer_state(model_path + ".state")
+            self.log(f"restored optimizer state from {model_path}.state")
 
     def load_model(self):
         base = os.path.basename(self.name_model_in)
@@ -158,6 +173,7 @@ class LearnTask:
         self.net_type = struct.unpack_from("<i", data, 0)[0]
         self.trainer = self._create_net()
         self.trainer.load_model(data, 4)
+        self._load_state_sidecar(self.name_model_in)
         self.start_counter += 1
 
     def copy_model(self):
@@ -181,6 +197,9 @@ class LearnTask:
             f.write(struct.pack("<i", self.net_type))
             f.write(blob)
         os.replace(path + ".tmp", path)
+        if self.save_opt_state:
+            self.trainer.save_optimizer_state(path + ".state.tmp")
+            os.replace(path + ".state.tmp", path + ".state")
 
     def init(self):
         if self.task == "train" and self.continue_training:
@@ -328,6 +347,7 @@ class LearnTask:
             return
         if self.test_io:
             self.log("start I/O test")
+        self._start_watchdog()
         cc = self.max_round
         while self.start_counter <= self.num_round and cc > 0:
             cc -= 1
@@ -338,11 +358,14 @@ class LearnTask:
             while self.itr_train.next():
                 if not self.test_io:
                     self.trainer.update(self.itr_train.value())
+                self._last_progress = time.time()
                 sample_counter += 1
                 if sample_counter % self.print_step == 0:
                     elapsed = int(time.time() - start)
                     self.log("\r" + " " * 63 + "\r" +
                              f"round {self.start_counter - 1:8d}:[{sample_counter:8d}] {elapsed} sec elapsed", end="")
+                    if getattr(self.trainer, "profile_step", 0):
+                        self.log("\n" + self.trainer.timing_report(), end="")
             if not self.test_io:
                 line = self._eval_line(self.start_counter)
                 if self.rank == 0:
@@ -350,7 +373,29 @@ class LearnTask:
                     sys.stderr.flush()
             elapsed = int(time.time() - start)
             self.save_model()
+            self._last_progress = time.time()  # evaluation / checkpointing is progress too
         self.log(f"\nupdating end, {elapsed} sec in all")
+
+
+    def _start_watchdog(self):
+        """step_timeout > 0: a daemon thread ends the process (exit code 3) when no update
+        finished for that long -- a hung collective or kernel fails fast instead of holding
+        every rank of the job."""
+        if self.step_timeout <= 0:
+            return
+        import threading
+        self._last_progress = time.time()
+
+        def watch():
+            while True:
+                time.sleep(min(1.0, self.step_timeout / 4))
+                if time.time() - self._last_progress > self.step_timeout:
+                    sys.stderr.write(f"step_timeout: no update finished in {self.step_timeout:g} s "
+                                     f"(rank {self.rank}); aborting\n")
+                    sys.stderr.flush()
+                    os._exit(3)
+
+        threading.Thread(target=watch, daemon=True, name="cxxnet-watchdog").start()
 
 
 def _maybe_spawn_ranks(argv: List[str]) -> Optional[int]:

@@ -64,6 +64,14 @@ class NetTrainer:
         self.cuda_graph = int(os.environ.get("CXXNET_CUDA_GRAPH", "0"))
         self._graphs = {}
         self._graph_warm = {}
+        # failure detection: every N updates, fail fast if any gradient was non-finite
+        # (the reference only zeroes NaN inside clip, sgd_updater-inl.hpp:17)
+        self.check_nonfinite = 0
+        self._nf_flag = None
+        # observability: HIP-event timers around forward / backward+reduce / optimizer
+        self.profile_step = 0
+        self._timers = []
+        self.step_times = {"fwd": 0.0, "bwd": 0.0, "opt": 0.0, "steps": 0}
         self.cfg: List[Tuple[str, str]] = []
         self.metric = MetricSet()
         self.train_metric = MetricSet()
@@ -103,6 +111,10 @@ class NetTrainer:
             self.overlap_update = int(val)
         elif name == "cuda_graph":
             self.cuda_graph = int(val)
+        elif name == "check_nonfinite":
+            self.check_nonfinite = int(val)
+        elif name == "profile_step":
+            self.profile_step = int(val)
         if name.startswith("metric"):
             import re
             m = re.match(r"metric\[([^,\]]+),([^\]]+)\]", name)
@@ -275,14 +287,19 @@ class NetTrainer:
         self._set_batch(batch, local)
         net = self.net
         self._cur_batch = batch
-        if self._graph_step():
+        ev = self._events()
+        if self._graph_step(ev):
+            self._after_step(ev)
             return
         net.forward(True)
+        self._mark(ev, 1)
         evals = self._collect_eval() if self.eval_train else None
         if need_update:
             self.reducer.start_step()
             net.backprop(False, hook=self.reducer.hook, first=first)
             self.reducer.finish()
+            self._check_grads()
+            self._mark(ev, 2)
             if self.reducer.shard:
                 net.update(self.epoch_counter, self.reducer.owned_ranges())
                 self.reducer.gather_params()
@@ -290,6 +307,8 @@ class NetTrainer:
                 net.update(self.epoch_counter)
         else:
             net.backprop(False, first=first)
+            self._mark(ev, 2)
+        self._after_step(ev)
         if evals is not None:
             self.train_metric.add_eval(evals, self._label_fields(batch))
         self.sample_counter += 1
@@ -297,12 +316,98 @@ class NetTrainer:
             self.sample_counter = 0
             self.epoch_counter += 1
 
+    # ------------------------------------------------------------------ step instrumentation
+    def _events(self):
+        if not self.profile_step or self.net.device.type != "cuda":
+            return None
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev[0].record()
+        return ev
+
+    @staticmethod
+    def _mark(ev, i):
+        if ev is not None:
+            ev[i].record()
+
+    def _after_step(self, ev):
+        if ev is not None:
+            ev[3].record()
+            self._timers.append(ev)
+            if len(self._timers) >= 8:  # resolve in batches: no per-step host sync
+                self.flush_timers()
+
+    def flush_timers(self):
+        """Fold the recorded step events into step_times (ms totals)."""
+        if not self._timers:
+            return
+        self._timers[-1][3].synchronize()
+        st = self.step_times
+        for e in self._timers:
+            st["fwd"] += e[0].elapsed_time(e[1])
+            st["bwd"] += e[1].elapsed_time(e[2])
+            st["opt"] += e[2].elapsed_time(e[3])
+            st["steps"] += 1
+        self._timers = []
+
+    def timing_report(self, reset: bool = True) -> str:
+        """`fwd x ms, bwd+comm y ms, opt z ms per step, N img/s` since the last report."""
+        self.flush_timers()
+        st = self.step_times
+        n = st["steps"]
+        if n == 0:
+            return ""
+        tot = (st["fwd"] + st["bwd"] + st["opt"]) / n
+        ips = self._local_batch() * self.world / (tot / 1000.0) if tot > 0 else 0.0
+        out = (f"fwd {st['fwd'] / n:.2f} ms, bwd+comm {st['bwd'] / n:.2f} ms, opt {st['opt'] / n:.2f} ms "
+               f"per step, {ips:.0f} img/s")
+        if reset:
+            self.step_times = {"fwd": 0.0, "bwd": 0.0, "opt": 0.0, "steps": 0}
+        return out
+
+    def _check_grads(self):
+        """Fail fast on non-finite gradients (check_nonfinite = N: flag accumulated on the
+        device every update, read back every N updates)."""
+        if not self.check_nonfinite:
+            return
+        from .. import ops
+        g = self.net.arena.g
+        if self._nf_flag is None:
+            self._nf_flag = torch.zeros(1, dtype=torch.int32, device=g.device)
+        ops.nonfinite(g, self._nf_flag)
+        if (self.epoch_counter + 1) % self.check_nonfinite == 0 and int(self._nf_flag.item()):
+            raise FloatingPointError(f"non-finite gradient detected by update {self.epoch_counter + 1} "
+                                     f"(check_nonfinite = {self.check_nonfinite})")
+
+    # ------------------------------------------------------------------ optimizer state sidecar
+    def save_optimizer_state(self, path: str):
+        """Momentum / second moment and counters next to a model file (the model file itself
+        stays byte-compatible with the reference layout, which has no optimizer state)."""
+        if self.reducer is not None:
+            self.reducer.sync_master()
+        a = self.net.arena
+        state = {"m1": a.m1.detach().cpu(), "epoch_counter": torch.tensor([self.epoch_counter]),
+                 "step_counter": self.net.ctx.step_counter.detach().cpu()}
+        if a.m2 is not None:
+            state["m2"] = a.m2.detach().cpu()
+        torch.save(state, path)
+
+    def load_optimizer_state(self, path: str):
+        state = torch.load(path, map_location="cpu", weights_only=True)
+        a = self.net.arena
+        if state["m1"].numel() != a.m1.numel():
+            raise ValueError(f"optimizer state {path}: {state['m1'].numel()} values, net has {a.m1.numel()}")
+        a.m1.copy_(state["m1"])
+        if "m2" in state:
+            a.ensure_second_moment()
+            a.m2.copy_(state["m2"])
+        self.net.ctx.step_counter.copy_(state["step_counter"])
+
     def _graph_eligible(self) -> bool:
         net = self.net
         return (self.cuda_graph > 0 and net.device.type == "cuda" and self.world == 1 and self.update_period == 1
                 and self.reducer is not None and self.reducer.update_fn is None and not self.reducer.shard)
 
-    def _graph_step(self) -> bool:
+    def _graph_step(self, ev=None) -> bool:
         """One training step as two HIP-graph replays (forward, backward) plus the eager
         fused optimizer.  The first step of each batch size runs eagerly (it autotunes the
         GEMM tiles and allocates the layers' persistent buffers); the second captures.
@@ -333,8 +438,11 @@ class NetTrainer:
             gr = self._graphs[key] = (gf, gb)
         gf, gb = gr
         gf.replay()
+        self._mark(ev, 1)
         evals = self._collect_eval() if self.eval_train else None
         gb.replay()
+        self._check_grads()
+        self._mark(ev, 2)
         net.update(self.epoch_counter)
         if evals is not None:
             self.train_metric.add_eval(evals, self._label_fields(self._cur_batch))

@@ -152,3 +152,64 @@ def test_checkpoint_byte_exact_roundtrip(conf):
     # layout: int32 net_type | NetParam(152) ...
     num_nodes, num_layers = struct.unpack_from("<ii", raw, 4)
     assert (num_nodes, num_layers) == (4, 4)
+
+
+def test_optimizer_state_sidecar_roundtrip(conf):
+    """save_optimizer_state = 1 writes <model>.state (momentum + counters) beside each
+    byte-compatible model file; continue = 1 restores it."""
+    import torch
+    path, tmp, _ = conf
+    t = LearnTask()
+    assert t.run([path, "max_round=2", "num_round=2", "save_optimizer_state=1"]) == 0
+    mdir = tmp / "models"
+    assert (mdir / "0002.model").exists() and (mdir / "0002.model.state").exists()
+    m1 = t.trainer.net.arena.m1.clone()
+    assert m1.abs().max() > 0
+    t2 = LearnTask()
+    for k, v in [("save_optimizer_state", "1"), ("continue", "1"), ("model_dir", str(mdir)), ("dev", "cpu"),
+                 ("silent", "1")]:
+        t2.set_param(k, v)
+    from cxxnet_amd import native
+    for k, v in native.rt().parse_config_file(path):
+        t2.set_param(k, v)
+    t2.set_param("continue", "1")
+    t2.set_param("save_optimizer_state", "1")
+    t2.init()
+    assert torch.equal(t2.trainer.net.arena.m1, m1)
+    # without the key the momentum starts from zero, as in the reference
+    t3 = LearnTask()
+    for k, v in native.rt().parse_config_file(path):
+        t3.set_param(k, v)
+    t3.set_param("continue", "1")
+    t3.init()
+    assert t3.trainer.net.arena.m1.abs().max() == 0
+
+
+def test_check_nonfinite_fails_fast(conf):
+    import torch
+    from cxxnet_amd.io.data import DataBatch
+    from cxxnet_amd.nnet import NetTrainer
+    from cxxnet_amd.models import load_conf
+    tr = NetTrainer()
+    for k, v in load_conf("mnist_mlp", [("dev", "cpu"), ("batch_size", "8"), ("silent", "1"),
+                                        ("check_nonfinite", "1")]):
+        tr.set_param(k, v)
+    tr.init_model()
+    shape = tr.net_cfg.input_shape
+    tr.update(DataBatch(torch.randn(8, *shape), torch.zeros(8, 1)))  # finite: passes
+    x = torch.randn(8, *shape)
+    x[0, 0, 0, 0] = float("nan")
+    with pytest.raises(FloatingPointError):
+        tr.update(DataBatch(x, torch.zeros(8, 1)))
+
+
+def test_step_timeout_watchdog_aborts():
+    """A stalled job exits with code 3 within ~step_timeout instead of hanging."""
+    import subprocess
+    import sys
+    code = ("import time\nfrom cxxnet_amd.cli import LearnTask\nt = LearnTask()\nt.set_param('step_timeout', '0.5')\n"
+            "t._start_watchdog()\ntime.sleep(30)\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 3, (r.returncode, r.stderr)
+    assert "step_timeout" in r.stderr

@@ -124,3 +124,20 @@ def test_cuda_graph_step_matches_eager(model, batch):
     assert _rel(graph.net.arena.m1, eager.net.arena.m1) < 0.05
     assert _rel(graph.net.arena.w, eager.net.arena.w) < 1e-3
     assert "train-error" in graph.train_metric.print("train")
+
+
+def test_profile_step_timers_and_nonfinite_check_on_gpu():
+    """profile_step = 1: HIP-event fwd / bwd / opt timings; check_nonfinite = 1: the
+    device flag kernel catches a NaN gradient."""
+    pairs = _pairs("alexnet", 8, profile_step="1", check_nonfinite="1")
+    tr = _trainer(pairs, "gpu")
+    c, h, w = tr.net_cfg.input_shape
+    x = torch.randn(8, c, h, w).cuda()
+    y = torch.zeros(8, 1).cuda()
+    for _ in range(3):
+        tr.update(DataBatch(x, y))
+    rep = tr.timing_report()
+    assert "fwd" in rep and "img/s" in rep, rep
+    x[0, 0, 0, 0] = float("nan")
+    with pytest.raises(FloatingPointError):
+        tr.update(DataBatch(x, y))
