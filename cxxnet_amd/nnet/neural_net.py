@@ -46,6 +46,7 @@ class NeuralNet:
         self.cfg = cfg
         self.max_batch = int(batch_size)
         self.device = torch.device(device)
+        self.trace_layers = 0
         self.ctx = LayerContext(self.device, seed)
         self.ctx.label_name_map = dict(cfg.label_name_map)
         self.ctx.step_counter = torch.zeros(1, dtype=torch.int32, device=self.device)
@@ -261,11 +262,20 @@ class NeuralNet:
         # temporarily narrow node buffers to the current batch
         return conn_nodes
 
+    def _range(self, i: int, phase: str):
+        """roctx range per layer (trace_layers = 1): rocprofv3 --marker-trace shows which
+        layer each kernel belongs to."""
+        if not self.trace_layers or self.device.type != "cuda":
+            return _NoRange
+        conn = self.connections[i]
+        return _LayerRange(f"{phase}:{i}:{conn.layer.type_name}")
+
     def forward(self, is_train: bool):
         self.ctx.step_counter.add_(1)
         with _BatchView(self):
-            for conn in self.connections:
-                conn.layer.forward(is_train, conn.nodes_in, conn.nodes_out)
+            for i, conn in enumerate(self.connections):
+                with self._range(i, "fwd"):
+                    conn.layer.forward(is_train, conn.nodes_in, conn.nodes_out)
 
     def backprop(self, prop_to_input: bool = False, hook=None, first: bool = False):
         """Reverse pass.  hook(layer_index) runs after each layer's backprop (used by the
@@ -281,7 +291,8 @@ class NeuralNet:
         with _BatchView(self):
             for i in range(len(self.connections) - 1, -1, -1):
                 conn = self.connections[i]
-                conn.layer.backprop(i != 0 or prop_to_input, conn.nodes_in, conn.nodes_out)
+                with self._range(i, "bwd"):
+                    conn.layer.backprop(i != 0 or prop_to_input, conn.nodes_in, conn.nodes_out)
                 if hook is not None:
                     hook(i)
 
@@ -291,6 +302,30 @@ class NeuralNet:
     def start_round(self, r: int):
         if self.updater is not None:
             self.updater.start_round(r)
+
+
+class _NoRangeT:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NoRange = _NoRangeT()
+
+
+class _LayerRange:
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        torch.cuda.nvtx.range_push(self.name)  # roctx on ROCm builds
+        return self
+
+    def __exit__(self, *exc):
+        torch.cuda.nvtx.range_pop()
+        return False
 
 
 class _BatchView:

@@ -70,6 +70,7 @@ class NetTrainer:
         self._nf_flag = None
         # observability: HIP-event timers around forward / backward+reduce / optimizer
         self.profile_step = 0
+        self.trace_layers = int(os.environ.get("CXXNET_TRACE_LAYERS", "0"))  # roctx range per layer
         self._timers = []
         self.step_times = {"fwd": 0.0, "bwd": 0.0, "opt": 0.0, "steps": 0}
         self.cfg: List[Tuple[str, str]] = []
@@ -115,6 +116,8 @@ class NetTrainer:
             self.check_nonfinite = int(val)
         elif name == "profile_step":
             self.profile_step = int(val)
+        elif name == "trace_layers":
+            self.trace_layers = int(val)
         if name.startswith("metric"):
             import re
             m = re.match(r"metric\[([^,\]]+),([^\]]+)\]", name)
@@ -167,6 +170,7 @@ class NetTrainer:
 
     def _post_init(self):
         self._forward_global_params(self.net)
+        self.net.trace_layers = self.trace_layers
         self._init_eval_nodes()
         self.reducer = GradReducer(self.net.arena, self.bucket_mb, True, self.comm_dtype,
                                    shard=bool(self.shard_update))

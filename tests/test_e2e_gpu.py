@@ -141,3 +141,12 @@ def test_profile_step_timers_and_nonfinite_check_on_gpu():
     x[0, 0, 0, 0] = float("nan")
     with pytest.raises(FloatingPointError):
         tr.update(DataBatch(x, y))
+
+
+def test_trace_layers_ranges_run_on_gpu():
+    pairs = _pairs("alexnet", 4, trace_layers="1", threshold="0")
+    tr = _trainer(pairs, "gpu")
+    assert tr.net.trace_layers == 1
+    c, h, w = tr.net_cfg.input_shape
+    tr.update(DataBatch(torch.randn(4, c, h, w).cuda(), torch.zeros(4, 1).cuda()))
+    torch.cuda.synchronize()
