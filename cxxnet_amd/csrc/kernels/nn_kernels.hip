@@ -362,9 +362,13 @@ static inline dim3 partials_grid(int nb, int C) { return dim3((C + 31) / 32, (nb
 // elements: the index split is three 32-bit fast divisions (the grid-stride forms above
 // spend most of their issue slots on 64-bit divisions).  Same semantics, including the
 // relu' bit.
+// SS / KS > 0: stride / square kernel fixed at compile time (3x3/2, 3x3/1, 2x2/2 -- every
+// pooling of the model zoo): constant divisions and fully unrolled windows
+template <int SS, int KS>
 __global__ void pool_fwd_rows(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, uint8_t *__restrict__ arg, int H,
-                              int W, int C, int Ho, int Wo, int KH, int KW, int S, int P, int mode, int relu,
+                              int W, int C, int Ho, int Wo, int KHr, int KWr, int Sr, int P, int mode, int relu,
                               FastDiv fd_cv, FastDiv fd_row, FastDiv fd_h, uint32_t total) {
+  const int S = SS > 0 ? SS : Sr, KH = KS > 0 ? KS : KHr, KW = KS > 0 ? KS : KWr;
   const int CV = C / 8;
   const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
@@ -416,10 +420,12 @@ __global__ void pool_fwd_rows(const bf16_t *__restrict__ x, bf16_t *__restrict__
         make_uint2(am[0] | am[1] << 8 | am[2] << 16 | am[3] << 24, am[4] | am[5] << 8 | am[6] << 16 | am[7] << 24);
 }
 
+template <int SS, int KS>
 __global__ void pool_bwd_rows(const bf16_t *__restrict__ x, const uint8_t *__restrict__ arg,
                               const bf16_t *__restrict__ dy, bf16_t *__restrict__ dx, int H, int W, int C, int Ho,
-                              int Wo, int KH, int KW, int S, int P, int mode, int relu, FastDiv fd_cv,
+                              int Wo, int KHr, int KWr, int Sr, int P, int mode, int relu, FastDiv fd_cv,
                               FastDiv fd_row, FastDiv fd_h, uint32_t total) {
+  const int S = SS > 0 ? SS : Sr, KH = KS > 0 ? KS : KHr, KW = KS > 0 ? KS : KWr;
   const int CV = C / 8;
   const uint32_t gidx = blockIdx.x * blockDim.x + threadIdx.x;
   if (gidx >= total) return;
@@ -1065,10 +1071,17 @@ CXN_API int cxn_pool_fwd(const void *x, void *y, void *arg, int N, int H, int W,
   if (C % 8 == 0) {
     const long total = static_cast<long>(N) * Ho * Wo * (C / 8);
     if (total >= (1L << 31)) return -2;  // fdiv (mulhi + n) stays exact below 2^31
-    pool_fwd_rows<<<cdiv(total, NT), NT, 0, S_>>>(
-        (const bf16_t *)x, (bf16_t *)y, (uint8_t *)arg, H, W, C, Ho, Wo, KH, KW, S, P, mode, relu,
-        make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(Wo * (C / 8))),
-        make_fastdiv(static_cast<uint32_t>(Ho)), static_cast<uint32_t>(total));
+#define CXN_POOL_FWD(SSV, KSV)                                                                              \
+  pool_fwd_rows<SSV, KSV><<<cdiv(total, NT), NT, 0, S_>>>(                                                  \
+      (const bf16_t *)x, (bf16_t *)y, (uint8_t *)arg, H, W, C, Ho, Wo, KH, KW, S, P, mode, relu,             \
+      make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(Wo * (C / 8))),        \
+      make_fastdiv(static_cast<uint32_t>(Ho)), static_cast<uint32_t>(total))
+    const int sq = KH == KW ? KH : 0;
+    if (S == 2 && sq == 3) CXN_POOL_FWD(2, 3);
+    else if (S == 1 && sq == 3) CXN_POOL_FWD(1, 3);
+    else if (S == 2 && sq == 2) CXN_POOL_FWD(2, 2);
+    else CXN_POOL_FWD(0, 0);
+#undef CXN_POOL_FWD
   } else {
     pool_fwd<1><<<nblocks(static_cast<long>(N) * Ho * Wo * C), NT, 0, S_>>>(
         (const bf16_t *)x, (bf16_t *)y, (uint8_t *)arg, N, H, W, C, Ho, Wo, KH, KW, S, P, mode, relu);
@@ -1081,10 +1094,17 @@ CXN_API int cxn_pool_bwd(const void *x, const void *arg, const void *dy, void *d
   if (C % 8 == 0 && db == nullptr) {
     const long total = static_cast<long>(N) * H * W * (C / 8);
     if (total >= (1L << 31)) return -2;  // fdiv (mulhi + n) stays exact below 2^31
-    pool_bwd_rows<<<cdiv(total, NT), NT, 0, S_>>>(
-        (const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, H, W, C, Ho, Wo, KH, KW, S, P, mode,
-        relu, make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(W * (C / 8))),
-        make_fastdiv(static_cast<uint32_t>(H)), static_cast<uint32_t>(total));
+#define CXN_POOL_BWD(SSV, KSV)                                                                                  \
+  pool_bwd_rows<SSV, KSV><<<cdiv(total, NT), NT, 0, S_>>>(                                                      \
+      (const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, H, W, C, Ho, Wo, KH, KW, S, P, mode, \
+      relu, make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(W * (C / 8))),          \
+      make_fastdiv(static_cast<uint32_t>(H)), static_cast<uint32_t>(total))
+    const int sq = KH == KW ? KH : 0;
+    if (S == 2 && sq == 3) CXN_POOL_BWD(2, 3);
+    else if (S == 1 && sq == 3) CXN_POOL_BWD(1, 3);
+    else if (S == 2 && sq == 2) CXN_POOL_BWD(2, 2);
+    else CXN_POOL_BWD(0, 0);
+#undef CXN_POOL_BWD
     RET;
   }
   if (C % 8 == 0) {
