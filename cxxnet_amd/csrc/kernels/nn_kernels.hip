@@ -370,7 +370,9 @@ __global__ void pool_fwd_rows(const bf16_t *__restrict__ x, bf16_t *__restrict__
                               FastDiv fd_cv, FastDiv fd_row, FastDiv fd_h, uint32_t total) {
   const int S = SS > 0 ? SS : Sr, KH = KS > 0 ? KS : KHr, KW = KS > 0 ? KS : KWr;
   const int CV = C / 8;
-  const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  // XCD-aware: consecutive logical blocks (overlapping windows read the same input rows)
+  // run on one XCD and share its L2 instead of re-fetching the overlap per XCD
+  const uint32_t idx = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (idx >= total) return;
   const int row = static_cast<int>(fdiv(idx, fd_row));           // n * Ho + ho
   const int e = static_cast<int>(idx) - row * (Wo * CV);
@@ -427,7 +429,7 @@ __global__ void pool_bwd_rows(const bf16_t *__restrict__ x, const uint8_t *__res
                               FastDiv fd_row, FastDiv fd_h, uint32_t total) {
   const int S = SS > 0 ? SS : Sr, KH = KS > 0 ? KS : KHr, KW = KS > 0 ? KS : KWr;
   const int CV = C / 8;
-  const uint32_t gidx = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t gidx = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;  // as pool_fwd_rows
   if (gidx >= total) return;
   const int row = static_cast<int>(fdiv(gidx, fd_row));          // n * H + h
   const int e = static_cast<int>(gidx) - row * (W * CV);
