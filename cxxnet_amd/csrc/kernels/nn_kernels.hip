@@ -389,24 +389,45 @@ __global__ void pool_fwd_rows(const bf16_t *__restrict__ x, bf16_t *__restrict__
     am[q] = 0;
   }
   const bf16_t *xb = x + static_cast<long>(n) * H * W * C + cv * 8;
-  for (int h = max(hs, 0); h < he; ++h)
-    for (int w = max(ws, 0); w < we; ++w) {
-      float v[8];
-      unpack8(*reinterpret_cast<const uint4 *>(xb + (static_cast<long>(h) * W + w) * C), v);
-      const uint32_t off = static_cast<uint32_t>((h - hs) * KW + (w - ws));
+  auto take = [&](const uint4 raw, uint32_t off) {
+    float v[8];
+    unpack8(raw, v);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float a = (relu & 1) ? fmaxf(v[q], 0.f) : v[q];
-        if (mode == 0) {
-          if (a > acc[q]) {
-            acc[q] = a;
-            am[q] = off;
-          }
-        } else {
-          acc[q] += a;
+    for (int q = 0; q < 8; ++q) {
+      const float a = (relu & 1) ? fmaxf(v[q], 0.f) : v[q];
+      if (mode == 0) {
+        if (a > acc[q]) {
+          acc[q] = a;
+          am[q] = off;
         }
+      } else {
+        acc[q] += a;
       }
     }
+  };
+  if constexpr (KS > 0) {
+    // fixed window: all KS*KS loads issued back to back (clamped addresses, edge taps
+    // masked), then reduced in the same h-major order as the generic loop (first max wins)
+    uint4 raw[KS * KS];
+#pragma unroll
+    for (int kh = 0; kh < KS; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < KS; ++kw) {
+        const int h = min(max(hs + kh, 0), H - 1), w = min(max(ws + kw, 0), W - 1);
+        raw[kh * KS + kw] = *reinterpret_cast<const uint4 *>(xb + (static_cast<long>(h) * W + w) * C);
+      }
+#pragma unroll
+    for (int kh = 0; kh < KS; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < KS; ++kw)
+        if (hs + kh >= 0 && hs + kh < he && ws + kw >= 0 && ws + kw < we)
+          take(raw[kh * KS + kw], static_cast<uint32_t>(kh * KW + kw));
+  } else {
+    for (int h = max(hs, 0); h < he; ++h)
+      for (int w = max(ws, 0); w < we; ++w)
+        take(*reinterpret_cast<const uint4 *>(xb + (static_cast<long>(h) * W + w) * C),
+             static_cast<uint32_t>((h - hs) * KW + (w - ws)));
+  }
   if (mode == 2) {
     const float inv = 1.0f / (KH * KW);
 #pragma unroll
@@ -445,24 +466,48 @@ __global__ void pool_bwd_rows(const bf16_t *__restrict__ x, const uint8_t *__res
   const int wlo = max(0, (w + P - KW + S) / S), whi = min(Wo - 1, (w + P) / S);
   const float inv = 1.0f / (KH * KW);
   const long nb = static_cast<long>(n) * Ho;
-  for (int ho = hlo; ho <= hhi; ++ho)
-    for (int wo = wlo; wo <= whi; ++wo) {
-      const long o = ((nb + ho) * Wo + wo) * C + cv * 8;
-      const uint32_t off = static_cast<uint32_t>((h - (ho * S - P)) * KW + (w - (wo * S - P)));
-      float gv[8];
-      unpack8(*reinterpret_cast<const uint4 *>(dy + o), gv);
-      if (mode == 0) {
-        const uint2 a2 = *reinterpret_cast<const uint2 *>(arg + o);
+  auto take = [&](const uint4 d, const uint2 a2, int ho, int wo) {
+    const uint32_t off = static_cast<uint32_t>((h - (ho * S - P)) * KW + (w - (wo * S - P)));
+    float gv[8];
+    unpack8(d, gv);
+    if (mode == 0) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          g[q] += (((a2.x >> (8 * q)) & 0xff) == off) ? gv[q] : 0.f;
-          g[q + 4] += (((a2.y >> (8 * q)) & 0xff) == off) ? gv[q + 4] : 0.f;
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) g[q] += mode == 2 ? gv[q] * inv : gv[q];
+      for (int q = 0; q < 4; ++q) {
+        g[q] += (((a2.x >> (8 * q)) & 0xff) == off) ? gv[q] : 0.f;
+        g[q + 4] += (((a2.y >> (8 * q)) & 0xff) == off) ? gv[q + 4] : 0.f;
       }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) g[q] += mode == 2 ? gv[q] * inv : gv[q];
     }
+  };
+  if constexpr (KS > 0 && SS > 0) {
+    // at most T x T windows cover one input pixel: issue every dy / argmax load first
+    // (clamped, masked), then accumulate in the generic loop's order
+    constexpr int T = (KS + SS - 1) / SS;
+    uint4 d[T * T];
+    uint2 a[T * T];
+#pragma unroll
+    for (int i = 0; i < T; ++i)
+#pragma unroll
+      for (int j = 0; j < T; ++j) {
+        const long o = ((nb + min(hlo + i, Ho - 1)) * Wo + min(wlo + j, Wo - 1)) * C + cv * 8;
+        d[i * T + j] = *reinterpret_cast<const uint4 *>(dy + o);
+        if (mode == 0) a[i * T + j] = *reinterpret_cast<const uint2 *>(arg + o);
+      }
+#pragma unroll
+    for (int i = 0; i < T; ++i)
+#pragma unroll
+      for (int j = 0; j < T; ++j)
+        if (hlo + i <= hhi && wlo + j <= whi) take(d[i * T + j], a[i * T + j], hlo + i, wlo + j);
+  } else {
+    for (int ho = hlo; ho <= hhi; ++ho)
+      for (int wo = wlo; wo <= whi; ++wo) {
+        const long o = ((nb + ho) * Wo + wo) * C + cv * 8;
+        take(*reinterpret_cast<const uint4 *>(dy + o),
+             mode == 0 ? *reinterpret_cast<const uint2 *>(arg + o) : make_uint2(0u, 0u), ho, wo);
+      }
+  }
   if (relu == 1)
 #pragma unroll
     for (int q = 0; q < 8; ++q) g[q] = xv[q] > 0.f ? g[q] : 0.f;
