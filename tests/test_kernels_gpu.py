@@ -269,16 +269,17 @@ def test_bias_grad(rows, C):
     assert relerr(db, db_ref) < 1e-3
 
 
+@pytest.mark.parametrize("n", [10007, 4200011])  # the large case runs the 2-deep unrolled loop
 @pytest.mark.parametrize("algo", ["sgd", "nag", "adam"])
-def test_fused_update(algo):
-    n = 10007
+def test_fused_update(algo, n):
     w = rnd(n, seed=22)
     g = rnd(n, seed=23)
     m = rnd(n, scale=0.1, seed=24)
     m2 = rnd(n, scale=0.1, seed=25).abs()
     # 4-aligned segments with and without a < 4 tail, and an unaligned slice (element-wise path)
-    segs = [(0, 5000, 0.01, 0.0005, 0.9, 0.0), (5000, 3001, 0.02, 0.0, 0.9, 0.5),
-            (8001, n - 8001, 0.03, 0.001, 0.8, 0.0)]
+    a = n // 2 // 4 * 4
+    segs = [(0, a, 0.01, 0.0005, 0.9, 0.0), (a, 3001, 0.02, 0.0, 0.9, 0.5),
+            (a + 3001, n - a - 3001, 0.03, 0.001, 0.8, 0.0)]
     ref = [t.clone() for t in (w, g, m, m2)]
     wb_ref = torch.empty(n)
     ops.fused_update(algo, ref[0], ref[1], ref[2], ref[3], wb_ref, segs)
