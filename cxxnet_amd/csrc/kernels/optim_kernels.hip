@@ -34,8 +34,10 @@ __device__ __forceinline__ float clipg(float g, float c) {
 // One element's step; returns the new weight.  m2 is used by adam only.
 __device__ __forceinline__ float step1(int algo, const Seg &sg, float wv, float gv, float &m1, float &m2, float d1,
                                        float d2) {
-  gv = clipg(gv, sg.clip);
   if (algo == 0) {
+    // only the SGD updater clips (reference sgd_updater-inl.hpp:77-81); NAG and Adam
+    // ignore clip_gradient
+    gv = clipg(gv, sg.clip);
     m1 = sg.mom * m1 - sg.lr * (gv + sg.wd * wv);
     return wv + m1;
   }

@@ -81,14 +81,14 @@ class FullConnectLayer(Layer):
         x = nodes_in[0].mat()
         if is_train and self._gathering():
             # backprop overwrites the input node with its gradient: gather it now
-            self._x_all = _all_gather_rows(x)
+            self._x_all = _all_gather_rows(x, nodes_in[0].shape[0])
         ops.fc_forward(x, self.w.wb, bias, nodes_out[0].mat(), relu=self.fuse_relu)
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
         x, dy = nodes_in[0].mat(), nodes_out[0].mat()
         overwrite = getattr(self.ctx, "grad_overwrite", False)
         if self._gathering():
-            dy_all = _all_gather_rows(dy)
+            dy_all = _all_gather_rows(dy, nodes_out[0].shape[0])
             x_all = self._x_all.wait()
             ops.fc_backward_weight(x_all, dy_all.wait(), self.w.g, overwrite=overwrite)
             self._x_all = None
@@ -125,12 +125,19 @@ class _Gathered:
         return self.out
 
 
-def _all_gather_rows(t: torch.Tensor) -> _Gathered:
-    """Async all-gather of a (rows, cols) matrix over the data-parallel ranks
-    (every rank holds the same number of rows: the trainer's batch split)."""
+def _all_gather_rows(t: torch.Tensor, rows: int) -> _Gathered:
+    """Async all-gather of a (rows, cols) matrix over the data-parallel ranks.  Every
+    rank's slice is zero-padded to `rows` (the node's capacity = the trainer's
+    ceil(B/world) split, equal on all ranks), so an uneven split -- the last rank holding
+    fewer rows, as the reference allows -- still gathers equal-sized pieces; zero rows of
+    both x and dy add nothing to dW = dy^T x."""
     import torch.distributed as dist
     world = dist.get_world_size()
     src = t.contiguous()
+    if src.shape[0] < rows:
+        pad = torch.zeros((rows,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+        pad[: src.shape[0]] = src
+        src = pad
     out = torch.empty((world * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
     return _Gathered(out, dist.all_gather_into_tensor(out, src, async_op=True))
 

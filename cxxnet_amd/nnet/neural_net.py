@@ -39,6 +39,7 @@ class Connection:
         self.nodes_in = nodes_in
         self.nodes_out = nodes_out
         self.shared = shared
+        self.owner = None  # index of the connection that owns the parameters
 
 
 class NeuralNet:
@@ -84,10 +85,12 @@ class NeuralNet:
                 if not prim.layer.allow_sharing:
                     raise ValueError("some layer you set shared do not allow sharing")
                 self.connections.append(Connection(prim.layer, prim.type, nin, nout, shared=True))
+                self.connections[-1].owner = prim.owner
             else:
                 layer = create_layer(info.type, self.ctx)
                 layer.layer_index = i
                 self.connections.append(Connection(layer, info.type, nin, nout))
+                self.connections[-1].owner = i
         self._pad_input_channels()
         for i, c_ in enumerate(self.connections):
             if not c_.shared:
@@ -258,10 +261,6 @@ class NeuralNet:
             fields[name] = lab[:, a:b]
         self.ctx.label_fields = fields
 
-    def _batched(self, conn_nodes):
-        # temporarily narrow node buffers to the current batch
-        return conn_nodes
-
     def _range(self, i: int, phase: str):
         """roctx range per layer (trace_layers = 1): rocprofv3 --marker-trace shows which
         layer each kernel belongs to."""
@@ -270,10 +269,15 @@ class NeuralNet:
         conn = self.connections[i]
         return _LayerRange(f"{phase}:{i}:{conn.layer.type_name}")
 
-    def forward(self, is_train: bool):
+    def forward(self, is_train: bool, pre_hook=None):
+        """pre_hook(layer_index) runs before each layer: the data-parallel reducer uses it
+        to make the compute stream wait for the bucket holding that layer's weights (the
+        reference's per-layer UpdateWait, neural_net-inl.hpp:125-131) and nothing more."""
         self.ctx.step_counter.add_(1)
         with _BatchView(self):
             for i, conn in enumerate(self.connections):
+                if pre_hook is not None:
+                    pre_hook(conn.owner)
                 with self._range(i, "fwd"):
                     conn.layer.forward(is_train, conn.nodes_in, conn.nodes_out)
 

@@ -53,6 +53,10 @@ class NetTrainer:
         self.bucket_mb = 64.0
         self.comm_dtype = "fp32"
         self.shard_update = 0
+        # data-parallel reduction: auto = sharded (reduce-scatter / sliced update /
+        # all-gather) on the GPU, replicated all-reduce elsewhere or with fullc_gather
+        self.dp_mode = "auto"
+        self.dp_force = int(os.environ.get("CXXNET_DIST_FORCE", "0"))
         self.test_on_server = 0
         # overlapped per-bucket optimizer: on by default only under data parallelism
         # (1 GPU: the memory-bound update just competes with the memory-bound
@@ -106,6 +110,12 @@ class NetTrainer:
             self.comm_dtype = val
         elif name in ("update_on_server", "dp_shard_update"):
             self.shard_update = int(val)
+        elif name == "dp_mode":
+            if val not in ("auto", "shard", "allreduce"):
+                raise ValueError(f"dp_mode must be auto, shard or allreduce, not {val}")
+            self.dp_mode = val
+        elif name == "dp_force":
+            self.dp_force = int(val)
         elif name == "test_on_server":
             self.test_on_server = int(val)
         elif name == "overlap_update":
@@ -145,9 +155,17 @@ class NetTrainer:
         step = max((self.batch_size + self.world - 1) // self.world, 1)
         return step
 
+    def _use_shard(self) -> bool:
+        if self.shard_update or self.dp_mode == "shard":
+            return True
+        if self.dp_mode == "allreduce":
+            return False
+        gather = any(k == "fullc_gather" and v.strip() not in ("", "0") for k, v in self.cfg)
+        return self._device().type == "cuda" and (self.world > 1 or bool(self.dp_force)) and not gather
+
     def _make_net(self) -> NeuralNet:
         net = NeuralNet(self.net_cfg, self._local_batch(), self._device(), seed=self.seed)
-        net.ctx.dp_shard = bool(self.shard_update)
+        net.ctx.dp_shard = self._use_shard()
         return net
 
     def _forward_global_params(self, net: NeuralNet):
@@ -173,8 +191,8 @@ class NetTrainer:
         self.net.trace_layers = self.trace_layers
         self._init_eval_nodes()
         self.reducer = GradReducer(self.net.arena, self.bucket_mb, True, self.comm_dtype,
-                                   shard=bool(self.shard_update))
-        if self.overlap_update == 1 or (self.overlap_update == -1 and self.world > 1):
+                                   shard=self._use_shard(), force=bool(self.dp_force))
+        if self.overlap_update == 1 or (self.overlap_update == -1 and self.reducer.active):
             net = self.net
             self.reducer.enable_overlapped_update(lambda ranges: net.update(self.epoch_counter, ranges))
         self.reducer.broadcast_params()
@@ -295,7 +313,7 @@ class NetTrainer:
         if self._graph_step(ev):
             self._after_step(ev)
             return
-        net.forward(True)
+        net.forward(True, pre_hook=self.reducer.before_forward)
         self._mark(ev, 1)
         evals = self._collect_eval() if self.eval_train else None
         if need_update:
@@ -304,10 +322,12 @@ class NetTrainer:
             self.reducer.finish()
             self._check_grads()
             self._mark(ev, 2)
-            if self.reducer.shard:
+            if self.reducer.handles_update:
+                pass  # per bucket on the side stream; the next forward gates on it
+            elif self.reducer.shard:
                 net.update(self.epoch_counter, self.reducer.owned_ranges())
                 self.reducer.gather_params()
-            elif self.reducer.update_fn is None:
+            else:
                 net.update(self.epoch_counter)
         else:
             net.backprop(False, first=first)
@@ -495,6 +515,7 @@ class NetTrainer:
         return out
 
     def forward_to(self, node_ids: List[int], batch) -> List[np.ndarray]:
+        self.reducer.sync()
         self._set_batch(batch)
         self.net.forward(False)
         return [self._gather(self._node_output(n).contiguous().float()).cpu().numpy() for n in node_ids]
@@ -561,6 +582,8 @@ class NetTrainer:
         return w.reshape(w.shape[0], -1).numpy() if w.dim() > 1 else w.reshape(1, -1).numpy()
 
     def set_weight(self, weight: np.ndarray, layer_name: str, tag: str):
+        if self.reducer is not None:
+            self.reducer.sync_master()
         layer, p = self._param(layer_name, tag)
         w = torch.as_tensor(np.asarray(weight, dtype=np.float32))
         if hasattr(layer, "from_logical") and tag == "wmat":

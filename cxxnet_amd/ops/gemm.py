@@ -168,10 +168,30 @@ def _use(op: str) -> bool:
     return _glds_cfg["on"] and op in _glds_cfg["ops"]
 
 
+TUNE_REJECTED = []  # (signature, tile, relative error) of candidates that failed the output check
+
+
+def _agrees(a: torch.Tensor, ref: torch.Tensor, tol: float = 2e-2) -> float:
+    """Norm-relative difference of a candidate's output from the reference tile's output
+    (inf when the candidate produced non-finite values the reference did not)."""
+    a, ref = a.float(), ref.float()
+    if not bool(torch.isfinite(a).all()) and bool(torch.isfinite(ref).all()):
+        return float("inf")
+    den = ref.norm().item()
+    return (a - ref).norm().item() / max(den, 1e-30)
+
+
 def _tuned_tile(key, run, out, default, extra=(), tune=True):
     """Tile for a GEMM signature: the fastest candidate, timed once per process on a
     scratch output (the first call of each shape pays a few extra launches and one host
-    sync); the heuristic pick when tuning is off or a graph is being captured."""
+    sync); the heuristic pick when tuning is off or a graph is being captured.
+
+    A candidate is eligible only if its output agrees with the heuristic tile's output on
+    the same operands (norm-relative difference < 2e-2; bf16 rounding and split-K order
+    differ by ~1e-3): a tile that computes the wrong thing fast can never win on time
+    (commit cecf60b withdrew 96-row tiles that were timing-eligible at 0.8 relative error).
+    Scratch outputs start from the live output's contents, so masked (mask_relu) and
+    accumulating epilogues see the same inputs for every candidate."""
     if _glds_cfg["tile"] >= 0:
         return _glds_cfg["tile"]
     key = "|".join(str(k) for k in key)
@@ -180,12 +200,27 @@ def _tuned_tile(key, run, out, default, extra=(), tune=True):
         return t
     if not (tune and _glds_cfg["tune"]) or torch.cuda.is_current_stream_capturing():
         return default()
+    init = out.clone()
+    ref = init.clone()
+    dflt = default()
+    ref_tile = dflt
+    have_ref = bool(run(dflt, ref))
+    if not have_ref and REG in extra:
+        ref.copy_(init)
+        ref_tile = REG
+        have_ref = bool(run(REG, ref))
     scratch = torch.empty_like(out)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     best, best_ms = None, float("inf")
     for tile in GLDS_CANDS + tuple(extra):
+        scratch.copy_(init)
         if not run(tile, scratch):
             continue
+        if have_ref and tile != ref_tile:
+            err = _agrees(scratch, ref)
+            if not err < 2e-2:
+                TUNE_REJECTED.append((key, tile, err))
+                continue
         ts = []
         for _ in range(3):
             s.record()
@@ -196,7 +231,7 @@ def _tuned_tile(key, run, out, default, extra=(), tune=True):
         ms = sorted(ts)[1]
         if ms < best_ms:
             best, best_ms = tile, ms
-    _TUNE[key] = best if best is not None else default()
+    _TUNE[key] = best if best is not None else dflt
     return _TUNE[key]
 
 

@@ -27,7 +27,7 @@ def fused_update(algo: str, w: torch.Tensor, g: torch.Tensor, st1: torch.Tensor,
         for off, n, lr, wd, mom, clip in segs:
             ws, gs, ms = w[off:off + n], g[off:off + n], st1[off:off + n]
             gv = gs.clone()
-            if clip != 0.0:
+            if clip != 0.0 and a == 0:  # SGD only (reference sgd_updater-inl.hpp:77-81)
                 gv = torch.nan_to_num(gv, nan=0.0).clamp(-clip, clip)
             if a == 0:
                 ms.mul_(mom).add_(-lr * (gv + wd * ws))

@@ -149,9 +149,15 @@ class ArenaUpdater:
 
     def update(self, epoch: int, ranges=None):
         """ranges: optional [start, end) arena ranges to update (sharded data
-        parallelism updates only this rank's slice)."""
+        parallelism updates only this rank's slice; the overlapped update calls this once
+        per gradient bucket).  The schedules are evaluated ONCE per epoch, however many
+        calls an update is split into: the momentum schedule accumulates on every
+        ScheduleEpoch call (reference param.h:84-87), once per update."""
         a = self.arena
-        segs = self.segments(epoch)
+        if getattr(self, "_seg_epoch", None) != epoch:
+            self._segs = self.segments(epoch)
+            self._seg_epoch = epoch
+        segs = self._segs
         if ranges is not None:
             segs = _clip_segments(segs, ranges)
         # gradients are reset by the next cycle's first backprop (NeuralNet.backprop(first=True))

@@ -1,0 +1,52 @@
+"""bench.py launcher contract on the CPU (gloo ranks): `--gpus N` without torchrun spawns N
+ranks itself, reports the process group's size, and a rank-count mismatch exits non-zero."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, timeout=600):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env["OMP_NUM_THREADS"] = "2"
+    return subprocess.run([sys.executable] + args, cwd=ROOT, env=env, capture_output=True, text=True,
+                          timeout=timeout)
+
+
+def _json(stdout):
+    lines = [l for l in stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+def test_bench_self_launches_two_ranks():
+    r = _run(["bench.py", "--gpus", "2", "--device", "cpu", "--model", "mnist_mlp", "--batch", "8",
+              "--steps", "2", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _json(r.stdout)
+    assert out["n_gpus"] == 2 and out["world_size"] == 2
+    assert out["scaling"] == "weak" and out["config"]["global_batch"] == 16
+    assert len(out["per_rank_ms_per_step"]) == 2
+    assert out["dp"]["comm_bytes_per_step_per_rank"] > 0
+    assert "AlexNet" not in out["metric"]
+
+
+def test_bench_strong_scaling_splits_global_batch():
+    r = _run(["bench.py", "--gpus", "2", "--device", "cpu", "--model", "mnist_mlp", "--batch", "10",
+              "--steps", "2", "--warmup", "1", "--scaling", "strong", "--dp-mode", "shard"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _json(r.stdout)
+    assert out["scaling"] == "strong"
+    assert out["config"]["global_batch"] == 10 and out["config"]["per_gpu_batch"] == 5
+    assert out["dp"]["mode"] == "shard"
+
+
+def test_bench_rank_mismatch_fails():
+    r = _run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr", "127.0.0.1",
+              "--master-port", "29561", "bench.py", "--gpus", "2", "--device", "cpu", "--model", "mnist_mlp",
+              "--batch", "8", "--steps", "1", "--warmup", "0"])
+    assert r.returncode != 0
+    assert "process group holds 1" in r.stderr

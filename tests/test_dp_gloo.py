@@ -62,11 +62,10 @@ def _make(batch, extra=()):
     return tr
 
 
-def _worker(rank, world, port, steps, out, update_period, shard=0):
+def _worker(rank, world, port, steps, out, update_period, shard=0, B=8):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from cxxnet_amd.io.data import DataBatch
-    B = 8
     extra = [("update_period", str(update_period))]
     if shard == 2:  # fullc_gather on both fc layers instead of sharding
         extra += [("fullc_gather", "1")]
@@ -91,20 +90,22 @@ def _worker(rank, world, port, steps, out, update_period, shard=0):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("update_period,shard", [(1, 0), (2, 0), (1, 1), (2, 1), (1, 2), (2, 2)])
-def test_dp_two_ranks_equals_single_process(tmp_path, update_period, shard):
+@pytest.mark.parametrize("update_period,shard,B", [(1, 0, 8), (2, 0, 8), (1, 1, 8), (2, 1, 8), (1, 2, 8), (2, 2, 8),
+                                                   (1, 0, 7), (1, 2, 7)])
+def test_dp_two_ranks_equals_single_process(tmp_path, update_period, shard, B):
     """shard=1: update_on_server (reduce-scatter, sliced update, all-gather);
-    shard=2: fullc_gather (fc weight gradients from all-gathered activations)."""
+    shard=2: fullc_gather (fc weight gradients from all-gathered activations).
+    B=7: uneven ceil split (4 + 3 rows), as the reference allows."""
     from cxxnet_amd.io.data import DataBatch
     steps = 4
     out = str(tmp_path / "dp.pt")
-    mp.spawn(_worker, args=(2, _free_port(), steps, out, update_period, shard), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), steps, out, update_period, shard, B), nprocs=2, join=True)
     r0 = torch.load(out, weights_only=True)
     r1 = torch.load(out + ".r1", weights_only=True)
     assert torch.equal(r0["w"], r1["w"]), "replicas diverged"
     # single process, whole batch
-    tr = _make(8, [("update_period", str(update_period))])
-    x, y = _data(8)
+    tr = _make(B, [("update_period", str(update_period))])
+    x, y = _data(B)
     for _ in range(steps):
         tr.update(DataBatch(x, y))
     n = tr.net.arena.total  # the 2-rank arena may carry extra zero padding

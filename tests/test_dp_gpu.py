@@ -40,9 +40,9 @@ def _data(B):
     return torch.randn(B, 3, 8, 8, generator=g), torch.randint(0, 5, (B, 1), generator=g).float()
 
 
-def _worker(rank, world, port, steps, out, extra):
+def _worker(rank, world, port, steps, out, extra, backend="gloo"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), CXXNET_DIST_BACKEND="gloo")
+                      LOCAL_RANK=str(rank), CXXNET_DIST_BACKEND=backend, CXXNET_DIST_FORCE="1")
     import torch.distributed as dist
     from cxxnet_amd.io.data import DataBatch
     from cxxnet_amd.parallel import init_distributed
@@ -54,11 +54,13 @@ def _worker(rank, world, port, steps, out, extra):
         tr.update(DataBatch(x.cuda(), y.cuda()))
     torch.cuda.synchronize()
     assert tr.reducer.check_consistency() == 0.0
+    tr.reducer.sync_master()  # sharded: each rank updated only its slice of the fp32 masters
     torch.save(tr.net.arena.w.cpu(), out + f".r{rank}")
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("extra", [(), (("dp_comm_dtype", "bf16"),), (("update_period", "2"),)])
+@pytest.mark.parametrize("extra", [(), (("dp_comm_dtype", "bf16"),), (("update_period", "2"),),
+                                   (("dp_mode", "allreduce"),)])
 def test_dp_two_ranks_gpu_equals_single(tmp_path, extra):
     steps = 4
     out = str(tmp_path / "w")
@@ -77,3 +79,24 @@ def test_dp_two_ranks_gpu_equals_single(tmp_path, extra):
     n = w.numel()
     err = ((r0[:n] - w).norm() / (w - w0).norm()).item()  # relative to the distance trained
     assert err < 5e-2, err
+
+
+@pytest.mark.parametrize("mode", ["shard", "allreduce"])
+def test_rccl_single_rank_forced_is_exact(tmp_path, mode):
+    """The RCCL ("nccl") backend at world 1 with dp_force: reduce-scatter / all-reduce,
+    the side-stream waits on the async work handles, the sliced overlapped update, the
+    bf16 all-gather and the per-bucket forward gating all execute on the MI355X.  With
+    one rank every collective is an identity and the fused update is elementwise, so the
+    weights must equal the plain single-GPU run bit for bit."""
+    steps = 3
+    out = str(tmp_path / "w")
+    extra = [("dp_mode", mode), ("dp_bucket_mb", "0.002")]
+    mp.spawn(_worker, args=(1, _free_port(), steps, out, extra, "nccl"), nprocs=1, join=True)
+    r0 = torch.load(out + ".r0", weights_only=True)
+    from cxxnet_amd.io.data import DataBatch
+    tr = _make(8, [])
+    x, y = _data(8)
+    for _ in range(steps):
+        tr.update(DataBatch(x.cuda(), y.cuda()))
+    torch.cuda.synchronize()
+    assert torch.equal(r0[: tr.net.arena.total], tr.net.arena.w.cpu())
