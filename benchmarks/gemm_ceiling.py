@@ -21,6 +21,11 @@ N = 256
 CONVS = {"conv1": (4, 227, 96, 11, 4, 0, 1), "conv2": (96, 27, 256, 5, 1, 2, 2), "conv3": (256, 13, 384, 3, 1, 1, 1),
          "conv4": (384, 13, 384, 3, 1, 1, 2), "conv5": (384, 13, 256, 3, 1, 1, 2)}
 FCS = {"fc6": (9216, 4096), "fc7": (4096, 4096), "fc8": (4096, 1000)}
+# VGG-16 (batch 64): the distinct 3x3 / pad 1 conv shapes (C, H, Cout) and its fc layers
+VGG_CONVS = {"c1_1": (4, 224, 64), "c1_2": (64, 224, 64), "c2_1": (64, 112, 128), "c2_2": (128, 112, 128),
+             "c3_1": (128, 56, 256), "c3_2": (256, 56, 256), "c4_1": (256, 28, 512), "c4_2": (512, 28, 512),
+             "c5": (512, 14, 512)}
+VGG_FCS = {"fc6": (25088, 4096), "fc7": (4096, 4096), "fc8": (4096, 1000)}
 
 
 def timeit(fn, iters):
@@ -39,7 +44,17 @@ def timeit(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--model", default="alexnet", choices=["alexnet", "vgg16"])
+    ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--no-lib", action="store_true")
     a = ap.parse_args()
+    global N, CONVS, FCS
+    if a.model == "vgg16":
+        N = a.batch or 64
+        CONVS = {k: (c, h, co, 3, 1, 1, 1) for k, (c, h, co) in VGG_CONVS.items()}
+        FCS = VGG_FCS
+    elif a.batch:
+        N = a.batch
     bf = torch.bfloat16
     dev = "cuda"
     for name, (C, H, Cout, K, s, p, g) in CONVS.items():
@@ -63,15 +78,15 @@ def main():
                       lambda: torch.nn.grad.conv2d_weight(xn, wn.shape, yn, s, p, 1, g)),
         }
         for kind, (ours, lib) in res.items():
-            if name == "conv1" and kind == "dgrad":
+            if name in ("conv1", "c1_1") and kind == "dgrad":
                 continue
             t0 = timeit(ours, a.iters)
             try:
-                t1 = timeit(lib, a.iters)
+                t1 = timeit(lib, a.iters) if not a.no_lib else float("nan")
             except Exception as ex:  # noqa: BLE001
                 t1 = float("nan")
                 print("lib failed", name, kind, ex, file=sys.stderr)
-            print(json.dumps({"op": f"{name}_{kind}", "ours_us": round(t0, 1), "lib_us": round(t1, 1),
+            print(json.dumps({"model": a.model, "batch": N, "op": f"{name}_{kind}", "ours_us": round(t0, 1), "lib_us": round(t1, 1),
                               "ours_tflops": round(flop / t0 / 1e6, 1), "lib_tflops": round(flop / t1 / 1e6, 1)}),
                   flush=True)
     for name, (nin, nout) in FCS.items():
@@ -88,10 +103,13 @@ def main():
             "wgrad": (lambda: ops.fc_backward_weight(x, dy, dw, overwrite=True), lambda: torch.mm(dy.t(), x)),
         }
         for kind, (ours, lib) in res.items():
-            t0, t1 = timeit(ours, a.iters), timeit(lib, a.iters)
-            print(json.dumps({"op": f"{name}_{kind}", "ours_us": round(t0, 1), "lib_us": round(t1, 1),
+            t0 = timeit(ours, a.iters)
+            t1 = timeit(lib, a.iters) if not a.no_lib else float("nan")
+            print(json.dumps({"model": a.model, "batch": N, "op": f"{name}_{kind}", "ours_us": round(t0, 1), "lib_us": round(t1, 1),
                               "ours_tflops": round(flop / t0 / 1e6, 1), "lib_tflops": round(flop / t1 / 1e6, 1)}),
                   flush=True)
+    if a.no_lib:
+        return
     # plain large GEMM: the library's best case on this box
     m = k = n = 8192
     A = torch.randn(m, k, device=dev).to(bf)

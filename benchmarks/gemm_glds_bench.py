@@ -20,6 +20,9 @@ BF = torch.bfloat16
 CONV = {"conv1": (4, 227, 96, 11, 4, 0, 1), "conv2": (96, 27, 256, 5, 1, 2, 2), "conv3": (256, 13, 384, 3, 1, 1, 1),
         "conv4": (384, 13, 384, 3, 1, 1, 2), "conv5": (384, 13, 256, 3, 1, 1, 2)}
 FC = {"fc6": (9216, 4096), "fc7": (4096, 4096), "fc8": (4096, 1000)}
+# VGG-16 at batch 64 ("vgg.c3_2_fwd"): 3x3 pad 1 convs (C, H, Cout)
+VGG = {"c1_2": (64, 224, 64), "c2_1": (64, 112, 128), "c2_2": (128, 112, 128), "c3_1": (128, 56, 256),
+       "c3_2": (256, 56, 256), "c4_1": (256, 28, 512), "c4_2": (512, 28, 512), "c5": (512, 14, 512)}
 
 
 def timeit(fn, iters):
@@ -36,7 +39,16 @@ def timeit(fn, iters):
 
 
 def make(name):
-    layer, kind = name.split("_")
+    global N
+    N = 256
+    if name.startswith("vgg."):
+        layer, kind = name[4:].rsplit("_", 1)
+        C, H, Cout = VGG[layer]
+        CONV[name] = (C, H, Cout, 3, 1, 1, 1)
+        layer = name
+        N = 64
+    else:
+        layer, kind = name.split("_")
     g = torch.Generator(device="cuda").manual_seed(0)
     if layer in FC:
         nin, nout = FC[layer]

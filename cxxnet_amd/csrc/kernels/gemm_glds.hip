@@ -268,7 +268,11 @@ __device__ __forceinline__ bf16x8 frag(const char *tile, int base, int kk, int l
 }
 
 // ---------------------------------------------------------------------------------- kernel
-template <int BM, int BN, int WGM, int WGN, int STAGES, int AMODE, int BMODE, int EPI>
+// PIPE bit 0: s_setprio(1) around each MFMA cluster (hipcc then keeps the cluster between the
+//             barriers instead of spreading it among the DMA issue -- cdna guide T5);
+// PIPE bit 1: both k-steps' fragments are read before the first MFMA (the k=32 reads are in
+//             flight under the k=0 MFMAs).
+template <int BM, int BN, int WGM, int WGN, int STAGES, int AMODE, int BMODE, int EPI, int PIPE = 0>
 __global__ void __launch_bounds__(64 * WGM * WGN, 1)
 gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_tiles, int ktiles_total) {
   constexpr int NW = WGM * WGN;  // 4 waves, or 8 (two per SIMD) for the large tiles
@@ -338,6 +342,30 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
   auto compute = [&](int st) {
     const char *sa = smem + st * STAGE_BYTES;
     const char *sb = sa + A_BYTES;
+    if constexpr ((PIPE & 2) != 0) {
+      bf16x8 fa0[MR], fb0[NR], fa1[MR], fb1[NR];
+#pragma unroll
+      for (int m = 0; m < MR; ++m) fa0[m] = frag<AMODE>(sa, wi_ * WM + m * 16, 0, lane);
+#pragma unroll
+      for (int n = 0; n < NR; ++n) fb0[n] = frag<BMODE>(sb, wj_ * WN + n * 16, 0, lane);
+#pragma unroll
+      for (int m = 0; m < MR; ++m) fa1[m] = frag<AMODE>(sa, wi_ * WM + m * 16, 32, lane);
+#pragma unroll
+      for (int n = 0; n < NR; ++n) fb1[n] = frag<BMODE>(sb, wj_ * WN + n * 16, 32, lane);
+      if constexpr ((PIPE & 1) != 0) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int m = 0; m < MR; ++m)
+#pragma unroll
+        for (int n = 0; n < NR; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0[m], fb0[n], acc[m][n], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < MR; ++m)
+#pragma unroll
+        for (int n = 0; n < NR; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[m], fb1[n], acc[m][n], 0, 0, 0);
+      if constexpr ((PIPE & 1) != 0) __builtin_amdgcn_s_setprio(0);
+      return;
+    }
     static_for<2>([&](auto kkc) {
       constexpr int kk = decltype(kkc)::value * 32;
       bf16x8 fa[MR], fb[NR];
@@ -345,11 +373,13 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
       for (int m = 0; m < MR; ++m) fa[m] = frag<AMODE>(sa, wi_ * WM + m * 16, kk, lane);
 #pragma unroll
       for (int n = 0; n < NR; ++n) fb[n] = frag<BMODE>(sb, wj_ * WN + n * 16, kk, lane);
+      if constexpr ((PIPE & 1) != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int m = 0; m < MR; ++m)
 #pragma unroll
         for (int n = 0; n < NR; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
+      if constexpr ((PIPE & 1) != 0) __builtin_amdgcn_s_setprio(0);
     });
   };
 
@@ -457,7 +487,7 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, int STAGES, int AMODE, int BMODE, int EPI>
+template <int BM, int BN, int WGM, int WGN, int STAGES, int AMODE, int BMODE, int EPI, int PIPE = 0>
 void launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int ksplit, hipStream_t s) {
   const int ti = cdiv(A.rows, BM), tj = cdiv(B.rows, BN);
   const int ktiles = cdiv(A.kdim, BK);
@@ -465,8 +495,8 @@ void launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int
   const int per = cdiv(ktiles, ksplit);
   ksplit = cdiv(ktiles, per);
   dim3 grid(ti * tj, ksplit, groups);
-  hipLaunchKernelGGL((gemm_glds<BM, BN, WGM, WGN, STAGES, AMODE, BMODE, EPI>), grid, dim3(64 * WGM * WGN), 0, s, A, B, E, ti,
-                     tj, per, ktiles);
+  hipLaunchKernelGGL((gemm_glds<BM, BN, WGM, WGN, STAGES, AMODE, BMODE, EPI, PIPE>), grid, dim3(64 * WGM * WGN), 0, s,
+                     A, B, E, ti, tj, per, ktiles);
 }
 
 // Tile ids (BM x BN, wave grid, stages); MN-major operands need a 128-wide tile side:
@@ -480,11 +510,16 @@ void launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int
 // shape, profiles/r16_t96_tiles.jsonl), so no table or candidate list names them.
 #define CXG_T(ID, BM, BN, WGM, WGN, ST) \
   case ID: launch<BM, BN, WGM, WGN, ST, AM, BMo, EP>(A, B, E, groups, ksplit, s); return 0;
+#define CXG_TP(ID, BM, BN, WGM, WGN, ST, PIPE) \
+  case ID: launch<BM, BN, WGM, WGN, ST, AM, BMo, EP, PIPE>(A, B, E, groups, ksplit, s); return 0;
 #define CXG_KK_TILES                                                                                      \
   switch (tile) {                                                                                         \
     CXG_T(0, 128, 256, 1, 4, 3) CXG_T(1, 128, 128, 1, 4, 2) CXG_T(2, 128, 128, 2, 2, 3)                   \
     CXG_T(7, 64, 128, 1, 4, 2) CXG_T(10, 128, 64, 2, 2, 2) CXG_T(15, 64, 64, 2, 2, 3)                     \
     CXG_T(20, 128, 512, 1, 8, 2) CXG_T(21, 256, 256, 2, 4, 2) CXG_T(25, 64, 512, 1, 8, 2)                 \
+    CXG_TP(30, 128, 256, 2, 4, 3, 0) CXG_TP(31, 128, 256, 2, 4, 3, 3) CXG_TP(33, 128, 256, 1, 4, 3, 3)    \
+    CXG_TP(34, 256, 256, 2, 4, 2, 3) CXG_TP(35, 64, 256, 1, 4, 3, 0) CXG_TP(36, 128, 128, 2, 4, 3, 3)     \
+    CXG_TP(37, 64, 128, 1, 4, 2, 3) CXG_TP(38, 128, 256, 2, 4, 2, 3) CXG_TP(39, 64, 256, 2, 4, 3, 3)      \
     default: return -1;                                                                                   \
   }
 #define CXG_MK_TILES  /* A MN-major (BM = 128), B K-major */                                              \
@@ -498,6 +533,7 @@ void launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int
   switch (tile) {                                                                                         \
     CXG_T(1, 128, 128, 1, 4, 2) CXG_T(2, 128, 128, 2, 2, 3) CXG_T(13, 128, 128, 1, 4, 3)                  \
     CXG_T(17, 128, 128, 2, 2, 2) CXG_T(23, 128, 128, 2, 4, 3)                                             \
+    CXG_TP(36, 128, 128, 2, 4, 3, 3) CXG_TP(40, 128, 128, 1, 4, 2, 3) CXG_TP(41, 128, 128, 2, 2, 2, 3)    \
     default: return -1;                                                                                   \
   }
 #define CXG_CASE(AMV, BMV, EPV, TILES)                       \
@@ -524,6 +560,7 @@ int dispatch(int amode, int bmode, int epi, int tile, const GOperand &A, const G
 #undef CXG_MK_TILES
 #undef CXG_KK_TILES
 #undef CXG_T
+#undef CXG_TP
 
 }  // namespace
 

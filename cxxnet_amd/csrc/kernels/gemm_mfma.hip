@@ -220,6 +220,28 @@ __device__ __forceinline__ void load_tile(const Operand &op, rsrc_t rs, const bf
   }
 }
 
+// MN-major [BK][R] tiles of 64 or 128 columns are stored without a pad and with the 16-byte
+// chunks of k-row k XOR-permuted, so the ds_read_b64_tr_b16 fragment reads (a 32-lane half reads
+// k-rows {k0..k0+3, k0+8..k0+11}, 32 contiguous bytes each) hit 8 disjoint 8-bank groups.  The
+// padded layout (row stride R+8) put those rows 4 banks apart: 2-way conflicts, ~33% of the
+// LDS cycles of the weight-grad kernel (rocprofv3 SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE).
+template <int R>
+constexpr bool mn_swz() { return R == 128 || R == 64; }
+template <int R>
+constexpr int mn_stride() { return mn_swz<R>() ? R : R + PADM; }
+template <int R>
+__device__ __forceinline__ int mn_chunk_xor(int k) {
+  if constexpr (R == 128) return 2 * ((k & 3) | (((k >> 3) & 1) << 2));
+  else if constexpr (R == 64) return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
+  else return 0;
+}
+// element offset of (k, col) in an MN-major tile; col % 4 == 0 (the 8-byte unit is never split)
+template <int R>
+__device__ __forceinline__ int mn_off(int k, int col) {
+  if constexpr (mn_swz<R>()) return k * R + (((col >> 3) ^ mn_chunk_xor<R>(k)) << 3) + (col & 7);
+  else return k * (R + PADM) + col;
+}
+
 template <int MODE, int R, int VEC>
 __device__ __forceinline__ void store_tile(bf16_t *lds, const Stage<R, VEC> &st) {
   const int tid = threadIdx.x;
@@ -236,7 +258,7 @@ __device__ __forceinline__ void store_tile(bf16_t *lds, const Stage<R, VEC> &st)
 #pragma unroll
     for (int s = 0; s < Stage<R, VEC>::NV; ++s) {
       const int v = tid + NT * s;
-      *reinterpret_cast<V *>(lds + (v / VPK) * (R + PADM) + (v % VPK) * VEC) = st.v[s];
+      *reinterpret_cast<V *>(lds + mn_off<R>(v / VPK, (v % VPK) * VEC)) = st.v[s];
     }
   }
 }
@@ -249,8 +271,9 @@ __device__ __forceinline__ bf16x8 load_frag(const bf16_t *lds, int row, int kk) 
     return *reinterpret_cast<const bf16x8 *>(lds + (row + (lane & 15)) * (BK + PADK) + kk + 8 * (lane >> 4));
   } else {
     const int i = lane & 15, g = lane >> 4;
-    const bf16_t *p0 = lds + (kk + 8 * g + (i >> 2)) * (R + PADM) + row + 4 * (i & 3);
-    const bf16_t *p1 = p0 + 4 * (R + PADM);
+    const int k = kk + 8 * g + (i >> 2);
+    const bf16_t *p0 = lds + mn_off<R>(k, row + 4 * (i & 3));
+    const bf16_t *p1 = lds + mn_off<R>(k + 4, row + 4 * (i & 3));
     s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p0));
     s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p1));
     typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -261,7 +284,7 @@ __device__ __forceinline__ bf16x8 load_frag(const bf16_t *lds, int row, int kk) 
 
 template <int MODE, int R>
 constexpr int tile_elems() {
-  return KMajorLayout<MODE>::kmajor ? R * (BK + PADK) : BK * (R + PADM);
+  return KMajorLayout<MODE>::kmajor ? R * (BK + PADK) : BK * mn_stride<R>();
 }
 
 template <int BM, int BN, int WAVES_M, int AMODE, int BMODE, int VA, int VB, int EPI, int PF>

@@ -88,6 +88,10 @@ class GradReducer:
         self.update_fn = None      # overlapped per-bucket optimizer (enable_overlapped_update)
         self.side = None
         self.extra_ranges = []     # fullc_gather segments: updated after backward
+        # RCCL runs reduce-scatter / all-gather IN PLACE (output = this rank's chunk of the
+        # input): no staging buffers and no copies; gloo gets separate buffers
+        self.inplace = (self.comm_dtype == torch.float32 and dist.is_available() and dist.is_initialized()
+                        and dist.get_backend(group) == "nccl")
         if self.shard:
             self._shard_buckets(limit)
         else:
@@ -135,6 +139,8 @@ class GradReducer:
             lis = [li for a, b, li in segs if a < end and b > start]
             self.buckets.append(Bucket(start, end, min(lis) if lis else -1))
             start = end
+        if self.inplace:
+            return
         for b in self.buckets:
             c = (b.end - b.start) // self.world
             b.out = torch.empty(c, dtype=self.comm_dtype, device=self.arena.g.device)
@@ -210,6 +216,12 @@ class GradReducer:
     def _launch(self, b: Bucket):
         g = self.arena.g[b.start:b.end]
         if self.shard:
+            if self.inplace:
+                lo, hi = b.own(self.rank, self.world)
+                b.buf = None
+                b.work = dist.reduce_scatter_tensor(self.arena.g[lo:hi], g, op=dist.ReduceOp.SUM,
+                                                    group=self.group, async_op=True)
+                return
             src = g if self.comm_dtype == torch.float32 else g.to(self.comm_dtype)
             b.buf = src  # keep the (possibly converted) source alive until the op is done
             b.work = dist.reduce_scatter_tensor(b.out, src, op=dist.ReduceOp.SUM, group=self.group,
@@ -234,7 +246,7 @@ class GradReducer:
             self.side.wait_event(ev)
             if self.active:
                 b.work.wait()  # the side stream waits for the collective (no host block)
-                if self.shard:
+                if self.shard and not self.inplace:
                     lo, hi = b.own(self.rank, self.world)
                     self.arena.g[lo:hi].copy_(b.out)
                 elif b.buf is not None:
@@ -248,9 +260,12 @@ class GradReducer:
                 a = self.arena
                 sh = a.wb if a.wb is not None else a.w
                 lo, hi = b.own(self.rank, self.world)
-                b.agin.copy_(sh[lo:hi])
+                src = sh[lo:hi]
+                if not self.inplace:
+                    b.agin.copy_(src)
+                    src = b.agin
                 # issued with the side stream current: RCCL's stream waits for the update
-                b.ag_work = dist.all_gather_into_tensor(sh[b.start:b.end], b.agin, group=self.group,
+                b.ag_work = dist.all_gather_into_tensor(sh[b.start:b.end], src, group=self.group,
                                                         async_op=True)
                 b.ag_work.wait()  # the side stream waits for the gather
                 b.ag_work = None
@@ -287,8 +302,9 @@ class GradReducer:
         for b in self.buckets:
             b.work.wait()
             if self.shard:
-                lo, hi = b.own(self.rank, self.world)
-                self.arena.g[lo:hi].copy_(b.out)
+                if not self.inplace:
+                    lo, hi = b.own(self.rank, self.world)
+                    self.arena.g[lo:hi].copy_(b.out)
                 b.buf = None
             elif b.buf is not None:
                 self.arena.g[b.start:b.end].copy_(b.buf)
@@ -327,8 +343,11 @@ class GradReducer:
         works = []
         for b in self.buckets:
             lo, hi = b.own(self.rank, self.world)
-            b.agin.copy_(sh[lo:hi])
-            works.append(dist.all_gather_into_tensor(sh[b.start:b.end], b.agin, group=self.group, async_op=True))
+            src = sh[lo:hi]
+            if not self.inplace:
+                b.agin.copy_(src)
+                src = b.agin
+            works.append(dist.all_gather_into_tensor(sh[b.start:b.end], src, group=self.group, async_op=True))
         for w in works:
             w.wait()
 

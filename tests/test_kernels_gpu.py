@@ -352,3 +352,23 @@ def test_image_u8_fast_path(mode):
     got = out.float().cpu()
     assert relerr(got[..., :3], ref) < 1e-2
     assert got[..., 3].abs().max().item() == 0
+
+
+@pytest.fixture
+def register_kernel_only():
+    """Route every GEMM to the register-staged kernel (gemm_mfma.hip), whose MN-major tiles
+    use the XOR-swizzled LDS image; the LDS-DMA kernel is restored afterwards."""
+    from cxxnet_amd.ops import gemm
+    gemm.set_glds(False)
+    yield
+    gemm.set_glds(True)
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_backward_weight_register_kernel(case, register_kernel_only):
+    test_conv_backward_weight(case)
+
+
+@pytest.mark.parametrize("B,nin,nout", FC_CASES)
+def test_fc_register_kernel(B, nin, nout, register_kernel_only):
+    test_fc(B, nin, nout)
