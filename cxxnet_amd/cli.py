@@ -355,6 +355,7 @@ class LearnTask:
             sample_counter = 0
             self.trainer.start_round(self.start_counter)
             self.itr_train.before_first()
+            t_mark, n_mark = time.perf_counter(), 0
             while self.itr_train.next():
                 if not self.test_io:
                     self.trainer.update(self.itr_train.value())
@@ -365,7 +366,13 @@ class LearnTask:
                     self.log("\r" + " " * 63 + "\r" +
                              f"round {self.start_counter - 1:8d}:[{sample_counter:8d}] {elapsed} sec elapsed", end="")
                     if getattr(self.trainer, "profile_step", 0):
-                        self.log("\n" + self.trainer.timing_report(), end="")
+                        # wall clock over the last print_step updates (the host runs at most a
+                        # few steps ahead of the GPU, so this is the training rate) + HIP-event
+                        # split of the GPU step
+                        now = time.perf_counter()
+                        ips = (sample_counter - n_mark) * self.trainer.batch_size / max(now - t_mark, 1e-9)
+                        t_mark, n_mark = now, sample_counter
+                        self.log(f"\nwall {ips:.0f} img/s; " + self.trainer.timing_report(), end="")
             if not self.test_io:
                 line = self._eval_line(self.start_counter)
                 if self.rank == 0:

@@ -61,3 +61,8 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t orig, uint32_t nwg) {
 }
 
 static inline int cdiv(long a, long b) { return static_cast<int>((a + b - 1) / b); }
+
+// Deterministic mode (cxn_set_deterministic): reductions that would combine partial sums with
+// atomics in a run-dependent order (cross-block channel sums, bias-grad partials) use one
+// ordered pass instead, so two identical runs produce bitwise-identical results.
+extern int cxn_deterministic;

@@ -592,6 +592,10 @@ int dispatch(const GemmArgs &g, const Operand &A, const Operand &B, const Epilog
   CXN_CASE(DIRECT_K, GATHER_K, 4, 4, EPI_BF16, 3)
   CXN_CASE(DIRECT_K, GATHER_K, 4, 4, EPI_BF16, 4)
   // convolution weight-grad (transposed gather on A), split-K fp32 atomics
+  CXN_CASE(GATHER_MN, DIRECT_MN, 8, 8, EPI_F32, 0)  // deterministic mode: per-slice fp32 slabs
+  CXN_CASE(GATHER_MN, DIRECT_MN, 8, 8, EPI_F32, 5)
+  CXN_CASE(GATHER_MN, DIRECT_MN, 4, 8, EPI_F32, 0)
+  CXN_CASE(GATHER_MN, DIRECT_MN, 4, 8, EPI_F32, 5)
   CXN_CASE(GATHER_MN, DIRECT_MN, 8, 8, EPI_F32_ATOMIC, 0)
   CXN_CASE(GATHER_MN, DIRECT_MN, 8, 8, EPI_F32_ATOMIC, 5)
   CXN_CASE(GATHER_MN, DIRECT_MN, 4, 8, EPI_F32_ATOMIC, 0)

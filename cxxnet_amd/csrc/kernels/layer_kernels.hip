@@ -256,6 +256,7 @@ CXN_API int cxn_chan_reduce(const void *x, const void *g, const float *mean, flo
   const int cg = (C + 63) / 64;
   int rb = static_cast<int>((rows + 255) / 256);
   if (rb > 1024 / cg + 1) rb = 1024 / cg + 1;
+  if (cxn_deterministic) rb = 1;  // no cross-block atomics: one block per channel group
   const int rpb = static_cast<int>((rows + rb - 1) / rb);
   rb = static_cast<int>((rows + rpb - 1) / rpb);
   if (rb < 1) rb = 1;

@@ -356,7 +356,10 @@ __global__ void partials_reduce(const float *__restrict__ part, int nb, int C, f
     atomicAdd(db + c, t);
   }
 }
-static inline dim3 partials_grid(int nb, int C) { return dim3((C + 31) / 32, (nb + 63) / 64); }
+static inline dim3 partials_grid(int nb, int C) {
+  // one row chunk (a single fixed-order pass, one add per column) in deterministic mode
+  return dim3((C + 31) / 32, cxn_deterministic ? 1 : (nb + 63) / 64);
+}
 
 // One-element-per-thread forms of pool_fwd / pool_bwd for C % 8 == 0 and < 2^32
 // elements: the index split is three 32-bit fast divisions (the grid-stride forms above
@@ -931,6 +934,25 @@ __global__ void colsum_bf16(const bf16_t *__restrict__ dy, float *__restrict__ p
 
 // Split-K finalisation: out[r][c] = epilogue(sum_s ws[s][r][c]) with optional bias[c],
 // relu, and mask_relu (keep where the OLD out value is > 0).  8 columns per thread.
+// out[i] += sum_s ws[s][i], slabs summed in slice order: the deterministic replacement for
+// split-K fp32 atomics (conv weight-grad in deterministic mode).
+__global__ void splitk_accumulate(const float *__restrict__ ws, int nsplit, long slab, float *__restrict__ out) {
+  for (long i = (static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x) * 4; i < slab;
+       i += static_cast<long>(gridDim.x) * blockDim.x * 4) {
+    if (i + 4 <= slab) {
+      f32x4 acc = *reinterpret_cast<const f32x4 *>(out + i);
+      for (int s = 0; s < nsplit; ++s) acc += *reinterpret_cast<const f32x4 *>(ws + s * slab + i);
+      *reinterpret_cast<f32x4 *>(out + i) = acc;
+    } else {
+      for (long e = i; e < slab; ++e) {
+        float a = out[e];
+        for (int s = 0; s < nsplit; ++s) a += ws[s * slab + e];
+        out[e] = a;
+      }
+    }
+  }
+}
+
 __global__ void splitk_finalize(const float *__restrict__ ws, int nsplit, long slab, bf16_t *out, long rows,
                                 int cols, const float *__restrict__ bias, int relu, int mask_relu) {
   // grid: blockIdx.y = row, x over 8-column groups (no 64-bit division per element)
@@ -1069,6 +1091,101 @@ __global__ void pad_rows(const bf16_t *__restrict__ src, bf16_t *__restrict__ ds
   }
 }
 
+
+// ------------------------------------------------------------------ evaluation metrics
+// Training / eval metrics on the device (reference src/utils/metric.h:20-236), one wave per
+// instance row of fp32 scores p[B][K] against labels lab[B][lw]:
+//   kind 0 error   : first-max argmax != label[0]   (K == 1: score > 0 is class 1)
+//   kind 1 logloss : -log(clamp(p[label[0]], 1e-15, 1 - 1e-15))   (K == 1: binary form)
+//   kind 2 rec@n   : (#distinct labels whose score has fewer than n strictly larger scores) / lw
+// (the reference breaks exact ties at random; here tied scores count as not larger).
+// Each block writes the sums over its rows to part[block][metric]; metric_accum adds the
+// block partials, in block order, into a float64 accumulator (deterministic, no atomics).
+struct MetricSpec {
+  int nm;
+  int kind[8];
+  int arg[8];
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(256) metric_rows(const float *__restrict__ p, int ldp, const float *__restrict__ lab,
+                                                  int ldl, int lw, int B, int K, MetricSpec ms, float *__restrict__ part) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float acc[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) acc[m] = 0.f;
+  for (int r = blockIdx.x * 4 + wave; r < B; r += gridDim.x * 4) {
+    const float *pr = p + static_cast<long>(r) * ldp;
+    const float *lr = lab + static_cast<long>(r) * ldl;
+    const int l0 = static_cast<int>(lr[0]);
+    // first-max argmax
+    float mv = -INFINITY;
+    int mi = 0x7fffffff;
+    for (int j = lane; j < K; j += 64) {
+      const float v = pr[j];
+      if (v > mv) { mv = v; mi = j; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(mv, o, 64);
+      const int oi = __shfl_xor(mi, o, 64);
+      if (ov > mv || (ov == mv && oi < mi)) { mv = ov; mi = oi; }
+    }
+    for (int m = 0; m < ms.nm; ++m) {
+      float v = 0.f;
+      if (ms.kind[m] == 0) {
+        const int pred = K == 1 ? (pr[0] > 0.f ? 1 : 0) : mi;
+        v = pred != l0 ? 1.f : 0.f;
+      } else if (ms.kind[m] == 1) {
+        if (K != 1) {
+          const float q = fminf(fmaxf(pr[l0], 1e-15f), 1.f - 1e-15f);
+          v = -logf(q);
+        } else {
+          const float py = fminf(fmaxf(pr[0], 1e-15f), 1.f - 1e-15f), y = lr[0];
+          v = -(y * logf(py) + (1.f - y) * logf(1.f - py));
+        }
+      } else {
+        const int n = ms.arg[m];
+        int hits = 0;
+        for (int c = 0; c < lw; ++c) {
+          const int lc = static_cast<int>(lr[c]);
+          bool dup = false;
+          for (int d = 0; d < c; ++d) dup |= static_cast<int>(lr[d]) == lc;
+          if (dup || lc < 0 || lc >= K) continue;
+          const float sl = pr[lc];
+          float cnt = 0.f;
+          for (int j = lane; j < K; j += 64) cnt += pr[j] > sl ? 1.f : 0.f;
+          cnt = wave_sum(cnt);
+          hits += cnt < static_cast<float>(n) ? 1 : 0;
+        }
+        v = static_cast<float>(hits) / static_cast<float>(lw);
+      }
+      acc[m] += v;  // identical in every lane of the wave
+    }
+  }
+  __shared__ float red[4][8];
+  if (lane == 0)
+#pragma unroll
+    for (int m = 0; m < 8; ++m) red[wave][m] = acc[m];
+  __syncthreads();
+  if (threadIdx.x < ms.nm)
+    part[blockIdx.x * ms.nm + threadIdx.x] =
+        red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+__global__ void metric_accum(const float *__restrict__ part, int nb, int nm, double *__restrict__ acc) {
+  const int m = threadIdx.x;
+  if (m < nm) {
+    double s = 0.0;
+    for (int b = 0; b < nb; ++b) s += part[b * nm + m];
+    acc[m] += s;
+  }
+}
 }  // namespace
 
 // ================================================================== C ABI
@@ -1248,6 +1365,24 @@ CXN_API int cxn_dropout(const void *x, void *y, long n, unsigned seed, const int
   dropout_apply<<<nblocks(n / 8 + 1), NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, n, seed, counter, thresh, 1.0f / pkeep);
   RET;
 }
+
+// acc: float64 [nm] metric sums (+= this batch); part: fp32 workspace of >= 256*nm floats.
+CXN_API int cxn_metric_eval(const float *p, int ldp, const float *lab, int ldl, int lw, int B, int K, int nm,
+                            const int *kinds, const int *args, double *acc, float *part, void *stream) {
+  if (nm < 1 || nm > 8 || B < 1) return nm < 1 || B < 1 ? 0 : -1;
+  MetricSpec ms{};
+  ms.nm = nm;
+  for (int m = 0; m < nm; ++m) {
+    ms.kind[m] = kinds[m];
+    ms.arg[m] = args[m];
+  }
+  int nb = (B + 3) / 4;
+  if (nb > 256) nb = 256;
+  metric_rows<<<nb, 256, 0, S_>>>(p, ldp, lab, ldl, lw, B, K, ms, part);
+  metric_accum<<<1, 64, 0, S_>>>(part, nb, nm, acc);
+  RET;
+}
+
 CXN_API int cxn_softmax(const void *x, void *y, float *pf, int rows, int K, void *stream) {
   softmax_rows<<<cdiv(rows, 4), 256, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, pf, rows, K);
   RET;
@@ -1272,6 +1407,21 @@ CXN_API int cxn_colsum(const void *dy, float *db, long rows, int C, float *ws, l
   partials_reduce<<<partials_grid(static_cast<int>(grid.x), C), NT, 0, S_>>>(ws, static_cast<int>(grid.x), C, db);
   RET;
 }
+int cxn_deterministic = 0;
+CXN_API int cxn_set_deterministic(int on) {
+  cxn_deterministic = on ? 1 : 0;
+  return 0;
+}
+
+CXN_API int cxn_splitk_accumulate(const float *ws, int nsplit, long slab, float *out, void *stream) {
+  if ((reinterpret_cast<uintptr_t>(ws) | reinterpret_cast<uintptr_t>(out)) & 15 || slab % 4) return -1;
+  long b = (slab / 4 + NT - 1) / NT;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  splitk_accumulate<<<static_cast<int>(b), NT, 0, S_>>>(ws, nsplit, slab, out);
+  RET;
+}
+
 CXN_API int cxn_splitk_finalize(const float *ws, int nsplit, long slab, void *out, long rows, int cols,
                                 const float *bias, int relu, int mask_relu, void *stream) {
   if (cols % 8) return -2;

@@ -19,7 +19,7 @@ import torch
 from .. import native
 from ..layers.base import BinReader, BinWriter
 from ..parallel.dp import GradReducer, world_info
-from ..utils.metric import MetricSet
+from ..utils.metric import DeviceMetricSet, MetricSet
 from .neural_net import NeuralNet
 
 
@@ -72,6 +72,7 @@ class NetTrainer:
         # (the reference only zeroes NaN inside clip, sgd_updater-inl.hpp:17)
         self.check_nonfinite = 0
         self._nf_flag = None
+        self.deterministic = int(os.environ.get("CXXNET_DETERMINISTIC", "0"))
         # observability: HIP-event timers around forward / backward+reduce / optimizer
         self.profile_step = 0
         self.trace_layers = int(os.environ.get("CXXNET_TRACE_LAYERS", "0"))  # roctx range per layer
@@ -80,6 +81,7 @@ class NetTrainer:
         self.cfg: List[Tuple[str, str]] = []
         self.metric = MetricSet()
         self.train_metric = MetricSet()
+        self.metric_specs: List[Tuple[str, str]] = []  # (metric, label field)
         self.eval_nodes: List[Tuple[str, int]] = []
         self.net_cfg = native.rt().NetConfig()
         self.net: Optional[NeuralNet] = None
@@ -124,6 +126,9 @@ class NetTrainer:
             self.cuda_graph = int(val)
         elif name == "check_nonfinite":
             self.check_nonfinite = int(val)
+        elif name == "deterministic":
+            # bitwise-reproducible steps on the GPU (ops.gemm.set_deterministic)
+            self.deterministic = int(val)
         elif name == "profile_step":
             self.profile_step = int(val)
         elif name == "trace_layers":
@@ -134,12 +139,14 @@ class NetTrainer:
             if m:
                 self.metric.add_metric(val, m.group(1))
                 self.train_metric.add_metric(val, m.group(1))
+                self.metric_specs.append((val, m.group(1)))
                 self.eval_nodes.append((m.group(2), 0))
             else:
                 m1 = re.match(r"metric\[([^\]]+)\]", name)
                 field = m1.group(1) if m1 else "label"
                 self.metric.add_metric(val, field)
                 self.train_metric.add_metric(val, field)
+                self.metric_specs.append((val, field))
                 self.eval_nodes.append(("", -1))
         self.cfg.append((name, val))
 
@@ -163,7 +170,14 @@ class NetTrainer:
         gather = any(k == "fullc_gather" and v.strip() not in ("", "0") for k, v in self.cfg)
         return self._device().type == "cuda" and (self.world > 1 or bool(self.dp_force)) and not gather
 
+    def _apply_modes(self):
+        if self._device().type == "cuda":
+            from ..ops import gemm
+            if self.deterministic or gemm.deterministic():
+                gemm.set_deterministic(bool(self.deterministic))
+
     def _make_net(self) -> NeuralNet:
+        self._apply_modes()
         net = NeuralNet(self.net_cfg, self._local_batch(), self._device(), seed=self.seed)
         net.ctx.dp_shard = self._use_shard()
         return net
@@ -186,7 +200,22 @@ class NetTrainer:
         if not self.eval_ids:
             self.eval_ids = []
 
+    @property
+    def device_metrics(self) -> bool:
+        return isinstance(self.train_metric, DeviceMetricSet)
+
+    def _use_device_metrics(self):
+        """On the GPU, metrics are accumulated on the device and read back only when
+        printed (DeviceMetricSet); the CPU path keeps the native host MetricSet."""
+        if self._device().type != "cuda" or self.device_metrics:
+            return
+        self.metric, self.train_metric = DeviceMetricSet(), DeviceMetricSet()
+        for name, field in self.metric_specs:
+            self.metric.add_metric(name, field)
+            self.train_metric.add_metric(name, field)
+
     def _post_init(self):
+        self._use_device_metrics()
         self._forward_global_params(self.net)
         self.net.trace_layers = self.trace_layers
         self._init_eval_nodes()
@@ -315,7 +344,7 @@ class NetTrainer:
             return
         net.forward(True, pre_hook=self.reducer.before_forward)
         self._mark(ev, 1)
-        evals = self._collect_eval() if self.eval_train else None
+        evals = self._train_eval(batch)
         if need_update:
             self.reducer.start_step()
             net.backprop(False, hook=self.reducer.hook, first=first)
@@ -463,7 +492,7 @@ class NetTrainer:
         gf, gb = gr
         gf.replay()
         self._mark(ev, 1)
-        evals = self._collect_eval() if self.eval_train else None
+        evals = self._train_eval(self._cur_batch)
         gb.replay()
         self._check_grads()
         self._mark(ev, 2)
@@ -496,6 +525,38 @@ class NetTrainer:
         outs = [torch.empty_like(pad) for _ in range(self.world)]
         dist.all_gather(outs, pad)
         return torch.cat([o[: int(s.item())] for o, s in zip(outs, sizes)], 0)
+
+    def _train_eval(self, batch):
+        """Training metrics of this step (eval_train): on the device they are accumulated
+        right here, enqueued behind the forward pass (the loss layer keeps its fp32 scores,
+        backprop only rewrites the bf16 node) -- no host copy; the host path returns the
+        scores for MetricSet.add_eval after the step."""
+        if not self.eval_train or not self.eval_ids:
+            return None
+        if self.device_metrics:
+            self.train_metric.add_eval(self._eval_scores(), self.net.ctx.label_fields)
+            return None
+        return self._collect_eval()
+
+    def _eval_scores(self) -> List[torch.Tensor]:
+        """Device (B, K) fp32 score views of the eval nodes, each node computed once."""
+        seen = {}
+        out = []
+        for nid in self.eval_ids:
+            if nid not in seen:
+                seen[nid] = self._node_output(nid).reshape(self.net.cur_batch, -1).float()
+            out.append(seen[nid])
+        return out
+
+    def _metric_reduce(self):
+        if self.world == 1:
+            return None
+        import torch.distributed as dist
+
+        def red(t):
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            return t
+        return red
 
     def _collect_eval(self) -> List[np.ndarray]:
         out = []
@@ -545,12 +606,25 @@ class NetTrainer:
     def evaluate(self, it, data_name: str) -> str:
         ret = ""
         if self.eval_train != 0:
-            ret += self.train_metric.print("train")
+            if self.device_metrics:
+                ret += self.train_metric.print("train", self._metric_reduce())
+            else:
+                ret += self.train_metric.print("train")
             self.train_metric.clear()
         if it is None:
             return ret
         self.metric.clear()
         it.before_first()
+        if self.device_metrics:
+            while it.next():
+                batch = it.value()
+                self.reducer.sync()
+                b = self._set_batch(batch)
+                self.net.forward(False)
+                n = batch.batch_size - batch.num_batch_padd  # valid rows of the global batch
+                lo = min(self.rank * self._local_batch(), batch.batch_size)
+                self.metric.add_eval(self._eval_scores(), self.net.ctx.label_fields, rows=max(0, min(b, n - lo)))
+            return ret + self.metric.print(data_name, self._metric_reduce())
         while it.next():
             batch = it.value()
             scores = self.forward_to(self.eval_ids, batch)

@@ -162,6 +162,26 @@ def save_tune_db(path=None):
         json.dump(dict(sorted(_TUNE.items())), f, indent=0)
 
 
+_DET = {"on": False}
+
+
+def set_deterministic(on: bool = True):
+    """Deterministic mode: bitwise-reproducible training steps.  The conv weight-grad
+    split-K writes one fp32 slab per K slice and sums the slabs in slice order (no fp32
+    atomics), cross-block channel / bias-grad sums run as one ordered pass (the kernels'
+    cxn_set_deterministic flag), and GEMM tile autotuning is off (timing-dependent picks
+    could differ between runs): the shipped table or the heuristic tile is used."""
+    _DET["on"] = bool(on)
+    if on:
+        _glds_cfg["tune"] = False
+    if torch.cuda.is_available():
+        native.kernels().cxn_set_deterministic(1 if on else 0)
+
+
+def deterministic() -> bool:
+    return _DET["on"]
+
+
 def set_glds(on: bool = True, tile: int = -1, tune: bool = True, ops=None):
     """Enable/disable the LDS-DMA GEMM path, force its tile, turn autotuning off, or pick
     the op classes it serves (subset of cf, cd, cw, fc, fw)."""
@@ -382,6 +402,14 @@ def _row_padded_weights(w, g: ConvGeom):
 
 
 _wgpad = {}
+_detws = {}
+
+
+def _det_ws(n, device):
+    buf = _detws.get(str(device))
+    if buf is None or buf.numel() < n:
+        buf = _detws[str(device)] = torch.empty(n, dtype=torch.float32, device=device)
+    return buf[:n]
 
 
 def _wgrad_pad_buf(cout, kr, device):
@@ -501,6 +529,17 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
         _gemm(A, B, GATHER_MN, DIRECT_MN, va, 8, o, g.cg_out * kd, kd, epi=EPI_F32_ATOMIC, groups=g.groups,
               ksplit=split, tile=tile)
         return True
+    if _DET["on"]:
+        # one fp32 slab per K slice, summed in slice order into dw: bitwise reproducible
+        tile = _pick(WGRAD_TILES, kd, g.cg_out, g.groups, min_blocks=1)
+        split = _effective_split(P, _auto_split(kd, g.cg_out, g.groups, P, tile))
+        slab = g.Cout * kd
+        ws = _det_ws(split * slab, dw.device)
+        _gemm(A, B, GATHER_MN, DIRECT_MN, va, 8, ws, g.cg_out * kd, kd, epi=EPI_F32, groups=g.groups,
+              ksplit=split, tile=tile, kstride=slab)
+        native.check(native.kernels().cxn_splitk_accumulate(ws.data_ptr(), split, slab, dw.data_ptr(), _stream()),
+                     "splitk_accumulate")
+        return
     if _use("cw") and va == 8:
         def run(t, o):
             if t == REG:

@@ -150,3 +150,36 @@ def test_trace_layers_ranges_run_on_gpu():
     c, h, w = tr.net_cfg.input_shape
     tr.update(DataBatch(torch.randn(4, c, h, w).cuda(), torch.zeros(4, 1).cuda()))
     torch.cuda.synchronize()
+
+
+def test_device_metrics_match_host_metrics():
+    """GPU training / eval metrics accumulate on the device (DeviceMetricSet); they must
+    equal the native host metrics computed from the same scores read back to the host."""
+    from cxxnet_amd.utils.metric import DeviceMetricSet, MetricSet
+    batch = 16
+    pairs = _pairs("alexnet", batch, eval_train="1") + [("metric", "error"), ("metric", "logloss"),
+                                                          ("metric", "rec@5")]
+    tr = _trainer(pairs, "gpu")
+    assert isinstance(tr.train_metric, DeviceMetricSet)
+    c, h, w = tr.net_cfg.input_shape
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(batch, c, h, w, generator=g).cuda()
+    y = torch.randint(0, 1000, (batch, 1), generator=g).float().cuda()
+    b = DataBatch(x, y)
+    scores = tr.forward_to([len(tr.net.nodes) - 1], b)[0].reshape(batch, -1)
+    host = MetricSet()
+    for n in ("error", "logloss", "rec@5"):
+        host.add_metric(n)
+    host.add_eval([scores] * 3, {"label": y.cpu().numpy()})
+    tr.metric.clear()
+    tr._set_batch(b)
+    tr.net.forward(False)
+    tr.metric.add_eval(tr._eval_scores(), tr.net.ctx.label_fields)
+    hv = [float(s.split(":")[1]) for s in host.print("t").split("\t")[1:]]
+    dv = tr.metric.values()
+    assert all(abs(a - b_) <= 1e-4 * max(1.0, abs(a)) for a, b_ in zip(hv, dv)), (hv, dv)
+    # training-time accumulation: no host copy per step, one line on print
+    for _ in range(3):
+        tr.update(b)
+    line = tr.evaluate(None, "train")
+    assert line.count("train-") == 3 and "nan" not in line
