@@ -1047,33 +1047,36 @@ __global__ void sum_bf16(const uint4 *s0, const uint4 *s1, const uint4 *s2, cons
 }
 
 // strided channel copy for ch_concat / slicing: dst[p][doff + c] = src[p][soff + c], c < Cc
+// mode 0: copy; 1: accumulate (dst += src); 2: relu'-masked copy (dst holds relu(z): keep
+// src where dst > 0) -- the backward of a ch_concat whose input came from a fused conv+relu
 __global__ void channel_copy(const bf16_t *__restrict__ src, int Cs, int soff, bf16_t *__restrict__ dst, int Cd,
-                             int doff, int Cc, long npix, int accumulate) {
+                             int doff, int Cc, long npix, int mode) {
   const long total = npix * Cc;
   for (long i = grid_stride_start(); i < total; i += grid_stride()) {
     const long p = i / Cc;
     const int c = i % Cc;
     const float v = bf2f(src[p * Cs + soff + c]);
     bf16_t *d = dst + p * Cd + doff + c;
-    *d = f2bf(accumulate ? bf2f(*d) + v : v);
+    const float o = bf2f(*d);
+    *d = f2bf(mode == 1 ? o + v : (mode == 2 && !(o > 0.f)) ? 0.f : v);
   }
 }
 
 // 8-channel (16-byte) form of channel_copy when every stride/offset/count is a multiple of 8
 // (all GoogLeNet concat branches): one uint4 per lane, 32-bit index math (total8 < 2^31).
 __global__ void channel_copy8(const uint4 *__restrict__ src, int Cs8, int soff8, uint4 *__restrict__ dst, int Cd8,
-                              int doff8, int Cc8, uint32_t total8, int accumulate) {
+                              int doff8, int Cc8, uint32_t total8, int mode) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total8; i += gridDim.x * blockDim.x) {
     const uint32_t p = i / static_cast<uint32_t>(Cc8);
     const uint32_t c = i - p * static_cast<uint32_t>(Cc8);
     uint4 v = src[static_cast<size_t>(p) * Cs8 + soff8 + c];
     uint4 *d = dst + static_cast<size_t>(p) * Cd8 + doff8 + c;
-    if (accumulate) {
+    if (mode != 0) {
       float a[8], b[8];
       unpack8(v, a);
       unpack8(*d, b);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) a[e] += b[e];
+      for (int e = 0; e < 8; ++e) a[e] = mode == 1 ? a[e] + b[e] : (b[e] > 0.f ? a[e] : 0.f);
       v = pack8(a);
     }
     *d = v;

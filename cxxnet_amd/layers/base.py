@@ -27,6 +27,18 @@ class Node:
         self.cp = 0
         self.data: Optional[torch.Tensor] = None
         self.fp32_view: Optional[torch.Tensor] = None  # loss layers expose fp32 predictions here
+        # zero-copy split outputs: `data` aliases the split input (read-only in forward) and the
+        # consumer writes its input gradient into this private buffer instead
+        self.grad_buf: Optional[torch.Tensor] = None
+
+    @property
+    def gdst(self) -> torch.Tensor:
+        """Where a layer writes the gradient w.r.t. this node (normally the node itself)."""
+        return self.grad_buf if self.grad_buf is not None else self.data
+
+    def gmat(self) -> torch.Tensor:
+        g = self.gdst
+        return g.view(g.shape[0], -1)
 
     def set_shape(self, b, c, h, w, cp=None):
         self.shape = (int(b), int(c), int(h), int(w))

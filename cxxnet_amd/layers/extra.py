@@ -68,8 +68,14 @@ class BiasLayer(Layer):
 
 
 class SplitLayer(Layer):
-    """`split` -- reference src/layer/split_layer-inl.hpp:12-45: 1 -> n copies, grads summed."""
+    """`split` -- reference src/layer/split_layer-inl.hpp:12-45: 1 -> n copies, grads summed.
+
+    Zero-copy on the GPU (the executor sets `alias` when every consumer of every output only
+    reads its input in forward: conv / fullc / pooling / lrn): the outputs ARE the input buffer,
+    each consumer writes its data-gradient into its output node's private grad buffer, and
+    backward sums those into the input node -- no forward copies."""
     type_name = "split"
+    alias = False
 
     def init_connection(self, nodes_in, nodes_out):
         _check(len(nodes_in) == 1 and len(nodes_out) >= 1, "SplitLayer: only support 1-n connection")
@@ -77,6 +83,8 @@ class SplitLayer(Layer):
             o.set_shape(*nodes_in[0].shape, cp=nodes_in[0].cp)
 
     def forward(self, is_train, nodes_in, nodes_out):
+        if self.alias:
+            return
         # one read of the input per 4 outputs (ops.fanout_copy), not one per output
         ops.fanout_copy(nodes_in[0].data, [o.data for o in nodes_out])
 
@@ -84,7 +92,7 @@ class SplitLayer(Layer):
         if not prop_grad:
             return
         # the output gradients summed in one pass (fp32 accumulation, one rounding)
-        ops.sum_into(nodes_in[0].data, [o.data for o in nodes_out])
+        ops.sum_into(nodes_in[0].gdst, [o.gdst for o in nodes_out])
 
 
 class ConcatLayer(Layer):
@@ -95,6 +103,9 @@ class ConcatLayer(Layer):
         super().__init__(ctx)
         self.dim = dim
         self.type_name = "ch_concat" if dim == 1 else "concat"
+        # inputs that hold relu(z) of a fused conv/fullc -> relu producer: the gradient slice
+        # copied back into them is masked by relu'(z) (the activation they still hold)
+        self.grad_mask_inputs = set()
 
     def init_connection(self, nodes_in, nodes_out):
         _check(len(nodes_in) > 1 and len(nodes_out) == 1, "Concat layer only support n-1 connection")
@@ -142,15 +153,16 @@ class ConcatLayer(Layer):
         if not prop_grad:
             return
         if self.dim == 1:
-            for src, dst, off, c in self._pieces(nodes_in, nodes_out):
-                ops.channel_copy(dst, off, src, 0, c)
+            for k, (src, dst, off, c) in enumerate(self._pieces(nodes_in, nodes_out)):
+                ops.channel_copy(dst, off, nodes_in[k].gdst, 0, c, mask_relu=k in self.grad_mask_inputs)
         else:
             out = nodes_out[0].data
             B, H, W, C = out.shape
             off = 0
-            for n in nodes_in:
+            for k, n in enumerate(nodes_in):
                 wi = n.data.shape[2]
-                ops.channel_copy(out.view(B * H, W * C), off * C, n.data.view(B * H, wi * C), 0, wi * C)
+                ops.channel_copy(out.view(B * H, W * C), off * C, n.gdst.view(B * H, wi * C), 0, wi * C,
+                                 mask_relu=k in self.grad_mask_inputs)
                 off += wi
 
 

@@ -7,6 +7,8 @@ the same node holds the activation in forward and its gradient in backward).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import ops
@@ -17,6 +19,9 @@ from .base import BinReader, BinWriter, Layer, Node, ParamSpec
 def _check(cond, msg):
     if not cond:
         raise ValueError(msg)
+
+
+_WGRAD_BIAS_FOLD = os.environ.get("CXXNET_WGRAD_BIAS_FOLD", "0") == "1"
 
 
 def _bias_init(val):
@@ -97,7 +102,7 @@ class FullConnectLayer(Layer):
         if self.b is not None:
             ops.bias_grad(dy, self.b.g)
         if prop_grad:
-            ops.fc_backward_data(dy, self.w.wb, x, mask_relu=self.grad_mask_relu)
+            ops.fc_backward_data(dy, self.w.wb, nodes_in[0].gmat(), mask_relu=self.grad_mask_relu)
 
     def save_model(self, fo: BinWriter):
         fo.write(self.lp.to_bytes())
@@ -226,13 +231,18 @@ class ConvolutionLayer(Layer):
     def backprop(self, prop_grad, nodes_in, nodes_out):
         x, dy = nodes_in[0].data, nodes_out[0].data
         self.geo.N = x.shape[0]
-        ops.conv_backward_weight(x, dy, self.w.g, self.geo)
-        if self.b is not None:
+        # CXXNET_WGRAD_BIAS_FOLD=1: the bias gradient rides along in the register-staged weight-grad
+        # GEMM (it streams dy anyway).  Off by default: on GoogLeNet b128 the folded kernels ran
+        # +331 us/step against the 303 us/step of separate colsum passes they replace
+        # (profiles/r2_inception_bias_fold.md)
+        fold = _WGRAD_BIAS_FOLD and self.b is not None
+        folded = ops.conv_backward_weight(x, dy, self.w.g, self.geo, db=self.b.g if fold else None)
+        if self.b is not None and not folded:
             ops.bias_grad(dy.view(-1, dy.shape[-1]), self.b.g)
         if prop_grad:
             if self._wt is None or self._wt.shape != self.w.wb.shape:
                 self._wt = torch.empty_like(self.w.wb)
-            ops.conv_backward_data(dy, self.w.wb, x, self.geo, self._wt, mask_relu=self.grad_mask_relu)
+            ops.conv_backward_data(dy, self.w.wb, nodes_in[0].gdst, self.geo, self._wt, mask_relu=self.grad_mask_relu)
 
     def save_model(self, fo: BinWriter):
         fo.write(self.lp.to_bytes())
@@ -342,7 +352,7 @@ class PoolingLayer(Layer):
         relu = self.relu or self.grad_mask_relu
         if relu and self._mask_in_state():
             relu = 2  # relu' of the argmax was recorded by the forward: no read of x
-        ops.pool_backward(x, self.state, nodes_out[0].data, x, lp.kernel_height, lp.kernel_width, lp.stride,
+        ops.pool_backward(x, self.state, nodes_out[0].data, nodes_in[0].gdst, lp.kernel_height, lp.kernel_width, lp.stride,
                           lp.pad_y, self.mode, relu)
 
 
@@ -383,7 +393,7 @@ class LRNLayer(Layer):
             return
         x = nodes_in[0].data
         # in place: the LDS-staged kernel reads a pixel's whole channel row before writing it
-        ops.lrn_backward(x, nodes_out[0].data, x, self.nsize, self.alpha, self.beta, self.knorm)
+        ops.lrn_backward(x, nodes_out[0].data, nodes_in[0].gdst, self.nsize, self.alpha, self.beta, self.knorm)
 
 
 # ============================================================================ dropout

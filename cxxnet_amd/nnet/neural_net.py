@@ -30,6 +30,10 @@ from .arena import ParamArena
 from ..io.data import U8Images
 
 K_CONV, K_FULLC, K_RELU, K_MAXPOOL, K_DROPOUT = 10, 1, 3, 11, 8
+K_SPLIT, K_CONCAT, K_CHCONCAT, K_SUMPOOL, K_AVGPOOL, K_LRN = 23, 18, 28, 12, 13, 15
+# layers that only READ their input node in forward and write the input gradient through
+# Node.gdst: they may consume a zero-copy split output
+_SPLIT_SAFE = (K_CONV, K_FULLC, K_MAXPOOL, K_SUMPOOL, K_AVGPOOL, K_LRN)
 
 
 class Connection:
@@ -145,26 +149,77 @@ class NeuralNet:
                 continue
             j = real[0][0]
             cj = self.connections[j]
-            if j == 0 or cj.shared or cj.type not in (K_CONV, K_FULLC, K_MAXPOOL) or len(cj.nodes_in) != 1:
+            if j == 0 or cj.shared:
+                continue
+            if cj.type in (K_CONCAT, K_CHCONCAT):
+                # concat backward copies the gradient slice back into b masked by relu'(z)
+                p.layer.fuse_relu = True
+                conn.layer.fused_into_producer = True
+                cj.layer.grad_mask_inputs.add(cj.nodes_in.index(b))
+                self.aliases[id(b)] = a
+                continue
+            if cj.type not in (K_CONV, K_FULLC, K_MAXPOOL) or len(cj.nodes_in) != 1:
                 continue
             # commit: producer epilogue applies relu, b aliases a, consumer masks the gradient
             p.layer.fuse_relu = True
             conn.layer.fused_into_producer = True
             cj.layer.grad_mask_relu = True
             self.aliases[id(b)] = a
+        self._fuse_split(producers, consumers)
+
+    def _fuse_split(self, producers, consumers):
+        """Zero-copy split: when the split is its input's only reader and every output feeds
+        exactly one read-only-in-forward layer, the outputs alias the input buffer and each
+        consumer's data-gradient goes to the output node's private grad buffer (summed by the
+        split's backward).  Saves one full activation copy per branch per step."""
+        self.split_alias = {}
+        for i, conn in enumerate(self.connections):
+            if conn.type != K_SPLIT or conn.shared or len(conn.nodes_in) != 1:
+                continue
+            a = conn.nodes_in[0]
+            if len(consumers.get(id(a), [])) != 1:
+                continue
+            ok = True
+            for o in conn.nodes_out:
+                cons = consumers.get(id(o), [])
+                if o is a or len(producers.get(id(o), [])) != 1 or len(cons) != 1 or cons[0][1]:
+                    ok = False
+                    break
+                j = cons[0][0]
+                cj = self.connections[j]
+                if j == 0 or cj.type not in _SPLIT_SAFE or len(cj.nodes_in) != 1 or cj.layer.grad_mask_relu:
+                    ok = False
+                    break
+            if not ok:
+                continue
+            conn.layer.alias = True
+            for o in conn.nodes_out:
+                self.split_alias[id(o)] = a
 
     def _alloc_nodes(self):
         dt = self.ctx.act_dtype
-        aliases = getattr(self, "aliases", {})
+        aliases = dict(getattr(self, "aliases", {}))
+        splits = getattr(self, "split_alias", {})
+        aliases.update(splits)
         for n in self.nodes:
             if id(n) not in aliases:
                 n.alloc(self.device, dt)
-        for n in self.nodes:
-            if id(n) in aliases:
+        pending = [n for n in self.nodes if id(n) in aliases]
+        for _ in range(len(pending) + 1):  # resolve chains (split of a relu alias, ...)
+            left = []
+            for n in pending:
                 src = aliases[id(n)]
                 if src.data is None:
-                    src.alloc(self.device, dt)
-                n.data = src.data
+                    left.append(n)
+                else:
+                    n.data = src.data
+            pending = left
+            if not pending:
+                break
+        assert not pending, "unresolved node aliases"
+        for n in self.nodes:
+            if id(n) in splits:
+                n.grad_buf = torch.zeros_like(n.data)
 
     def _build_arena(self):
         specs = []
@@ -343,16 +398,19 @@ class _BatchView:
         if net.cur_batch == net.max_batch:
             self.saved = None
             return
-        self.saved = [(n, n.data) for n in net.nodes]
+        self.saved = [(n, n.data, n.grad_buf) for n in net.nodes]
         seen = {}
-        for n, d in self.saved:
+        for n, d, g in self.saved:
             key = d.data_ptr()
             if key not in seen:
                 seen[key] = d[: net.cur_batch]
             n.data = seen[key]
+            if g is not None:
+                n.grad_buf = g[: net.cur_batch]
 
     def __exit__(self, *exc):
         if self.saved is not None:
-            for n, d in self.saved:
+            for n, d, g in self.saved:
                 n.data = d
+                n.grad_buf = g
         return False

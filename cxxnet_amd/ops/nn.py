@@ -421,8 +421,9 @@ def sum_into(y, srcs):
         first = y
 
 
-def channel_copy(src, soff, dst, doff, cc, accumulate=False):
-    """dst[..., doff:doff+cc] (+)= src[..., soff:soff+cc] for NHWC tensors with equal pixel counts."""
+def channel_copy(src, soff, dst, doff, cc, accumulate=False, mask_relu=False):
+    """dst[..., doff:doff+cc] (+)= src[..., soff:soff+cc] for NHWC tensors with equal pixel counts.
+    mask_relu: dst holds relu(z) on entry; the copy keeps src only where dst > 0 (relu')."""
     Cs, Cd = src.shape[-1], dst.shape[-1]
     npix = src.numel() // Cs
     if not src.is_cuda:
@@ -430,8 +431,11 @@ def channel_copy(src, soff, dst, doff, cc, accumulate=False):
         s = src.view(npix, Cs)[:, soff:soff + cc]
         if accumulate:
             d.add_(s)
+        elif mask_relu:
+            d.copy_(torch.where(d > 0, s, torch.zeros_like(s)))
         else:
             d.copy_(s)
         return
+    mode = 2 if mask_relu else int(bool(accumulate))
     native.check(_k().cxn_channel_copy(src.data_ptr(), Cs, soff, dst.data_ptr(), Cd, doff, cc, npix,
-                                       int(accumulate), _stream()), "channel_copy")
+                                       mode, _stream()), "channel_copy")

@@ -183,3 +183,32 @@ def test_device_metrics_match_host_metrics():
         tr.update(b)
     line = tr.evaluate(None, "train")
     assert line.count("train-") == 3 and "nan" not in line
+
+
+def test_zero_copy_split_and_concat_relu_fusion_match_unfused(monkeypatch):
+    """GoogLeNet graph: zero-copy split (outputs alias the input, data-grads go to private
+    grad buffers) and relu fused into the conv epilogue in front of ch_concat (relu'-masked
+    gradient copy) must compute what the unfused executor computes."""
+    batch = 4
+    pairs = _pairs("inception_v1", batch)
+    fused = _trainer(pairs, "gpu")
+    monkeypatch.setenv("CXXNET_FUSE", "0")
+    plain = _trainer(pairs, "gpu")
+    monkeypatch.delenv("CXXNET_FUSE")
+    net = fused.net
+    assert any(getattr(c.layer, "alias", False) for c in net.connections), "no split was aliased"
+    assert any(getattr(c.layer, "grad_mask_inputs", None) for c in net.connections), "no concat relu fusion"
+    assert not any(getattr(c.layer, "alias", False) for c in plain.net.connections)
+    plain.net.arena.w.copy_(fused.net.arena.w)
+    plain.net.arena.sync_shadow()
+    c, h, w = fused.net_cfg.input_shape
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(batch, c, h, w, generator=g).cuda()
+    y = torch.randint(0, 1000, (batch, 1), generator=g).float().cuda()
+    for _ in range(2):
+        fused.update(DataBatch(x, y))
+        plain.update(DataBatch(x, y))
+    torch.cuda.synchronize()
+    w0 = fused.net.arena.w
+    assert _rel(plain.net.arena.m1, fused.net.arena.m1) < 1e-2
+    assert _rel(plain.net.arena.w, w0) < 1e-4
