@@ -499,6 +499,277 @@ void launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int
                      A, B, E, ti, tj, per, ktiles);
 }
 
+
+// ======================================================================================
+// Segmented 8-wave pipeline (tiles 50-51): the big-tile form for K-major operands
+// (conv forward / data-grad, fc forward).
+//
+// The cdna guide's lesson for this regime: at ~1 block per CU the lever is keeping LDS-DMA
+// loads in flight ACROSS barriers, with counted waits, and releasing LDS at a finer grain
+// than a whole K-tile.  Here every K-tile (BK = 64) is split into two k-halves and the LDS
+// holds four k-half slots (2 K-tiles x 2 halves) of [BM + BN][32] bf16 = 64-byte rows:
+//   * one SEGMENT = one k-half of one K-tile: wait for its slot -> barrier -> issue the DMAs
+//     of the k-half three segments ahead into the slot the previous segment just released
+//     -> read fragments -> MR x NR MFMAs (one 16x16x32 k-step) between s_setprio(1)/(0);
+//   * a wave waits with a constant `s_waitcnt vmcnt(2 * NPH)`: two later k-halves stay in
+//     flight across every barrier, so a DMA has three segments (~3 x 1000 MFMA cycles per
+//     SIMD at 256x256) to land; past the end of the K slice the DMAs are all-OOB dummies so
+//     the count never changes;
+//   * 8 waves (2 x 4), 2 per SIMD: per wave a (BM/2) x 64 output tile, so a 256 x 256 block
+//     reads 24 KiB of fragments per 64 MFMAs per wave (vs 4 KiB per 16 for 64 x 128 tiles);
+//   * 64-byte rows, 16 rows per 1-KiB DMA; chunk swizzle `c ^ 2*((row >> 3) & 1)` on the
+//     source address keeps both the DMA image lane-linear and every ds_read_b128 lane group
+//     of the fragment reads on 16 distinct 16-byte bank slots.
+template <int MODE, int R>
+struct SegOp {  // one operand's DMAs for a k-half slot: R rows x 32 k, 8 waves
+  static constexpr int NI = R / 128;  // 1-KiB DMA instructions per wave per slot
+  static_assert(kmajor(MODE) && R % 128 == 0, "segmented kernel: K-major operands, 128-row multiples");
+  int s0[NI], s1[NI], s2[NI];
+  int lchunk;
+
+  __device__ __forceinline__ void init(const GOperand &op, int row0, uint32_t goff, int wave, int lane) {
+    lchunk = (lane & 3) ^ (2 * (lane >> 5));  // rows 16q + lane/4: (row >> 3) & 1 == lane >> 5
+#pragma unroll
+    for (int s = 0; s < NI; ++s) {
+      const int r = row0 + 16 * (wave + 8 * s) + (lane >> 2);
+      if constexpr (MODE == K_DIRECT) {
+        s0[s] = r < op.rows ? static_cast<int>(goff + static_cast<uint32_t>(r * op.ld) * 2u) : -1;
+        s1[s] = s2[s] = 0;
+      } else {
+        if (r < op.rows) {
+          const uint32_t n = fdiv(static_cast<uint32_t>(r), op.fd_hw);
+          const uint32_t rem = static_cast<uint32_t>(r) - n * static_cast<uint32_t>(op.Ho * op.Wo);
+          const uint32_t ho = fdiv(rem, op.fd_wo);
+          const uint32_t wo = rem - ho * op.Wo;
+          s0[s] = static_cast<int>(n) * op.H * op.W * op.C;
+          s1[s] = static_cast<int>(ho) * op.stride - op.pad_h;
+          s2[s] = static_cast<int>(wo) * op.stride - op.pad_w;
+        } else {
+          s0[s] = -1;
+          s1[s] = s2[s] = 0;
+        }
+      }
+    }
+  }
+
+  struct Prep {
+    int k, kh, kw;
+    uint32_t cb;
+    bool kin;
+  };
+  // the lane's 8 k of segment seg (K-tile kt_beg + seg/2, half seg%2)
+  __device__ __forceinline__ Prep prep(const GOperand &op, int kt, int half, int kt_end, uint32_t goff) const {
+    Prep p;
+    p.k = kt * BK + half * 32 + lchunk * 8;
+    p.kin = kt < kt_end && p.k < op.kdim;
+    if constexpr (MODE == K_GATHER) {
+      const uint32_t r = fdiv(static_cast<uint32_t>(p.k), op.fd_cg);
+      const int c = p.k - static_cast<int>(r) * op.Cg;
+      const uint32_t q = fdiv(r, op.fd_kw);
+      p.kh = p.kin ? static_cast<int>(q) : -(1 << 20);
+      p.kw = static_cast<int>(r - q * op.KW);
+      p.cb = goff + static_cast<uint32_t>(c) * 2u;
+    } else {
+      p.kh = p.kw = 0;
+      p.cb = 0;
+    }
+    return p;
+  }
+
+  template <int S>
+  __device__ __forceinline__ uint32_t offset(const GOperand &op, const Prep &p) const {
+    uint32_t off;
+    if constexpr (MODE == K_DIRECT) {
+      off = (p.kin && s0[S] >= 0) ? static_cast<uint32_t>(s0[S]) + static_cast<uint32_t>(p.k) * 2u : OOB;
+    } else {
+      const int hi = s1[S] + p.kh, wi = s2[S] + p.kw;
+      const bool ok = s0[S] >= 0 && static_cast<unsigned>(hi) < static_cast<unsigned>(op.H) &&
+                      static_cast<unsigned>(wi) < static_cast<unsigned>(op.W);
+      off = ok ? p.cb + static_cast<uint32_t>(s0[S] + (hi * op.W + wi) * op.C) * 2u : OOB;
+    }
+    asm volatile("" : "+v"(off));
+    return off;
+  }
+};
+
+// 16x16x32 fragment of rows [base, base + 16) of a 64-byte-row slot image
+__device__ __forceinline__ bf16x8 seg_frag(const char *tile, int base, int lane) {
+  const int row = base + (lane & 15);
+  const int ch = (lane >> 4) ^ (2 * ((lane >> 3) & 1));
+  return *reinterpret_cast<const bf16x8 *>(tile + row * 64 + ch * 16);
+}
+
+// (A variant with waves 4-7 staggered half a segment behind their SIMD partners -- two
+// barriers per segment -- measured 5-25% slower on every shape: profiles/r2_sweep_segmented.jsonl.)
+template <int BM, int BN, int AMODE, int BMODE, int EPI>
+__global__ void __launch_bounds__(512, 1)
+gemm_seg(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_tiles, int ktiles_total) {
+  constexpr int NW = 8, WGM = 2, WGN = 4;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int MR = WM / 16, NR = WN / 16;
+  using OA = SegOp<AMODE, BM>;
+  using OB = SegOp<BMODE, BN>;
+  constexpr int NPH = OA::NI + OB::NI;         // DMA instructions per wave per segment
+  constexpr int A_BYTES = BM * 64, SLOT = (BM + BN) * 64;
+  constexpr int EPI_BYTES = NW * 16 * (WM + 4) * 4;
+  constexpr int SMEM = 4 * SLOT > EPI_BYTES ? 4 * SLOT : EPI_BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int g = blockIdx.z;
+  const uint32_t ntile = static_cast<uint32_t>(tiles_i) * tiles_j;
+  const uint32_t tile = xcd_remap(blockIdx.x, ntile);
+  const int ti = tile % tiles_i, tj = tile / tiles_i;
+  const int i0 = ti * BM, j0 = tj * BN;
+  const int kt_beg = blockIdx.y * ksplit_tiles;
+  const int kt_end = min(kt_beg + ksplit_tiles, ktiles_total);
+  if (kt_beg >= kt_end) return;
+  const int nseg = 2 * (kt_end - kt_beg);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const rsrc_t rA = make_rsrc(A.ptr, A.nbytes);
+  const rsrc_t rB = make_rsrc(B.ptr, B.nbytes);
+  const uint32_t goA = static_cast<uint32_t>(g * A.gstride) * 2u;
+  const uint32_t goB = static_cast<uint32_t>(g * B.gstride) * 2u;
+  OA oa;
+  OB ob;
+  oa.init(A, i0, goA, wave, lane);
+  ob.init(B, j0, goB, wave, lane);
+
+  // all DMAs of segment `seg` into slot seg & 3 (all-OOB dummies past the slice)
+  auto issue = [&](int seg) {
+    const int kt = kt_beg + (seg >> 1), half = seg & 1;
+    const typename OA::Prep pa = oa.prep(A, kt, half, kt_end, goA);
+    const typename OB::Prep pb = ob.prep(B, kt, half, kt_end, goB);
+    char *sl = smem + (seg & 3) * SLOT;
+    static_for<OA::NI>([&](auto sc) {
+      constexpr int q = decltype(sc)::value;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void *)(sl + (wave + NW * q) * 1024), 16,
+                                               oa.template offset<q>(A, pa), 0, 0, 0);
+    });
+    static_for<OB::NI>([&](auto sc) {
+      constexpr int q = decltype(sc)::value;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void *)(sl + A_BYTES + (wave + NW * q) * 1024), 16,
+                                               ob.template offset<q>(B, pb), 0, 0, 0);
+    });
+  };
+
+  const int wi_ = wave % WGM, wj_ = wave / WGM;
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0);
+  issue(1);
+  issue(2);
+  for (int seg = 0; seg < nseg; ++seg) {
+    wait_vmcnt<2 * NPH>();                         // this wave's DMAs of segment `seg` landed
+    __builtin_amdgcn_s_waitcnt(0xc07f);            // lgkmcnt(0): its reads of segment seg-1 returned
+    block_barrier();                               // ... for every wave
+    issue(seg + 3);                                // into slot (seg - 1) & 3, released just now
+    const char *sa = smem + (seg & 3) * SLOT;
+    const char *sb = sa + A_BYTES;
+    bf16x8 fa[MR], fb[NR];
+#pragma unroll
+    for (int n = 0; n < NR; ++n) fb[n] = seg_frag(sb, wj_ * WN + n * 16, lane);
+#pragma unroll
+    for (int m = 0; m < MR; ++m) fa[m] = seg_frag(sa, wi_ * WM + m * 16, lane);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+#pragma unroll
+      for (int n = 0; n < NR; ++n)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  wait_vmcnt<0>();
+  __syncthreads();  // slots are reused by the epilogue
+
+  // ---- epilogue (as gemm_glds): each wave stages 16 output rows (j) x WM columns (i) in LDS
+  const int Mi = A.rows, Nj = B.rows;
+  const int ibase = i0 + wi_ * WM, jbase = j0 + wj_ * WN;
+  float *ep = reinterpret_cast<float *>(smem) + wave * 16 * (WM + 4);
+  const float *bias = E.bias ? E.bias + g * E.bias_gstride : nullptr;
+#pragma unroll
+  for (int n = 0; n < NR; ++n) {
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+      *reinterpret_cast<f32x4 *>(ep + (lane & 15) * (WM + 4) + m * 16 + (lane >> 4) * 4) = acc[m][n];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    if constexpr (EPI == EPI_BF16) {
+      bf16_t *out = reinterpret_cast<bf16_t *>(E.out) + g * E.gstride;
+      constexpr int LPR = WM / 8;
+      constexpr int RPI = 64 / LPR;
+      const int il = (lane % LPR) * 8;
+      const int i = ibase + il;
+      const bool vec_store = ((E.ldc & 7) == 0) && (i + 8 <= Mi);
+#pragma unroll
+      for (int jl = lane / LPR; jl < 16; jl += RPI) {
+        const int j = jbase + n * 16 + jl;
+        if (j < Nj && i < Mi) {
+          const f32x4 x0 = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il);
+          const f32x4 x1 = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il + 4);
+          float f[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            f[e] = f[e] * E.alpha + ((bias && i + e < Mi) ? bias[i + e] : 0.f);
+            if (E.relu) f[e] = fmaxf(f[e], 0.f);
+          }
+          bf16_t *dst = out + static_cast<long>(j) * E.ldc + i;
+          if (vec_store) {
+            if (E.mask_relu) {
+              float old[8];
+              unpack8(*reinterpret_cast<const uint4 *>(dst), old);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) f[e] = old[e] > 0.f ? f[e] : 0.f;
+            }
+            *reinterpret_cast<uint4 *>(dst) = pack8(f);
+          } else {
+            for (int e = 0; e < 8 && i + e < Mi; ++e) {
+              if (E.mask_relu && !(bf2f(dst[e]) > 0.f)) f[e] = 0.f;
+              dst[e] = f2bf(f[e]);
+            }
+          }
+        }
+      }
+    } else {  // EPI_F32: split-K slab (fc forward)
+      float *out = reinterpret_cast<float *>(E.out) + g * E.gstride + blockIdx.y * E.kstride;
+      constexpr int LPR = WM / 4;
+      constexpr int RPI = 64 / LPR;
+      const int il = (lane % LPR) * 4;
+      const int i = ibase + il;
+      const bool vec = ((E.ldc & 3) == 0) && (i + 4 <= Mi);
+#pragma unroll
+      for (int jl = lane / LPR; jl < 16; jl += RPI) {
+        const int j = jbase + n * 16 + jl;
+        if (j < Nj && i < Mi) {
+          f32x4 v = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il) * E.alpha;
+          float *dst = out + static_cast<long>(j) * E.ldc + i;
+          if (vec) {
+            *reinterpret_cast<f32x4 *>(dst) = v;
+          } else {
+            for (int e = 0; e < 4 && i + e < Mi; ++e) dst[e] = v[e];
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+  }
+}
+
+template <int BM, int BN, int AMODE, int BMODE, int EPI>
+void launch_seg(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int ksplit, hipStream_t s) {
+  const int ti = cdiv(A.rows, BM), tj = cdiv(B.rows, BN);
+  const int ktiles = cdiv(A.kdim, BK);
+  ksplit = ksplit < 1 ? 1 : (ksplit > ktiles ? ktiles : ksplit);
+  const int per = cdiv(ktiles, ksplit);
+  ksplit = cdiv(ktiles, per);
+  dim3 grid(ti * tj, ksplit, groups);
+  hipLaunchKernelGGL((gemm_seg<BM, BN, AMODE, BMODE, EPI>), grid, dim3(512), 0, s, A, B, E, ti, tj, per, ktiles);
+}
+
 // Tile ids (BM x BN, wave grid, stages); MN-major operands need a 128-wide tile side:
 //   0: 128x256 (1x4) 3      1: 128x128 (1x4) 2      2: 128x128 (2x2) 3      7: 64x128 (1x4) 2
 //  10: 128x64 (2x2) 2      13: 128x128 (1x4) 3     15: 64x64 (2x2) 3       17: 128x128 (2x2) 2
@@ -544,6 +815,19 @@ void launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int
 
 int dispatch(int amode, int bmode, int epi, int tile, const GOperand &A, const GOperand &B, const GEpi &E,
              int groups, int ksplit, hipStream_t s) {
+  // segmented 8-wave pipeline: 50 = 256x256, 51 = 128x256 (K-major A and B)
+#define CXG_SEG(AMV, BMV, EPV)                                                                      \
+  if (amode == AMV && bmode == BMV && epi == EPV) {                                                 \
+    if (tile == 50) { launch_seg<256, 256, AMV, BMV, EPV>(A, B, E, groups, ksplit, s); return 0; }  \
+    if (tile == 51) { launch_seg<128, 256, AMV, BMV, EPV>(A, B, E, groups, ksplit, s); return 0; }  \
+  }
+  if (tile >= 50 && tile <= 51) {
+    CXG_SEG(K_DIRECT, K_GATHER, EPI_BF16)
+    CXG_SEG(K_DIRECT, K_DIRECT, EPI_BF16)
+    CXG_SEG(K_DIRECT, K_DIRECT, EPI_F32)
+    return -1;
+  }
+#undef CXG_SEG
   CXG_CASE(K_DIRECT, K_GATHER, EPI_BF16, CXG_KK_TILES)    // conv fwd / dgrad
   CXG_CASE(K_DIRECT, K_ROWGATHER, EPI_BF16, CXG_KK_TILES)  // conv fwd, few input channels (conv1)
   CXG_CASE(K_DIRECT, K_DIRECT, EPI_BF16, CXG_KK_TILES)    // fc fwd

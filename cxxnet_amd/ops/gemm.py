@@ -112,7 +112,10 @@ GLDS_TILES = {0: (128, 256), 1: (128, 128), 2: (128, 128), 4: (192, 256), 5: (64
               # pipelined variants (gemm_glds.hip PIPE: setprio around the MFMA clusters, both
               # k-steps' fragments read ahead of the MFMAs) and 8-wave 128x256 / 64x256 tiles
               30: (128, 256), 31: (128, 256), 33: (128, 256), 34: (256, 256), 35: (64, 256), 36: (128, 128),
-              37: (64, 128), 38: (128, 256), 39: (64, 256), 40: (128, 128), 41: (128, 128)}
+              37: (64, 128), 38: (128, 256), 39: (64, 256), 40: (128, 128), 41: (128, 128),
+              # segmented 8-wave pipeline (gemm_seg): k-half LDS slots, two k-halves of DMAs in
+              # flight across every barrier
+              50: (256, 256), 51: (128, 256)}
 # operand loaders of gemm_glds.hip
 GL_K, GL_KG, GL_MN, GL_MNG, GL_KR = 0, 1, 2, 3, 4  # K_DIRECT, K_GATHER, MN_DIRECT, MN_GATHER, K_ROWGATHER
 EPI_F32_ACC_G, EPI_F32_ATOMIC_G = 2, 3
@@ -131,7 +134,7 @@ _glds_cfg = {"on": os.environ.get("CXXNET_GEMM_GLDS", "1") != "0",
 # AlexNet shape (profiles/r14_glds_tiles.jsonl); 2 and 0 cover wide-i GEMMs (fc); the 8-wave
 # 128x256 / 64x256 tiles and the pipelined variants (30-41) win conv2/conv3 forward, fc6 forward
 # and several VGG shapes (profiles/r2_sweep_tiles.jsonl).
-GLDS_CANDS = (1, 7, 10, 15, 2, 0, 13, 17, 21, 25, 30, 31, 34, 37, 38, 39, 40, 41)
+GLDS_CANDS = (1, 7, 10, 15, 2, 0, 13, 17, 21, 25, 30, 31, 34, 37, 38, 39, 40, 41, 50, 51)
 # Pseudo-tile: the register-staged kernel (gemm_mfma.hip) with its heuristic tile.  A candidate
 # for conv forward / data-grad / weight-grad, where it still wins some shapes (conv2 forward on
 # AlexNet timed alone: 172 vs 186 us, profiles/r15_glds_8wave.jsonl "old_us").

@@ -1,0 +1,18 @@
+#!/bin/bash
+# PMC counters for one probe op at forced GEMM tiles.  bash tools/pmc_tile.sh <tag> <op> <tile...>
+set -o pipefail
+TAG=$1; OP=$2; shift 2
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/pmct_$TAG
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+for T in "$@"; do
+i=0
+for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAIT_ANY" \
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT" \
+           "TA_BUSY_avr TA_TA_BUSY_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum FETCH_SIZE"; do
+  i=$((i+1))
+  CXXNET_GLDS_TILE=$T timeout -s KILL 90 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $OUT/t${T}_p$i -o p -- python3 $R/benchmarks/kernel_probe.py $OP > $OUT/t${T}_p$i.log 2>&1 || { echo "pmc tile $T pass $i failed"; tail -5 $OUT/t${T}_p$i.log; }
+done
+done
+echo done
