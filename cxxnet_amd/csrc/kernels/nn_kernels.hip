@@ -1095,6 +1095,39 @@ __global__ void pad_rows(const bf16_t *__restrict__ src, bf16_t *__restrict__ ds
 }
 
 
+// Max-unpool with the reference's tie semantics (src/layer/pooling_layer-inl.hpp:55-86,
+// `unpool<red::maximum>`): EVERY input of a window that equals the window's max receives
+// that window's gradient (pool_tie = all).  Gather form: one thread per input element sums
+// over the windows covering it; y is the saved pooled output.  relu: the pooled values were
+// max(relu(x)) and the gradient is masked by relu'(x).
+__global__ void pool_bwd_tie_all(const bf16_t *__restrict__ x, const bf16_t *__restrict__ y,
+                                 const bf16_t *__restrict__ dy, bf16_t *__restrict__ dx, int N, int H, int W, int C,
+                                 int Ho, int Wo, int KH, int KW, int S, int P, int relu) {
+  const long total = static_cast<long>(N) * H * W * C;
+  for (long i = grid_stride_start(); i < total; i += grid_stride()) {
+    const int c = static_cast<int>(i % C);
+    const long pix = i / C;
+    const int w = static_cast<int>(pix % W);
+    const long nh = pix / W;
+    const int h = static_cast<int>(nh % H);
+    const int n = static_cast<int>(nh / H);
+    float xv = bf2f(x[i]);
+    if (relu) xv = fmaxf(xv, 0.f);
+    // windows ho with ho*S - P <= h <= ho*S - P + KH - 1
+    const int hp = h + P, wp = w + P;
+    const int ho0 = hp - KH + 1 > 0 ? (hp - KH + 1 + S - 1) / S : 0, ho1 = min(Ho - 1, hp / S);
+    const int wo0 = wp - KW + 1 > 0 ? (wp - KW + 1 + S - 1) / S : 0, wo1 = min(Wo - 1, wp / S);
+    float g = 0.f;
+    for (int ho = ho0; ho <= ho1; ++ho)
+      for (int wo = wo0; wo <= wo1; ++wo) {
+        const long o = ((static_cast<long>(n) * Ho + ho) * Wo + wo) * C + c;
+        if (bf2f(y[o]) == xv) g += bf2f(dy[o]);
+      }
+    if (relu && !(bf2f(x[i]) > 0.f)) g = 0.f;
+    dx[i] = f2bf(g);
+  }
+}
+
 // ------------------------------------------------------------------ evaluation metrics
 // Training / eval metrics on the device (reference src/utils/metric.h:20-236), one wave per
 // instance row of fp32 scores p[B][K] against labels lab[B][lw]:
@@ -1253,6 +1286,13 @@ CXN_API int cxn_pool_fwd(const void *x, void *y, void *arg, int N, int H, int W,
     pool_fwd<1><<<nblocks(static_cast<long>(N) * Ho * Wo * C), NT, 0, S_>>>(
         (const bf16_t *)x, (bf16_t *)y, (uint8_t *)arg, N, H, W, C, Ho, Wo, KH, KW, S, P, mode, relu);
   }
+  RET;
+}
+
+CXN_API int cxn_pool_bwd_tie_all(const void *x, const void *y, const void *dy, void *dx, int N, int H, int W, int C,
+                                 int Ho, int Wo, int KH, int KW, int S, int P, int relu, void *stream) {
+  pool_bwd_tie_all<<<nblocks(static_cast<long>(N) * H * W * C), NT, 0, S_>>>(
+      (const bf16_t *)x, (const bf16_t *)y, (const bf16_t *)dy, (bf16_t *)dx, N, H, W, C, Ho, Wo, KH, KW, S, P, relu);
   RET;
 }
 CXN_API int cxn_pool_bwd(const void *x, const void *arg, const void *dy, void *dx, int N, int H, int W, int C, int Ho,

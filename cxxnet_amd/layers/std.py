@@ -304,8 +304,16 @@ class ActivationLayer(Layer):
 # ============================================================================ pooling
 class PoolingLayer(Layer):
     """`max_pooling`/`sum_pooling`/`avg_pooling`/`relu_max_pooling` --
-    reference src/layer/pooling_layer-inl.hpp:11-114 (ceil-mode windows, value-compare
-    unpool).  Extension: `pad` is honoured (the reference parses but ignores it)."""
+    reference src/layer/pooling_layer-inl.hpp:11-114 (ceil-mode windows).  Extension: `pad`
+    is honoured (the reference parses but ignores it).
+
+    Max-unpool ties: the reference compares values, so EVERY input equal to a window's max
+    gets the gradient (`unpool<red::maximum>`, :55-86).  The default here (`pool_tie = first`)
+    routes it to the first maximum only, recorded as a uint8 offset in forward (no saved
+    output, no re-read of it in backward).  `pool_tie = all` reproduces the reference: the
+    pooled output is saved and the backward compares values (ops.pool_backward_tie_all).
+    Ties only occur between bit-identical activations (e.g. windows of relu zeros, which get
+    no gradient through a fused relu either way)."""
 
     def __init__(self, ctx, mode, relu=False):
         super().__init__(ctx)
@@ -313,6 +321,15 @@ class PoolingLayer(Layer):
         self.relu = relu
         self.type_name = ("relu_" if relu else "") + {"max": "max", "sum": "sum", "avg": "avg"}[mode] + "_pooling"
         self.state = None
+        self.tie_all = False
+        self.ysave = None
+
+    def set_param(self, name, val):
+        super().set_param(name, val)
+        if name == "pool_tie":
+            if val not in ("first", "all"):
+                raise ValueError("pool_tie must be first or all")
+            self.tie_all = val == "all"
 
     def init_connection(self, nodes_in, nodes_out):
         _check(len(nodes_in) == 1 and len(nodes_out) == 1, "PoolingLayer: only support 1-1 connection")
@@ -333,15 +350,23 @@ class PoolingLayer(Layer):
             self.state = torch.empty(y.data.shape, dtype=torch.uint8, device=y.data.device)
         return self.state
 
+    def _tie_all(self) -> bool:
+        return self.tie_all and self.mode == "max"
+
     def forward(self, is_train, nodes_in, nodes_out):
         lp = self.lp
         st = self._state(nodes_out[0]) if is_train else None
         ops.pool_forward(nodes_in[0].data, nodes_out[0].data, st, lp.kernel_height, lp.kernel_width, lp.stride,
                          lp.pad_y, self.mode, self.relu, mark_mask=self._mask_in_state())
+        if is_train and self._tie_all():
+            y = nodes_out[0].data
+            if self.ysave is None or self.ysave.shape != y.shape:
+                self.ysave = torch.empty_like(y)
+            self.ysave.copy_(y)  # the output node is overwritten by its gradient before backprop
 
     def _mask_in_state(self) -> bool:
         lp = self.lp
-        return (self.ctx.is_gpu and (self.relu or self.grad_mask_relu)
+        return (self.ctx.is_gpu and (self.relu or self.grad_mask_relu) and not self._tie_all()
                 and ops.pool_mask_in_state(self.mode, lp.kernel_height, lp.kernel_width))
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
@@ -350,6 +375,10 @@ class PoolingLayer(Layer):
         lp = self.lp
         x = nodes_in[0].data
         relu = self.relu or self.grad_mask_relu
+        if self._tie_all():
+            ops.pool_backward_tie_all(x, self.ysave, nodes_out[0].data, nodes_in[0].gdst, lp.kernel_height,
+                                      lp.kernel_width, lp.stride, lp.pad_y, relu=relu)
+            return
         if relu and self._mask_in_state():
             relu = 2  # relu' of the argmax was recorded by the forward: no read of x
         ops.pool_backward(x, self.state, nodes_out[0].data, nodes_in[0].gdst, lp.kernel_height, lp.kernel_width, lp.stride,

@@ -81,6 +81,7 @@ _SIGS = {
     "cxn_gemm_wgrad_bias": [ctypes.POINTER(CxnOperand), ctypes.POINTER(CxnOperand), _I, _P, _L, _I, _P, _L, _I, _I,
                             _I, _P],
     "cxn_set_deterministic": [_I],
+    "cxn_pool_bwd_tie_all": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "cxn_metric_eval": [_P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "cxn_nchw_f32_to_nhwc_bf16": [_P, _P, _I, _I, _I, _I, _I, _F, _P],
     "cxn_image_u8_to_nhwc_bf16": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _P, _P],

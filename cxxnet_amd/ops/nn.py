@@ -191,6 +191,33 @@ def pool_backward(x, state, dy, dx, KH, KW, S, P, mode: str, relu=False, dbias=N
                                    _stream()), "pool_bwd")
 
 
+def pool_backward_tie_all(x, y, dy, dx, KH, KW, S, P, relu=False):
+    """Max-unpool with the reference tie rule (pooling_layer-inl.hpp:55-86): every input
+    equal to its window's max y gets that window's gradient; relu: max over relu(x), the
+    gradient masked by relu'(x).  y: the saved pooled output."""
+    N, H, W, C = x.shape
+    Ho, Wo = dy.shape[1], dy.shape[2]
+    if not x.is_cuda:
+        xv = x.clamp_min(0) if relu else x
+        g = torch.zeros((N, H + 2 * P + KH + S, W + 2 * P + KW + S, C), dtype=dy.dtype)
+        xp = torch.full_like(g, float("nan"))  # padding never equals a max
+        xp[:, P:P + H, P:P + W, :] = xv
+        for ho in range(Ho):
+            hs = ho * S
+            for wo in range(Wo):
+                ws = wo * S
+                win = xp[:, hs:hs + KH, ws:ws + KW, :]
+                eq = (win == y[:, ho:ho + 1, wo:wo + 1, :]).to(g.dtype)
+                g[:, hs:hs + KH, ws:ws + KW, :] += eq * dy[:, ho:ho + 1, wo:wo + 1, :]
+        g = g[:, P:P + H, P:P + W, :]
+        if relu:
+            g = g * (x > 0).to(g.dtype)
+        dx.copy_(g)
+        return
+    native.check(_k().cxn_pool_bwd_tie_all(x.data_ptr(), y.data_ptr(), dy.data_ptr(), dx.data_ptr(), N, H, W, C,
+                                           Ho, Wo, KH, KW, S, P, int(bool(relu)), _stream()), "pool_bwd_tie_all")
+
+
 # ----------------------------------------------------------------------------- LRN
 def _lrn_norm(x, nsize, alpha, knorm):
     C = x.shape[-1]

@@ -212,3 +212,70 @@ def test_zero_copy_split_and_concat_relu_fusion_match_unfused(monkeypatch):
     w0 = fused.net.arena.w
     assert _rel(plain.net.arena.m1, fused.net.arena.m1) < 1e-2
     assert _rel(plain.net.arena.w, w0) < 1e-4
+
+
+def _traj(tr, batches):
+    losses = []
+    for x, y in batches:
+        tr.update(DataBatch(x, y))
+        line = tr.evaluate(None, "train")
+        losses.append(float(line.split("train-logloss:")[1].split("\t")[0]))
+    return losses
+
+
+def _wdist(a, b, w0):
+    """Per-layer weight discrepancy relative to the distance trained from the common start."""
+    out = []
+    for (li, sa), (_, sb), (_, s0) in zip(a.net.arena.specs, b.net.arena.specs, w0):
+        wa = sa.w.detach().float().cpu()
+        wb = sb.w.detach().float().cpu()[..., : wa.shape[-1]]
+        d0 = s0[..., : wa.shape[-1]]
+        out.append(((wa - wb).norm() / (wa - d0).norm().clamp_min(1e-12)).item())
+    return out
+
+
+@pytest.mark.timeout(600)
+def test_alexnet_trajectory_gpu_vs_cpu_fp32():
+    """The real AlexNet graph -- max pooling, LRN, dropout ON, relu fusion -- at batch 64 for 10
+    SGD steps on the GPU (bf16 activations, HIP kernels) against the CPU fp32 executor started
+    from the same (bf16-representable) weights with identical dropout masks (counter hash).
+
+    Tolerances come from a measured noise floor: the same CPU fp32 run restarted with
+    bf16-rounded inputs and one bf16 ulp of weight noise diverges from the reference by
+    `floor`; the GPU run must stay within a small multiple of it."""
+    batch, steps = 64, 10
+    pairs = _pairs("alexnet", batch, eval_train="1") + [("metric", "logloss")]
+    cpu = _trainer(pairs, "cpu")
+    cpu2 = _trainer(pairs, "cpu")
+    gpu = _trainer(pairs, "gpu")
+    cpu.net.arena.w.copy_(cpu.net.arena.w.to(torch.bfloat16).float())
+    g = torch.Generator().manual_seed(11)
+    noise = torch.randn(cpu.net.arena.w.shape, generator=g)
+    cpu2.net.arena.w.copy_(cpu.net.arena.w * (1.0 + noise * 2.0 ** -9))  # ~1 bf16 ulp
+    for (_, sc), (_, sg) in zip(cpu.net.arena.specs, gpu.net.arena.specs):
+        sg.w.zero_()
+        sg.w[..., : sc.shape[-1]].copy_(sc.w)
+    gpu.net.arena.sync_shadow()
+    w0 = [(li, s.w.detach().clone()) for li, s in cpu.net.arena.specs]
+    c, h, w = cpu.net_cfg.input_shape
+    data = []
+    for _ in range(steps):
+        x = torch.randn(batch, c, h, w, generator=g).to(torch.bfloat16).float()
+        y = torch.randint(0, 1000, (batch, 1), generator=g).float()
+        data.append((x, y))
+    l_cpu = _traj(cpu, data)
+    l_cpu2 = _traj(cpu2, [(x.to(torch.bfloat16).float(), y) for x, y in data])
+    l_gpu = _traj(gpu, [(x.cuda(), y.cuda()) for x, y in data])
+    torch.cuda.synchronize()
+    floor_loss = max(abs(a - b) / a for a, b in zip(l_cpu, l_cpu2))
+    err_loss = max(abs(a - b) / a for a, b in zip(l_cpu, l_gpu))
+    floor_w = _wdist(cpu, cpu2, w0)
+    err_w = _wdist(cpu, gpu, w0)
+    print(f"\nloss cpu {l_cpu}\nloss gpu {l_gpu}\nrel loss err {err_loss:.3g} (floor {floor_loss:.3g})\n"
+          f"weight err per layer {[round(v, 4) for v in err_w]}\nfloor {[round(v, 4) for v in floor_w]}")
+    assert l_gpu[-1] < l_gpu[0]  # it trains
+    # measured on MI355X (tools/gpu_r2h.sh): loss error 4.7x the floor (0.0075 vs 0.0016); per
+    # layer weight error 1.0-1.4x the floor (e.g. conv3 0.165 vs 0.140, fc7 0.264 vs 0.218)
+    assert err_loss < 8 * floor_loss
+    for e, f in zip(err_w, floor_w):
+        assert e < 2 * f + 0.02, (err_w, floor_w)

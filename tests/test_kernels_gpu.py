@@ -390,3 +390,59 @@ def test_conv_weight_grad_folds_bias_grad(case, register_kernel_only):
     assert folded
     assert relerr(dw, dw_ref) < 1e-2
     assert relerr(db, 0.25 + dy.reshape(-1, geo.Cout).sum(0)) < 1e-3
+
+
+@pytest.mark.parametrize("relu,k,s,p,H", [(False, 3, 2, 0, 27), (True, 3, 2, 0, 28), (False, 3, 1, 1, 14),
+                                          (False, 2, 2, 0, 28)])
+def test_pool_tie_all(relu, k, s, p, H):
+    """pool_tie = all kernel vs the CPU value-compare unpool, on data with many exact ties
+    (values quantized to a few levels) and even sizes whose last windows run past the edge."""
+    N, C = 2, 16
+    g = torch.Generator().manual_seed(H + k)
+    x = (torch.randint(-2, 3, (N, H, H, C), generator=g).float() * 0.5)
+    Ho = ops.pool_out_size(H, k, s, p)
+    y = torch.empty(N, Ho, Ho, C)
+    ops.pool_forward(x, y, None, k, k, s, p, "max", relu)
+    dy = rnd(N, Ho, Ho, C, seed=41)
+    dx_ref = torch.empty_like(x)
+    ops.pool_backward_tie_all(x, y, dy, dx_ref, k, k, s, p, relu=relu)
+    xd = x.to(DEV, torch.bfloat16)
+    yd = torch.empty(N, Ho, Ho, C, dtype=torch.bfloat16, device=DEV)
+    ops.pool_forward(xd, yd, None, k, k, s, p, "max", relu)
+    dx = torch.empty_like(xd)
+    ops.pool_backward_tie_all(xd, yd, dy.to(DEV, torch.bfloat16), dx, k, k, s, p, relu=relu)
+    torch.cuda.synchronize()
+    assert torch.equal(yd.float().cpu(), y)
+    assert relerr(dx, dx_ref) < 1e-2
+
+
+@pytest.mark.parametrize("mode,k,s,H", [("max", 3, 2, 28), ("max", 2, 2, 28), ("max", 3, 2, 56), ("max", 3, 1, 14),
+                                        ("avg", 3, 2, 28), ("avg", 2, 2, 56)])
+@pytest.mark.parametrize("fused_relu", [False, True])
+def test_pool_rows_even_sizes_and_relu_state(mode, k, s, H, fused_relu):
+    """The production fast paths (pool_fwd_rows / pool_bwd_rows): even H/W, so the last window
+    runs past the edge (GoogLeNet 112/56/28), and -- max mode after a fused conv+relu -- relu'
+    read from bit 7 of the forward's argmax offsets (relu = 2, no dbias)."""
+    N, C = 2, 64
+    p = 1 if s == 1 else 0
+    x = rnd(N, H, H, C, seed=51)
+    if fused_relu:
+        x = x.clamp_min(0)
+    Ho = ops.pool_out_size(H, k, s, p)
+    dy = rnd(N, Ho, Ho, C, seed=52)
+    y_ref = torch.empty(N, Ho, Ho, C)
+    st_ref = torch.empty(N, Ho, Ho, C, dtype=torch.uint8)
+    ops.pool_forward(x, y_ref, st_ref, k, k, s, p, mode, False)
+    dx_ref = torch.empty_like(x)
+    ops.pool_backward(x, st_ref, dy, dx_ref, k, k, s, p, mode, fused_relu)
+    xd = x.to(DEV, torch.bfloat16)
+    y = torch.empty(N, Ho, Ho, C, dtype=torch.bfloat16, device=DEV)
+    st = torch.empty(N, Ho, Ho, C, dtype=torch.uint8, device=DEV)
+    mark = fused_relu and mode == "max"
+    ops.pool_forward(xd, y, st, k, k, s, p, mode, False, mark_mask=mark)
+    dx = torch.empty_like(xd)
+    relu = (2 if mark else 1) if fused_relu else 0
+    ops.pool_backward(xd, st, dy.to(DEV, torch.bfloat16), dx, k, k, s, p, mode, relu)
+    torch.cuda.synchronize()
+    assert relerr(y, y_ref) < 1e-2
+    assert relerr(dx, dx_ref) < 2e-2

@@ -343,3 +343,33 @@ def test_exotic_layers_train_cpu():
     assert torch.isfinite(tr.net.nodes[-1].fp32_view).all()
     for _, s in tr.net.arena.specs:
         assert not torch.equal(before[s.offset:s.offset + s.numel], tr.net.arena.w[s.offset:s.offset + s.numel]), s.tag
+
+
+def test_pool_tie_all_matches_reference_unpool():
+    """pool_tie = all: the reference's value-compare unpool (pooling_layer-inl.hpp:55-86):
+    every input equal to its window's max receives that window's gradient."""
+    import torch
+    from cxxnet_amd import ops
+    N, H, W, C, K, S = 1, 5, 5, 2, 3, 2
+    x = torch.zeros(N, H, W, C)
+    x[0, 0, 0, 0] = 1.0
+    x[0, 0, 2, 0] = 1.0          # tie with (0,0) inside window (0,0), and the max of window (0,1)
+    Ho = ops.pool_out_size(H, K, S)
+    y = torch.empty(N, Ho, Ho, C)
+    ops.pool_forward(x, y, None, K, K, S, 0, "max")
+    dy = torch.arange(1, N * Ho * Ho * C + 1, dtype=torch.float32).view(N, Ho, Ho, C)
+    dx = torch.empty_like(x)
+    ops.pool_backward_tie_all(x, y, dy, dx, K, K, S, 0)
+    # brute force
+    ref = torch.zeros_like(x)
+    for ho in range(Ho):
+        for wo in range(Ho):
+            for c in range(C):
+                win = x[0, ho * S:ho * S + K, wo * S:wo * S + K, c]
+                m = win.max()
+                for kh in range(win.shape[0]):
+                    for kw in range(win.shape[1]):
+                        if win[kh, kw] == m:
+                            ref[0, ho * S + kh, wo * S + kw, c] += dy[0, ho, wo, c]
+    assert torch.equal(dx, ref)
+    assert dx[0, 0, 0, 0] == dy[0, 0, 0, 0] and dx[0, 0, 2, 0] == dy[0, 0, 0, 0] + dy[0, 0, 1, 0]
