@@ -21,7 +21,13 @@ from concurrent.futures import ThreadPoolExecutor
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
-OUT = os.path.join(PKG, "_native")
+# CXXNET_NATIVE_DIR selects another output / load directory (the --asan build goes to
+# cxxnet_amd/_native_asan so the production libraries are never replaced by it)
+OUT = os.environ.get("CXXNET_NATIVE_DIR") or os.path.join(PKG, "_native")
+ASAN_DIR = os.path.join(PKG, "_native_asan")
+# host sanitizer flags (--asan): AddressSanitizer + UBSan on the host C++ (runtime, C ABI)
+SAN_FLAGS = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined", "-g"]
+_san = {"on": False}
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 ARCH = os.environ.get("CXXNET_OFFLOAD_ARCH", "gfx950")
@@ -55,8 +61,8 @@ def build_runtime(verbose=False, force=False) -> str:
     target = os.path.join(OUT, RT_NAME)
     if force or _newer(target, deps):
         os.makedirs(OUT, exist_ok=True)
-        cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wall", "-Wno-unused-result",
-               "-fvisibility=hidden",
+        cmd = ["g++", "-O1" if _san["on"] else "-O2", "-std=c++17", "-shared", "-fPIC", "-Wall",
+               "-Wno-unused-result", "-fvisibility=hidden"] + (SAN_FLAGS if _san["on"] else []) + [
                "-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"],
                src, "-o", target + ".tmp", "-lz", "-lpthread"]
         _run(cmd, verbose)
@@ -98,7 +104,8 @@ def build_wrapper(verbose=False, force=False) -> str:
     if force or _newer(target, deps):
         libdir = sysconfig.get_config_var("LIBDIR")
         ver = sysconfig.get_config_var("LDVERSION")
-        cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wall",
+        cmd = ["g++", "-O1" if _san["on"] else "-O2", "-std=c++17", "-shared", "-fPIC", "-Wall"] + \
+              (SAN_FLAGS if _san["on"] else []) + [
                "-I" + sysconfig.get_paths()["include"], "-I" + os.path.join(CSRC, "capi"),
                src, "-o", target + ".tmp", "-L" + libdir, "-lpython" + ver,
                "-Wl,-rpath," + libdir]
@@ -114,8 +121,39 @@ def build_all(verbose=False, force=False):
     return rt, k, w
 
 
+def build_asan(verbose=False, force=False):
+    """Host-sanitizer build (AddressSanitizer + UBSan) of the C++ runtime and the CXN* C ABI into
+    cxxnet_amd/_native_asan; the HIP kernel library is linked in unchanged (device code is not
+    sanitized: GPU ASan is not available on this pool).  Use it with
+        CXXNET_NATIVE_DIR=cxxnet_amd/_native_asan LD_PRELOAD="$(g++ -print-file-name=libasan.so)
+        $(g++ -print-file-name=libubsan.so)" ASAN_OPTIONS=detect_leaks=0 python -m pytest -m "not gpu"
+    (tools/asan_cpu_tests.sh)."""
+    global OUT
+    saved = OUT
+    OUT = ASAN_DIR
+    _san["on"] = True
+    try:
+        os.makedirs(OUT, exist_ok=True)
+        rt = build_runtime(verbose, force)
+        w = build_wrapper(verbose, force)
+        k = os.path.join(OUT, KERNEL_LIB)
+        src = os.path.join(saved, KERNEL_LIB)
+        if not os.path.exists(src):
+            OUT = saved
+            build_kernels(verbose)
+            OUT = ASAN_DIR
+        if not os.path.exists(k) or os.path.getmtime(k) < os.path.getmtime(src):
+            import shutil
+            shutil.copy2(src, k)
+        return rt, k, w
+    finally:
+        OUT = saved
+        _san["on"] = False
+
+
 if __name__ == "__main__":
     force = "--force" in sys.argv
-    for p in build_all(verbose=True, force=force):
+    built = build_asan(verbose=True, force=force) if "--asan" in sys.argv else build_all(verbose=True, force=force)
+    for p in built:
         if p:
             print("built", p)

@@ -17,7 +17,9 @@ import sysconfig
 import threading
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-_NATIVE = os.path.join(_PKG, "_native")
+_NATIVE = os.environ.get("CXXNET_NATIVE_DIR") or os.path.join(_PKG, "_native")
+if not os.path.isabs(_NATIVE):
+    _NATIVE = os.path.abspath(_NATIVE)
 _lock = threading.Lock()
 _rt = None
 _k = None
