@@ -17,8 +17,9 @@ MI355X-first design:
   * The page reader is native (``_cxxnet_rt.ImageBinReader``: a C++ thread streams
     64 MB pages ahead of the consumer).
   * Records are pulled serially (deterministic order and RNG), then decoded and
-    geometrically augmented by a thread pool.  Pillow releases the GIL in its
-    decoders, so this scales over host cores.
+    geometrically augmented by worker processes that write straight into a shared
+    batch buffer (io/augment.py; a thread pool when decode_process = 0).  The batch
+    lands in page-locked memory for a straight host-to-device DMA.
   * A batch leaves the host as uint8 (``U8Images``).  Mean subtraction, contrast,
     illumination, scale and the NHWC-bf16 conversion happen on the GPU in one fused
     kernel (``ops.image_to_nhwc``).  That is 4x less PCIe traffic than fp32 and
@@ -32,8 +33,6 @@ so warped pixels are not bit-identical to OpenCV's INTER_CUBIC (parity unpinned)
 """
 from __future__ import annotations
 
-import io as _io
-import math
 import os
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass
@@ -43,6 +42,7 @@ import numpy as np
 import torch
 
 from .. import native
+from .augment import AugmentParam, DecodePool, ShmBuffer, _augment_one, default_decode_process, shm_available
 from .data import DataBatch, DataIterator, U8Images
 
 
@@ -230,155 +230,6 @@ class ImageBinXSource(ImageBinSource):
                     yield Record(page[j][0], page[j][1], objs[j])
 
 
-# ----------------------------------------------------------------------------- augmenter
-class AugmentParam:
-    """Every key of AugmentIterator::SetParam and ImageAugmenter::SetParam."""
-
-    def __init__(self):
-        self.shape = (3, 224, 224)
-        self.rand_crop = 0
-        self.rand_mirror = 0
-        self.mirror = 0
-        self.crop_y_start = -1
-        self.crop_x_start = -1
-        self.scale = 1.0
-        self.image_mean = ""
-        self.mean_value: Optional[Tuple[float, float, float]] = None
-        self.max_random_contrast = 0.0
-        self.max_random_illumination = 0.0
-        self.max_rotate_angle = 0
-        self.max_shear_ratio = 0.0
-        self.max_aspect_ratio = 0.0
-        self.min_crop_size = -1
-        self.max_crop_size = -1
-        self.min_random_scale = 1.0
-        self.max_random_scale = 1.0
-        self.min_img_size = 0.0
-        self.max_img_size = 1e10
-        self.fill_value = 255
-        self.rotate = -1
-        self.rotate_list: List[int] = []
-        self.seed = 0
-        self.silent = 0
-
-    def set_param(self, name, val):
-        if name == "input_shape":
-            a = [int(x) for x in val.split(",")]
-            if len(a) != 3:
-                raise ValueError("input_shape must be three consecutive integers without space example: 1,1,200")
-            self.shape = tuple(a)
-        elif name == "seed_data":
-            self.seed = int(val)
-        elif name == "divideby":
-            self.scale = 1.0 / float(val)
-        elif name == "scale":
-            self.scale = float(val)
-        elif name == "mean_value":
-            a = [float(x) for x in val.split(",")]
-            if len(a) != 3:
-                raise ValueError("mean value must be three consecutive float without space example: 128,127.5,128.2")
-            self.mean_value = tuple(a)
-        elif name == "image_mean":
-            self.image_mean = val
-        elif name == "rotate_list":
-            self.rotate_list = [int(x) for x in val.split(",") if x]
-        elif name in ("rand_crop", "rand_mirror", "mirror", "crop_y_start", "crop_x_start", "max_rotate_angle",
-                      "min_crop_size", "max_crop_size", "fill_value", "rotate", "silent"):
-            setattr(self, name, int(float(val)))
-        elif name in ("max_random_contrast", "max_random_illumination", "max_shear_ratio", "max_aspect_ratio",
-                      "min_random_scale", "max_random_scale", "min_img_size", "max_img_size"):
-            setattr(self, name, float(val))
-
-    def need_affine(self) -> bool:
-        """ImageAugmenter::NeedProcess (image_augmenter-inl.hpp:156-161)."""
-        if self.max_rotate_angle > 0 or self.max_shear_ratio > 0 or self.rotate > 0 or self.rotate_list:
-            return True
-        return self.min_crop_size > 0 and self.max_crop_size > 0
-
-
-def _decode(payload) -> np.ndarray:
-    from PIL import Image
-    im = Image.open(_io.BytesIO(payload) if isinstance(payload, (bytes, bytearray)) else payload)
-    im = im.convert("RGB")
-    return np.asarray(im)
-
-
-def _affine(img: np.ndarray, p: AugmentParam, rng: np.random.Generator) -> np.ndarray:
-    """Random rotate/shear/scale/aspect warp, then crop to the input shape
-    (ImageAugmenter::Process, image_augmenter-inl.hpp:74-121)."""
-    from PIL import Image
-    H, W = img.shape[:2]
-    s = rng.random() * p.max_shear_ratio * 2 - p.max_shear_ratio
-    angle = int(rng.integers(p.max_rotate_angle * 2)) - p.max_rotate_angle if p.max_rotate_angle > 0 else 0
-    if p.rotate > 0:
-        angle = p.rotate
-    if p.rotate_list:
-        # the reference samples NextUInt32(size-1): the last entry is never drawn
-        angle = p.rotate_list[int(rng.integers(len(p.rotate_list) - 1)) if len(p.rotate_list) > 1 else 0]
-    a = math.cos(angle / 180.0 * math.pi)
-    b = math.sin(angle / 180.0 * math.pi)
-    scale = rng.random() * (p.max_random_scale - p.min_random_scale) + p.min_random_scale
-    ratio = rng.random() * p.max_aspect_ratio * 2 - p.max_aspect_ratio + 1
-    hs = 2 * scale / (1 + ratio)
-    ws = ratio * hs
-    new_w = int(max(p.min_img_size, min(p.max_img_size, scale * W)))
-    new_h = int(max(p.min_img_size, min(p.max_img_size, scale * H)))
-    m00, m01 = hs * a - s * b * ws, hs * b + s * a * ws
-    m10, m11 = -b * ws, a * ws
-    m02 = (new_w - (m00 * W + m01 * H)) / 2
-    m12 = (new_h - (m10 * W + m11 * H)) / 2
-    det = m00 * m11 - m01 * m10
-    i00, i01, i10, i11 = m11 / det, -m01 / det, -m10 / det, m00 / det
-    inv = (i00, i01, -(i00 * m02 + i01 * m12), i10, i11, -(i10 * m02 + i11 * m12))
-    fill = (p.fill_value,) * 3
-    out = Image.fromarray(img).transform((new_w, new_h), Image.AFFINE, inv, resample=Image.BICUBIC, fillcolor=fill)
-    res = np.asarray(out)
-    ch, cw = p.shape[1], p.shape[2]
-    y, x = res.shape[0] - ch, res.shape[1] - cw
-    if y < 0 or x < 0:
-        raise ValueError("augmented image is smaller than input_shape")
-    if p.rand_crop:
-        y, x = int(rng.integers(y + 1)), int(rng.integers(x + 1))
-    else:
-        y, x = y // 2, x // 2
-    return res[y:y + ch, x:x + cw]
-
-
-def _augment_one(payload, p: AugmentParam, seed: int, mean_mode: int):
-    """Decode + geometric augmentation of one instance.  Returns (pixels (h,w,C) uint8,
-    (crop_y, crop_x, mirrored), (contrast, illumination))."""
-    rng = np.random.default_rng(seed)
-    img = _decode(payload)
-    if p.need_affine():
-        img = _affine(img, p, rng)
-    ch, cw = p.shape[1], p.shape[2]
-    if ch == 1:  # flat input: no crop (reference: img_ = data * scale_)
-        return img, (0, 0, 0), (1.0, 0.0)
-    H, W = img.shape[:2]
-    if H < ch or W < cw:
-        raise ValueError("Data size must be bigger than the input size to net.")
-    yy, xx = H - ch, W - cw
-    if p.rand_crop and (yy or xx):
-        yy, xx = int(rng.integers(yy + 1)), int(rng.integers(xx + 1))
-    else:
-        yy, xx = yy // 2, xx // 2
-    if H != ch and p.crop_y_start != -1:
-        yy = p.crop_y_start
-    if W != cw and p.crop_x_start != -1:
-        xx = p.crop_x_start
-    contrast = rng.random() * p.max_random_contrast * 2 - p.max_random_contrast + 1
-    illum = rng.random() * p.max_random_illumination * 2 - p.max_random_illumination
-    if mean_mode == 0:
-        mirror = bool(p.rand_mirror and rng.random() < 0.5)   # `mirror=1` is ignored here (reference)
-        contrast, illum = 1.0, 0.0
-    else:
-        mirror = bool((p.rand_mirror and rng.random() < 0.5) or p.mirror == 1)
-    crop = img[yy:yy + ch, xx:xx + cw]
-    if mirror:
-        crop = crop[:, ::-1]
-    return crop, (yy, xx, int(mirror)), (contrast, illum)
-
-
 # ----------------------------------------------------------------------------- batch iterator
 def _dist_rows(batch_size: int) -> Tuple[int, int]:
     """Rows of the global batch this rank trains on (same rule as NetTrainer._slice)."""
@@ -396,8 +247,14 @@ def _dist_rows(batch_size: int) -> Tuple[int, int]:
 class ImageBatchIterator(DataIterator):
     """BatchAdaptIterator(AugmentIterator(<source>)) with a parallel decode stage.
 
-    Extra keys (new): decode_thread (default min(8, cpus)), shard_decode (default 1:
-    under torch.distributed each rank decodes only its own rows of the batch)."""
+    Extra keys (new): decode_process (default min(16, host cores) when there are at
+    least 4, else 0: decode in that many worker processes, io/augment.py, writing into
+    a shared-memory batch; 0 = use threads), decode_thread (threads when decode_process
+    is 0; default min(8, cpus)), shard_decode (default 1: under torch.distributed each
+    rank decodes only its own rows of the batch).  Results do not depend on either
+    setting: every record's augmentation RNG is seeded from the iterator's stream."""
+
+    fresh_batches = True  # every next() returns newly allocated tensors
 
     def __init__(self, source: _Source):
         self.source = source
@@ -408,6 +265,10 @@ class ImageBatchIterator(DataIterator):
         self.test_skipread = 0
         self.silent = 0
         self.decode_thread = min(8, os.cpu_count() or 1)
+        self.decode_process = -1
+        self._shm = None
+        self._shm_fin = None
+        self._procs = None
         self.shard_decode = 1
         self._pool: Optional[ThreadPoolExecutor] = None
         self.mean: Optional[torch.Tensor] = None
@@ -433,6 +294,8 @@ class ImageBatchIterator(DataIterator):
             self.silent = int(val)
         elif name == "decode_thread":
             self.decode_thread = max(1, int(val))
+        elif name == "decode_process":
+            self.decode_process = int(val)
         elif name == "shard_decode":
             self.shard_decode = int(val)
 
@@ -441,6 +304,10 @@ class ImageBatchIterator(DataIterator):
         self.source.init()
         self._seed_rng = np.random.default_rng(self.aug.seed)
         self._pool = ThreadPoolExecutor(self.decode_thread, thread_name_prefix="cxxnet-decode")
+        if self.decode_process < 0:
+            self.decode_process = default_decode_process()
+        if not shm_available():
+            self.decode_process = 0
         C, h, w = self.aug.shape
         if self.aug.mean_value is not None and any(v > 0 for v in self.aug.mean_value):
             # the reference subtracts mean_value[i] from channel i (iter_augment_proc-inl.hpp:64-67,128)
@@ -550,27 +417,73 @@ class ImageBatchIterator(DataIterator):
         lo, hi = (_dist_rows(B) if self.shard_decode else (0, B))
         rows = [(i, r) for i, r in enumerate(recs) if lo <= i < hi]
         # seeds are drawn for every record so results do not depend on the sharding
-        seeds = [int(s) for s in self._seed_rng.integers(0, 2 ** 63 - 1, size=len(recs))]
+        seeds = self._seed_rng.integers(0, 2 ** 63 - 1, size=len(recs)).tolist()
+        prm = np.zeros((B, 4), dtype=np.int32)
+        cm = np.zeros((B, 2), dtype=np.float32)
+        cm[:, 0] = 1.0
+        if self.decode_process > 0 and h > 1:
+            pix = self._decode_procs(rows, seeds, (B, h, w, C), prm, cm)
+        else:
+            pix = self._decode_threads(rows, seeds, (B, h, w, C), prm, cm)
+        prm, cm = torch.from_numpy(prm), torch.from_numpy(cm)
+        data = U8Images(pix, prm, cm, self.mean, self.mean_mode, self.aug.scale)
+        return DataBatch(data, label, index, padd)
+
+    @staticmethod
+    def _host_buffer(shape) -> torch.Tensor:
+        """Destination of one batch: page-locked when a GPU will consume it, so the
+        host-to-device copy is a straight DMA."""
+        return torch.empty(shape, dtype=torch.uint8, pin_memory=torch.cuda.is_available())
+
+    def _decode_threads(self, rows, seeds, shape, prm, cm) -> torch.Tensor:
+        B, h, w, C = shape
         outs = list(self._pool.map(lambda a: _augment_one(a[1].payload, self.aug, seeds[a[0]], self.mean_mode),
                                    rows))
         if h == 1:  # flat input: keep the decoded size
-            hh, ww = outs[0][0].shape[:2] if outs else (1, 1)
-        else:
-            hh, ww = h, w
-        pix = torch.zeros((B, hh, ww, C), dtype=torch.uint8)
-        prm = torch.zeros((B, 4), dtype=torch.int32)
-        cm = torch.zeros((B, 2), dtype=torch.float32)
-        cm[:, 0] = 1.0
+            h, w = outs[0][0].shape[:2] if outs else (1, 1)
+        dst = self._host_buffer((B, h, w, C))
+        pix = dst.numpy()
+        done = np.zeros(B, dtype=bool)
         for (i, _), (img, p, c) in zip(rows, outs):
-            if img.shape[2] != C:
-                img = img[..., :C]
-            pix[i] = torch.from_numpy(np.ascontiguousarray(img))
-            prm[i, :3] = torch.tensor(p, dtype=torch.int32)
-            cm[i] = torch.tensor(c, dtype=torch.float32)
-        if torch.cuda.is_available():
-            pix = pix.pin_memory()
-        data = U8Images(pix, prm, cm, self.mean, self.mean_mode, self.aug.scale)
-        return DataBatch(data, label, index, padd)
+            pix[i] = img[..., :C]
+            prm[i, :3] = p
+            cm[i] = c
+            done[i] = True
+        pix[~done] = 0  # padding rows / other ranks' rows
+        return dst
+
+    def _decode_procs(self, rows, seeds, shape, prm, cm) -> torch.Tensor:
+        nbytes = int(np.prod(shape))
+        if self._shm is None or self._shm.size < nbytes:
+            self._free_shm()
+            import weakref
+            self._shm = ShmBuffer(nbytes)
+            self._shm_fin = weakref.finalize(self, self._shm.close)
+            self._shm_fin.atexit = False  # io.augment's exit hook runs it after the prefetch threads stop
+        if self._procs is None:
+            import weakref
+            self._procs = DecodePool(self.decode_process)
+            weakref.finalize(self, self._procs.close).atexit = False
+        items = [(i, r.payload if isinstance(r.payload, (str, bytes)) else bytes(r.payload), seeds[i])
+                 for i, r in rows]
+        dst = self._host_buffer(shape)
+        pix = dst.numpy()
+        src = self._shm.array(shape)
+        done = np.zeros(shape[0], dtype=bool)
+        for lo, hi, res in self._procs.imap(self._shm, shape, self.aug, self.mean_mode, items):
+            for i, p, c in res:
+                prm[i, :3] = p
+                cm[i] = c
+            r0, r1 = items[lo][0], items[hi - 1][0] + 1  # rows of a chunk are consecutive
+            np.copyto(pix[r0:r1], src[r0:r1])
+            done[r0:r1] = True
+        pix[~done] = 0  # padding rows / other ranks' rows
+        return dst
+
+    def _free_shm(self):
+        if self._shm_fin is not None:
+            self._shm_fin()
+        self._shm = self._shm_fin = None
 
     def value(self):
         if self._head:
@@ -581,6 +494,11 @@ class ImageBatchIterator(DataIterator):
         if self._pool is not None:
             self._pool.shutdown(wait=False)
             self._pool = None
+        if self._procs is not None:
+            self._procs.close()
+            self._procs = None
+        self._free_shm()
+
 
 
 def save_mean_image(path: str, mean: torch.Tensor):

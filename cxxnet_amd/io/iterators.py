@@ -10,12 +10,14 @@ from __future__ import annotations
 
 import queue
 import threading
+import weakref
 from typing import List, Optional, Tuple
 
 import numpy as np
 import torch
 
 from .. import native
+from .augment import on_exit
 from .data import DataBatch, DataIterator
 
 
@@ -173,6 +175,18 @@ class SyntheticIterator(DataIterator):
         return self.batch
 
 
+_LIVE_BUFFERS: "weakref.WeakSet" = weakref.WeakSet()
+
+
+@on_exit
+def _stop_live_buffers():
+    """Join prefetch threads before the interpreter finalizes: a daemon thread that is
+    inside a native call (the page reader) when Python tears down is killed while
+    unwinding through C++ frames, which aborts the process."""
+    for it in list(_LIVE_BUFFERS):
+        it._stop()
+
+
 class ThreadBufferIterator(DataIterator):
     """`iter = threadbuffer` -- background prefetch of whole batches (reference
     ThreadBufferIterator, iter_batch_proc-inl.hpp:136-224; buffer_size default 2)."""
@@ -192,14 +206,22 @@ class ThreadBufferIterator(DataIterator):
 
     def _run(self, q: "queue.Queue", stop: threading.Event):
         self.base.before_first()
+        # a base that allocates every batch afresh (the image iterators, whose pixels
+        # sit in page-locked memory) is handed over as is; others reuse their buffers
+        fresh = getattr(self.base, "fresh_batches", False)
         while not stop.is_set():
-            if not self.base.next():
-                q.put(None)
+            b = self.base.value() if self.base.next() else None
+            if b is not None and not fresh:
+                b = DataBatch(b.data.clone(), b.label.clone(), None if b.inst_index is None else b.inst_index.copy(),
+                              b.num_batch_padd, [e.clone() for e in b.extra_data])
+            while not stop.is_set():
+                try:
+                    q.put(b, timeout=0.1)
+                    break
+                except queue.Full:
+                    continue
+            if b is None:
                 return
-            b = self.base.value()
-            b = DataBatch(b.data.clone(), b.label.clone(), None if b.inst_index is None else b.inst_index.copy(),
-                          b.num_batch_padd, [e.clone() for e in b.extra_data])
-            q.put(b)
 
     def _stop(self):
         if self.thread is not None:
@@ -214,6 +236,7 @@ class ThreadBufferIterator(DataIterator):
 
     def before_first(self):
         self._stop()
+        _LIVE_BUFFERS.add(self)
         self.q = queue.Queue(maxsize=self.buffer_size)
         self.stop = threading.Event()
         self.thread = threading.Thread(target=self._run, args=(self.q, self.stop), daemon=True)
@@ -235,6 +258,7 @@ class ThreadBufferIterator(DataIterator):
 
     def close(self):
         self._stop()
+        self.base.close()
 
 
 class DenseBufferIterator(DataIterator):

@@ -124,6 +124,29 @@ def test_rand_crop_mirror_deterministic(imgset):
         assert torch.equal(x[0], y[0])
 
 
+@pytest.mark.parametrize("kind", ["imgbin", "imgbinx", "img"])
+def test_process_and_thread_decode_agree(imgset, kind):
+    """decode_process (forkserver workers writing into shared memory) and the thread
+    pool produce the same batches, random crop / mirror / contrast included, and the
+    threadbuffer hands the batches over intact."""
+    d, _ = imgset
+    runs = {}
+    for mode in ("thread", "process"):
+        kw = dict(rand_crop=1, rand_mirror=1, seed_data=5, max_random_contrast=0.2, mean_value="1,2,3",
+                  decode_process=(0 if mode == "thread" else 2), round_batch=1)
+        cfg = _cfg(kind, d, **kw)
+        cfg.insert(-1, ("iter", "threadbuffer"))
+        it = create_iterator(cfg)
+        it.init()
+        runs[mode] = _collect(it)
+        raw = it.value().data
+        assert raw.pix.dtype == torch.uint8 and raw.pix.shape == (4, 32, 32, 3)
+        it.close()
+    assert len(runs["thread"]) == len(runs["process"]) == 3
+    for x, y in zip(runs["thread"], runs["process"]):
+        assert torch.equal(x[0], y[0]) and torch.equal(x[1], y[1]) and (x[2] == y[2]).all()
+
+
 def test_mean_image_created_and_used(imgset, tmp_path):
     d, arrays = imgset
     mpath = tmp_path / "mean.bin"
