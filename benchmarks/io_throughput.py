@@ -50,7 +50,19 @@ def make_dataset(root, n, size, seed=0):
     return nbytes / n
 
 
-def run(root, it_type, mode, workers, batches, batch):
+def make_trainer(model, batch):
+    from cxxnet_amd.models import load_conf
+    from cxxnet_amd.nnet import NetTrainer
+    pairs = load_conf(model, [("batch_size", str(batch)), ("eval_train", "0"), ("dev", "gpu"), ("silent", "1")])
+    tr = NetTrainer()
+    for k, v in pairs:
+        if not k.startswith("metric"):
+            tr.set_param(k, v)
+    tr.init_model()
+    return tr
+
+
+def run(root, it_type, mode, workers, batches, batch, tr=None):
     threads, procs = (workers, 0) if mode == "thread" else (1, workers)
     from cxxnet_amd.io.iterators import create_iterator
     cfg = [("iter", it_type), ("image_list", os.path.join(root, "train.lst")),
@@ -73,7 +85,12 @@ def run(root, it_type, mode, workers, batches, batch):
             it.before_first()
             continue
         b = it.value()
+        if tr is not None:
+            tr.update(b)
         n += 1
+    if tr is not None:
+        import torch
+        torch.cuda.synchronize()
     el = time.perf_counter() - t0
     it.close()
     return batches * batch / el
@@ -89,18 +106,25 @@ def main():
     ap.add_argument("--batches", type=int, default=12)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--dir", default="")
+    ap.add_argument("--train", default="", help="also train this model (GPU) on the decoded batches")
     a = ap.parse_args()
     root = a.dir or tempfile.mkdtemp(prefix="cxxnet_io_")
-    avg = make_dataset(root, a.n, a.size)
     from cxxnet_amd.tools.im2bin import pack
-    pack(os.path.join(root, "train.lst"), root + "/", os.path.join(root, "train.bin"))
+    if os.path.exists(os.path.join(root, "train.bin")):  # reuse a dataset made by an earlier run
+        imgs = os.listdir(os.path.join(root, "img"))
+        avg = sum(os.path.getsize(os.path.join(root, "img", f)) for f in imgs) / max(len(imgs), 1)
+    else:
+        avg = make_dataset(root, a.n, a.size)
+        pack(os.path.join(root, "train.lst"), root + "/", os.path.join(root, "train.bin"))
     cores = os.cpu_count()
+    tr = make_trainer(a.train, a.batch) if a.train else None
     for it_type in a.iters.split(","):
         for mode in a.modes.split(","):
             for t in [int(v) for v in a.workers.split(",")]:
-                ips = run(root, it_type, mode, t, a.batches, a.batch)
+                ips = run(root, it_type, mode, t, a.batches, a.batch, tr)
                 per_core = ips / min(t, cores)
                 print(json.dumps({"iter": it_type, "mode": mode, "workers": t, "host_cpus": cores,
+                                  "train": a.train or None,
                                   "img_per_s": round(ips, 1),
                                   "img_per_s_per_busy_core": round(per_core, 1), "jpeg_side": a.size,
                                   "avg_jpeg_bytes": int(avg),

@@ -9,6 +9,7 @@ Set/GetWeight, CopyModelFrom (finetune copy-by-name), and the model file:
 """
 from __future__ import annotations
 
+import functools
 import os
 import struct
 from typing import List, Optional, Tuple
@@ -62,10 +63,13 @@ class NetTrainer:
         # (1 GPU: the memory-bound update just competes with the memory-bound
         # pool/LRN backward, measured -1.7%)
         self.overlap_update = int(os.environ.get("CXXNET_OVERLAP_UPDATE", "-1"))
-        # HIP-graph replay of the forward and backward passes (1 GPU, update_period 1):
-        # every layer kernel of a step is launched by two graph replays instead of one
-        # host call each; the optimizer stays an eager launch so lr schedules still apply
-        self.cuda_graph = int(os.environ.get("CXXNET_CUDA_GRAPH", "0"))
+        # HIP-graph replay of the forward and backward passes (update_period 1): every
+        # layer kernel of a step is launched by graph replays instead of one host call
+        # each; the optimizer and (data parallel) the collectives stay eager launches, so
+        # lr schedules still apply.  1 = on, 0 = off.
+        # -1 (auto): on under data parallelism at per-GPU batch <= 64, where the Python
+        # launch cost of ~150 kernels would otherwise approach the GPU step time
+        self.cuda_graph = int(os.environ.get("CXXNET_CUDA_GRAPH", "-1"))
         self._graphs = {}
         self._graph_warm = {}
         # failure detection: every N updates, fail fast if any gradient was non-finite
@@ -456,19 +460,89 @@ class NetTrainer:
         self.net.ctx.step_counter.copy_(state["step_counter"])
 
     def _graph_eligible(self) -> bool:
-        net = self.net
-        return (self.cuda_graph > 0 and net.device.type == "cuda" and self.world == 1 and self.update_period == 1
-                and self.reducer is not None and self.reducer.update_fn is None and not self.reducer.shard)
+        net, red = self.net, self.reducer
+        if not (self.cuda_graph != 0 and net.device.type == "cuda" and self.update_period == 1 and red is not None):
+            return False
+        if self.cuda_graph < 0:
+            return red.handles_update and self._local_batch() <= 64
+        if red.handles_update:  # data parallel: segmented graphs around the collectives
+            return True
+        return self.world == 1 and not red.shard
+
+    def _capture_plans(self):
+        """Record the forward and backward passes as lists of HIP graphs with eager calls
+        between them.  Without a reducer hook this is one graph per pass.  Under data
+        parallelism (overlapped per-bucket update) the forward is cut before each layer
+        that must wait for a bucket (the wait is an eager stream-event wait) and the
+        backward is cut after each layer that completes a bucket (the eager call launches
+        its RCCL collective and side-stream update), so collectives and waits stay
+        outside the graphs and replays keep the eager schedule."""
+        net, red = self.net, self.reducer
+        dp = red.handles_update
+        red.sync()
+        torch.cuda.synchronize()
+        pool = torch.cuda.graph_pool_handle()
+        cur = {}
+
+        def begin(plan):
+            g = torch.cuda.CUDAGraph()
+            g.capture_begin(pool=pool)
+            cur["g"], cur["plan"] = g, plan
+
+        def end():
+            cur["g"].capture_end()
+            cur["plan"].append(cur["g"])
+
+        def cut(fn):
+            plan = cur["plan"]
+            end()
+            plan.append(fn)
+            begin(plan)
+
+        waited, ready = set(), set()
+
+        def fwd_hook(li):
+            new = [bi for bi in red.layer_buckets.get(li, ()) if bi not in waited]
+            if new:
+                waited.update(new)
+                cut(functools.partial(red.before_forward, li))
+
+        def bwd_hook(li):
+            bs = [bi for bi, b in enumerate(red.buckets) if bi not in ready and li <= b.li_min]
+            if bs:
+                ready.update(bs)
+                cut(functools.partial(red.ready_buckets, bs))
+
+        fwd, bwd = [], []
+        with torch.cuda.stream(torch.cuda.Stream()):
+            begin(fwd)
+            net.forward(True, pre_hook=fwd_hook if dp else None)
+            end()
+            begin(bwd)
+            net.backprop(False, hook=bwd_hook if dp else None, first=True)
+            end()
+        torch.cuda.synchronize()
+        return fwd, bwd
+
+    @staticmethod
+    def _replay(plan):
+        for item in plan:
+            if isinstance(item, torch.cuda.CUDAGraph):
+                item.replay()
+            else:
+                item()
 
     def _graph_step(self, ev=None) -> bool:
-        """One training step as two HIP-graph replays (forward, backward) plus the eager
-        fused optimizer.  The first step of each batch size runs eagerly (it autotunes the
-        GEMM tiles and allocates the layers' persistent buffers); the second captures.
-        Inputs and labels live in static node / label buffers, so a replay reads the batch
-        that _set_batch just staged.  Returns False to take the eager path."""
+        """One training step as HIP-graph replays of the forward and backward passes plus
+        the eager optimizer (1 GPU) or, under data parallelism, graph segments around the
+        eager bucket collectives and the side-stream per-bucket update.  The first step of
+        each batch size runs eagerly (it autotunes the GEMM tiles and allocates the layers'
+        persistent buffers); the second captures.  Inputs and labels live in static node /
+        label buffers, so a replay reads the batch that _set_batch just staged.  Returns
+        False to take the eager path."""
         if not self._graph_eligible():
             return False
-        net = self.net
+        net, red = self.net, self.reducer
         key = net.cur_batch
         gr = self._graphs.get(key)
         if gr is None:
@@ -476,27 +550,29 @@ class NetTrainer:
                 self._graph_warm[key] = 1
                 return False
             try:
-                torch.cuda.synchronize()
-                gf, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gf):
-                    net.forward(True)
-                with torch.cuda.graph(gb, pool=gf.pool()):
-                    net.backprop(False, first=True)
+                gr = self._capture_plans()
             except Exception as e:  # a layer that syncs with the host (e.g. pairtest): stay eager
                 if not self.silent:
                     print(f"cuda_graph: capture failed ({type(e).__name__}: {e}); running eagerly")
                 self.cuda_graph = 0
                 torch.cuda.synchronize()
                 return False
-            gr = self._graphs[key] = (gf, gb)
-        gf, gb = gr
-        gf.replay()
+            self._graphs[key] = gr
+        fwd, bwd = gr
+        self._replay(fwd)
         self._mark(ev, 1)
         evals = self._train_eval(self._cur_batch)
-        gb.replay()
-        self._check_grads()
-        self._mark(ev, 2)
-        net.update(self.epoch_counter)
+        if red.handles_update:
+            red.start_step()
+            self._replay(bwd)
+            red.finish()
+            self._check_grads()
+            self._mark(ev, 2)
+        else:
+            self._replay(bwd)
+            self._check_grads()
+            self._mark(ev, 2)
+            net.update(self.epoch_counter)
         if evals is not None:
             self.train_metric.add_eval(evals, self._label_fields(self._cur_batch))
         self.epoch_counter += 1

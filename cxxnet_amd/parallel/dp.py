@@ -274,6 +274,13 @@ class GradReducer:
             b.done.record(self.side)
             b.pending = True
 
+    def ready_buckets(self, indices):
+        """Launch buckets `indices` (their gradients are final on the compute stream)."""
+        for bi in indices:
+            b = self.buckets[bi]
+            if not b.ready:
+                self._ready(b)
+
     def hook(self, layer_index: int):
         """Called after each layer's backprop (reverse order)."""
         if not self.overlap or not (self.active or self.update_fn is not None):

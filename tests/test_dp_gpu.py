@@ -28,7 +28,8 @@ def _make(batch, extra=()):
     from cxxnet_amd.nnet import NetTrainer
     tr = NetTrainer()
     for k, v in list(native.rt().parse_config(CONF)) + [("batch_size", str(batch)), ("dev", "gpu"),
-                                                        ("eval_train", "0"), ("silent", "1"), ("seed", "5")] + \
+                                                        ("eval_train", "0"), ("silent", "1"), ("seed", "5"),
+                                                        ("cuda_graph", "0")] + \
             list(extra):
         tr.set_param(k, v)
     tr.init_model()
@@ -54,13 +55,17 @@ def _worker(rank, world, port, steps, out, extra, backend="gloo"):
         tr.update(DataBatch(x.cuda(), y.cuda()))
     torch.cuda.synchronize()
     assert tr.reducer.check_consistency() == 0.0
+    if any(k == "cuda_graph" and v == "1" for k, v in extra):
+        assert tr._graphs, "the data-parallel step did not run as graph segments"
+        fwd, bwd = next(iter(tr._graphs.values()))
+        assert sum(callable(i) and not isinstance(i, torch.cuda.CUDAGraph) for i in fwd + bwd) > 0
     tr.reducer.sync_master()  # sharded: each rank updated only its slice of the fp32 masters
     torch.save(tr.net.arena.w.cpu(), out + f".r{rank}")
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("extra", [(), (("dp_comm_dtype", "bf16"),), (("update_period", "2"),),
-                                   (("dp_mode", "allreduce"),)])
+                                   (("dp_mode", "allreduce"),), (("cuda_graph", "1"),)])
 def test_dp_two_ranks_gpu_equals_single(tmp_path, extra):
     steps = 4
     out = str(tmp_path / "w")
@@ -81,16 +86,19 @@ def test_dp_two_ranks_gpu_equals_single(tmp_path, extra):
     assert err < 5e-2, err
 
 
+@pytest.mark.parametrize("graph", [0, 1])
 @pytest.mark.parametrize("mode", ["shard", "allreduce"])
-def test_rccl_single_rank_forced_is_exact(tmp_path, mode):
+def test_rccl_single_rank_forced_is_exact(tmp_path, mode, graph):
     """The RCCL ("nccl") backend at world 1 with dp_force: reduce-scatter / all-reduce,
     the side-stream waits on the async work handles, the sliced overlapped update, the
     bf16 all-gather and the per-bucket forward gating all execute on the MI355X.  With
     one rank every collective is an identity and the fused update is elementwise, so the
-    weights must equal the plain single-GPU run bit for bit."""
-    steps = 3
+    weights must equal the plain single-GPU run bit for bit.  graph=1 replays the
+    forward / backward as HIP-graph segments cut around the bucket collectives and waits
+    (step 1 eager, step 2 captures, steps 3-5 replay)."""
+    steps = 5
     out = str(tmp_path / "w")
-    extra = [("dp_mode", mode), ("dp_bucket_mb", "0.002")]
+    extra = [("dp_mode", mode), ("dp_bucket_mb", "0.002"), ("cuda_graph", str(graph))]
     mp.spawn(_worker, args=(1, _free_port(), steps, out, extra, "nccl"), nprocs=1, join=True)
     r0 = torch.load(out + ".r0", weights_only=True)
     from cxxnet_amd.io.data import DataBatch
