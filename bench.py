@@ -53,10 +53,11 @@ def _args(argv=None):
     ap.add_argument("--input", default="u8", choices=["u8", "f32"],
                     help="u8: decoded-image batches (uint8 HWC) normalised on the GPU by the fused augment kernel, "
                          "as the imgbin pipeline delivers them; f32: float NCHW batches")
-    ap.add_argument("--graph", type=int, default=0,
-                    help="replay forward/backward as HIP graphs (1 GPU; the optimizer stays eager). Off by default: "
-                         "the AlexNet and GoogLeNet steps are GPU-bound, graph replay measured -0.4%%/+0.5%% "
-                         "(profiles/r16_graph_ab.jsonl)")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="replay forward/backward as HIP graphs (the optimizer and collectives stay eager). "
+                         "-1 (default) = the trainer's auto rule: on under data parallelism at per-GPU batch <= 64 "
+                         "(strong scaling); the 1-GPU AlexNet / GoogLeNet steps are GPU-bound, graph replay measured "
+                         "-0.4%%/+0.5%% (profiles/r16_graph_ab.jsonl)")
     ap.add_argument("--dp-mode", default="auto", choices=["auto", "shard", "allreduce"],
                     help="gradient reduction: auto = sharded reduce-scatter/all-gather on the GPU")
     ap.add_argument("--bucket-mb", type=float, default=64.0)

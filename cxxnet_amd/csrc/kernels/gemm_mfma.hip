@@ -57,10 +57,6 @@ struct Epilogue {
   int relu;
   int mask_relu;      // bf16 out: keep a value only where the OLD output value is > 0
   long kstride;       // EPI_F32 with split-K: K-slice s writes its own slab at out + s*kstride
-  // conv weight-grad (B = dy, MN-major): bgrad[j] += sum over this block's k of B(j, k), i.e.
-  // the bias gradient sum_{n,h,w} dy, folded into the GEMM that already streams dy (K5+K6)
-  float *bgrad = nullptr;
-  long bgrad_gstride = 0;
 };
 
 template <int MODE>
@@ -267,18 +263,6 @@ __device__ __forceinline__ void store_tile(bf16_t *lds, const Stage<R, VEC> &st)
   }
 }
 
-// Column sums of a staged MN-major tile (bias gradient fold): every vector a thread stages
-// covers the same VEC rows (columns of the GEMM), so the sums stay in VEC registers.
-template <int R, int VEC>
-__device__ __forceinline__ void accum_cols(const Stage<R, VEC> &st, float *acc) {
-#pragma unroll
-  for (int s = 0; s < Stage<R, VEC>::NV; ++s) {
-    const bf16_t *e = reinterpret_cast<const bf16_t *>(&st.v[s]);
-#pragma unroll
-    for (int q = 0; q < VEC; ++q) acc[q] += bf2f(e[q]);
-  }
-}
-
 // Fragment for v_mfma_f32_16x16x32_bf16: lane l holds rows (l&15), k = 8*(l>>4) + e.
 template <int MODE, int R>
 __device__ __forceinline__ bf16x8 load_frag(const bf16_t *lds, int row, int kk) {
@@ -370,18 +354,6 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
 #pragma unroll
     for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // bias-gradient fold (weight-grad only): the i-tile-0 blocks sum the dy columns they stage
-  constexpr bool kBiasFold = (BMODE == DIRECT_MN && EPI == EPI_F32_ATOMIC);
-  const bool fold = kBiasFold && E.bgrad != nullptr && ti == 0;
-  float bacc[VB];
-#pragma unroll
-  for (int q = 0; q < VB; ++q) bacc[q] = 0.f;
-  auto fold_b = [&](const Stage<BN, VB> &st) {
-    if constexpr (kBiasFold) {
-      if (fold) accum_cols<BN, VB>(st, bacc);
-    }
-  };
-
   const bf16_t *const as0 = As0, *const bs0 = Bs0;
   auto compute = [&](int cur) {
     const bf16_t *as = as0 + cur * A_ELEMS;
@@ -412,7 +384,6 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
     load_tile<BMODE, BN, VB>(B, rB, gB, goB, j0, kt_beg * BK, sb, rowB);
     store_tile<AMODE, BM, VA>(As0, sa);
     store_tile<BMODE, BN, VB>(Bs0, sb);
-    fold_b(sb);
     __syncthreads();
     int cur = 0;
     for (int kt = kt_beg; kt < kt_end; ++kt) {
@@ -425,7 +396,6 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
       if (more) {
         store_tile<AMODE, BM, VA>(As0 + (cur ^ 1) * A_ELEMS, sa);
         store_tile<BMODE, BN, VB>(Bs0 + (cur ^ 1) * B_ELEMS, sb);
-        fold_b(sb);
       }
       __syncthreads();
       cur ^= 1;
@@ -442,7 +412,6 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
     load_tile<BMODE, BN, VB>(B, rB, gB, goB, j0, koff(kt_beg + 1), sb1, rowB);
     store_tile<AMODE, BM, VA>(As0, sa0);
     store_tile<BMODE, BN, VB>(Bs0, sb0);
-    fold_b(sb0);
     __syncthreads();
     for (int kt = kt_beg; kt < kt_end; kt += 2) {
       load_tile<AMODE, BM, VA>(A, rA, gA, goA, i0, koff(kt + 2), sa0, rowA);
@@ -451,7 +420,6 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
       if (kt + 1 < kt_end) {
         store_tile<AMODE, BM, VA>(As0 + A_ELEMS, sa1);
         store_tile<BMODE, BN, VB>(Bs0 + B_ELEMS, sb1);
-        fold_b(sb1);
       }
       __syncthreads();
       if (kt + 1 >= kt_end) break;
@@ -461,26 +429,6 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
       if (kt + 2 < kt_end) {
         store_tile<AMODE, BM, VA>(As0, sa0);
         store_tile<BMODE, BN, VB>(Bs0, sb0);
-        fold_b(sb0);
-      }
-      __syncthreads();
-    }
-  }
-
-  if constexpr (kBiasFold) {
-    if (fold) {  // block-uniform: reduce the per-thread column sums through LDS, one atomic per column
-      constexpr int VPK = BN / VB, GRP = NT / VPK;
-      static_assert(GRP * BN * 4 <= SMEM, "bias fold scratch");
-      float *red = reinterpret_cast<float *>(smem);
-      const int colg = threadIdx.x % VPK, grp = threadIdx.x / VPK;
-#pragma unroll
-      for (int q = 0; q < VB; ++q) red[grp * BN + colg * VB + q] = bacc[q];
-      __syncthreads();
-      if (threadIdx.x < BN) {
-        float t = 0.f;
-        for (int gq = 0; gq < GRP; ++gq) t += red[gq * BN + threadIdx.x];
-        const int j = j0 + static_cast<int>(threadIdx.x);
-        if (j < B.rows) atomicAdd(E.bgrad + g * E.bgrad_gstride + j, t);
       }
       __syncthreads();
     }
@@ -700,25 +648,6 @@ CXN_API int cxn_gemm(const CxnOperand *a, const CxnOperand *b, int amode, int bm
   if (A.kdim != B.kdim) return -2;
   if (A.rows <= 0 || B.rows <= 0 || A.kdim <= 0) return 0;
   Epilogue E{out, out_gstride, ldc, alpha, bias, bias_gstride, relu, mask_relu, kstride};
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  int rc = dispatch(g, A, B, E, s);
-  if (rc != 0) return rc;
-  return hipGetLastError() == hipSuccess ? 0 : -3;
-}
-
-// Conv weight-grad with the bias gradient folded in: dw (+)= A . B^T (fp32 atomics, split-K)
-// and bgrad[g*bgrad_gstride + j] += sum_k B(j, k).  Same operands as cxn_gemm's GATHER_MN x
-// DIRECT_MN weight-grad case.
-CXN_API int cxn_gemm_wgrad_bias(const CxnOperand *a, const CxnOperand *b, int va, void *out, long out_gstride,
-                                int ldc, float *bgrad, long bgrad_gstride, int tile, int groups, int ksplit,
-                                void *stream) {
-  GemmArgs g{GATHER_MN, DIRECT_MN, va, 8, EPI_F32_ATOMIC, tile, groups < 1 ? 1 : groups, ksplit < 1 ? 1 : ksplit};
-  Operand A = to_operand(*a, GATHER_MN, va), B = to_operand(*b, DIRECT_MN, 8);
-  if (A.kdim != B.kdim) return -2;
-  if (A.rows <= 0 || B.rows <= 0 || A.kdim <= 0) return 0;
-  Epilogue E{out, out_gstride, ldc, 1.f, nullptr, 0, 0, 0, 0};
-  E.bgrad = bgrad;
-  E.bgrad_gstride = bgrad_gstride;
   hipStream_t s = static_cast<hipStream_t>(stream);
   int rc = dispatch(g, A, B, E, s);
   if (rc != 0) return rc;

@@ -7,7 +7,6 @@ the same node holds the activation in forward and its gradient in backward).
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -21,7 +20,6 @@ def _check(cond, msg):
         raise ValueError(msg)
 
 
-_WGRAD_BIAS_FOLD = os.environ.get("CXXNET_WGRAD_BIAS_FOLD", "0") == "1"
 
 
 def _bias_init(val):
@@ -231,13 +229,8 @@ class ConvolutionLayer(Layer):
     def backprop(self, prop_grad, nodes_in, nodes_out):
         x, dy = nodes_in[0].data, nodes_out[0].data
         self.geo.N = x.shape[0]
-        # CXXNET_WGRAD_BIAS_FOLD=1: the bias gradient rides along in the register-staged weight-grad
-        # GEMM (it streams dy anyway).  Off by default: on GoogLeNet b128 the folded kernels ran
-        # +331 us/step against the 303 us/step of separate colsum passes they replace
-        # (profiles/r2_inception_bias_fold.md)
-        fold = _WGRAD_BIAS_FOLD and self.b is not None
-        folded = ops.conv_backward_weight(x, dy, self.w.g, self.geo, db=self.b.g if fold else None)
-        if self.b is not None and not folded:
+        ops.conv_backward_weight(x, dy, self.w.g, self.geo)
+        if self.b is not None:
             ops.bias_grad(dy.view(-1, dy.shape[-1]), self.b.g)
         if prop_grad:
             if self._wt is None or self._wt.shape != self.w.wb.shape:

@@ -80,8 +80,6 @@ _SIGS = {
     "cxn_ins_pool_bwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _U, _P, _P],
     "cxn_splitk_finalize": [_P, _I, _L, _P, _L, _I, _P, _I, _I, _P],
     "cxn_splitk_accumulate": [_P, _I, _L, _P, _P],
-    "cxn_gemm_wgrad_bias": [ctypes.POINTER(CxnOperand), ctypes.POINTER(CxnOperand), _I, _P, _L, _I, _P, _L, _I, _I,
-                            _I, _P],
     "cxn_set_deterministic": [_I],
     "cxn_pool_bwd_tie_all": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "cxn_metric_eval": [_P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],

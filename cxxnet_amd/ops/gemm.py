@@ -509,18 +509,18 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False):
     reg(dx)
 
 
-def conv_backward_weight(x, dy, dw, g: ConvGeom, db=None) -> bool:
+def conv_backward_weight(x, dy, dw, g: ConvGeom):
     """dw += sum over pixels of dy (x) im2col(x).  dw fp32 [Cout][KH][KW][Cg].
-    db (fp32 [Cout], optional): when the register-staged kernel runs, the bias gradient
-    sum_{n,h,w} dy is accumulated into it by the same GEMM (it already streams dy) and True
-    is returned; False means the caller still owes db (ops.bias_grad)."""
+    (Folding the bias gradient into this GEMM was measured a wash on GoogLeNet and its
+    extra registers slowed every weight-grad kernel by 5-25%: profiles/r2_inception_bias_fold.md,
+    profiles/r2_ab_bias_fold_regression.md.)"""
     if not x.is_cuda:
         xn = x.permute(0, 3, 1, 2)
         dyn = dy.permute(0, 3, 1, 2)
         gw = torch.nn.grad.conv2d_weight(xn, (g.Cout, g.cg_in, g.KH, g.KW), dyn, stride=g.stride,
                                          padding=(g.pad_y, g.pad_x), groups=g.groups)
         dw.add_(gw.permute(0, 2, 3, 1))
-        return False
+        return
     cg = g.cg_in
     va = 8 if cg % 8 == 0 else 4
     kd = g.kdim
@@ -529,17 +529,9 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom, db=None) -> bool:
             pad_h=g.pad_y, pad_w=g.pad_x, dil=1, Cg=cg)
     B = _op(dy, g.cg_out, g.Cout, g.cg_out, P)
 
-    folded = [False]
-
     def reg(o):
         tile = _pick(WGRAD_TILES, kd, g.cg_out, g.groups, min_blocks=1)
         split = _auto_split(kd, g.cg_out, g.groups, P, tile)
-        if db is not None and o is dw:  # the live output (not a tuning scratch): fold the bias grad
-            native.check(native.kernels().cxn_gemm_wgrad_bias(
-                A, B, va, o.data_ptr(), g.cg_out * kd, kd, db.data_ptr(), g.cg_out, tile, g.groups, split,
-                _stream()), "gemm_wgrad_bias")
-            folded[0] = True
-            return True
         _gemm(A, B, GATHER_MN, DIRECT_MN, va, 8, o, g.cg_out * kd, kd, epi=EPI_F32_ATOMIC, groups=g.groups,
               ksplit=split, tile=tile)
         return True
@@ -553,7 +545,7 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom, db=None) -> bool:
               ksplit=split, tile=tile, kstride=slab)
         native.check(native.kernels().cxn_splitk_accumulate(ws.data_ptr(), split, slab, dw.data_ptr(), _stream()),
                      "splitk_accumulate")
-        return False
+        return
     if _use("cw") and va == 8:
         def run(t, o):
             if t == REG:
@@ -567,7 +559,7 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom, db=None) -> bool:
         # shapes missing from the table keep the register kernel: timed alone, the LDS-DMA form
         # wins shapes where it loses inside the step (conv2/conv3 above)
         if run(_tuned_tile(key, run, dw, lambda: REG, extra=(REG,), tune=False), dw):
-            return folded[0]
+            return
     if va != 8 and g.groups == 1 and g.pad_y == 0 and g.pad_x == 0 and g.C % 4 == 0 and _use("cwr"):
         # few input channels (conv1): the KW*C im2col rows of one kernel row are one contiguous run
         # of x, so the transposed gather reads each run as Cg = roundup(KW*C, 8) "channels" of a
@@ -587,9 +579,8 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom, db=None) -> bool:
         if run(_tuned_tile(key, run, ws, lambda: 1), ws):
             L = g.KW * g.C
             dw.view(g.Cout, g.KH, L).add_(ws.view(g.Cout, g.KH, lp)[:, :, :L])
-            return False
+            return
     reg(dw)
-    return folded[0]
 
 
 # ----------------------------------------------------------------------------- fully connected

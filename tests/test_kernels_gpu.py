@@ -374,24 +374,6 @@ def test_fc_register_kernel(B, nin, nout, register_kernel_only):
     test_fc(B, nin, nout)
 
 
-@pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_weight_grad_folds_bias_grad(case, register_kernel_only):
-    """The register-staged weight-grad GEMM also accumulates the bias gradient (column sums
-    of dy) -- reference K5 fused into K6."""
-    geo = _geom(*case)
-    x = rnd(geo.N, geo.H, geo.W, geo.C, seed=31)
-    dy = rnd(geo.N, geo.Ho, geo.Wo, geo.Cout, seed=32)
-    dw_ref = torch.zeros(geo.Cout, geo.KH, geo.KW, geo.cg_in)
-    ops.conv_backward_weight(x, dy, dw_ref, geo)
-    dw = torch.zeros(geo.Cout, geo.KH, geo.KW, geo.cg_in, device=DEV)
-    db = torch.full((geo.Cout,), 0.25, device=DEV)
-    folded = ops.conv_backward_weight(x.to(DEV, torch.bfloat16), dy.to(DEV, torch.bfloat16), dw, geo, db=db)
-    torch.cuda.synchronize()
-    assert folded
-    assert relerr(dw, dw_ref) < 1e-2
-    assert relerr(db, 0.25 + dy.reshape(-1, geo.Cout).sum(0)) < 1e-3
-
-
 @pytest.mark.parametrize("relu,k,s,p,H", [(False, 3, 2, 0, 27), (True, 3, 2, 0, 28), (False, 3, 1, 1, 14),
                                           (False, 2, 2, 0, 28)])
 def test_pool_tie_all(relu, k, s, p, H):
