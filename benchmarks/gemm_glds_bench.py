@@ -19,7 +19,8 @@ N = 256
 BF = torch.bfloat16
 CONV = {"conv1": (4, 227, 96, 11, 4, 0, 1), "conv2": (96, 27, 256, 5, 1, 2, 2), "conv3": (256, 13, 384, 3, 1, 1, 1),
         "conv4": (384, 13, 384, 3, 1, 1, 2), "conv5": (384, 13, 256, 3, 1, 1, 2)}
-FC = {"fc6": (9216, 4096), "fc7": (4096, 4096), "fc8": (4096, 1000)}
+FC = {"fc6": (9216, 4096), "fc7": (4096, 4096), "fc8": (4096, 1000),
+      "sq8192": (8192, 8192), "sq4096": (4096, 4096)}  # square GEMMs (batch = nin): main-loop ceiling
 # VGG-16 at batch 64 ("vgg.c3_2_fwd"): 3x3 pad 1 convs (C, H, Cout)
 VGG = {"c1_2": (64, 224, 64), "c2_1": (64, 112, 128), "c2_2": (128, 112, 128), "c3_1": (128, 56, 256),
        "c3_2": (256, 56, 256), "c4_1": (256, 28, 512), "c4_2": (512, 28, 512), "c5": (512, 14, 512)}
@@ -50,6 +51,8 @@ def make(name):
     else:
         layer, kind = name.split("_")
     g = torch.Generator(device="cuda").manual_seed(0)
+    if layer.startswith("sq"):
+        N = FC[layer][0]
     if layer in FC:
         nin, nout = FC[layer]
         x = torch.randn(N, nin, device="cuda", generator=g).to(BF)
@@ -64,7 +67,7 @@ def make(name):
             dy = torch.randn(N, nout, device="cuda", generator=g).to(BF)
             dw = torch.empty(nout, nin, device="cuda")
             return (lambda: ops.fc_backward_weight(x, dy, dw, overwrite=True)), dw, 2.0 * N * nin * nout
-        return (lambda: ops.fc_forward(x, w, b, y, relu=True)), y, 2.0 * N * nin * nout
+        return (lambda: ops.fc_forward(x, w, b, y, relu=not layer.startswith("sq"))), y, 2.0 * N * nin * nout
     C, H, Cout, K, s, p, grp = CONV[layer]
     Ho, Wo = G.conv_out_size(H, H, K, K, s, p, p)
     geo = G.ConvGeom(N, H, H, C, Ho, Wo, Cout, K, K, s, p, p, grp)

@@ -14,13 +14,14 @@ CASES = {"conv1": (4, 227, 96, 11, 4, 0, 1), "conv2": (96, 27, 256, 5, 1, 2, 2),
          "conv4": (384, 13, 384, 3, 1, 1, 2), "conv5": (384, 13, 256, 3, 1, 1, 2)}
 
 
-FCS = {"fc6": (9216, 4096), "fc7": (4096, 4096), "fc8": (4096, 1000)}
+FCS = {"fc6": (9216, 4096), "fc7": (4096, 4096), "fc8": (4096, 1000), "sq8192": (8192, 8192), "sq4096": (4096, 4096)}
 VGG = {"c1_2": (64, 224, 64), "c2_2": (128, 112, 128), "c3_2": (256, 56, 256), "c4_2": (512, 28, 512),
        "c5": (512, 14, 512)}
 
 
 def run_fc(layer, kind, iters):
     nin, nout = FCS[layer]
+    N = nin if layer.startswith("sq") else globals()["N"]
     bf = torch.bfloat16
     x = torch.randn(N, nin, device="cuda").to(bf)
     w = (torch.randn(nout, nin, device="cuda") * 0.02).to(bf)

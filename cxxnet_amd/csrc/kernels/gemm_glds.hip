@@ -599,6 +599,81 @@ __device__ __forceinline__ bf16x8 seg_frag(const char *tile, int base, int lane)
   return *reinterpret_cast<const bf16x8 *>(tile + row * 64 + ch * 16);
 }
 
+// Epilogue of the 8-wave kernels: each wave stages 16 output rows (j) x WM columns (i) of its
+// fp32 tile in LDS, then writes contiguous row segments: bf16 (+bias, relu, relu'-mask of the old
+// value) or an fp32 split-K slab.
+template <int EPI, int MR, int NR, int WM>
+__device__ __forceinline__ void seg_epilogue(f32x4 (&acc)[MR][NR], char *smem, const GEpi &E, int g, int Mi,
+                                             int Nj, int ibase, int jbase, int wave, int lane) {
+  float *ep = reinterpret_cast<float *>(smem) + wave * 16 * (WM + 4);
+  const float *bias = E.bias ? E.bias + g * E.bias_gstride : nullptr;
+#pragma unroll
+  for (int n = 0; n < NR; ++n) {
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+      *reinterpret_cast<f32x4 *>(ep + (lane & 15) * (WM + 4) + m * 16 + (lane >> 4) * 4) = acc[m][n];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    if constexpr (EPI == EPI_BF16) {
+      bf16_t *out = reinterpret_cast<bf16_t *>(E.out) + g * E.gstride;
+      constexpr int LPR = WM / 8;
+      constexpr int RPI = 64 / LPR;
+      const int il = (lane % LPR) * 8;
+      const int i = ibase + il;
+      const bool vec_store = ((E.ldc & 7) == 0) && (i + 8 <= Mi);
+#pragma unroll
+      for (int jl = lane / LPR; jl < 16; jl += RPI) {
+        const int j = jbase + n * 16 + jl;
+        if (j < Nj && i < Mi) {
+          const f32x4 x0 = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il);
+          const f32x4 x1 = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il + 4);
+          float f[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            f[e] = f[e] * E.alpha + ((bias && i + e < Mi) ? bias[i + e] : 0.f);
+            if (E.relu) f[e] = fmaxf(f[e], 0.f);
+          }
+          bf16_t *dst = out + static_cast<long>(j) * E.ldc + i;
+          if (vec_store) {
+            if (E.mask_relu) {
+              float old[8];
+              unpack8(*reinterpret_cast<const uint4 *>(dst), old);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) f[e] = old[e] > 0.f ? f[e] : 0.f;
+            }
+            *reinterpret_cast<uint4 *>(dst) = pack8(f);
+          } else {
+            for (int e = 0; e < 8 && i + e < Mi; ++e) {
+              if (E.mask_relu && !(bf2f(dst[e]) > 0.f)) f[e] = 0.f;
+              dst[e] = f2bf(f[e]);
+            }
+          }
+        }
+      }
+    } else {  // EPI_F32: split-K slab (fc forward)
+      float *out = reinterpret_cast<float *>(E.out) + g * E.gstride + blockIdx.y * E.kstride;
+      constexpr int LPR = WM / 4;
+      constexpr int RPI = 64 / LPR;
+      const int il = (lane % LPR) * 4;
+      const int i = ibase + il;
+      const bool vec = ((E.ldc & 3) == 0) && (i + 4 <= Mi);
+#pragma unroll
+      for (int jl = lane / LPR; jl < 16; jl += RPI) {
+        const int j = jbase + n * 16 + jl;
+        if (j < Nj && i < Mi) {
+          f32x4 v = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il) * E.alpha;
+          float *dst = out + static_cast<long>(j) * E.ldc + i;
+          if (vec) {
+            *reinterpret_cast<f32x4 *>(dst) = v;
+          } else {
+            for (int e = 0; e < 4 && i + e < Mi; ++e) dst[e] = v[e];
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+  }
+}
+
 // (A variant with waves 4-7 staggered half a segment behind their SIMD partners -- two
 // barriers per segment -- measured 5-25% slower on every shape: profiles/r2_sweep_segmented.jsonl.)
 template <int BM, int BN, int AMODE, int BMODE, int EPI>
@@ -687,76 +762,7 @@ gemm_seg(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_ti
   wait_vmcnt<0>();
   __syncthreads();  // slots are reused by the epilogue
 
-  // ---- epilogue (as gemm_glds): each wave stages 16 output rows (j) x WM columns (i) in LDS
-  const int Mi = A.rows, Nj = B.rows;
-  const int ibase = i0 + wi_ * WM, jbase = j0 + wj_ * WN;
-  float *ep = reinterpret_cast<float *>(smem) + wave * 16 * (WM + 4);
-  const float *bias = E.bias ? E.bias + g * E.bias_gstride : nullptr;
-#pragma unroll
-  for (int n = 0; n < NR; ++n) {
-#pragma unroll
-    for (int m = 0; m < MR; ++m)
-      *reinterpret_cast<f32x4 *>(ep + (lane & 15) * (WM + 4) + m * 16 + (lane >> 4) * 4) = acc[m][n];
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    if constexpr (EPI == EPI_BF16) {
-      bf16_t *out = reinterpret_cast<bf16_t *>(E.out) + g * E.gstride;
-      constexpr int LPR = WM / 8;
-      constexpr int RPI = 64 / LPR;
-      const int il = (lane % LPR) * 8;
-      const int i = ibase + il;
-      const bool vec_store = ((E.ldc & 7) == 0) && (i + 8 <= Mi);
-#pragma unroll
-      for (int jl = lane / LPR; jl < 16; jl += RPI) {
-        const int j = jbase + n * 16 + jl;
-        if (j < Nj && i < Mi) {
-          const f32x4 x0 = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il);
-          const f32x4 x1 = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il + 4);
-          float f[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            f[e] = f[e] * E.alpha + ((bias && i + e < Mi) ? bias[i + e] : 0.f);
-            if (E.relu) f[e] = fmaxf(f[e], 0.f);
-          }
-          bf16_t *dst = out + static_cast<long>(j) * E.ldc + i;
-          if (vec_store) {
-            if (E.mask_relu) {
-              float old[8];
-              unpack8(*reinterpret_cast<const uint4 *>(dst), old);
-#pragma unroll
-              for (int e = 0; e < 8; ++e) f[e] = old[e] > 0.f ? f[e] : 0.f;
-            }
-            *reinterpret_cast<uint4 *>(dst) = pack8(f);
-          } else {
-            for (int e = 0; e < 8 && i + e < Mi; ++e) {
-              if (E.mask_relu && !(bf2f(dst[e]) > 0.f)) f[e] = 0.f;
-              dst[e] = f2bf(f[e]);
-            }
-          }
-        }
-      }
-    } else {  // EPI_F32: split-K slab (fc forward)
-      float *out = reinterpret_cast<float *>(E.out) + g * E.gstride + blockIdx.y * E.kstride;
-      constexpr int LPR = WM / 4;
-      constexpr int RPI = 64 / LPR;
-      const int il = (lane % LPR) * 4;
-      const int i = ibase + il;
-      const bool vec = ((E.ldc & 3) == 0) && (i + 4 <= Mi);
-#pragma unroll
-      for (int jl = lane / LPR; jl < 16; jl += RPI) {
-        const int j = jbase + n * 16 + jl;
-        if (j < Nj && i < Mi) {
-          f32x4 v = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il) * E.alpha;
-          float *dst = out + static_cast<long>(j) * E.ldc + i;
-          if (vec) {
-            *reinterpret_cast<f32x4 *>(dst) = v;
-          } else {
-            for (int e = 0; e < 4 && i + e < Mi; ++e) dst[e] = v[e];
-          }
-        }
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-  }
+  seg_epilogue<EPI, MR, NR, WM>(acc, smem, E, g, A.rows, B.rows, i0 + wi_ * WM, j0 + wj_ * WN, wave, lane);
 }
 
 template <int BM, int BN, int AMODE, int BMODE, int EPI>
@@ -768,6 +774,153 @@ void launch_seg(const GOperand &A, const GOperand &B, const GEpi &E, int groups,
   ksplit = cdiv(ktiles, per);
   dim3 grid(ti * tj, ksplit, groups);
   hipLaunchKernelGGL((gemm_seg<BM, BN, AMODE, BMODE, EPI>), grid, dim3(512), 0, s, A, B, E, ti, tj, per, ktiles);
+}
+
+// ======================================================================================
+// Ping-pong 8-wave pipeline (tiles 60 / 61: 256 x 256 with 4 / 5 k-half LDS slots, K-major
+// operands -- conv forward / data-grad, fc forward).
+//
+// The two waves that share a SIMD belong to different wave GROUPS (group = wave >> 2, which
+// is also the wave's half of the A rows), and group 1 runs one s_barrier behind group 0.
+// Every PHASE is   wait vmcnt -> issue 2 DMAs -> fragment reads -> barrier -> MFMAs -> barrier,
+// so while one group computes, the other issues its DMAs and LDS reads: the MFMA pipe of each
+// SIMD alternates between its two waves instead of idling through both waves' load phases at
+// the same time (the cdna guide's 8-phase template).
+//   * LDS: NS k-half slots (segment u = 32 k of the block's K range, slot u % NS) of
+//     [256 A rows + 256 B rows] x 64 B -- the gemm_seg image (SegOp DMAs, seg_frag reads);
+//   * segment u = two phases: P0 reads B n-frags 0-3 and A m-frags 0-3 and runs 16 MFMAs,
+//     P1 reads A m-frags 4-7 and runs the other 16 (per wave 128 x 64 outputs, 48 fragment
+//     VGPRs live at most);
+//   * P0 issues the B DMAs and P1 the A DMAs of segment u + NS - 1.  With the one-barrier lag
+//     a slot may be re-filled two phases after its last read, and a DMA must be retired by a
+//     wait one phase before its first read: `s_waitcnt vmcnt(2 (2 NS - 5))` at the top of every
+//     phase (the DMAs of the 2 NS - 5 most recent phases stay in flight) satisfies both;
+//   * past the end of the K slice the DMAs are all-OOB dummies, so the count never changes.
+template <int AMODE, int BMODE, int EPI, int NS>
+__global__ void __launch_bounds__(512, 1)
+gemm_pp(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_tiles, int ktiles_total) {
+  constexpr int BM = 256, BN = 256, NW = 8;
+  constexpr int WM = 128, WN = 64, MR = 8, NR = 4;
+  using OA = SegOp<AMODE, BM>;
+  using OB = SegOp<BMODE, BN>;
+  static_assert(OA::NI == 2 && OB::NI == 2, "2 DMAs per wave per operand and segment");
+  constexpr int A_BYTES = BM * 64, SLOT = (BM + BN) * 64;
+  constexpr int EPI_BYTES = NW * 16 * (WM + 4) * 4;
+  constexpr int SMEM = NS * SLOT > EPI_BYTES ? NS * SLOT : EPI_BYTES;
+  static_assert(NS == 4 || NS == 5, "4 or 5 k-half slots");
+  // segment u is issued at segment u - (NS - 1); its first read (phase 2u) needs it retired by the
+  // wait of phase 2u - 1, which may leave the DMAs of the 2NS - 5 phases before it in flight
+  constexpr int VM = 2 * (2 * NS - 5);
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int g = blockIdx.z;
+  const uint32_t ntile = static_cast<uint32_t>(tiles_i) * tiles_j;
+  const uint32_t tile = xcd_remap(blockIdx.x, ntile);
+  const int ti = tile % tiles_i, tj = tile / tiles_i;
+  const int i0 = ti * BM, j0 = tj * BN;
+  const int kt_beg = blockIdx.y * ksplit_tiles;
+  const int kt_end = min(kt_beg + ksplit_tiles, ktiles_total);
+  if (kt_beg >= kt_end) return;
+  const int nseg = 2 * (kt_end - kt_beg);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;  // group = A-row half; B column quarter
+  const rsrc_t rA = make_rsrc(A.ptr, A.nbytes);
+  const rsrc_t rB = make_rsrc(B.ptr, B.nbytes);
+  const uint32_t goA = static_cast<uint32_t>(g * A.gstride) * 2u;
+  const uint32_t goB = static_cast<uint32_t>(g * B.gstride) * 2u;
+  OA oa;
+  OB ob;
+  oa.init(A, i0, goA, wave, lane);
+  ob.init(B, j0, goB, wave, lane);
+
+  auto issue_a = [&](int seg) {
+    const typename OA::Prep pa = oa.prep(A, kt_beg + (seg >> 1), seg & 1, kt_end, goA);
+    char *sl = smem + (seg % NS) * SLOT;
+    static_for<OA::NI>([&](auto sc) {
+      constexpr int q = decltype(sc)::value;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void *)(sl + (wave + NW * q) * 1024), 16,
+                                               oa.template offset<q>(A, pa), 0, 0, 0);
+    });
+  };
+  auto issue_b = [&](int seg) {
+    const typename OB::Prep pb = ob.prep(B, kt_beg + (seg >> 1), seg & 1, kt_end, goB);
+    char *sl = smem + (seg % NS) * SLOT + A_BYTES;
+    static_for<OB::NI>([&](auto sc) {
+      constexpr int q = decltype(sc)::value;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void *)(sl + (wave + NW * q) * 1024), 16,
+                                               ob.template offset<q>(B, pb), 0, 0, 0);
+    });
+  };
+
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: segments 0 .. NS-2 in full; segment 0 landed for every wave before anyone reads it
+#pragma unroll
+  for (int u = 0; u < NS - 1; ++u) {
+    issue_a(u);
+    issue_b(u);
+  }
+  wait_vmcnt<4 * (NS - 2)>();
+  block_barrier();
+  if (wr == 1) block_barrier();  // group 1 runs one barrier behind group 0
+
+  bf16x8 fa[MR], fb[NR];
+  for (int seg = 0; seg < nseg; ++seg) {
+    const char *sa = smem + (seg % NS) * SLOT;
+    const char *sb = sa + A_BYTES;
+    // ---- phase 0: B fragments and A m-frags 0-3; B DMAs of segment seg + NS - 1; 16 MFMAs
+    // (segment seg was retired by every wave's wait in the previous phase)
+#pragma unroll
+    for (int n = 0; n < NR; ++n) fb[n] = seg_frag(sb, wc * WN + n * 16, lane);
+#pragma unroll
+    for (int m = 0; m < MR / 2; ++m) fa[m] = seg_frag(sa, wr * WM + m * 16, lane);
+    issue_b(seg + NS - 1);
+    block_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int m = 0; m < MR / 2; ++m)
+#pragma unroll
+      for (int n = 0; n < NR; ++n)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    block_barrier();
+    // ---- phase 1: A m-frags 4-7; A DMAs of segment seg + NS - 1; retire segment seg + 1; 16 MFMAs
+#pragma unroll
+    for (int m = MR / 2; m < MR; ++m) fa[m] = seg_frag(sa, wr * WM + m * 16, lane);
+    wait_vmcnt<VM>();
+    issue_a(seg + NS - 1);
+    block_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int m = MR / 2; m < MR; ++m)
+#pragma unroll
+      for (int n = 0; n < NR; ++n)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    block_barrier();
+  }
+  if (wr == 0) block_barrier();  // equal barrier counts for both groups
+  wait_vmcnt<0>();
+  __syncthreads();  // slots are reused by the epilogue
+
+  seg_epilogue<EPI, MR, NR, WM>(acc, smem, E, g, A.rows, B.rows, i0 + wr * WM, j0 + wc * WN, wave, lane);
+}
+
+template <int AMODE, int BMODE, int EPI, int NS>
+void launch_pp(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int ksplit, hipStream_t s) {
+  const int ti = cdiv(A.rows, 256), tj = cdiv(B.rows, 256);
+  const int ktiles = cdiv(A.kdim, BK);
+  ksplit = ksplit < 1 ? 1 : (ksplit > ktiles ? ktiles : ksplit);
+  const int per = cdiv(ktiles, ksplit);
+  ksplit = cdiv(ktiles, per);
+  dim3 grid(ti * tj, ksplit, groups);
+  hipLaunchKernelGGL((gemm_pp<AMODE, BMODE, EPI, NS>), grid, dim3(512), 0, s, A, B, E, ti, tj, per, ktiles);
 }
 
 // Tile ids (BM x BN, wave grid, stages); MN-major operands need a 128-wide tile side:
@@ -828,6 +981,19 @@ int dispatch(int amode, int bmode, int epi, int tile, const GOperand &A, const G
     return -1;
   }
 #undef CXG_SEG
+  // ping-pong 8-wave pipeline, 256x256 (K-major A and B): 60 = 4 k-half slots, 61 = 5
+#define CXG_PP(AMV, BMV, EPV)                                                                         \
+  if (amode == AMV && bmode == BMV && epi == EPV) {                                                   \
+    if (tile == 60) { launch_pp<AMV, BMV, EPV, 4>(A, B, E, groups, ksplit, s); return 0; }            \
+    if (tile == 61) { launch_pp<AMV, BMV, EPV, 5>(A, B, E, groups, ksplit, s); return 0; }            \
+  }
+  if (tile == 60 || tile == 61) {
+    CXG_PP(K_DIRECT, K_GATHER, EPI_BF16)
+    CXG_PP(K_DIRECT, K_DIRECT, EPI_BF16)
+    CXG_PP(K_DIRECT, K_DIRECT, EPI_F32)
+    return -1;
+  }
+#undef CXG_PP
   CXG_CASE(K_DIRECT, K_GATHER, EPI_BF16, CXG_KK_TILES)    // conv fwd / dgrad
   CXG_CASE(K_DIRECT, K_ROWGATHER, EPI_BF16, CXG_KK_TILES)  // conv fwd, few input channels (conv1)
   CXG_CASE(K_DIRECT, K_DIRECT, EPI_BF16, CXG_KK_TILES)    // fc fwd
