@@ -566,8 +566,9 @@ __global__ void lrn_fwd(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, lo
 // (norm recomputed from x: no state tensor is stored)
 // LDS-staged LRN backward: block = NT/(C/8) pixels, one thread per 8 channels.
 // LDS per pixel: x, g and t = g*x*norm^(-b-1), each with `half` zero pads at both ends.
+// mask_relu: the input is relu(z) of a fused producer -> also apply relu'(z) = (x > 0).
 __global__ void lrn_bwd_lds(const bf16_t *x, const bf16_t *dy, bf16_t *dx, long npix, int C, int half, float salpha,
-                            float beta, float knorm) {
+                            float beta, float knorm, int mask_relu) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tpp = C / 8;
   const int ppb = blockDim.x / tpp;
@@ -620,6 +621,7 @@ __global__ void lrn_bwd_lds(const bf16_t *x, const bf16_t *dy, bf16_t *dx, long 
       float s = 0.f;
       for (int d = -half; d <= half; ++d) s += ts[c + d];
       out[e] = ng[e] - 2.f * beta * salpha * xv[e] * s;
+      if (mask_relu && !(xv[e] > 0.f)) out[e] = 0.f;
     }
     *reinterpret_cast<uint4 *>(dx + pix * C + c0) = pack8(out);
   }
@@ -693,7 +695,7 @@ __global__ void lrn_fwd_shfl(const bf16_t *__restrict__ x, bf16_t *__restrict__ 
 // dx may alias x (each lane reads its x/g before any write; the halo comes by shuffle).
 template <int H>
 __global__ void lrn_bwd_shfl(const bf16_t *x, const bf16_t *__restrict__ dy, bf16_t *dx, long npix, int C,
-                             float salpha, float beta, float knorm) {
+                             float salpha, float beta, float knorm, int mask_relu) {
   const LrnLane L = lrn_lane(npix, C);
   const long off = L.pix * C + L.cv * 8;
   float xv[8], gv[8], sq[8], s[8];
@@ -719,12 +721,15 @@ __global__ void lrn_bwd_shfl(const bf16_t *x, const bf16_t *__restrict__ dy, bf1
   if (!L.active) return;
   float out[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) out[e] = ng[e] - 2.f * beta * salpha * xv[e] * ts[e];
+  for (int e = 0; e < 8; ++e) {
+    out[e] = ng[e] - 2.f * beta * salpha * xv[e] * ts[e];
+    if (mask_relu && !(xv[e] > 0.f)) out[e] = 0.f;
+  }
   *reinterpret_cast<uint4 *>(dx + off) = pack8(out);
 }
 
 __global__ void lrn_bwd(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, bf16_t *__restrict__ dx,
-                        long npix, int C, int half, float salpha, float beta, float knorm) {
+                        long npix, int C, int half, float salpha, float beta, float knorm, int mask_relu) {
   const int CV = C / 8;
   const long total = npix * CV;
   for (long idx = grid_stride_start(); idx < total; idx += grid_stride()) {
@@ -758,6 +763,7 @@ __global__ void lrn_bwd(const bf16_t *__restrict__ x, const bf16_t *__restrict__
       float s = 0.f;
       for (int d = -half; d <= half; ++d) s += tv[j + d];
       out[e] = gb[j] * exp2f(-beta * __log2f(normv[j])) - 2.f * beta * salpha * xb[j] * s;
+      if (mask_relu && !(xb[j] > 0.f)) out[e] = 0.f;
     }
     *reinterpret_cast<uint4 *>(dx + pix * C + c0) = pack8(out);
   }
@@ -890,9 +896,11 @@ __global__ void loss_grad(const float *__restrict__ p32, bf16_t *__restrict__ no
 
 // ------------------------------------------------------------------ bias gradient
 // db[c] += sum_r dy[r][c]  (dy bf16 [rows][C], C % 8 == 0).  Block = CB column-vectors x RG row
-// groups; per-thread fp32 partials, LDS tree over RG, one atomic per channel per block.
+// groups; per-thread fp32 partials, LDS tree over RG, then one fp32 atomic per channel per block
+// into db (one launch), or, in deterministic mode (db == nullptr), one partial row per block
+// for the fixed-order partials_reduce.
 __global__ void colsum_bf16(const bf16_t *__restrict__ dy, float *__restrict__ part, long rows, int C,
-                            int rows_per_block) {
+                            int rows_per_block, float *__restrict__ db) {
   const int CV = C / 8;
   const int CB = min(CV - static_cast<int>(blockIdx.y) * 64, 64);
   const int RG = NT / CB;
@@ -928,7 +936,10 @@ __global__ void colsum_bf16(const bf16_t *__restrict__ dy, float *__restrict__ p
     const int c = q / 8, e = q % 8;
     float s = 0.f;
     for (int g = 0; g < RG; ++g) s += red[g * CB + c][e];
-    part[static_cast<long>(blockIdx.x) * C + (blockIdx.y * 64 + c) * 8 + e] = s;  // reduced by partials_reduce
+    if (db != nullptr)
+      atomicAdd(db + (blockIdx.y * 64 + c) * 8 + e, s);
+    else
+      part[static_cast<long>(blockIdx.x) * C + (blockIdx.y * 64 + c) * 8 + e] = s;  // reduced by partials_reduce
   }
 }
 
@@ -1361,7 +1372,7 @@ CXN_API int cxn_lrn_fwd(const void *x, void *y, long npix, int C, int nsize, flo
   RET;
 }
 CXN_API int cxn_lrn_bwd(const void *x, const void *dy, void *dx, long npix, int C, int nsize, float alpha, float beta,
-                        float knorm, void *stream) {
+                        float knorm, int mask_relu, void *stream) {
   if (C % 8 != 0) return -1;
   const int half = nsize / 2;
   const int tpp = C / 8;  // threads per pixel
@@ -1370,11 +1381,11 @@ CXN_API int cxn_lrn_bwd(const void *x, const void *dy, void *dx, long npix, int 
     const int blocks = static_cast<int>((waves + NT / 64 - 1) / (NT / 64));
     const float sa = alpha / nsize;
     switch (half) {
-      case 0: lrn_bwd_shfl<0><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm); break;
-      case 1: lrn_bwd_shfl<1><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm); break;
-      case 2: lrn_bwd_shfl<2><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm); break;
-      case 3: lrn_bwd_shfl<3><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm); break;
-      default: lrn_bwd_shfl<4><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm); break;
+      case 0: lrn_bwd_shfl<0><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm, mask_relu); break;
+      case 1: lrn_bwd_shfl<1><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm, mask_relu); break;
+      case 2: lrn_bwd_shfl<2><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm, mask_relu); break;
+      case 3: lrn_bwd_shfl<3><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm, mask_relu); break;
+      default: lrn_bwd_shfl<4><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm, mask_relu); break;
     }
     RET;
   }
@@ -1385,12 +1396,12 @@ CXN_API int cxn_lrn_bwd(const void *x, const void *dy, void *dx, long npix, int 
     const int blocks = static_cast<int>((npix + ppb - 1) / ppb);
     const size_t smem = static_cast<size_t>(ppb) * (C + 2 * half) * 3 * sizeof(float);
     lrn_bwd_lds<<<blocks, NT, smem, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, half,
-                                          alpha / nsize, beta, knorm);
+                                          alpha / nsize, beta, knorm, mask_relu);
     RET;
   }
   if (half > 4 || x == dx) return -1;
   lrn_bwd<<<nblocks(npix * C / 8), NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C,
-                                                 half, alpha / nsize, beta, knorm);
+                                                 half, alpha / nsize, beta, knorm, mask_relu);
   RET;
 }
 CXN_API int cxn_act_fwd(const void *x, void *y, void *y2, long n, int kind, float b, void *stream) {
@@ -1444,9 +1455,17 @@ CXN_API int cxn_colsum(const void *dy, float *db, long rows, int C, float *ws, l
   int rpb = 512;
   // keep the partials within the caller's workspace
   while (static_cast<long>(cdiv(rows, rpb)) * C > ws_elems && rpb < (1 << 24)) rpb *= 2;
+  // atomics straight into db: at most ~512 adders per channel (VGG conv1_2's 3.2M rows at 512
+  // rows per block put 6272 atomics on each of 64 addresses and ran slower than two passes)
+  if (!cxn_deterministic)
+    while (cdiv(rows, rpb) > 512) rpb *= 2;
   if (static_cast<long>(cdiv(rows, rpb)) * C > ws_elems) return -2;
   dim3 grid(cdiv(rows, rpb), cdiv(CV, 64));
-  colsum_bf16<<<grid, NT, 0, S_>>>((const bf16_t *)dy, ws, rows, C, rpb);
+  if (!cxn_deterministic) {  // per-block atomics straight into db
+    colsum_bf16<<<grid, NT, 0, S_>>>((const bf16_t *)dy, ws, rows, C, rpb, db);
+    RET;
+  }
+  colsum_bf16<<<grid, NT, 0, S_>>>((const bf16_t *)dy, ws, rows, C, rpb, nullptr);
   partials_reduce<<<partials_grid(static_cast<int>(grid.x), C), NT, 0, S_>>>(ws, static_cast<int>(grid.x), C, db);
   RET;
 }

@@ -7,12 +7,16 @@ the same node holds the activation in forward and its gradient in backward).
 """
 from __future__ import annotations
 
+import os
 
 import torch
 
 from .. import ops
 from ..ops.gemm import ConvGeom, conv_out_size
 from .base import BinReader, BinWriter, Layer, Node, ParamSpec
+
+# CXXNET_CONV_PREPAD=0 disables the zero-bordered-copy path of few-channel padded convs
+_PREPAD = os.environ.get("CXXNET_CONV_PREPAD", "1") != "0"
 
 
 def _check(cond, msg):
@@ -160,6 +164,8 @@ class ConvolutionLayer(Layer):
         self.fuse_relu = False
         self.geo = None
         self._wt = None
+        self._xpad = None
+        self._prepad_on = False
 
     def init_connection(self, nodes_in, nodes_out):
         _check(len(nodes_in) == 1 and len(nodes_out) == 1, "ConvolutionLayer: only support 1-1 connection")
@@ -183,6 +189,11 @@ class ConvolutionLayer(Layer):
                             lp.pad_y, lp.pad_x, G)
         cg_l, cg_p = c // G, x.cp // G
         kh, kw, co = lp.kernel_height, lp.kernel_width, lp.num_channel
+        # few input channels with padding (VGG's 3x3 pad-1 first conv on 4 channels): forward and
+        # weight-grad run on a zero-bordered copy of x, so the row-gather GEMM (whole kernel-row
+        # runs, pad 0 only) serves them instead of the per-tap gather with 4-channel chunks
+        self._prepad_on = (cg_p % 8 != 0 and G == 1 and (lp.pad_y or lp.pad_x) and x.cp % 4 == 0
+                           and _PREPAD)
 
         def init_w(t):
             logical = torch.empty(G, co // G, cg_l * kh * kw)
@@ -221,15 +232,34 @@ class ConvolutionLayer(Layer):
     def b(self):
         return self.params[1] if len(self.params) > 1 else None
 
+    def _padded(self, x, refresh):
+        """(input, geometry) for forward / weight-grad: x itself, or (pre-pad path) the
+        zero-bordered copy of x with a pad-0 geometry.  refresh=False reuses the forward's copy
+        (x is unchanged until this layer's own backprop writes its gradient)."""
+        g = self.geo
+        if not (self._prepad_on and x.is_cuda):
+            return x, g
+        N = x.shape[0]
+        H2, W2 = g.H + 2 * g.pad_y, g.W + 2 * g.pad_x
+        if self._xpad is None or self._xpad.shape[0] < N:
+            self._xpad = torch.zeros(N, H2, W2, g.C, dtype=x.dtype, device=x.device)
+            refresh = True
+        xp = self._xpad[:N]
+        if refresh:
+            xp[:, g.pad_y:g.pad_y + g.H, g.pad_x:g.pad_x + g.W].copy_(x)
+        return xp, ConvGeom(N, H2, W2, g.C, g.Ho, g.Wo, g.Cout, g.KH, g.KW, g.stride, 0, 0, g.groups)
+
     def forward(self, is_train, nodes_in, nodes_out):
         self.geo.N = nodes_in[0].data.shape[0]
         bias = self.b.w if self.b is not None else None
-        ops.conv_forward(nodes_in[0].data, self.w.wb, bias, nodes_out[0].data, self.geo, relu=self.fuse_relu)
+        x, geo = self._padded(nodes_in[0].data, True)
+        ops.conv_forward(x, self.w.wb, bias, nodes_out[0].data, geo, relu=self.fuse_relu)
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
         x, dy = nodes_in[0].data, nodes_out[0].data
         self.geo.N = x.shape[0]
-        ops.conv_backward_weight(x, dy, self.w.g, self.geo)
+        xw, geo = self._padded(x, False)
+        ops.conv_backward_weight(xw, dy, self.w.g, geo)
         if self.b is not None:
             ops.bias_grad(dy.view(-1, dy.shape[-1]), self.b.g)
         if prop_grad:
@@ -415,7 +445,8 @@ class LRNLayer(Layer):
             return
         x = nodes_in[0].data
         # in place: the LDS-staged kernel reads a pixel's whole channel row before writing it
-        ops.lrn_backward(x, nodes_out[0].data, nodes_in[0].gdst, self.nsize, self.alpha, self.beta, self.knorm)
+        ops.lrn_backward(x, nodes_out[0].data, nodes_in[0].gdst, self.nsize, self.alpha, self.beta, self.knorm,
+                         mask_relu=self.grad_mask_relu)
 
 
 # ============================================================================ dropout

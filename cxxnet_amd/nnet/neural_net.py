@@ -158,7 +158,7 @@ class NeuralNet:
                 cj.layer.grad_mask_inputs.add(cj.nodes_in.index(b))
                 self.aliases[id(b)] = a
                 continue
-            if cj.type not in (K_CONV, K_FULLC, K_MAXPOOL) or len(cj.nodes_in) != 1:
+            if cj.type not in (K_CONV, K_FULLC, K_MAXPOOL, K_LRN) or len(cj.nodes_in) != 1:
                 continue
             # commit: producer epilogue applies relu, b aliases a, consumer masks the gradient
             p.layer.fuse_relu = True

@@ -237,8 +237,9 @@ def lrn_forward(x, y, nsize, alpha, beta, knorm):
                                   float(knorm), _stream()), "lrn_fwd")
 
 
-def lrn_backward(x, dy, dx, nsize, alpha, beta, knorm):
-    """dx = d LRN / dx (dx may alias x; it must not alias dy)."""
+def lrn_backward(x, dy, dx, nsize, alpha, beta, knorm, mask_relu=False):
+    """dx = d LRN / dx (dx may alias x; it must not alias dy).  mask_relu: x is relu(z) of a
+    fused producer, so dx is also multiplied by relu'(z) = (x > 0)."""
     if not x.is_cuda:
         norm = _lrn_norm(x, nsize, alpha, knorm)
         t = dy * x * norm.pow(-beta - 1)
@@ -246,11 +247,14 @@ def lrn_backward(x, dy, dx, nsize, alpha, beta, knorm):
         half = nsize // 2
         tp = F.pad(t, (half, half))
         s = sum(tp[..., i:i + C] for i in range(nsize))
-        dx.copy_(dy * norm.pow(-beta) - 2 * beta * alpha / nsize * x * s)
+        g = dy * norm.pow(-beta) - 2 * beta * alpha / nsize * x * s
+        if mask_relu:
+            g = torch.where(x > 0, g, torch.zeros_like(g))
+        dx.copy_(g)
         return
     N, H, W, C = x.shape
     native.check(_k().cxn_lrn_bwd(x.data_ptr(), dy.data_ptr(), dx.data_ptr(), N * H * W, C, nsize, float(alpha),
-                                  float(beta), float(knorm), _stream()), "lrn_bwd")
+                                  float(beta), float(knorm), int(bool(mask_relu)), _stream()), "lrn_bwd")
 
 
 # ----------------------------------------------------------------------------- activations

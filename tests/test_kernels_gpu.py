@@ -181,25 +181,32 @@ def test_pool_mask_in_state(relu_fwd):
     assert relerr(db, 0.5 + dx_ref.reshape(-1, C).sum(0)) < 2e-2
 
 
+@pytest.mark.parametrize("mask", [False, True])
 @pytest.mark.parametrize("C,nsize", [(96, 5), (256, 5), (40, 3), (64, 9), (1024, 5)])
-def test_lrn(C, nsize):
+def test_lrn(C, nsize, mask):
     """Shuffle kernels (C <= 512: whole pixels per wave, halo by ds_bpermute; odd pixel
-    count leaves a partial last wave) and the LDS fallback (C = 1024)."""
+    count leaves a partial last wave) and the LDS fallback (C = 1024).  mask: the input is
+    relu(z) of a fused producer (about half the values exactly 0) and the data-gradient is
+    also multiplied by relu'(z)."""
     N, H, W = 2, 13, 13
     x = rnd(N, H, W, C, scale=2.0, seed=15)
+    if mask:
+        x = x.clamp_min(0)
     dy = rnd(N, H, W, C, seed=16)
     args = (nsize, 0.001, 0.75, 1.0)
     y_ref = torch.empty_like(x)
     ops.lrn_forward(x, y_ref, *args)
     dx_ref = torch.empty_like(x)
-    ops.lrn_backward(x, dy, dx_ref, *args)
+    ops.lrn_backward(x, dy, dx_ref, *args, mask_relu=mask)
+    if mask:
+        assert (dx_ref[x == 0] == 0).all() and (dx_ref[x > 0] != 0).any()
     xd = x.to(DEV, torch.bfloat16)
     y = torch.empty_like(xd)
     ops.lrn_forward(xd, y, *args)
     dx = torch.empty_like(xd)
-    ops.lrn_backward(xd, dy.to(DEV, torch.bfloat16), dx, *args)
+    ops.lrn_backward(xd, dy.to(DEV, torch.bfloat16), dx, *args, mask_relu=mask)
     xi = xd.clone()
-    ops.lrn_backward(xi, dy.to(DEV, torch.bfloat16), xi, *args)  # in place (the layer's usage)
+    ops.lrn_backward(xi, dy.to(DEV, torch.bfloat16), xi, *args, mask_relu=mask)  # in place (the layer's usage)
     torch.cuda.synchronize()
     assert relerr(y, y_ref) < 1e-2
     assert relerr(dx, dx_ref) < 2e-2
