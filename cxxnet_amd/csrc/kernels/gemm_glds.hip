@@ -48,7 +48,7 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef __attribute__((address_space(3))) void lds_void;
 
 enum { K_DIRECT = 0, K_GATHER = 1, MN_DIRECT = 2, MN_GATHER = 3, K_ROWGATHER = 4 };
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_ACC = 2, EPI_F32_ATOMIC = 3 };
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_ACC = 2, EPI_F32_ATOMIC = 3, EPI_F32_SGD = 4 };
 
 struct GOperand {
   const bf16_t *ptr;
@@ -69,7 +69,19 @@ struct GEpi {
   long bias_gstride;
   int relu, mask_relu;
   long kstride;
+  // EPI_F32_SGD (fc weight-grad fused with the SGD step): the gradient element never goes to
+  // memory; w (fp32 master), m (momentum) and the bf16 shadow wb are updated in place, with
+  // the fused optimizer's exact arithmetic (optim_kernels.hip step1, algo 0)
+  float *sgd_w, *sgd_m;
+  bf16_t *sgd_wb;
+  float lr, wd, mom, clip;
 };
+
+__device__ __forceinline__ float sgd_step(const GEpi &E, float g, float &m, float w) {
+  if (E.clip != 0.f) g = (g != g) ? 0.f : fminf(fmaxf(g, -E.clip), E.clip);
+  m = fmaf(E.mom, m, -E.lr * fmaf(E.wd, w, g));  // as optim_kernels.hip step1 (SGD)
+  return w + m;
+}
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void *p, uint32_t nbytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, static_cast<int>(nbytes), 0x00020000);
@@ -473,12 +485,37 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
         const int j = jbase + n * 16 + jl;
         if (j < Nj && i < Mi) {
           f32x4 v = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il) * E.alpha;
-          float *dst = out + static_cast<long>(j) * E.ldc + i;
-          if (vec) {
-            if constexpr (EPI == EPI_F32_ACC) v += *reinterpret_cast<const f32x4 *>(dst);
-            *reinterpret_cast<f32x4 *>(dst) = v;
+          if constexpr (EPI == EPI_F32_SGD) {
+            const long idx = static_cast<long>(j) * E.ldc + i;
+            if (vec) {
+              f32x4 wv = *reinterpret_cast<const f32x4 *>(E.sgd_w + idx);
+              f32x4 mv = *reinterpret_cast<const f32x4 *>(E.sgd_m + idx);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                float mm = mv[e];
+                wv[e] = sgd_step(E, v[e], mm, wv[e]);
+                mv[e] = mm;
+              }
+              *reinterpret_cast<f32x4 *>(E.sgd_w + idx) = wv;
+              *reinterpret_cast<f32x4 *>(E.sgd_m + idx) = mv;
+              *reinterpret_cast<uint2 *>(E.sgd_wb + idx) = make_uint2(pack2(wv[0], wv[1]), pack2(wv[2], wv[3]));
+            } else {
+              for (int e = 0; e < 4 && i + e < Mi; ++e) {
+                float mm = E.sgd_m[idx + e];
+                const float wn = sgd_step(E, v[e], mm, E.sgd_w[idx + e]);
+                E.sgd_m[idx + e] = mm;
+                E.sgd_w[idx + e] = wn;
+                E.sgd_wb[idx + e] = f2bf(wn);
+              }
+            }
           } else {
-            for (int e = 0; e < 4 && i + e < Mi; ++e) dst[e] = (EPI == EPI_F32_ACC ? dst[e] : 0.f) + v[e];
+            float *dst = out + static_cast<long>(j) * E.ldc + i;
+            if (vec) {
+              if constexpr (EPI == EPI_F32_ACC) v += *reinterpret_cast<const f32x4 *>(dst);
+              *reinterpret_cast<f32x4 *>(dst) = v;
+            } else {
+              for (int e = 0; e < 4 && i + e < Mi; ++e) dst[e] = (EPI == EPI_F32_ACC ? dst[e] : 0.f) + v[e];
+            }
           }
         }
       }
@@ -1003,6 +1040,7 @@ int dispatch(int amode, int bmode, int epi, int tile, const GOperand &A, const G
   CXG_CASE(MN_DIRECT, K_DIRECT, EPI_F32, CXG_MK_TILES)    // fc dgrad split-K
   CXG_CASE(MN_DIRECT, MN_DIRECT, EPI_F32, CXG_MM_TILES)   // fc wgrad (store)
   CXG_CASE(MN_DIRECT, MN_DIRECT, EPI_F32_ACC, CXG_MM_TILES)  // fc wgrad (+=)
+  CXG_CASE(MN_DIRECT, MN_DIRECT, EPI_F32_SGD, CXG_MM_TILES)  // fc wgrad fused with the SGD step
   return -1;
 }
 #undef CXG_CASE
@@ -1074,9 +1112,33 @@ CXN_API int cxn_gemm_glds(const CxnOperandG *a, const CxnOperandG *b, int amode,
   GOperand A{}, B{};
   fill(A, a, amode);
   fill(B, b, bmode);
-  GEpi E{out, out_gstride, ldc, alpha, bias, bias_gstride, relu, mask_relu, kstride};
+  if (epi == EPI_F32_SGD) return -1;  // only through cxn_gemm_glds_sgd
+  GEpi E{out, out_gstride, ldc, alpha, bias, bias_gstride, relu, mask_relu, kstride,
+         nullptr, nullptr, nullptr, 0.f, 0.f, 0.f, 0.f};
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int rc = dispatch(amode, bmode, epi, tile, A, B, E, groups < 1 ? 1 : groups, ksplit < 1 ? 1 : ksplit, s);
+  if (rc != 0) return rc;
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// fc weight-grad fused with the SGD step (single GPU, update_period 1): for every element of
+// dw = alpha * B^T A (MN-major x and dy, ldc = nin) the epilogue applies
+//   g = clip(dw); m = mom*m - lr*(g + wd*w); w += m; wb = bf16(w)
+// to the layer's master / momentum / shadow slices instead of storing dw.
+CXN_API int cxn_gemm_glds_sgd(const CxnOperandG *a, const CxnOperandG *b, int ldc, float alpha, float *w, float *m,
+                              void *wb, float lr, float wd, float mom, float clip, int tile, void *stream) {
+  if (a->kdim != b->kdim) return -1;
+  if (!supported(a, MN_DIRECT) || !supported(b, MN_DIRECT)) return -1;
+  if (a->rows % 4 != 0 || ldc % 4 != 0 || (reinterpret_cast<uintptr_t>(w) & 15) || (reinterpret_cast<uintptr_t>(m) & 15) ||
+      (reinterpret_cast<uintptr_t>(wb) & 7))
+    return -1;
+  if (a->rows <= 0 || b->rows <= 0 || a->kdim <= 0) return 0;
+  GOperand A{}, B{};
+  fill(A, a, MN_DIRECT);
+  fill(B, b, MN_DIRECT);
+  GEpi E{nullptr, 0, ldc, alpha, nullptr, 0, 0, 0, 0, w, m, static_cast<bf16_t *>(wb), lr, wd, mom, clip};
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int rc = dispatch(MN_DIRECT, MN_DIRECT, EPI_F32_SGD, tile, A, B, E, 1, 1, s);
   if (rc != 0) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -38,7 +38,9 @@ __device__ __forceinline__ float step1(int algo, const Seg &sg, float wv, float 
     // only the SGD updater clips (reference sgd_updater-inl.hpp:77-81); NAG and Adam
     // ignore clip_gradient
     gv = clipg(gv, sg.clip);
-    m1 = sg.mom * m1 - sg.lr * (gv + sg.wd * wv);
+    // explicit fmas: the fc weight-gradient GEMM's fused step (gemm_glds.hip sgd_step) does
+    // the same operations in the same order, so both give the same bits
+    m1 = fmaf(sg.mom, m1, -sg.lr * fmaf(sg.wd, wv, gv));
     return wv + m1;
   }
   if (algo == 1) {

@@ -96,6 +96,10 @@ class LayerContext:
         self.is_gpu = self.device.type == "cuda"
         self.act_dtype = torch.bfloat16 if self.is_gpu else torch.float32
         self.seed = seed
+        # set by the trainer around an update step's backprop: the arena updater when the fc
+        # weight steps are fused into their weight-gradient GEMMs, and the step's epoch
+        self.sgd_fuse = None
+        self.epoch = 0
         self.gen = torch.Generator(device="cpu")
         self.gen.manual_seed(seed)
         self.label_fields: Dict[str, torch.Tensor] = {}

@@ -41,6 +41,7 @@ class FullConnectLayer(Layer):
         super().__init__(ctx)
         self.fullc_gather = 0
         self.fuse_relu = False
+        self._dx = None
 
     def set_param(self, name, val):
         super().set_param(name, val)
@@ -91,9 +92,41 @@ class FullConnectLayer(Layer):
             self._x_all = _all_gather_rows(x, nodes_in[0].shape[0])
         ops.fc_forward(x, self.w.wb, bias, nodes_out[0].mat(), relu=self.fuse_relu)
 
+    def _fused_sgd(self, x, dy, prop_grad, nodes_in) -> bool:
+        """Single-GPU SGD step of the weights fused into the weight-gradient GEMM
+        (ctx.sgd_fuse = the arena updater, set by the trainer when eligible).  The data
+        gradient reads the OLD shadow weights, so it runs first, into a scratch buffer (x,
+        which the weight-gradient still needs, lives where it goes); the scratch is copied
+        back (with relu' when fused) after the update."""
+        upd = getattr(self.ctx, "sgd_fuse", None)
+        if upd is None or not (getattr(self.ctx, "grad_overwrite", False) and self.w.overwrite) or not x.is_cuda:
+            return False
+        spec = self.w
+        lr, wd, mom, clip = upd.hyper(spec, self.ctx.epoch)
+        a = upd.arena
+        m = a.m1[spec.offset:spec.offset + spec.numel].view(spec.shape)
+        gx = None
+        if prop_grad:
+            if self._dx is None or self._dx.shape[0] < x.shape[0] or self._dx.shape[1] != x.shape[1]:
+                self._dx = torch.empty_like(x)
+            gx = self._dx[:x.shape[0]]
+            ops.fc_backward_data(dy, spec.wb, gx)
+        if ops.fc_backward_weight_sgd(x, dy, spec.w, m, spec.wb, lr, wd, mom, clip):
+            upd.fused_offsets.add(spec.offset)
+        else:  # the kernel does not cover this shape: plain gradient, updated by the updater
+            ops.fc_backward_weight(x, dy, spec.g, overwrite=True)
+        if gx is not None:
+            dst = nodes_in[0].gmat()
+            ops.channel_copy(gx, 0, dst, 0, dst.shape[1], mask_relu=self.grad_mask_relu)
+        return True
+
     def backprop(self, prop_grad, nodes_in, nodes_out):
         x, dy = nodes_in[0].mat(), nodes_out[0].mat()
-        overwrite = getattr(self.ctx, "grad_overwrite", False)
+        overwrite = getattr(self.ctx, "grad_overwrite", False) and self.w.overwrite
+        if not self._gathering() and self._fused_sgd(x, dy, prop_grad, nodes_in):
+            if self.b is not None:
+                ops.bias_grad(dy, self.b.g)
+            return
         if self._gathering():
             dy_all = _all_gather_rows(dy, nodes_out[0].shape[0])
             x_all = self._x_all.wait()

@@ -222,6 +222,12 @@ class NeuralNet:
                 n.grad_buf = torch.zeros_like(n.data)
 
     def _build_arena(self):
+        # a shared layer's backprop runs once per use: its gradients must accumulate, so
+        # they are zeroed at the start of an update cycle instead of overwritten
+        for conn in self.connections:
+            if conn.shared:
+                for spec in conn.layer.params:
+                    spec.overwrite = False
         specs = []
         for i, conn in enumerate(self.connections):
             if not conn.shared:

@@ -20,6 +20,9 @@ import torch
 from .. import native
 from ..layers.base import BinReader, BinWriter
 from ..parallel.dp import GradReducer, world_info
+
+# CXXNET_FUSE_FC_SGD=0 keeps the fc weight steps in the fused optimizer launch
+_FUSE_FC_SGD = os.environ.get("CXXNET_FUSE_FC_SGD", "1") != "0"
 from ..utils.metric import DeviceMetricSet, MetricSet
 from .neural_net import NeuralNet
 
@@ -351,7 +354,12 @@ class NetTrainer:
         evals = self._train_eval(batch)
         if need_update:
             self.reducer.start_step()
-            net.backprop(False, hook=self.reducer.hook, first=first)
+            net.ctx.sgd_fuse = self._sgd_fuse_target()
+            net.ctx.epoch = self.epoch_counter
+            try:
+                net.backprop(False, hook=self.reducer.hook, first=first)
+            finally:
+                net.ctx.sgd_fuse = None
             self.reducer.finish()
             self._check_grads()
             self._mark(ev, 2)
@@ -458,6 +466,19 @@ class NetTrainer:
             a.ensure_second_moment()
             a.m2.copy_(state["m2"])
         self.net.ctx.step_counter.copy_(state["step_counter"])
+
+    def _sgd_fuse_target(self):
+        """The arena updater when the fc weight steps may run inside the weight-gradient
+        GEMM (FullConnectLayer._fused_sgd): one GPU, SGD, one micro-batch per update, no
+        non-finite check (the gradient never reaches memory).  Under data parallelism the
+        gradients must be reduced before the step, so it stays separate."""
+        net, red = self.net, self.reducer
+        if not _FUSE_FC_SGD or net.device.type != "cuda" or self.update_period != 1 or self.check_nonfinite:
+            return None
+        upd = net.updater
+        if upd is None or upd.algo != "sgd" or red is None or red.active or red.handles_update:
+            return None
+        return upd
 
     def _graph_eligible(self) -> bool:
         net, red = self.net, self.reducer

@@ -621,6 +621,28 @@ def fc_backward_data(dy, w, dx, mask_relu=False):
     _gemm_bf16_out(A, Bo, DIRECT_MN, DIRECT_K, dx, nin, mask_relu=mask_relu)
 
 
+def fc_backward_weight_sgd(x, dy, w, m, wb, lr, wd, mom, clip) -> bool:
+    """The fc weight-gradient dy^T . x fused with the SGD step of those weights: the
+    epilogue applies m = mom*m - lr*(clip(g) + wd*w); w += m; wb = bf16(w) to the fp32
+    master w, momentum m and bf16 shadow wb ([nout][nin] slices of the arena) and the
+    gradient never goes to memory.  Same arithmetic as the fused optimizer, so the
+    result is bitwise the unfused one.  False when the LDS-DMA kernel does not cover the
+    shape (the caller then takes the unfused path)."""
+    if not (x.is_cuda and _glds_cfg["on"] and _use("fw")):
+        return False
+    Bn, nin = x.shape
+    nout = dy.shape[1]
+    A = _op(x, 0, nin, nin, Bn)
+    Bo = _op(dy, 0, nout, nout, Bn)
+    tile = _TUNE.get(f"fw|{nin}|{nout}|{Bn}", 1) if _glds_cfg["tile"] < 0 else _glds_cfg["tile"]
+    rc = native.kernels().cxn_gemm_glds_sgd(A, Bo, nin, 1.0, w.data_ptr(), m.data_ptr(), wb.data_ptr(), float(lr),
+                                            float(wd), float(mom), float(clip), tile, _stream())
+    if rc == -1:
+        return False
+    native.check(rc, "gemm_glds_sgd")
+    return True
+
+
 def fc_backward_weight(x, dy, dw, overwrite=False):
     """dw[nout][nin] += dy^T . x  (fp32 accumulate; overwrite=True stores instead)."""
     if not x.is_cuda:

@@ -111,6 +111,9 @@ class ArenaUpdater:
         self.algo = algo
         self.arena = arena
         self.entries = []  # (ParamSpec, UpdaterParam)
+        # arena offsets whose SGD step already ran this step inside the fc weight-gradient
+        # GEMM (ops.fc_backward_weight_sgd); update() skips them once, then clears the set
+        self.fused_offsets = set()
         self.beta1 = 0.1
         self.beta2 = 0.001
         for li, spec in segments:
@@ -147,6 +150,17 @@ class ArenaUpdater:
                 segs.append((spec.offset, spec.numel, p.learning_rate, p.wd, p.momentum, p.clip_gradient))
         return segs
 
+    def hyper(self, spec, epoch: int):
+        """(lr, wd, momentum, clip) of `spec` for this epoch's update (the same cached
+        schedule values update() uses)."""
+        if getattr(self, "_seg_epoch", None) != epoch:
+            self._segs = self.segments(epoch)
+            self._seg_epoch = epoch
+        for off, _, lr, wd, mom, clip in self._segs:
+            if off == spec.offset:
+                return lr, wd, mom, clip
+        raise KeyError(f"no updater segment at arena offset {spec.offset}")
+
     def update(self, epoch: int, ranges=None):
         """ranges: optional [start, end) arena ranges to update (sharded data
         parallelism updates only this rank's slice; the overlapped update calls this once
@@ -158,6 +172,9 @@ class ArenaUpdater:
             self._segs = self.segments(epoch)
             self._seg_epoch = epoch
         segs = self._segs
+        if self.fused_offsets:
+            segs = [sg for sg in segs if sg[0] not in self.fused_offsets]
+            self.fused_offsets = set()
         if ranges is not None:
             segs = _clip_segments(segs, ranges)
         # gradients are reset by the next cycle's first backprop (NeuralNet.backprop(first=True))
