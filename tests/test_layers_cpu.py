@@ -373,3 +373,22 @@ def test_pool_tie_all_matches_reference_unpool():
                             ref[0, ho * S + kh, wo * S + kw, c] += dy[0, ho, wo, c]
     assert torch.equal(dx, ref)
     assert dx[0, 0, 0, 0] == dy[0, 0, 0, 0] and dx[0, 0, 2, 0] == dy[0, 0, 0, 0] + dy[0, 0, 1, 0]
+
+
+@pytest.mark.parametrize("algo", ["sgd", "nag", "adam"])
+def test_clip_gradient_is_sgd_only(algo):
+    """Only the reference SGD updater clips (sgd_updater-inl.hpp:77-81); NAG and Adam ignore
+    clip_gradient (nag_updater-inl.hpp:66-72, adam_updater-inl.hpp:74-82)."""
+    from cxxnet_amd import ops
+    n = 64
+    g0 = torch.linspace(-3, 3, n)
+    runs = []
+    for clip in (0.0, 0.5):
+        w, g, m, m2 = torch.ones(n), g0.clone(), torch.zeros(n), torch.zeros(n)
+        ops.fused_update(algo, w, g, m, m2, None, [(0, n, 0.1, 0.0, 0.9, clip)])
+        runs.append(w)
+    if algo == "sgd":
+        assert not torch.equal(runs[0], runs[1])
+        assert torch.allclose(runs[1], 1 - 0.1 * g0.clamp(-0.5, 0.5))
+    else:
+        assert torch.equal(runs[0], runs[1])
