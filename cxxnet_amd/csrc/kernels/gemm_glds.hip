@@ -981,6 +981,7 @@ void launch_pp(const GOperand &A, const GOperand &B, const GEpi &E, int groups, 
     CXG_TP(30, 128, 256, 2, 4, 3, 0) CXG_TP(31, 128, 256, 2, 4, 3, 3) CXG_TP(33, 128, 256, 1, 4, 3, 3)    \
     CXG_TP(34, 256, 256, 2, 4, 2, 3) CXG_TP(35, 64, 256, 1, 4, 3, 0) CXG_TP(36, 128, 128, 2, 4, 3, 3)     \
     CXG_TP(37, 64, 128, 1, 4, 2, 3) CXG_TP(38, 128, 256, 2, 4, 2, 3) CXG_TP(39, 64, 256, 2, 4, 3, 3)      \
+    CXG_TP(70, 96, 256, 1, 4, 2, 3) CXG_TP(71, 96, 128, 1, 4, 2, 3) CXG_TP(72, 96, 128, 2, 2, 2, 0)       \
     default: return -1;                                                                                   \
   }
 #define CXG_MK_TILES  /* A MN-major (BM = 128), B K-major */                                              \

@@ -943,6 +943,66 @@ __global__ void colsum_bf16(const bf16_t *__restrict__ dy, float *__restrict__ p
   }
 }
 
+// Every deferred bias gradient of a backward pass in one launch (blockIdx.y = segment):
+// db_s[c] += sum_r dy_s[r][c], C_s % 8 == 0, per-block partials -> one atomic per channel.
+// A layer's backward only queues its (dy, db); NeuralNet.backprop flushes the queue once at
+// the end (dy buffers are not rewritten later in the pass), which replaces one or two small
+// launches per conv / fc layer -- GoogLeNet has 57 -- by one.
+constexpr int COLSUM_MAXSEG = 64;
+struct ColsumSeg {
+  const bf16_t *dy;
+  float *db;
+  long rows;
+  int C, rpb, nblk;
+};
+struct ColsumTable {
+  ColsumSeg s[COLSUM_MAXSEG];
+};
+__global__ void colsum_multi(ColsumTable tab) {
+  const ColsumSeg sg = tab.s[blockIdx.y];
+  if (static_cast<int>(blockIdx.x) >= sg.nblk) return;
+  const int CV = sg.C / 8;
+  const int t = threadIdx.x;
+  const long r0 = static_cast<long>(blockIdx.x) * sg.rpb;
+  const long r1 = min(sg.rows, r0 + sg.rpb);
+  __shared__ float red[NT][9];
+  for (int cb = 0; cb < CV; cb += 64) {
+    const int CB = min(CV - cb, 64);
+    const int RG = NT / CB;
+    const int cvl = t % CB, rg = t / CB;
+    const int cv = cb + cvl;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (rg < RG) {
+      constexpr int U = 4;
+      for (long r = r0 + rg; r < r1; r += RG * U) {
+        uint4 q[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long rr = r + static_cast<long>(u) * RG;
+          q[u] = rr < r1 ? *reinterpret_cast<const uint4 *>(sg.dy + rr * sg.C + cv * 8) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          float v[8];
+          unpack8(q[u], v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[e] += v[e];
+        }
+      }
+    }
+    __syncthreads();  // red is reused by the next column chunk
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[t][e] = (rg < RG) ? acc[e] : 0.f;
+    __syncthreads();
+    for (int q = t; q < CB * 8; q += NT) {
+      const int c = q / 8, e = q % 8;
+      float sum = 0.f;
+      for (int gq = 0; gq < RG; ++gq) sum += red[gq * CB + c][e];
+      atomicAdd(sg.db + (cb + c) * 8 + e, sum);
+    }
+  }
+}
+
 // Split-K finalisation: out[r][c] = epilogue(sum_s ws[s][r][c]) with optional bias[c],
 // relu, and mask_relu (keep where the OLD out value is > 0).  8 columns per thread.
 // out[i] += sum_s ws[s][i], slabs summed in slice order: the deterministic replacement for
@@ -1091,6 +1151,40 @@ __global__ void channel_copy8(const uint4 *__restrict__ src, int Cs8, int soff8,
       v = pack8(a);
     }
     *d = v;
+  }
+}
+
+// Channel concat of up to 4 NHWC inputs in ONE launch (every channel count a multiple of 8).
+// Forward: out[p][off_k + c] = in_k[p][c].  Backward (bwd = 1): in_k[p][c] = out[p][off_k + c],
+// masked by relu'(old in_k) for inputs produced by a fused conv+relu (mask bit k).
+struct ConcatArgs {
+  uint4 *in[4];
+  int c8[4];    // channels / 8 per input
+  int off8[4];  // channel offset / 8 in the output
+};
+__global__ void concat8(ConcatArgs a, int n, uint4 *__restrict__ out, int Ct8, uint32_t total8, int bwd, int mask) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total8; i += gridDim.x * blockDim.x) {
+    const uint32_t p = i / static_cast<uint32_t>(Ct8);
+    const int c = static_cast<int>(i - p * static_cast<uint32_t>(Ct8));
+    int k = 0;
+#pragma unroll
+    for (int q = 1; q < 4; ++q)
+      if (q < n && c >= a.off8[q]) k = q;
+    uint4 *src_in = a.in[k] + static_cast<size_t>(p) * a.c8[k] + (c - a.off8[k]);
+    if (!bwd) {
+      out[i] = *src_in;
+    } else {
+      uint4 v = out[i];
+      if ((mask >> k) & 1) {
+        float g[8], x[8];
+        unpack8(v, g);
+        unpack8(*src_in, x);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = x[e] > 0.f ? g[e] : 0.f;
+        v = pack8(g);
+      }
+      *src_in = v;
+    }
   }
 }
 
@@ -1469,6 +1563,29 @@ CXN_API int cxn_colsum(const void *dy, float *db, long rows, int C, float *ws, l
   partials_reduce<<<partials_grid(static_cast<int>(grid.x), C), NT, 0, S_>>>(ws, static_cast<int>(grid.x), C, db);
   RET;
 }
+// dys / dbs / rows / Cs: n deferred bias gradients (C % 8 == 0 each)
+CXN_API int cxn_colsum_multi(const void *const *dys, float *const *dbs, const long *rows, const int *Cs, int n,
+                             void *stream) {
+  for (int base = 0; base < n; base += COLSUM_MAXSEG) {
+    ColsumTable tab;
+    const int cnt = n - base < COLSUM_MAXSEG ? n - base : COLSUM_MAXSEG;
+    int maxb = 1;
+    for (int i = 0; i < cnt; ++i) {
+      const int j = base + i;
+      if (Cs[j] % 8) return -1;
+      // <= 256 blocks (adders per channel) per segment, >= 512 rows per block
+      long nb = cdiv(rows[j], 512L);
+      if (nb > 256) nb = 256;
+      if (nb < 1) nb = 1;
+      const int rpb = static_cast<int>(cdiv(rows[j], nb));
+      tab.s[i] = ColsumSeg{static_cast<const bf16_t *>(dys[j]), dbs[j], rows[j], Cs[j], rpb,
+                           static_cast<int>(cdiv(rows[j], static_cast<long>(rpb)))};
+      if (tab.s[i].nblk > maxb) maxb = tab.s[i].nblk;
+    }
+    colsum_multi<<<dim3(maxb, cnt), NT, 0, S_>>>(tab);
+  }
+  RET;
+}
 int cxn_deterministic = 0;
 CXN_API int cxn_set_deterministic(int on) {
   cxn_deterministic = on ? 1 : 0;
@@ -1512,6 +1629,26 @@ CXN_API int cxn_sum_bf16(const void *s0, const void *s1, const void *s2, const v
   const long n8 = n / 8;
   sum_bf16<<<nblocks(n8), NT, 0, S_>>>((const uint4 *)s0, (const uint4 *)s1, (const uint4 *)s2, (const uint4 *)s3, ns,
                                        (uint4 *)y, n8);
+  RET;
+}
+// ins[k] (NHWC, cs[k] channels, k < n <= 4) <-> out (Ct channels), npix pixels; bwd: out -> ins
+CXN_API int cxn_concat(void *const *ins, const int *cs, int n, void *out, int Ct, long npix, int bwd, int mask,
+                       void *stream) {
+  if (n < 1 || n > 4 || Ct % 8) return -1;
+  ConcatArgs a{};
+  int off = 0;
+  for (int k = 0; k < n; ++k) {
+    if (cs[k] % 8) return -1;
+    a.in[k] = static_cast<uint4 *>(ins[k]);
+    a.c8[k] = cs[k] / 8;
+    a.off8[k] = off / 8;
+    off += cs[k];
+  }
+  if (off != Ct) return -1;
+  const long total8 = npix * (Ct / 8);
+  if (total8 >= (1L << 32)) return -1;
+  concat8<<<nblocks(total8), NT, 0, S_>>>(a, n, static_cast<uint4 *>(out), Ct / 8, static_cast<uint32_t>(total8), bwd,
+                                          mask);
   RET;
 }
 CXN_API int cxn_channel_copy(const void *src, int Cs, int soff, void *dst, int Cd, int doff, int Cc, long npix,

@@ -100,11 +100,22 @@ class LayerContext:
         # weight steps are fused into their weight-gradient GEMMs, and the step's epoch
         self.sgd_fuse = None
         self.epoch = 0
+        # bias gradients queued during a backward pass (NeuralNet.backprop flushes them in one
+        # launch); None = compute each one immediately
+        self.deferred_bias = None
         self.gen = torch.Generator(device="cpu")
         self.gen.manual_seed(seed)
         self.label_fields: Dict[str, torch.Tensor] = {}
         self.label_name_map: Dict[str, int] = {"label": 0}
         self.step = 0  # forward counter, feeds counter-based RNG (dropout)
+
+    def bias_grad(self, dy2d, db):
+        """db += column sums of dy2d, now or (deferred) at the end of the backward pass."""
+        if self.deferred_bias is not None and dy2d.is_cuda:
+            self.deferred_bias.append((dy2d, db))
+            return
+        from .. import ops
+        ops.bias_grad(dy2d, db)
 
 
 class Layer:

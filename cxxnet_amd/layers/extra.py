@@ -137,6 +137,8 @@ class ConcatLayer(Layer):
 
     def forward(self, is_train, nodes_in, nodes_out):
         if self.dim == 1:
+            if ops.concat_channels([n.data for n in nodes_in], nodes_out[0].data):
+                return
             for src, dst, off, c in self._pieces(nodes_in, nodes_out):
                 ops.channel_copy(src, 0, dst, off, c)
         else:
@@ -153,6 +155,9 @@ class ConcatLayer(Layer):
         if not prop_grad:
             return
         if self.dim == 1:
+            if ops.concat_channels([n.gdst for n in nodes_in], nodes_out[0].data, backward=True,
+                                   mask=self.grad_mask_inputs):
+                return
             for k, (src, dst, off, c) in enumerate(self._pieces(nodes_in, nodes_out)):
                 ops.channel_copy(dst, off, nodes_in[k].gdst, 0, c, mask_relu=k in self.grad_mask_inputs)
         else:

@@ -125,7 +125,7 @@ class FullConnectLayer(Layer):
         overwrite = getattr(self.ctx, "grad_overwrite", False) and self.w.overwrite
         if not self._gathering() and self._fused_sgd(x, dy, prop_grad, nodes_in):
             if self.b is not None:
-                ops.bias_grad(dy, self.b.g)
+                self.ctx.bias_grad(dy, self.b.g)
             return
         if self._gathering():
             dy_all = _all_gather_rows(dy, nodes_out[0].shape[0])
@@ -135,7 +135,7 @@ class FullConnectLayer(Layer):
         else:
             ops.fc_backward_weight(x, dy, self.w.g, overwrite=overwrite)
         if self.b is not None:
-            ops.bias_grad(dy, self.b.g)
+            self.ctx.bias_grad(dy, self.b.g)
         if prop_grad:
             ops.fc_backward_data(dy, self.w.wb, nodes_in[0].gmat(), mask_relu=self.grad_mask_relu)
 
@@ -294,7 +294,7 @@ class ConvolutionLayer(Layer):
         xw, geo = self._padded(x, False)
         ops.conv_backward_weight(xw, dy, self.w.g, geo)
         if self.b is not None:
-            ops.bias_grad(dy.view(-1, dy.shape[-1]), self.b.g)
+            self.ctx.bias_grad(dy.view(-1, dy.shape[-1]), self.b.g)
         if prop_grad:
             if self._wt is None or self._wt.shape != self.w.wb.shape:
                 self._wt = torch.empty_like(self.w.wb)

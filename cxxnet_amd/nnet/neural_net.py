@@ -353,6 +353,12 @@ class NeuralNet:
         self.ctx.grad_overwrite = bool(first)
         if first:
             self.arena.zero_accumulated_grads()
+        # without a per-layer hook (data-parallel buckets need every gradient of a layer when
+        # it returns) the bias gradients are queued and summed in ONE launch at the end: the
+        # dy buffers they read are not rewritten later in the pass
+        from ..ops.gemm import deterministic
+        defer = hook is None and self.ctx.is_gpu and not deterministic()
+        self.ctx.deferred_bias = [] if defer else None
         with _BatchView(self):
             for i in range(len(self.connections) - 1, -1, -1):
                 conn = self.connections[i]
@@ -360,6 +366,10 @@ class NeuralNet:
                     conn.layer.backprop(i != 0 or prop_to_input, conn.nodes_in, conn.nodes_out)
                 if hook is not None:
                     hook(i)
+            if defer:
+                pending, self.ctx.deferred_bias = self.ctx.deferred_bias, None
+                from .. import ops
+                ops.bias_grad_multi(pending)
 
     def update(self, epoch: int, ranges=None):
         self.updater.update(epoch, ranges)

@@ -356,8 +356,10 @@ class NetTrainer:
             self.reducer.start_step()
             net.ctx.sgd_fuse = self._sgd_fuse_target()
             net.ctx.epoch = self.epoch_counter
+            red = self.reducer
+            hook = red.hook if (red.active or red.update_fn is not None) else None
             try:
-                net.backprop(False, hook=self.reducer.hook, first=first)
+                net.backprop(False, hook=hook, first=first)
             finally:
                 net.ctx.sgd_fuse = None
             self.reducer.finish()

@@ -117,7 +117,9 @@ GLDS_TILES = {0: (128, 256), 1: (128, 128), 2: (128, 128), 4: (192, 256), 5: (64
               # flight across every barrier
               50: (256, 256), 51: (128, 256),
               # ping-pong 8-wave pipeline (gemm_pp): the two wave groups one barrier apart
-              60: (256, 256), 61: (256, 256)}
+              60: (256, 256), 61: (256, 256),
+              # 96-row tiles (K-major A): 96-output-channel convs (AlexNet conv1) without idle rows
+              70: (96, 256), 71: (96, 128), 72: (96, 128)}
 # operand loaders of gemm_glds.hip
 GL_K, GL_KG, GL_MN, GL_MNG, GL_KR = 0, 1, 2, 3, 4  # K_DIRECT, K_GATHER, MN_DIRECT, MN_GATHER, K_ROWGATHER
 EPI_F32_ACC_G, EPI_F32_ATOMIC_G = 2, 3

@@ -5,6 +5,7 @@ All activations are NHWC (see ops/gemm.py for the layout contract).
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import torch
@@ -399,6 +400,25 @@ def bias_grad(dy2d, db):
                  "colsum")
 
 
+def bias_grad_multi(items):
+    """Every (dy2d, db) of `items`: db[C] += sum over rows of dy2d, in one launch for the
+    GPU tensors with C % 8 == 0 (the rest one by one)."""
+    fast = [(d, b) for d, b in items if d.is_cuda and d.shape[1] % 8 == 0 and d.is_contiguous()]
+    for d, b in items:
+        if not (d.is_cuda and d.shape[1] % 8 == 0 and d.is_contiguous()):
+            bias_grad(d, b)
+    if not fast:
+        return
+    n = len(fast)
+    dys = (ctypes.c_void_p * n)(*[d.data_ptr() for d, _ in fast])
+    dbs = (ctypes.c_void_p * n)(*[b.data_ptr() for _, b in fast])
+    rows = (ctypes.c_long * n)(*[d.shape[0] for d, _ in fast])
+    cs = (ctypes.c_int * n)(*[d.shape[1] for d, _ in fast])
+    native.check(_k().cxn_colsum_multi(ctypes.cast(dys, ctypes.c_void_p), ctypes.cast(dbs, ctypes.c_void_p),
+                                       ctypes.cast(rows, ctypes.c_void_p), ctypes.cast(cs, ctypes.c_void_p), n,
+                                       _stream()), "colsum_multi")
+
+
 def cast_to_bf16(src_f32, dst_bf16):
     if not src_f32.is_cuda:
         dst_bf16.copy_(src_f32)
@@ -450,6 +470,29 @@ def sum_into(y, srcs):
         ptr = [t.data_ptr() for t in part] + [None] * (4 - len(part))
         native.check(_k().cxn_sum_bf16(*ptr, len(part), y.data_ptr(), y.numel(), _stream()), "sum")
         first = y
+
+
+def concat_channels(ins, out, backward=False, mask=()):
+    """NHWC channel concat of `ins` into `out` (forward) or the gradient slices of `out` back
+    into `ins` (backward; relu' for the input indices in `mask`), one launch on the GPU.
+    Returns False when the kernel does not cover the shapes (the caller copies per input)."""
+    if not out.is_cuda or len(ins) > 4:
+        return False
+    n = len(ins)
+    Ct = out.shape[-1]
+    npix = out.numel() // Ct
+    if any(t.numel() // t.shape[-1] != npix or not t.is_contiguous() or t.data_ptr() % 16 for t in ins) or \
+            not out.is_contiguous() or out.data_ptr() % 16:
+        return False
+    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in ins])
+    cs = (ctypes.c_int * n)(*[t.shape[-1] for t in ins])
+    m = sum(1 << k for k in mask)
+    rc = _k().cxn_concat(ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(cs, ctypes.c_void_p), n, out.data_ptr(), Ct,
+                         npix, int(bool(backward)), m, _stream())
+    if rc == -1:
+        return False
+    native.check(rc, "concat")
+    return True
 
 
 def channel_copy(src, soff, dst, doff, cc, accumulate=False, mask_relu=False):

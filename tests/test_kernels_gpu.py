@@ -435,3 +435,43 @@ def test_pool_rows_even_sizes_and_relu_state(mode, k, s, H, fused_relu):
     torch.cuda.synchronize()
     assert relerr(y, y_ref) < 1e-2
     assert relerr(dx, dx_ref) < 2e-2
+
+
+def test_bias_grad_multi_matches_single():
+    """The deferred one-launch bias gradients (colsum_multi): conv-like (many rows, few
+    channels), fc-like (few rows, 4096 channels: several 512-channel chunks per block) and a
+    ragged C (falls back to the scalar kernel)."""
+    shapes = [(200704, 64), (256, 4096), (43264, 384), (1000, 20)]
+    items, refs = [], []
+    for k, (r, c) in enumerate(shapes):
+        dy = rnd(r, c, seed=60 + k).to(DEV, torch.bfloat16)
+        db = torch.full((c,), 0.25, device=DEV)
+        items.append((dy, db))
+        refs.append(0.25 + dy.float().sum(0))
+    ops.bias_grad_multi(items)
+    torch.cuda.synchronize()
+    for (_, db), ref in zip(items, refs):
+        assert relerr(db, ref) < 1e-3
+
+
+def test_concat_channels_one_launch():
+    """ch_concat forward gather and backward scatter (relu' on the masked inputs) in one
+    launch, against per-input slicing."""
+    shapes = [64, 128, 32, 24]
+    ins = [rnd(3, 7, 5, c, seed=70 + k).to(DEV, torch.bfloat16) for k, c in enumerate(shapes)]
+    ins[1] = ins[1].clamp_min(0)  # relu(z) of a fused producer
+    out = torch.empty(3, 7, 5, sum(shapes), dtype=torch.bfloat16, device=DEV)
+    assert ops.concat_channels(ins, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, torch.cat(ins, -1))
+    g = rnd(3, 7, 5, sum(shapes), seed=80).to(DEV, torch.bfloat16)
+    acts = [t.clone() for t in ins]
+    assert ops.concat_channels(ins, g, backward=True, mask={1})
+    torch.cuda.synchronize()
+    off = 0
+    for k, c in enumerate(shapes):
+        ref = g[..., off:off + c]
+        if k == 1:
+            ref = torch.where(acts[1] > 0, ref, torch.zeros_like(ref))
+        assert torch.equal(ins[k], ref), k
+        off += c
