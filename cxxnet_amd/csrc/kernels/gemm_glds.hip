@@ -102,6 +102,20 @@ __device__ __forceinline__ void static_for(F &&f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
+// Lanes of ONE wave hand data to each other through LDS in the epilogues (stage the fp32 tile,
+// then read whole rows).  In the per-lane memory model that is a race unless fenced: when some
+// lanes sit out the row loop (WM = 48 / 96: 60 of 64 lanes busy) hipcc hoisted the idle lanes'
+// next staging stores above the other lanes' reads (96-row tiles: rows 12-15 x 12-15 of every
+// 16 x 16 block wrong).  Fence + wave barrier pin the order; emitted only for those tile
+// widths so the kernels of the shipped table keep their code.
+template <bool ON>
+__device__ __forceinline__ void wave_lds_handoff() {
+  if constexpr (ON) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 __device__ __forceinline__ void block_barrier() {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
@@ -422,6 +436,8 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
     for (int m = 0; m < MR; ++m)
       *reinterpret_cast<f32x4 *>(ep + (lane & 15) * (WM + 4) + m * 16 + (lane >> 4) * 4) = acc[m][n];
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    constexpr bool kPartialLanes = (64 / (WM / 8)) * (WM / 8) < 64 || (64 / (WM / 4)) * (WM / 4) < 64;
+    wave_lds_handoff<kPartialLanes>();
     if constexpr (EPI == EPI_BF16) {
       bf16_t *out = reinterpret_cast<bf16_t *>(E.out) + g * E.gstride;
       constexpr int LPR = WM / 8;    // lanes per output row (8 bf16 per lane)
@@ -521,6 +537,7 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
       }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
+    wave_lds_handoff<kPartialLanes>();
   }
 }
 
@@ -966,9 +983,10 @@ void launch_pp(const GOperand &A, const GOperand &B, const GEpi &E, int groups, 
 // 8 waves, two per SIMD (half the DMA bytes per MFMA of a 128x128 tile):
 //  20: 128x512 (1x8) 2     21: 256x256 (2x4) 2     23: 128x128 (2x4) 3     25: 64x512 (1x8) 2
 // (as plain 2-stage loops they tie the 4-wave tiles on AlexNet shapes: profiles/r15_glds_8wave.jsonl)
-// 96-row tiles (9: 96x128, 26: 96x64, 27: 96x256, 2x2 waves) were tried for 96-channel convs and
-// withdrawn: they ran 8-18% faster on conv1 but their outputs were wrong (max rel err 0.86 on every
-// shape, profiles/r16_t96_tiles.jsonl), so no table or candidate list names them.
+// 96-row tiles (70: 96x256 1x4, 71: 96x128 1x4, 72: 96x128 2x2) and the 160-row / 96-column
+// probes 73-75: the round-1 96-row tiles gave wrong outputs (profiles/r16_t96_tiles.jsonl) because
+// the epilogue's intra-wave LDS hand-off was unfenced (wave_lds_handoff); fixed, they are correct
+// and 72 ties the 128-row tile on AlexNet conv1 (the row gather, not the idle MFMA rows, bounds it).
 #define CXG_T(ID, BM, BN, WGM, WGN, ST) \
   case ID: launch<BM, BN, WGM, WGN, ST, AM, BMo, EP>(A, B, E, groups, ksplit, s); return 0;
 #define CXG_TP(ID, BM, BN, WGM, WGN, ST, PIPE) \
@@ -982,6 +1000,7 @@ void launch_pp(const GOperand &A, const GOperand &B, const GEpi &E, int groups, 
     CXG_TP(34, 256, 256, 2, 4, 2, 3) CXG_TP(35, 64, 256, 1, 4, 3, 0) CXG_TP(36, 128, 128, 2, 4, 3, 3)     \
     CXG_TP(37, 64, 128, 1, 4, 2, 3) CXG_TP(38, 128, 256, 2, 4, 2, 3) CXG_TP(39, 64, 256, 2, 4, 3, 3)      \
     CXG_TP(70, 96, 256, 1, 4, 2, 3) CXG_TP(71, 96, 128, 1, 4, 2, 3) CXG_TP(72, 96, 128, 2, 2, 2, 0)       \
+    CXG_TP(73, 160, 128, 1, 4, 2, 0) CXG_TP(74, 128, 96, 2, 2, 2, 0) CXG_TP(75, 64, 96, 2, 2, 2, 0)       \
     default: return -1;                                                                                   \
   }
 #define CXG_MK_TILES  /* A MN-major (BM = 128), B K-major */                                              \

@@ -119,7 +119,7 @@ GLDS_TILES = {0: (128, 256), 1: (128, 128), 2: (128, 128), 4: (192, 256), 5: (64
               # ping-pong 8-wave pipeline (gemm_pp): the two wave groups one barrier apart
               60: (256, 256), 61: (256, 256),
               # 96-row tiles (K-major A): 96-output-channel convs (AlexNet conv1) without idle rows
-              70: (96, 256), 71: (96, 128), 72: (96, 128)}
+              70: (96, 256), 71: (96, 128), 72: (96, 128), 73: (160, 128), 74: (128, 96), 75: (64, 96)}
 # operand loaders of gemm_glds.hip
 GL_K, GL_KG, GL_MN, GL_MNG, GL_KR = 0, 1, 2, 3, 4  # K_DIRECT, K_GATHER, MN_DIRECT, MN_GATHER, K_ROWGATHER
 EPI_F32_ACC_G, EPI_F32_ATOMIC_G = 2, 3
@@ -138,7 +138,7 @@ _glds_cfg = {"on": os.environ.get("CXXNET_GEMM_GLDS", "1") != "0",
 # AlexNet shape (profiles/r14_glds_tiles.jsonl); 2 and 0 cover wide-i GEMMs (fc); the 8-wave
 # 128x256 / 64x256 tiles and the pipelined variants (30-41) win conv2/conv3 forward, fc6 forward
 # and several VGG shapes (profiles/r2_sweep_tiles.jsonl).
-GLDS_CANDS = (1, 7, 10, 15, 2, 0, 13, 17, 21, 25, 30, 31, 34, 37, 38, 39, 40, 41, 50, 51)
+GLDS_CANDS = (1, 7, 10, 15, 2, 0, 13, 17, 21, 25, 30, 31, 34, 37, 38, 39, 40, 41, 50, 51, 72)
 # Pseudo-tile: the register-staged kernel (gemm_mfma.hip) with its heuristic tile.  A candidate
 # for conv forward / data-grad / weight-grad, where it still wins some shapes (conv2 forward on
 # AlexNet timed alone: 172 vs 186 us, profiles/r15_glds_8wave.jsonl "old_us").
@@ -222,7 +222,8 @@ def _tuned_tile(key, run, out, default, extra=(), tune=True):
     A candidate is eligible only if its output agrees with the heuristic tile's output on
     the same operands (norm-relative difference < 2e-2; bf16 rounding and split-K order
     differ by ~1e-3): a tile that computes the wrong thing fast can never win on time
-    (commit cecf60b withdrew 96-row tiles that were timing-eligible at 0.8 relative error).
+    (commit cecf60b withdrew 96-row tiles that were timing-eligible at 0.8 relative error; the cause,
+    an unfenced intra-wave LDS hand-off in the epilogue, is fixed in gemm_glds.hip wave_lds_handoff).
     Scratch outputs start from the live output's contents, so masked (mask_relu) and
     accumulating epilogues see the same inputs for every candidate."""
     if _glds_cfg["tile"] >= 0:
