@@ -430,6 +430,15 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
   const int ibase = i0 + wi_ * WM, jbase = j0 + wj_ * WN;
   float *ep = reinterpret_cast<float *>(smem) + wave * 16 * (WM + 4);
   const float *bias = E.bias ? E.bias + g * E.bias_gstride : nullptr;
+  // bf16 epilogue: a lane always serves the same 8 output columns (i), so their bias values
+  // are loaded once here instead of once per output row
+  constexpr int LPR_B = WM / 8;  // lanes per output row (8 bf16 per lane)
+  const int il_b = (lane % LPR_B) * 8;
+  float bias8[8];
+  if constexpr (EPI == EPI_BF16) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bias8[e] = (bias && ibase + il_b + e < Mi) ? bias[ibase + il_b + e] : 0.f;
+  }
 #pragma unroll
   for (int n = 0; n < NR; ++n) {
 #pragma unroll
@@ -440,9 +449,9 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
     wave_lds_handoff<kPartialLanes>();
     if constexpr (EPI == EPI_BF16) {
       bf16_t *out = reinterpret_cast<bf16_t *>(E.out) + g * E.gstride;
-      constexpr int LPR = WM / 8;    // lanes per output row (8 bf16 per lane)
+      constexpr int LPR = LPR_B;
       constexpr int RPI = 64 / LPR;  // rows per pass
-      const int il = (lane % LPR) * 8;
+      const int il = il_b;
       const int i = ibase + il;
       const bool vec_store = ((E.ldc & 7) == 0) && (i + 8 <= Mi);
 #pragma unroll
@@ -454,7 +463,7 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
           float f[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            f[e] = f[e] * E.alpha + ((bias && i + e < Mi) ? bias[i + e] : 0.f);
+            f[e] = f[e] * E.alpha + bias8[e];
             if (E.relu) f[e] = fmaxf(f[e], 0.f);
           }
           bf16_t *dst = out + static_cast<long>(j) * E.ldc + i;
