@@ -15,7 +15,7 @@ CASES = {"conv1": (4, 227, 96, 11, 4, 0, 1), "conv2": (96, 27, 256, 5, 1, 2, 2),
 
 
 FCS = {"fc6": (9216, 4096), "fc7": (4096, 4096), "fc8": (4096, 1000), "sq8192": (8192, 8192), "sq4096": (4096, 4096)}
-VGG = {"c1_2": (64, 224, 64), "c2_2": (128, 112, 128), "c3_2": (256, 56, 256), "c4_2": (512, 28, 512),
+VGG = {"c1_2": (64, 224, 64), "c2_1": (64, 112, 128), "c2_2": (128, 112, 128), "c3_2": (256, 56, 256), "c4_2": (512, 28, 512),
        "c5": (512, 14, 512)}
 
 

@@ -316,12 +316,13 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
   constexpr int SMEM = STAGES * STAGE_BYTES > EPI_BYTES ? STAGES * STAGE_BYTES : EPI_BYTES;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
-  const int g = blockIdx.z;
   const uint32_t ntile = static_cast<uint32_t>(tiles_i) * tiles_j;
-  const uint32_t tile = xcd_remap(blockIdx.x, ntile);
+  const GemmBlock wb = gemm_block(ntile);
+  const int g = wb.g;
+  const uint32_t tile = wb.tile;
   const int ti = tile % tiles_i, tj = tile / tiles_i;  // i fastest: neighbours share the B panel
   const int i0 = ti * BM, j0 = tj * BN;
-  const int kt_beg = blockIdx.y * ksplit_tiles;
+  const int kt_beg = wb.slice * ksplit_tiles;
   const int kt_end = min(kt_beg + ksplit_tiles, ktiles_total);
   if (kt_beg >= kt_end) return;
   const int nt = kt_end - kt_beg;
@@ -499,7 +500,7 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
       }
     } else {
       float *out = reinterpret_cast<float *>(E.out) + g * E.gstride;
-      if constexpr (EPI == EPI_F32) out += blockIdx.y * E.kstride;
+      if constexpr (EPI == EPI_F32) out += wb.slice * E.kstride;
       constexpr int LPR = WM / 4;    // lanes per row, 4 floats per lane (16-byte accesses)
       constexpr int RPI = 64 / LPR;
       const int il = (lane % LPR) * 4;
@@ -666,7 +667,7 @@ __device__ __forceinline__ bf16x8 seg_frag(const char *tile, int base, int lane)
 // fp32 tile in LDS, then writes contiguous row segments: bf16 (+bias, relu, relu'-mask of the old
 // value) or an fp32 split-K slab.
 template <int EPI, int MR, int NR, int WM>
-__device__ __forceinline__ void seg_epilogue(f32x4 (&acc)[MR][NR], char *smem, const GEpi &E, int g, int Mi,
+__device__ __forceinline__ void seg_epilogue(f32x4 (&acc)[MR][NR], char *smem, const GEpi &E, int g, int slice, int Mi,
                                              int Nj, int ibase, int jbase, int wave, int lane) {
   float *ep = reinterpret_cast<float *>(smem) + wave * 16 * (WM + 4);
   const float *bias = E.bias ? E.bias + g * E.bias_gstride : nullptr;
@@ -713,7 +714,7 @@ __device__ __forceinline__ void seg_epilogue(f32x4 (&acc)[MR][NR], char *smem, c
         }
       }
     } else {  // EPI_F32: split-K slab (fc forward)
-      float *out = reinterpret_cast<float *>(E.out) + g * E.gstride + blockIdx.y * E.kstride;
+      float *out = reinterpret_cast<float *>(E.out) + g * E.gstride + slice * E.kstride;
       constexpr int LPR = WM / 4;
       constexpr int RPI = 64 / LPR;
       const int il = (lane % LPR) * 4;
@@ -753,12 +754,13 @@ gemm_seg(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_ti
   constexpr int SMEM = 4 * SLOT > EPI_BYTES ? 4 * SLOT : EPI_BYTES;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
-  const int g = blockIdx.z;
   const uint32_t ntile = static_cast<uint32_t>(tiles_i) * tiles_j;
-  const uint32_t tile = xcd_remap(blockIdx.x, ntile);
+  const GemmBlock wb = gemm_block(ntile);
+  const int g = wb.g;
+  const uint32_t tile = wb.tile;
   const int ti = tile % tiles_i, tj = tile / tiles_i;
   const int i0 = ti * BM, j0 = tj * BN;
-  const int kt_beg = blockIdx.y * ksplit_tiles;
+  const int kt_beg = wb.slice * ksplit_tiles;
   const int kt_end = min(kt_beg + ksplit_tiles, ktiles_total);
   if (kt_beg >= kt_end) return;
   const int nseg = 2 * (kt_end - kt_beg);
@@ -825,7 +827,7 @@ gemm_seg(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_ti
   wait_vmcnt<0>();
   __syncthreads();  // slots are reused by the epilogue
 
-  seg_epilogue<EPI, MR, NR, WM>(acc, smem, E, g, A.rows, B.rows, i0 + wi_ * WM, j0 + wj_ * WN, wave, lane);
+  seg_epilogue<EPI, MR, NR, WM>(acc, smem, E, g, wb.slice, A.rows, B.rows, i0 + wi_ * WM, j0 + wj_ * WN, wave, lane);
 }
 
 template <int BM, int BN, int AMODE, int BMODE, int EPI>
@@ -876,12 +878,13 @@ gemm_pp(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
   constexpr int VM = 2 * (2 * NS - 5);
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
-  const int g = blockIdx.z;
   const uint32_t ntile = static_cast<uint32_t>(tiles_i) * tiles_j;
-  const uint32_t tile = xcd_remap(blockIdx.x, ntile);
+  const GemmBlock wb = gemm_block(ntile);
+  const int g = wb.g;
+  const uint32_t tile = wb.tile;
   const int ti = tile % tiles_i, tj = tile / tiles_i;
   const int i0 = ti * BM, j0 = tj * BN;
-  const int kt_beg = blockIdx.y * ksplit_tiles;
+  const int kt_beg = wb.slice * ksplit_tiles;
   const int kt_end = min(kt_beg + ksplit_tiles, ktiles_total);
   if (kt_beg >= kt_end) return;
   const int nseg = 2 * (kt_end - kt_beg);
@@ -972,7 +975,7 @@ gemm_pp(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
   wait_vmcnt<0>();
   __syncthreads();  // slots are reused by the epilogue
 
-  seg_epilogue<EPI, MR, NR, WM>(acc, smem, E, g, A.rows, B.rows, i0 + wr * WM, j0 + wc * WN, wave, lane);
+  seg_epilogue<EPI, MR, NR, WM>(acc, smem, E, g, wb.slice, A.rows, B.rows, i0 + wr * WM, j0 + wc * WN, wave, lane);
 }
 
 template <int AMODE, int BMODE, int EPI, int NS>

@@ -303,13 +303,14 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
   bf16_t *const As0 = reinterpret_cast<bf16_t *>(smem);
   bf16_t *const Bs0 = As0 + 2 * A_ELEMS;
 
-  const int g = blockIdx.z;
   const uint32_t nt = static_cast<uint32_t>(tiles_i) * tiles_j;
-  const uint32_t tile = xcd_remap(blockIdx.x, nt);
+  const GemmBlock wb = gemm_block(nt);
+  const int g = wb.g;
+  const uint32_t tile = wb.tile;
   // i-tiles fastest within a j panel: neighbouring blocks share the B (j) panel.
   const int ti = tile % tiles_i, tj = tile / tiles_i;
   const int i0 = ti * BM, j0 = tj * BN;
-  const int kt_beg = blockIdx.y * ksplit_tiles;
+  const int kt_beg = wb.slice * ksplit_tiles;
   const int kt_end = min(kt_beg + ksplit_tiles, ktiles_total);
   if (kt_beg >= kt_end) return;
 
@@ -494,7 +495,7 @@ gemm_kernel(Operand A, Operand B, Epilogue E, int tiles_i, int tiles_j, int kspl
     }
   } else {
     float *out = reinterpret_cast<float *>(E.out) + g * E.gstride;
-    if constexpr (EPI == EPI_F32) out += blockIdx.y * E.kstride;
+    if constexpr (EPI == EPI_F32) out += wb.slice * E.kstride;
     constexpr int LPR = WM;            // one fp32 per lane
     constexpr int RPI = 64 / LPR;
     const int il = lane % LPR;

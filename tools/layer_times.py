@@ -29,6 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--md", default=None)
+    ap.add_argument("--kernels", default=None, help="also write a per-layer kernel breakdown here")
     a = ap.parse_args()
     marks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Function"], r["Thread_Id"])
              for r in _rows(a.dir, "marker_api_trace.csv")]
@@ -39,6 +40,7 @@ def main():
         launch[r["Correlation_Id"]] = (int(r["Start_Timestamp"]), r["Thread_Id"])
     per = defaultdict(float)
     cnt = defaultdict(int)
+    kern = defaultdict(lambda: [0.0, 0])
     for k in _rows(a.dir, "kernel_trace.csv"):
         dur = (int(k["End_Timestamp"]) - int(k["Start_Timestamp"])) / 1e3  # us
         name = "other"
@@ -53,6 +55,9 @@ def main():
                 j -= 1
         per[name] += dur
         cnt[name] += 1
+        kk = kern[(name, k["Kernel_Name"][:90], k.get("Grid_Size_X", ""), k.get("Grid_Size_Y", ""))]
+        kk[0] += dur
+        kk[1] += 1
     total = sum(per.values())
     lines = [f"total kernel time {total / 1e3:.3f} ms", "", "| layer range | kernels | total us | share |",
              "|---|---|---|---|"]
@@ -63,6 +68,15 @@ def main():
     if a.md:
         with open(a.md, "w") as f:
             f.write(text + "\n")
+    if a.kernels:
+        rows = ["| layer range | kernel | grid | calls | total us | mean us |", "|---|---|---|---|---|---|"]
+        order = sorted(per, key=lambda n: -per[n])
+        for name in order:
+            ks = sorted(((v, key) for key, v in kern.items() if key[0] == name), key=lambda t: -t[0][0])
+            for (us, c), key in ks:
+                rows.append(f"| `{name}` | `{key[1]}` | {key[2]}x{key[3]} | {c} | {us:.1f} | {us / c:.1f} |")
+        with open(a.kernels, "w") as f:
+            f.write("\n".join(rows) + "\n")
 
 
 if __name__ == "__main__":
