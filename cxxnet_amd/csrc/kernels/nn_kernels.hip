@@ -957,13 +957,21 @@ struct ColsumSeg {
 };
 struct ColsumTable {
   ColsumSeg s[COLSUM_MAXSEG];
+  int b0[COLSUM_MAXSEG];  // first block of each segment on the flat grid
+  int n;
 };
 __global__ void colsum_multi(ColsumTable tab) {
-  const ColsumSeg sg = tab.s[blockIdx.y];
-  if (static_cast<int>(blockIdx.x) >= sg.nblk) return;
+  // flat grid, blocks split over segments by size (a 2-D grid of max-blocks x segments would
+  // launch tens of thousands of idle blocks for GoogLeNet's 57 segments)
+  const int bx = blockIdx.x;
+  int si = 0;
+  for (int i = 1; i < tab.n; ++i)
+    if (tab.b0[i] <= bx) si = i;
+  const ColsumSeg sg = tab.s[si];
+  const int blk = bx - tab.b0[si];
   const int CV = sg.C / 8;
   const int t = threadIdx.x;
-  const long r0 = static_cast<long>(blockIdx.x) * sg.rpb;
+  const long r0 = static_cast<long>(blk) * sg.rpb;
   const long r1 = min(sg.rows, r0 + sg.rpb);
   __shared__ float red[NT][9];
   for (int cb = 0; cb < CV; cb += 64) {
@@ -973,14 +981,15 @@ __global__ void colsum_multi(ColsumTable tab) {
     const int cv = cb + cvl;
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (rg < RG) {
-      constexpr int U = 4;
-      for (long r = r0 + rg; r < r1; r += RG * U) {
+      // 8 rows in flight per thread; whole groups of 8 without bounds checks
+      constexpr int U = 8;
+      const bf16_t *p = sg.dy + (r0 + rg) * sg.C + cv * 8;
+      const long step = static_cast<long>(RG) * sg.C;
+      long r = r0 + rg;
+      for (; r + (U - 1) * RG < r1; r += RG * U, p += U * step) {
         uint4 q[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const long rr = r + static_cast<long>(u) * RG;
-          q[u] = rr < r1 ? *reinterpret_cast<const uint4 *>(sg.dy + rr * sg.C + cv * 8) : make_uint4(0, 0, 0, 0);
-        }
+        for (int u = 0; u < U; ++u) q[u] = *reinterpret_cast<const uint4 *>(p + u * step);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           float v[8];
@@ -988,6 +997,12 @@ __global__ void colsum_multi(ColsumTable tab) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) acc[e] += v[e];
         }
+      }
+      for (; r < r1; r += RG, p += step) {
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4 *>(p), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += v[e];
       }
     }
     __syncthreads();  // red is reused by the next column chunk
@@ -1569,20 +1584,23 @@ CXN_API int cxn_colsum_multi(const void *const *dys, float *const *dbs, const lo
   for (int base = 0; base < n; base += COLSUM_MAXSEG) {
     ColsumTable tab;
     const int cnt = n - base < COLSUM_MAXSEG ? n - base : COLSUM_MAXSEG;
-    int maxb = 1;
+    int nblk = 0;
+    tab.n = cnt;
     for (int i = 0; i < cnt; ++i) {
       const int j = base + i;
       if (Cs[j] % 8) return -1;
-      // <= 256 blocks (adders per channel) per segment, >= 512 rows per block
-      long nb = cdiv(rows[j], 512L);
-      if (nb > 256) nb = 256;
+      // <= 1024 blocks (adders per channel) per segment, >= 256 rows per block: the largest
+      // segment (AlexNet conv1: 774k rows) needs ~4 blocks per CU to keep HBM busy
+      long nb = cdiv(rows[j], 256L);
+      if (nb > 1024) nb = 1024;
       if (nb < 1) nb = 1;
       const int rpb = static_cast<int>(cdiv(rows[j], nb));
       tab.s[i] = ColsumSeg{static_cast<const bf16_t *>(dys[j]), dbs[j], rows[j], Cs[j], rpb,
                            static_cast<int>(cdiv(rows[j], static_cast<long>(rpb)))};
-      if (tab.s[i].nblk > maxb) maxb = tab.s[i].nblk;
+      tab.b0[i] = nblk;
+      nblk += tab.s[i].nblk;
     }
-    colsum_multi<<<dim3(maxb, cnt), NT, 0, S_>>>(tab);
+    colsum_multi<<<nblk, NT, 0, S_>>>(tab);
   }
   RET;
 }
