@@ -176,6 +176,38 @@ __global__ void conv_weight_flip(const bf16_t *__restrict__ w, bf16_t *__restric
   }
 }
 
+// Every conv layer's flipped weights of a backward pass in one launch (flat grid, blocks split over
+// segments by size; 32-bit index math).  GoogLeNet flipped 56 weight tensors one launch each
+// (≈5.7 us apiece, 64-bit divisions per element): 0.3 ms of a 6.8 ms step.
+constexpr int FLIP_MAXSEG = 64;
+struct FlipSeg {
+  const bf16_t *w;
+  bf16_t *wt;
+  int Co, KH, KW, Ci, total;
+};
+struct FlipTable {
+  FlipSeg s[FLIP_MAXSEG];
+  int b0[FLIP_MAXSEG];
+  int n;
+};
+__global__ void conv_weight_flip_multi(FlipTable tab) {
+  const int bx = blockIdx.x;
+  int si = 0;
+  for (int i = 1; i < tab.n; ++i)
+    if (tab.b0[i] <= bx) si = i;
+  const FlipSeg sg = tab.s[si];
+  const int i = (bx - tab.b0[si]) * NT + static_cast<int>(threadIdx.x);
+  if (i >= sg.total) return;
+  int t = i;
+  const int ci = t % sg.Ci; t /= sg.Ci;
+  const int kw = t % sg.KW; t /= sg.KW;
+  const int kh = t % sg.KH; t /= sg.KH;
+  const int co = t % sg.Co;
+  const int g = t / sg.Co;
+  const int o = (((g * sg.Ci + ci) * sg.KH + (sg.KH - 1 - kh)) * sg.KW + (sg.KW - 1 - kw)) * sg.Co + co;
+  sg.wt[o] = sg.w[i];
+}
+
 // ------------------------------------------------------------------ pooling
 // mode: 0 max, 1 sum, 2 avg.  relu bit 0: apply relu before max (relu_max_pooling);
 // relu bit 1 (max mode, KH*KW < 128): set bit 7 of the recorded offset when the window
@@ -1384,6 +1416,27 @@ CXN_API int cxn_transpose(const void *x, void *y, int B, int R, int Cc, void *st
 CXN_API int cxn_conv_weight_flip(const void *w, void *wt, int G, int Co, int KH, int KW, int Ci, void *stream) {
   conv_weight_flip<<<nblocks(static_cast<long>(G) * Co * KH * KW * Ci), NT, 0, S_>>>((const bf16_t *)w, (bf16_t *)wt,
                                                                                      G, Co, KH, KW, Ci);
+  RET;
+}
+// ws / wts: n weight tensors [G][Co][KH][KW][Ci] -> [G][Ci][KH'][KW'][Co] (taps reversed);
+// dims: 5 ints per tensor (G, Co, KH, KW, Ci)
+CXN_API int cxn_conv_weight_flip_multi(const void *const *ws, void *const *wts, const int *dims, int n, void *stream) {
+  for (int base = 0; base < n; base += FLIP_MAXSEG) {
+    FlipTable tab;
+    const int cnt = n - base < FLIP_MAXSEG ? n - base : FLIP_MAXSEG;
+    int nblk = 0;
+    tab.n = cnt;
+    for (int i = 0; i < cnt; ++i) {
+      const int *d = dims + 5 * (base + i);
+      const long total = static_cast<long>(d[0]) * d[1] * d[2] * d[3] * d[4];
+      if (total >= (1L << 31)) return -2;
+      tab.s[i] = FlipSeg{static_cast<const bf16_t *>(ws[base + i]), static_cast<bf16_t *>(wts[base + i]), d[1], d[2],
+                         d[3], d[4], static_cast<int>(total)};
+      tab.b0[i] = nblk;
+      nblk += cdiv(total, NT);
+    }
+    if (nblk) conv_weight_flip_multi<<<nblk, NT, 0, S_>>>(tab);
+  }
   RET;
 }
 CXN_API int cxn_pool_fwd(const void *x, void *y, void *arg, int N, int H, int W, int C, int Ho, int Wo, int KH, int KW, int S,

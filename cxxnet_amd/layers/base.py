@@ -103,6 +103,9 @@ class LayerContext:
         # bias gradients queued during a backward pass (NeuralNet.backprop flushes them in one
         # launch); None = compute each one immediately
         self.deferred_bias = None
+        # conv layers whose flipped data-gradient weights were prepared for this backward pass
+        # (one multi-tensor launch in NeuralNet.backprop); None = each layer flips its own
+        self.flipped = None
         self.gen = torch.Generator(device="cpu")
         self.gen.manual_seed(seed)
         self.label_fields: Dict[str, torch.Tensor] = {}

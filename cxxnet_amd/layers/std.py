@@ -296,9 +296,15 @@ class ConvolutionLayer(Layer):
         if self.b is not None:
             self.ctx.bias_grad(dy.view(-1, dy.shape[-1]), self.b.g)
         if prop_grad:
-            if self._wt is None or self._wt.shape != self.w.wb.shape:
-                self._wt = torch.empty_like(self.w.wb)
-            ops.conv_backward_data(dy, self.w.wb, nodes_in[0].gdst, self.geo, self._wt, mask_relu=self.grad_mask_relu)
+            ready = self.ctx.flipped is not None and id(self) in self.ctx.flipped
+            ops.conv_backward_data(dy, self.w.wb, nodes_in[0].gdst, self.geo, self.flip_target()[1],
+                                   mask_relu=self.grad_mask_relu, wt_ready=ready)
+
+    def flip_target(self):
+        """(weights, flipped-weights buffer, geometry) of the data-gradient GEMM."""
+        if self._wt is None or self._wt.shape != self.w.wb.shape:
+            self._wt = torch.empty_like(self.w.wb)
+        return self.w.wb, self._wt, self.geo
 
     def save_model(self, fo: BinWriter):
         fo.write(self.lp.to_bytes())

@@ -90,6 +90,7 @@ _SIGS = {
     "cxn_nhwc_bf16_to_nchw_f32": [_P, _P, _I, _I, _I, _I, _I, _P],
     "cxn_transpose": [_P, _P, _I, _I, _I, _P],
     "cxn_conv_weight_flip": [_P, _P, _I, _I, _I, _I, _I, _P],
+    "cxn_conv_weight_flip_multi": [_P, _P, _P, _I, _P],
     "cxn_pool_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "cxn_pool_bwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _L, _P],
     "cxn_lrn_fwd": [_P, _P, _L, _I, _I, _F, _F, _F, _P],

@@ -359,6 +359,18 @@ class NeuralNet:
         from ..ops.gemm import deterministic
         defer = hook is None and self.ctx.is_gpu and not deterministic()
         self.ctx.deferred_bias = [] if defer else None
+        if self.ctx.is_gpu:
+            # every conv data-gradient's flipped weights in one launch (weights do not change
+            # during the pass: data-parallel bucket updates only start after a layer's backward)
+            flips, seen = [], set()
+            for i, conn in enumerate(self.connections):
+                lay = conn.layer
+                if hasattr(lay, "flip_target") and (i != 0 or prop_to_input) and id(lay) not in seen:
+                    seen.add(id(lay))
+                    flips.append(lay.flip_target())
+            from ..ops.gemm import conv_weight_flip_multi
+            conv_weight_flip_multi(flips)
+            self.ctx.flipped = seen
         with _BatchView(self):
             for i in range(len(self.connections) - 1, -1, -1):
                 conn = self.connections[i]
@@ -370,6 +382,7 @@ class NeuralNet:
                 pending, self.ctx.deferred_bias = self.ctx.deferred_bias, None
                 from .. import ops
                 ops.bias_grad_multi(pending)
+        self.ctx.flipped = None
 
     def update(self, epoch: int, ranges=None):
         self.updater.update(epoch, ranges)

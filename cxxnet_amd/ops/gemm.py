@@ -13,6 +13,7 @@ src/layer/fullc_layer-inl.hpp:101-130.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from dataclasses import dataclass
 
@@ -475,9 +476,26 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
     reg(y)
 
 
-def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False):
+def conv_weight_flip_multi(items):
+    """wt = w with (Cout, Cin) swapped and the taps reversed (the data-gradient GEMM's weight
+    operand), for every (w, wt, geometry) of `items` in one launch."""
+    items = [it for it in items if it[0].is_cuda]
+    if not items:
+        return
+    n = len(items)
+    ws = (ctypes.c_void_p * n)(*[w.data_ptr() for w, _, _ in items])
+    wts = (ctypes.c_void_p * n)(*[wt.data_ptr() for _, wt, _ in items])
+    dims = (ctypes.c_int * (5 * n))(*[v for _, _, g in items for v in (g.groups, g.cg_out, g.KH, g.KW, g.cg_in)])
+    native.check(native.kernels().cxn_conv_weight_flip_multi(ctypes.cast(ws, ctypes.c_void_p),
+                                                             ctypes.cast(wts, ctypes.c_void_p),
+                                                             ctypes.cast(dims, ctypes.c_void_p), n, _stream()),
+                 "conv_weight_flip_multi")
+
+
+def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False, wt_ready=False):
     """dx = conv_transpose(dy, w); dx overwritten.  mask_relu: dx holds relu(z) on entry
-    (fused producer->relu) and the result is multiplied by relu'(z)."""
+    (fused producer->relu) and the result is multiplied by relu'(z).  wt_ready: wt_buf already
+    holds the flipped weights (conv_weight_flip_multi at the start of the backward pass)."""
     if not dy.is_cuda:
         dyn = dy.permute(0, 3, 1, 2)
         out = torch.nn.grad.conv2d_input((g.N, g.C, g.H, g.W), _w_nchw(w), dyn, stride=g.stride,
@@ -491,9 +509,9 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False):
         raise ValueError("conv dgrad: output channels per group must be a multiple of 8 on the GPU path")
     if wt_buf is None:
         wt_buf = torch.empty_like(w)
-    k = native.kernels()
-    native.check(k.cxn_conv_weight_flip(w.data_ptr(), wt_buf.data_ptr(), g.groups, cg_out, g.KH, g.KW, cg_in,
-                                        _stream()), "conv_weight_flip")
+    if not wt_ready:
+        native.check(native.kernels().cxn_conv_weight_flip(w.data_ptr(), wt_buf.data_ptr(), g.groups, cg_out, g.KH,
+                                                           g.KW, cg_in, _stream()), "conv_weight_flip")
     kd = g.KH * g.KW * cg_out
     A = _op(wt_buf, cg_in * kd, kd, cg_in, kd)
     B = _op(dy, cg_out, 0, g.N * g.H * g.W, kd, H=g.Ho, W=g.Wo, C=g.Cout, Ho=g.H, Wo=g.W, KH=g.KH,

@@ -475,3 +475,25 @@ def test_concat_channels_one_launch():
             ref = torch.where(acts[1] > 0, ref, torch.zeros_like(ref))
         assert torch.equal(ins[k], ref), k
         off += c
+
+
+def test_conv_weight_flip_multi_matches_single():
+    """One launch flips every conv layer's weights exactly as the per-layer kernel does."""
+    from cxxnet_amd import native
+    from cxxnet_amd.ops import gemm as G
+    torch.manual_seed(5)
+    geos = [ConvGeom(2, 13, 13, 384, 13, 13, 256, 3, 3, 1, 1, 1, 2), ConvGeom(2, 27, 27, 96, 27, 27, 256, 5, 5, 1, 2, 2, 2),
+            ConvGeom(2, 28, 28, 192, 28, 28, 64, 1, 1, 1, 0, 0, 1), ConvGeom(2, 7, 7, 8, 7, 7, 16, 3, 3, 1, 1, 1, 1)]
+    items, refs = [], []
+    for g in geos:
+        w = torch.randn(g.Cout, g.KH, g.KW, g.cg_in, device=DEV).to(torch.bfloat16)
+        wt = torch.empty_like(w)
+        ref = torch.empty_like(w)
+        native.check(native.kernels().cxn_conv_weight_flip(w.data_ptr(), ref.data_ptr(), g.groups, g.cg_out, g.KH,
+                                                           g.KW, g.cg_in, G._stream()), "flip")
+        items.append((w, wt, g))
+        refs.append(ref)
+    G.conv_weight_flip_multi(items)
+    torch.cuda.synchronize()
+    for (_, wt, _), ref in zip(items, refs):
+        assert torch.equal(wt, ref)
