@@ -42,7 +42,11 @@ def timeit(fn, iters):
 def make(name):
     global N
     N = 256
-    if name.startswith("vgg."):
+    if name.startswith("conv:"):  # generic: conv:C:H:Cout:K:stride:pad:groups:N_kind
+        layer, kind = name.rsplit("_", 1)
+        C, H, Cout, K, st, pd, grp, N = (int(v) for v in layer.split(":")[1:])
+        CONV[layer] = (C, H, Cout, K, st, pd, grp)
+    elif name.startswith("vgg."):
         layer, kind = name[4:].rsplit("_", 1)
         C, H, Cout = VGG[layer]
         CONV[name] = (C, H, Cout, 3, 1, 1, 1)
@@ -96,7 +100,7 @@ def main():
                                      "fc6_wgrad,fc7_fwd,fc7_dgrad,fc7_wgrad,fc8_fwd,fc8_dgrad,fc8_wgrad")
     ap.add_argument("--tiles", default="0,1,2,7,10,13,15,17")
     a = ap.parse_args()
-    for name in a.ops.split(","):
+    for name in a.ops.replace(";", ",").split(","):
         run, out, flops = make(name)
         G.set_glds(False)
         run()

@@ -40,7 +40,10 @@ def run_fc(layer, kind, iters):
 
 def run(name, iters=5):
     n = N
-    if name.startswith("vgg_"):
+    if name.startswith("conv:"):  # generic: conv:C:H:Cout:K:stride:pad:groups:N_kind
+        layer, kind = name.rsplit("_", 1)
+        C, H, Cout, K, s, p, g, n = (int(v) for v in layer.split(":")[1:])
+    elif name.startswith("vgg_"):
         layer, kind = name[4:].rsplit("_", 1)
         C, H, Cout = VGG[layer]
         K, s, p, g = 3, 1, 1, 1

@@ -140,6 +140,9 @@ _glds_cfg = {"on": os.environ.get("CXXNET_GEMM_GLDS", "1") != "0",
 # 128x256 / 64x256 tiles and the pipelined variants (30-41) win conv2/conv3 forward, fc6 forward
 # and several VGG shapes (profiles/r2_sweep_tiles.jsonl).
 GLDS_CANDS = (1, 7, 10, 15, 2, 0, 13, 17, 21, 25, 30, 31, 34, 37, 38, 39, 40, 41, 50, 51, 72)
+# conv weight-grad shapes missing from the shipped table are timed on first use too (else the
+# register kernel runs them)
+_CW_TUNE = os.environ.get("CXXNET_CW_TUNE", "0") == "1"
 # Pseudo-tile: the register-staged kernel (gemm_mfma.hip) with its heuristic tile.  A candidate
 # for conv forward / data-grad / weight-grad, where it still wins some shapes (conv2 forward on
 # AlexNet timed alone: 172 vs 186 us, profiles/r15_glds_8wave.jsonl "old_us").
@@ -215,7 +218,7 @@ def _agrees(a: torch.Tensor, ref: torch.Tensor, tol: float = 2e-2) -> float:
     return (a - ref).norm().item() / max(den, 1e-30)
 
 
-def _tuned_tile(key, run, out, default, extra=(), tune=True):
+def _tuned_tile(key, run, out, default, extra=(), tune=True, cands=None):
     """Tile for a GEMM signature: the fastest candidate, timed once per process on a
     scratch output (the first call of each shape pays a few extra launches and one host
     sync); the heuristic pick when tuning is off or a graph is being captured.
@@ -247,7 +250,7 @@ def _tuned_tile(key, run, out, default, extra=(), tune=True):
     scratch = torch.empty_like(out)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     best, best_ms = None, float("inf")
-    for tile in GLDS_CANDS + tuple(extra):
+    for tile in (GLDS_CANDS if cands is None else tuple(cands)) + tuple(extra):
         scratch.copy_(init)
         if not run(tile, scratch):
             continue
@@ -380,6 +383,23 @@ def _auto_split(rows_i, rows_j, groups, kdim, tile=0, target=2 * NUM_CU, min_kti
     ktiles = -(-kdim // 64)
     split = max(1, min(target // max(tiles, 1), ktiles // min_ktiles))
     return split
+
+
+def _wgrad_cands(rows_i, rows_j, groups, kdim):
+    """(tile, K-slice count) candidates of the register-staged split-K weight-gradient GEMM,
+    encoded tile * 100000 + slices.  Its slices meet in fp32 atomics, whose cost grows with
+    the slice count (on GoogLeNet's 160->320 3x3 weight-grad 72 us at 14 slices, 553 us at
+    512) while too few slices leave CUs idle (its 64->64 1x1: 205 us at 32, 38 us at 512;
+    profiles/r2_wgrad_split_sweep.jsonl), so the count is timed per shape: the chip-filling
+    count (4 blocks per CU) and its halvings, for each weight-grad tile."""
+    ktiles = -(-kdim // 64)
+    out = []
+    for tile in WGRAD_TILES:
+        bm, bn = TILES[tile]
+        tiles = -(-rows_i // bm) * -(-rows_j // bn) * groups
+        occ = max(1, min(4 * NUM_CU // tiles, ktiles // 4))
+        out += [tile * 100000 + sp for sp in sorted({max(1, occ >> k) for k in range(5)})]
+    return tuple(out)
 
 
 # ----------------------------------------------------------------------------- convolution
@@ -552,12 +572,20 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
             pad_h=g.pad_y, pad_w=g.pad_x, dil=1, Cg=cg)
     B = _op(dy, g.cg_out, g.Cout, g.cg_out, P)
 
-    def reg(o):
-        tile = _pick(WGRAD_TILES, kd, g.cg_out, g.groups, min_blocks=1)
-        split = _auto_split(kd, g.cg_out, g.groups, P, tile)
+    def reg_run(code, o):
         _gemm(A, B, GATHER_MN, DIRECT_MN, va, 8, o, g.cg_out * kd, kd, epi=EPI_F32_ATOMIC, groups=g.groups,
-              ksplit=split, tile=tile)
+              ksplit=code % 100000, tile=code // 100000)
         return True
+
+    def reg_default():
+        tile = _pick(WGRAD_TILES, kd, g.cg_out, g.groups, min_blocks=1)
+        return tile * 100000 + _auto_split(kd, g.cg_out, g.groups, P, tile)
+
+    def reg(o):
+        if _glds_cfg["tile"] >= 0:  # a forced LDS-DMA tile id means nothing here
+            return reg_run(reg_default(), o)
+        key = ("cws", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
+        return reg_run(_tuned_tile(key, reg_run, o, reg_default, cands=_wgrad_cands(kd, g.cg_out, g.groups, P)), o)
     if _DET["on"]:
         # one fp32 slab per K slice, summed in slice order into dw: bitwise reproducible
         tile = _pick(WGRAD_TILES, kd, g.cg_out, g.groups, min_blocks=1)
@@ -581,7 +609,7 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
         key = ("cw", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
         # shapes missing from the table keep the register kernel: timed alone, the LDS-DMA form
         # wins shapes where it loses inside the step (conv2/conv3 above)
-        if run(_tuned_tile(key, run, dw, lambda: REG, extra=(REG,), tune=False), dw):
+        if run(_tuned_tile(key, run, dw, lambda: REG, extra=(REG,), tune=_CW_TUNE), dw):
             return
     if va != 8 and g.groups == 1 and g.pad_y == 0 and g.pad_x == 0 and g.C % 4 == 0 and _use("cwr"):
         # few input channels (conv1): the KW*C im2col rows of one kernel row are one contiguous run
