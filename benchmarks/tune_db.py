@@ -2,7 +2,10 @@
 training steps of each model at its benchmark batch so every GEMM signature is timed once,
 then write the table.
 
-  python benchmarks/tune_db.py [--models alexnet:256,inception_v1:64] [--out path]
+  python benchmarks/tune_db.py [--models alexnet:256,inception_v1:64] [--out path] [--keep]
+
+--keep extends the shipped table instead of re-timing it: only signatures it does not hold
+(e.g. the conv weight-grad split-K "cws" keys) are timed.
 """
 import argparse
 import os
@@ -18,12 +21,14 @@ def main():
     ap.add_argument("--models", default="alexnet:256,alexnet:32,alexnet:128,inception_v1:64,vgg16:32,mnist_conv:100,"
                                         "bowl:64")
     ap.add_argument("--out", default="")
+    ap.add_argument("--keep", action="store_true", help="keep the shipped entries, time only missing keys")
     a = ap.parse_args()
     from cxxnet_amd.io.data import DataBatch
     from cxxnet_amd.models import load_conf
     from cxxnet_amd.nnet import NetTrainer
     from cxxnet_amd.ops import gemm as G
-    G._TUNE.clear()
+    if not a.keep:
+        G._TUNE.clear()
     for spec in a.models.split(","):
         name, b = spec.split(":")
         b = int(b)

@@ -64,7 +64,7 @@ def check_conv(op, key, tile=None):
                                              stride=g.stride, padding=(g.pad_y, g.pad_x),
                                              groups=g.groups).permute(0, 2, 3, 1)
             return _relnorm(dx, ref)
-        if op == "cw":
+        if op in ("cw", "cws"):
             x = _rnd((g.N, g.H, g.W, g.C), 1.0, 5)
             dy = _rnd((g.N, g.Ho, g.Wo, g.Cout), 1.0, 6)
             dw = torch.zeros(g.Cout, g.KH, g.KW, g.cg_in, device=DEV)
@@ -109,7 +109,7 @@ def _table_cases():
 def test_shipped_table_entry(op, sig):
     """The table's tile at the table's exact signature (no tile forcing: the lookup
     inside the op picks it, as in training)."""
-    if op in ("cf", "cr", "cd", "cw"):
+    if op in ("cf", "cr", "cd", "cw", "cws"):
         if op == "cr":  # key: N, H, W, C, Cout, KH, KW, stride (no pad, one group)
             sig = sig + (0, 0, 1)
         err = check_conv(op, sig)
