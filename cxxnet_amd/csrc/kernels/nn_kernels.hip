@@ -980,9 +980,14 @@ __global__ void colsum_bf16(const bf16_t *__restrict__ dy, float *__restrict__ p
 // A layer's backward only queues its (dy, db); NeuralNet.backprop flushes the queue once at
 // the end (dy buffers are not rewritten later in the pass), which replaces one or two small
 // launches per conv / fc layer -- GoogLeNet has 57 -- by one.
+// A masked segment sums a max-pool's OUTPUT gradient instead of the conv's: every pool window
+// routes its gradient to exactly one input pixel, and relu' of that pixel is bit 7 of the
+// window's recorded offset (pool_fwd_rows, relu & 2), so sum_pixels dx = sum_windows dy * relu'
+// -- the bias gradient of the conv in front of a max-pool at 1/stride^2 of the bytes read.
 constexpr int COLSUM_MAXSEG = 64;
 struct ColsumSeg {
   const bf16_t *dy;
+  const uint8_t *mask;  // nullable: max-pool offsets [rows][C]; entries with bit 7 set count as 0
   float *db;
   long rows;
   int C, rpb, nblk;
@@ -1015,26 +1020,53 @@ __global__ void colsum_multi(ColsumTable tab) {
     if (rg < RG) {
       // 8 rows in flight per thread; whole groups of 8 without bounds checks
       constexpr int U = 8;
-      const bf16_t *p = sg.dy + (r0 + rg) * sg.C + cv * 8;
+      const long e0 = (r0 + rg) * sg.C + cv * 8;
+      const bf16_t *p = sg.dy + e0;
       const long step = static_cast<long>(RG) * sg.C;
       long r = r0 + rg;
-      for (; r + (U - 1) * RG < r1; r += RG * U, p += U * step) {
-        uint4 q[U];
+      if (sg.mask == nullptr) {
+        for (; r + (U - 1) * RG < r1; r += RG * U, p += U * step) {
+          uint4 q[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) q[u] = *reinterpret_cast<const uint4 *>(p + u * step);
+          for (int u = 0; u < U; ++u) q[u] = *reinterpret_cast<const uint4 *>(p + u * step);
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
+          for (int u = 0; u < U; ++u) {
+            float v[8];
+            unpack8(q[u], v);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[e] += v[e];
+          }
+        }
+        for (; r < r1; r += RG, p += step) {
           float v[8];
-          unpack8(q[u], v);
+          unpack8(*reinterpret_cast<const uint4 *>(p), v);
 #pragma unroll
           for (int e = 0; e < 8; ++e) acc[e] += v[e];
         }
-      }
-      for (; r < r1; r += RG, p += step) {
-        float v[8];
-        unpack8(*reinterpret_cast<const uint4 *>(p), v);
+      } else {
+        const uint8_t *mp = sg.mask + e0;
+        auto add = [&](const uint4 q, const uint2 m) {
+          float v[8];
+          unpack8(q, v);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] += v[e];
+          for (int e = 0; e < 4; ++e) {
+            acc[e] += ((m.x >> (8 * e + 7)) & 1u) ? 0.f : v[e];
+            acc[e + 4] += ((m.y >> (8 * e + 7)) & 1u) ? 0.f : v[e + 4];
+          }
+        };
+        for (; r + (U - 1) * RG < r1; r += RG * U, p += U * step, mp += U * step) {
+          uint4 q[U];
+          uint2 m[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            q[u] = *reinterpret_cast<const uint4 *>(p + u * step);
+            m[u] = *reinterpret_cast<const uint2 *>(mp + u * step);
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) add(q[u], m[u]);
+        }
+        for (; r < r1; r += RG, p += step, mp += step)
+          add(*reinterpret_cast<const uint4 *>(p), *reinterpret_cast<const uint2 *>(mp));
       }
     }
     __syncthreads();  // red is reused by the next column chunk
@@ -1631,9 +1663,10 @@ CXN_API int cxn_colsum(const void *dy, float *db, long rows, int C, float *ws, l
   partials_reduce<<<partials_grid(static_cast<int>(grid.x), C), NT, 0, S_>>>(ws, static_cast<int>(grid.x), C, db);
   RET;
 }
-// dys / dbs / rows / Cs: n deferred bias gradients (C % 8 == 0 each)
-CXN_API int cxn_colsum_multi(const void *const *dys, float *const *dbs, const long *rows, const int *Cs, int n,
-                             void *stream) {
+// dys / dbs / rows / Cs: n deferred bias gradients (C % 8 == 0 each); masks: nullable array of
+// nullable max-pool offset tensors (masked segments, see colsum_multi)
+CXN_API int cxn_colsum_multi(const void *const *dys, float *const *dbs, const long *rows, const int *Cs,
+                             const void *const *masks, int n, void *stream) {
   for (int base = 0; base < n; base += COLSUM_MAXSEG) {
     ColsumTable tab;
     const int cnt = n - base < COLSUM_MAXSEG ? n - base : COLSUM_MAXSEG;
@@ -1648,7 +1681,8 @@ CXN_API int cxn_colsum_multi(const void *const *dys, float *const *dbs, const lo
       if (nb > 1024) nb = 1024;
       if (nb < 1) nb = 1;
       const int rpb = static_cast<int>(cdiv(rows[j], nb));
-      tab.s[i] = ColsumSeg{static_cast<const bf16_t *>(dys[j]), dbs[j], rows[j], Cs[j], rpb,
+      tab.s[i] = ColsumSeg{static_cast<const bf16_t *>(dys[j]),
+                           masks ? static_cast<const uint8_t *>(masks[j]) : nullptr, dbs[j], rows[j], Cs[j], rpb,
                            static_cast<int>(cdiv(rows[j], static_cast<long>(rpb)))};
       tab.b0[i] = nblk;
       nblk += tab.s[i].nblk;

@@ -112,13 +112,14 @@ class LayerContext:
         self.label_name_map: Dict[str, int] = {"label": 0}
         self.step = 0  # forward counter, feeds counter-based RNG (dropout)
 
-    def bias_grad(self, dy2d, db):
-        """db += column sums of dy2d, now or (deferred) at the end of the backward pass."""
+    def bias_grad(self, dy2d, db, mask=None):
+        """db += column sums of dy2d (mask: see ops.bias_grad), now or (deferred) at the end
+        of the backward pass."""
         if self.deferred_bias is not None and dy2d.is_cuda:
-            self.deferred_bias.append((dy2d, db))
+            self.deferred_bias.append((dy2d, db, mask))
             return
         from .. import ops
-        ops.bias_grad(dy2d, db)
+        ops.bias_grad(dy2d, db, mask)
 
 
 class Layer:

@@ -12,7 +12,7 @@ import os
 import torch
 
 from .. import ops
-from ..ops.gemm import ConvGeom, conv_out_size
+from ..ops.gemm import ConvGeom, conv_out_size, deterministic
 from .base import BinReader, BinWriter, Layer, Node, ParamSpec
 
 # CXXNET_CONV_PREPAD=0 disables the zero-bordered-copy path of few-channel padded convs
@@ -199,6 +199,7 @@ class ConvolutionLayer(Layer):
         self._wt = None
         self._xpad = None
         self._prepad_on = False
+        self.bias_done = False  # set by a fused max-pool backward that already summed the bias gradient
 
     def init_connection(self, nodes_in, nodes_out):
         _check(len(nodes_in) == 1 and len(nodes_out) == 1, "ConvolutionLayer: only support 1-1 connection")
@@ -293,7 +294,9 @@ class ConvolutionLayer(Layer):
         self.geo.N = x.shape[0]
         xw, geo = self._padded(x, False)
         ops.conv_backward_weight(xw, dy, self.w.g, geo)
-        if self.b is not None:
+        if self.bias_done:  # summed by the max-pool behind this conv (NeuralNet._fuse_pool_bias)
+            self.bias_done = False
+        elif self.b is not None:
             self.ctx.bias_grad(dy.view(-1, dy.shape[-1]), self.b.g)
         if prop_grad:
             ready = self.ctx.flipped is not None and id(self) in self.ctx.flipped
@@ -385,6 +388,9 @@ class PoolingLayer(Layer):
         self.state = None
         self.tie_all = False
         self.ysave = None
+        # the conv in front whose bias gradient this pool's backward provides (executor fusion,
+        # NeuralNet._fuse_pool_bias); None = not fused
+        self.bias_of = None
 
     def set_param(self, name, val):
         super().set_param(name, val)
@@ -443,6 +449,13 @@ class PoolingLayer(Layer):
             return
         if relu and self._mask_in_state():
             relu = 2  # relu' of the argmax was recorded by the forward: no read of x
+        conv = self.bias_of
+        if conv is not None and conv.b is not None and relu in (0, 2) and x.is_cuda and not deterministic():
+            # the conv's bias gradient from this pool's output gradient (before it is consumed)
+            dy = nodes_out[0].data
+            self.ctx.bias_grad(dy.view(-1, dy.shape[-1]), conv.b.g,
+                               self.state.view(-1, dy.shape[-1]) if relu == 2 else None)
+            conv.bias_done = True
         ops.pool_backward(x, self.state, nodes_out[0].data, nodes_in[0].gdst, lp.kernel_height, lp.kernel_width, lp.stride,
                           lp.pad_y, self.mode, relu)
 

@@ -101,7 +101,7 @@ _SIGS = {
     "cxn_softmax": [_P, _P, _P, _I, _I, _P],
     "cxn_loss_grad": [_P, _P, _P, _I, _I, _I, _F, _I, _P],
     "cxn_colsum": [_P, _P, _L, _I, _P, _L, _P],
-    "cxn_colsum_multi": [_P, _P, _P, _P, _I, _P],
+    "cxn_colsum_multi": [_P, _P, _P, _P, _P, _I, _P],
     "cxn_concat": [_P, _P, _I, _P, _I, _L, _I, _I, _P],
     "cxn_cast_f32_bf16": [_P, _P, _L, _P],
     "cxn_add_bf16": [_P, _P, _P, _L, _P],

@@ -31,6 +31,7 @@ from ..io.data import U8Images
 
 K_CONV, K_FULLC, K_RELU, K_MAXPOOL, K_DROPOUT = 10, 1, 3, 11, 8
 K_SPLIT, K_CONCAT, K_CHCONCAT, K_SUMPOOL, K_AVGPOOL, K_LRN = 23, 18, 28, 12, 13, 15
+K_RELU_MAXPOOL = 21
 # layers that only READ their input node in forward and write the input gradient through
 # Node.gdst: they may consume a zero-copy split output
 _SPLIT_SAFE = (K_CONV, K_FULLC, K_MAXPOOL, K_SUMPOOL, K_AVGPOOL, K_LRN)
@@ -166,6 +167,33 @@ class NeuralNet:
             cj.layer.grad_mask_relu = True
             self.aliases[id(b)] = a
         self._fuse_split(producers, consumers)
+        self._fuse_pool_bias(producers, consumers)
+
+    def _fuse_pool_bias(self, producers, consumers):
+        """Bias gradient of a conv that feeds a max-pool, taken from the pool's OUTPUT gradient:
+        each window routes its gradient to one input pixel, relu' of that pixel is recorded in
+        the window's offset byte, so the pool sums dy_pool (masked) instead of the conv summing
+        its own stride^2-times larger dy (ops.bias_grad mask).  The conv's output (or the fused
+        relu's alias of it) must be read by the pool alone.  CXXNET_POOL_BIAS=0 turns it off."""
+        if os.environ.get("CXXNET_POOL_BIAS", "1") == "0":
+            return
+        for conn in self.connections:
+            lay = conn.layer
+            if conn.type not in (K_MAXPOOL, K_RELU_MAXPOOL) or conn.shared or len(conn.nodes_in) != 1:
+                continue
+            if getattr(lay, "mode", None) != "max":
+                continue
+            node = conn.nodes_in[0]
+            src = self.aliases.get(id(node), node)  # a fused relu's output aliases the conv output
+            prod = producers.get(id(src), [])
+            if len(prod) != 1:
+                continue
+            p = self.connections[prod[0]]
+            if p.type != K_CONV or p.shared or len(consumers.get(id(src), [])) != 1:
+                continue
+            if src is not node and len(consumers.get(id(node), [])) != 1:
+                continue
+            lay.bias_of = p.layer
 
     def _fuse_split(self, producers, consumers):
         """Zero-copy split: when the split is its input's only reader and every output feeds

@@ -388,10 +388,18 @@ def _workspace(n: int, device) -> torch.Tensor:
     return t
 
 
-def bias_grad(dy2d, db):
-    """db[C] += sum over rows of dy2d[rows][C]."""
+def bias_grad(dy2d, db, mask=None):
+    """db[C] += sum over rows of dy2d[rows][C].  mask (uint8 [rows][C], optional): max-pool
+    offsets recorded with relu' in bit 7 (pool_forward(mark_mask=True)); an entry whose bit 7
+    is set counts as zero -- dy2d is then a max-pool's output gradient and the sum is the
+    bias gradient of the conv in front of the pool (see colsum_multi)."""
     if not dy2d.is_cuda:
-        db.add_(dy2d.sum(0))
+        if mask is not None:
+            dy2d = dy2d * (mask < 128).to(dy2d.dtype)
+        db.add_(dy2d.float().sum(0))
+        return
+    if mask is not None:
+        bias_grad_multi([(dy2d, db, mask)])
         return
     rows, C = dy2d.shape
     n = max(4096, -(-rows // 512)) * C
@@ -401,21 +409,32 @@ def bias_grad(dy2d, db):
 
 
 def bias_grad_multi(items):
-    """Every (dy2d, db) of `items`: db[C] += sum over rows of dy2d, in one launch for the
-    GPU tensors with C % 8 == 0 (the rest one by one)."""
-    fast = [(d, b) for d, b in items if d.is_cuda and d.shape[1] % 8 == 0 and d.is_contiguous()]
-    for d, b in items:
-        if not (d.is_cuda and d.shape[1] % 8 == 0 and d.is_contiguous()):
-            bias_grad(d, b)
+    """Every (dy2d, db[, mask]) of `items`: db[C] += sum over rows of dy2d (masked as in
+    bias_grad), in one launch for the GPU tensors with C % 8 == 0 (the rest one by one)."""
+    items = [tuple(it) + (None,) * (3 - len(it)) for it in items]
+
+    def fast_ok(d, m):
+        return d.is_cuda and d.shape[1] % 8 == 0 and d.is_contiguous() and (m is None or m.is_contiguous())
+    fast = [it for it in items if fast_ok(it[0], it[2])]
+    for d, b, m in items:
+        if not fast_ok(d, m):
+            if m is not None and d.is_cuda:
+                bias_grad(d * (m < 128).to(d.dtype), b)
+            else:
+                bias_grad(d, b, m)
     if not fast:
         return
     n = len(fast)
-    dys = (ctypes.c_void_p * n)(*[d.data_ptr() for d, _ in fast])
-    dbs = (ctypes.c_void_p * n)(*[b.data_ptr() for _, b in fast])
-    rows = (ctypes.c_long * n)(*[d.shape[0] for d, _ in fast])
-    cs = (ctypes.c_int * n)(*[d.shape[1] for d, _ in fast])
+    dys = (ctypes.c_void_p * n)(*[d.data_ptr() for d, _, _ in fast])
+    dbs = (ctypes.c_void_p * n)(*[b.data_ptr() for _, b, _ in fast])
+    rows = (ctypes.c_long * n)(*[d.shape[0] for d, _, _ in fast])
+    cs = (ctypes.c_int * n)(*[d.shape[1] for d, _, _ in fast])
+    masks = None
+    if any(m is not None for _, _, m in fast):
+        masks = (ctypes.c_void_p * n)(*[m.data_ptr() if m is not None else None for _, _, m in fast])
     native.check(_k().cxn_colsum_multi(ctypes.cast(dys, ctypes.c_void_p), ctypes.cast(dbs, ctypes.c_void_p),
-                                       ctypes.cast(rows, ctypes.c_void_p), ctypes.cast(cs, ctypes.c_void_p), n,
+                                       ctypes.cast(rows, ctypes.c_void_p), ctypes.cast(cs, ctypes.c_void_p),
+                                       ctypes.cast(masks, ctypes.c_void_p) if masks is not None else None, n,
                                        _stream()), "colsum_multi")
 
 

@@ -454,6 +454,67 @@ def test_bias_grad_multi_matches_single():
         assert relerr(db, ref) < 1e-3
 
 
+def test_bias_grad_masked_pool_offsets():
+    """Masked colsum segments (the bias gradient of a conv in front of a max-pool, summed from
+    the pool's output gradient): entries whose offset byte has bit 7 (relu' = 0) count as 0;
+    mixed masked / unmasked segments in one launch, and the single-tensor entry point."""
+    shapes = [(186624, 96), (43264, 256), (1000, 24)]
+    items, refs = [], []
+    for k, (r, c) in enumerate(shapes):
+        dy = rnd(r, c, seed=80 + k).to(DEV, torch.bfloat16)
+        g = torch.Generator().manual_seed(90 + k)
+        off = torch.randint(0, 9, (r, c), generator=g, dtype=torch.uint8)
+        off |= (torch.rand(r, c, generator=g) < 0.4).to(torch.uint8) * 128
+        off = off.to(DEV)
+        db = torch.full((c,), 0.5, device=DEV)
+        m = off if k != 1 else None
+        items.append((dy, db, m))
+        keep = (off < 128).float() if m is not None else torch.ones(r, c, device=DEV)
+        refs.append(0.5 + (dy.float() * keep).sum(0))
+    ops.bias_grad_multi(items)
+    torch.cuda.synchronize()
+    for (_, db, _), ref in zip(items, refs):
+        assert relerr(db, ref) < 1e-3
+    dy, db, m = items[0][0], torch.zeros(96, device=DEV), items[0][2]
+    ops.bias_grad(dy, db, m)
+    assert relerr(db, refs[0] - 0.5) < 1e-3
+
+
+def test_pool_fused_conv_bias_grad_matches_unfused():
+    """conv -> relu -> max-pool: the conv's bias gradient taken by the pool from its output
+    gradient (NeuralNet._fuse_pool_bias) equals the conv's own column sum of its dy."""
+    from cxxnet_amd.io.data import DataBatch
+    from cxxnet_amd.models import load_conf
+    from cxxnet_amd.nnet import NetTrainer
+
+    grads = []
+    for fused in (True, False):
+        # update_period 2: the first update() is forward + backward only (gradients kept)
+        pairs = load_conf("alexnet", [("batch_size", "16"), ("dev", "gpu"), ("eval_train", "0"), ("silent", "1"),
+                                      ("update_period", "2")])
+        tr = NetTrainer()
+        for k, v in pairs:
+            if not k.startswith("metric"):
+                tr.set_param(k, v)
+        tr.init_model()
+        pools = [c.layer for c in tr.net.connections if getattr(c.layer, "bias_of", None) is not None]
+        assert len(pools) == 3  # conv1, conv2, conv5 sit in front of max-pools
+        convs = [p.bias_of for p in pools]
+        if not fused:
+            for p in pools:
+                p.bias_of = None
+        c, h, w = tr.net_cfg.input_shape
+        g = torch.Generator().manual_seed(5)
+        x = torch.randn(16, c, h, w, generator=g).to(DEV)
+        y = torch.randint(0, 1000, (16, 1), generator=g).float().to(DEV)
+        tr.update(DataBatch(x, y))
+        torch.cuda.synchronize()
+        grads.append([cv.b.g.clone() for cv in convs])
+    for a, b in zip(*grads):
+        assert b.abs().max().item() > 0
+        assert relerr(a, b) < 1e-2, relerr(a, b)
+
+
 def test_concat_channels_one_launch():
     """ch_concat forward gather and backward scatter (relu' on the masked inputs) in one
     launch, against per-input slicing."""
