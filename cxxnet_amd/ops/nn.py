@@ -408,16 +408,18 @@ def bias_grad(dy2d, db, mask=None):
                  "colsum")
 
 
+def bias_fast_ok(d, m=None) -> bool:
+    """Served by the one-launch colsum_multi kernel (no workspace, no temporaries)."""
+    return d.is_cuda and d.shape[1] % 8 == 0 and d.is_contiguous() and (m is None or m.is_contiguous())
+
+
 def bias_grad_multi(items):
     """Every (dy2d, db[, mask]) of `items`: db[C] += sum over rows of dy2d (masked as in
     bias_grad), in one launch for the GPU tensors with C % 8 == 0 (the rest one by one)."""
     items = [tuple(it) + (None,) * (3 - len(it)) for it in items]
-
-    def fast_ok(d, m):
-        return d.is_cuda and d.shape[1] % 8 == 0 and d.is_contiguous() and (m is None or m.is_contiguous())
-    fast = [it for it in items if fast_ok(it[0], it[2])]
+    fast = [it for it in items if bias_fast_ok(it[0], it[2])]
     for d, b, m in items:
-        if not fast_ok(d, m):
+        if not bias_fast_ok(d, m):
             if m is not None and d.is_cuda:
                 bias_grad(d * (m < 128).to(d.dtype), b)
             else:
