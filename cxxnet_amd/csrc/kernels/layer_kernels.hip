@@ -35,6 +35,25 @@ static inline int nblocks(long n, int cap = 256 * 16) {
   return static_cast<int>(b > cap ? cap : b);
 }
 
+// ------------------------------------------------------------------ parameter initialisation
+// Random weight init on the device (reference LayerParam::RandInitWeight, src/layer/param.h:
+// 114-138, draws on the host through mshadow's Random): element i takes the 24-bit uniforms
+// of hash(2i, seed) and hash(2i+1, seed); dist 0 = uniform a + (b - a) u, dist 1 = normal
+// a + b z with Box-Muller z = sqrt(-2 ln(1 - u1)) cos(2 pi u2).  ops.rand_fill's host path is
+// the same integer hash with float32 math, so CPU and GPU models of one seed start alike (to a
+// few ulps of logf/cosf); VGG-16's 138M parameters no longer go through a host RNG + copy.
+__global__ void rand_fill(float *__restrict__ out, uint32_t n, uint32_t seed, int dist, float a, float b) {
+  for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < n; i += gridDim.x * NT) {
+    const float u1 = static_cast<float>(hash_u32(2u * i, seed) >> 8) * 5.9604644775390625e-08f;
+    if (dist == 0) {
+      out[i] = a + (b - a) * u1;
+    } else {
+      const float u2 = static_cast<float>(hash_u32(2u * i + 1u, seed) >> 8) * 5.9604644775390625e-08f;
+      out[i] = a + b * (sqrtf(-2.0f * logf(1.0f - u1)) * cosf(6.283185307179586f * u2));
+    }
+  }
+}
+
 // ------------------------------------------------------------------ per-channel reductions
 // x, g: [rows][C] bf16.  out[q][c] += partial sums (caller zeroes out):
 //   mode 0: out0 = sum x                 mode 1: out0 = sum (x - mean)^2
@@ -250,6 +269,12 @@ __global__ void ins_pool_bwd(const bf16_t *__restrict__ x, const bf16_t *__restr
 #define RET return hipGetLastError() == hipSuccess ? 0 : -3
 
 // out must hold 3*C floats; it is zeroed here.
+CXN_API int cxn_rand_fill(float *out, long n, unsigned seed, int dist, float a, float b, void *stream) {
+  if (n < 0 || n > 0x7fffffffL) return -1;
+  if (n == 0) return 0;
+  rand_fill<<<nblocks(n, 256 * 64), NT, 0, S_>>>(out, static_cast<uint32_t>(n), seed, dist, a, b);
+  RET;
+}
 CXN_API int cxn_chan_reduce(const void *x, const void *g, const float *mean, float *out, long rows, int C, int mode,
                             void *stream) {
   if (hipMemsetAsync(out, 0, sizeof(float) * 3 * C, S_) != hipSuccess) return -3;

@@ -168,20 +168,23 @@ class Layer:
     def _init_weight(self, t: torch.Tensor, in_num: int, out_num: int):
         """LayerParam::RandInitWeight (reference src/layer/param.h:114-138), on a logical-layout tensor."""
         lp = self.lp
-        g = self.ctx.gen
+        # one seed per tensor from the context generator; the draws themselves run where t
+        # lives (ops.rand_fill: a HIP kernel on the GPU, the same hash on the host)
+        from ..ops.layer_ops import rand_fill
+        seed = int(torch.randint(0, 2**31 - 1, (1,), generator=self.ctx.gen).item())
         if lp.random_type == 0:
-            t.normal_(0.0, lp.init_sigma, generator=g)
+            rand_fill(t, seed, "normal", 0.0, lp.init_sigma)
         elif lp.random_type == 1:
             a = math.sqrt(3.0 / (in_num + out_num))
             if lp.init_uniform > 0:
                 a = lp.init_uniform
-            t.uniform_(-a, a, generator=g)
+            rand_fill(t, seed, "uniform", -a, a)
         elif lp.random_type == 2:
             if lp.num_hidden > 0:
                 sigma = math.sqrt(2.0 / lp.num_hidden)
             else:
                 sigma = math.sqrt(2.0 / (lp.num_channel * lp.kernel_width * lp.kernel_height))
-            t.normal_(0.0, sigma, generator=g)
+            rand_fill(t, seed, "normal", 0.0, sigma)
 
 
 # ----------------------------------------------------------------------------- binary io

@@ -260,7 +260,9 @@ class PReluLayer(Layer):
             if self.init_random == 0:
                 t.fill_(self.init_slope)
             else:
-                t.uniform_(0, 1, generator=self.ctx.gen).mul_(self.init_slope)
+                from ..ops.layer_ops import rand_fill
+                rand_fill(t, int(torch.randint(0, 2**31 - 1, (1,), generator=self.ctx.gen).item()), "uniform",
+                          0.0, self.init_slope)
         self.params = [ParamSpec("bias", (self.channel,), init)]
 
     def _noise(self, is_train):

@@ -230,7 +230,7 @@ class ConvolutionLayer(Layer):
                            and _PREPAD)
 
         def init_w(t):
-            logical = torch.empty(G, co // G, cg_l * kh * kw)
+            logical = torch.empty(G, co // G, cg_l * kh * kw, device=t.device)
             self._init_weight(logical, cg_l * kh * kw, co // G)
             t.copy_(self.from_logical(logical))
         self.params = [ParamSpec("wmat", (co, kh, kw, cg_p), init_w)]
@@ -244,7 +244,7 @@ class ConvolutionLayer(Layer):
         cg_l = lp.num_input_channel // G
         cg_p = self.cin_phys // G
         t = logical.reshape(co, cg_l, kh, kw).permute(0, 2, 3, 1)
-        out = torch.zeros(co, kh, kw, cg_p, dtype=logical.dtype)
+        out = torch.zeros(co, kh, kw, cg_p, dtype=logical.dtype, device=logical.device)
         out[..., :cg_l] = t
         return out
 

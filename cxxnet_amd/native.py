@@ -76,6 +76,7 @@ _SIGS = {
     "cxn_bn_stats": [_P, _P, _P, _P, _L, _I, _F, _P],
     "cxn_bn_fwd": [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
     "cxn_bn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
+    "cxn_rand_fill": [_P, _L, _U, _I, _F, _F, _P],
     "cxn_prelu": [_P, _P, _P, _P, _L, _I, _U, _P, _F, _I, _P],
     "cxn_insanity": [_P, _P, _P, _P, _L, _F, _F, _I, _U, _P, _I, _P],
     "cxn_ins_pool_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _U, _P, _P],

@@ -277,9 +277,10 @@ class NeuralNet:
         self._alloc_nodes()
         self._build_arena()
         for li, spec in self.arena.specs:
-            host = torch.zeros(spec.shape, dtype=torch.float32)
-            spec.init(host)
-            spec.w.copy_(host)
+            # drawn where the arena lives (device RNG kernel on the GPU), in logical layout
+            t = torch.zeros(spec.shape, dtype=torch.float32, device=self.device)
+            spec.init(t)
+            spec.w.copy_(t)
         self.arena.sync_shadow()
         self._init_updater()
 

@@ -27,6 +27,33 @@ def uniform_ref(n: int, seed: int, device="cpu") -> torch.Tensor:
     return _hash_u32(idx, seed & 0xFFFFFFFF).to(torch.float32) * 2.3283064365386963e-10
 
 
+def rand_fill(t: torch.Tensor, seed: int, dist: str, a: float, b: float):
+    """Fill fp32 tensor t in place: dist "uniform" a + (b - a) u, "normal" a + b z.  On the
+    GPU one rand_fill launch (layer_kernels.hip); on the host the same counter hash in int64
+    arithmetic and the same float32 Box-Muller, chunked to bound the index arrays."""
+    assert t.dtype == torch.float32 and t.is_contiguous()
+    n = t.numel()
+    d = 0 if dist == "uniform" else 1
+    seed &= 0xFFFFFFFF
+    if t.is_cuda:
+        native.check(_k().cxn_rand_fill(t.data_ptr(), n, seed, d, float(a), float(b), _stream()), "rand_fill")
+        return t
+    flat = t.view(-1)
+    step = 1 << 24
+    scale = torch.tensor(5.9604644775390625e-08, dtype=torch.float32)
+    for lo in range(0, n, step):
+        idx = torch.arange(lo, min(n, lo + step), dtype=torch.int64)
+        u1 = (_hash_u32(2 * idx, seed) >> 8).to(torch.float32) * scale
+        if d == 0:
+            v = torch.tensor(a, dtype=torch.float32) + torch.tensor(b - a, dtype=torch.float32) * u1
+        else:
+            u2 = (_hash_u32(2 * idx + 1, seed) >> 8).to(torch.float32) * scale
+            z = torch.sqrt(-2.0 * torch.log(1.0 - u1)) * torch.cos(6.283185307179586 * u2)
+            v = torch.tensor(a, dtype=torch.float32) + torch.tensor(b, dtype=torch.float32) * z
+        flat[lo:lo + idx.numel()] = v
+    return t
+
+
 # ----------------------------------------------------------------------------- batch norm
 class BNState:
     """Per-layer device buffers: mean, inv (fp32 [C]), workspaces, the saved input copy."""

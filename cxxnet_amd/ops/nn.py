@@ -398,7 +398,9 @@ def bias_grad(dy2d, db, mask=None):
             dy2d = dy2d * (mask < 128).to(dy2d.dtype)
         db.add_(dy2d.float().sum(0))
         return
-    if mask is not None:
+    if mask is not None or (bias_fast_ok(dy2d) and not _det()):
+        # one launch (per-block partials, one atomic per channel per block); the two-pass
+        # colsum below keeps a fixed summation order for deterministic mode
         bias_grad_multi([(dy2d, db, mask)])
         return
     rows, C = dy2d.shape
@@ -406,6 +408,11 @@ def bias_grad(dy2d, db, mask=None):
     ws = _workspace(n, dy2d.device)
     native.check(_k().cxn_colsum(dy2d.data_ptr(), db.data_ptr(), rows, C, ws.data_ptr(), ws.numel(), _stream()),
                  "colsum")
+
+
+def _det() -> bool:
+    from .gemm import deterministic
+    return deterministic()
 
 
 def bias_fast_ok(d, m=None) -> bool:

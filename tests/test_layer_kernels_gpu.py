@@ -196,3 +196,36 @@ def test_split_fanout_and_sum_kernels(nd):
     ops.sum_into(y, grads)
     ref = torch.stack([t.float() for t in grads]).sum(0)
     assert (y.float() - ref).abs().max().item() <= 0.02 * ref.abs().max().item() + 1e-6
+
+
+@pytest.mark.parametrize("dist,a,b", [("normal", 0.0, 0.01), ("uniform", -0.05, 0.05), ("normal", 0.3, 2.0)])
+def test_rand_fill_device_matches_host(dist, a, b):
+    """Weight init on the device (rand_fill kernel) draws what the host mirror draws: the
+    same integer hash, float32 Box-Muller (a few ulps apart through logf / cosf)."""
+    n = 1 << 20 | 77
+    gpu = L.rand_fill(torch.empty(n, device=DEV), 1234, dist, a, b).cpu()
+    cpu = L.rand_fill(torch.empty(n), 1234, dist, a, b)
+    assert (gpu - cpu).abs().max().item() <= 1e-5 * max(abs(a), abs(b), 1.0)
+    if dist == "normal":
+        assert abs(gpu.mean().item() - a) < 5e-3 * b and abs(gpu.std().item() / b - 1) < 5e-3
+    else:
+        assert gpu.min().item() >= a and gpu.max().item() < b
+
+
+def test_model_init_on_device_matches_cpu_model():
+    """A GPU model and a CPU model of one seed start from the same weights (device RNG)."""
+    from cxxnet_amd.models import load_conf
+    from cxxnet_amd.nnet import NetTrainer
+
+    ws = []
+    for dev in ("gpu", "cpu"):
+        pairs = load_conf("alexnet", [("batch_size", "2"), ("dev", dev), ("silent", "1")])
+        tr = NetTrainer()
+        for k, v in pairs:
+            tr.set_param(k, v)
+        tr.init_model()
+        ws.append([c.layer.params[0].w.detach().float().cpu().clone() for c in tr.net.connections
+                   if c.layer.params and not c.shared])
+    for g, c in zip(*ws):
+        gg, cc = g[..., :c.shape[-1]] if g.shape != c.shape else g, c
+        assert (gg.reshape(cc.shape) - cc).abs().max().item() <= 1e-6 + 1e-5 * cc.abs().max().item()

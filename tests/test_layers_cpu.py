@@ -392,3 +392,14 @@ def test_clip_gradient_is_sgd_only(algo):
         assert torch.allclose(runs[1], 1 - 0.1 * g0.clamp(-0.5, 0.5))
     else:
         assert torch.equal(runs[0], runs[1])
+
+
+def test_rand_fill_host_statistics_and_determinism():
+    from cxxnet_amd.ops.layer_ops import rand_fill
+    a = rand_fill(torch.empty(200003), 7, "normal", 0.0, 0.02)
+    b = rand_fill(torch.empty(200003), 7, "normal", 0.0, 0.02)
+    c = rand_fill(torch.empty(200003), 8, "normal", 0.0, 0.02)
+    assert torch.equal(a, b) and not torch.equal(a, c)
+    assert abs(a.mean().item()) < 3e-4 and abs(a.std().item() / 0.02 - 1) < 1e-2
+    u = rand_fill(torch.empty(100000), 7, "uniform", -1.0, 1.0)
+    assert u.min().item() >= -1.0 and u.max().item() < 1.0 and abs(u.mean().item()) < 1e-2
