@@ -84,6 +84,10 @@ class GradReducer:
         self.shard = bool(shard) and (self.world > 1 or self.force)
         self.comm_dtype = torch.bfloat16 if comm_dtype == "bf16" else torch.float32
         limit = max(1, int(bucket_mb * (1 << 20) / 4))
+        # at least ~4 buckets: a model whose gradients fit one bucket (GoogLeNet: 7M parameters,
+        # 28 MB) would otherwise reduce nothing until the whole backward is done, leaving the
+        # collective, the update and the all-gather exposed in front of the next forward
+        limit = min(limit, max(1 << 18, arena.total // 4))
         self.buckets: List[Bucket] = []
         self.update_fn = None      # overlapped per-bucket optimizer (enable_overlapped_update)
         self.side = None
