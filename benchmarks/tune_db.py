@@ -22,6 +22,8 @@ def main():
                                         "bowl:64")
     ap.add_argument("--out", default="")
     ap.add_argument("--keep", action="store_true", help="keep the shipped entries, time only missing keys")
+    ap.add_argument("--drop", default="", help="with --keep: first remove the entries of these op classes "
+                                                "(comma list, e.g. cws) so that they are re-timed")
     a = ap.parse_args()
     from cxxnet_amd.io.data import DataBatch
     from cxxnet_amd.models import load_conf
@@ -29,6 +31,9 @@ def main():
     from cxxnet_amd.ops import gemm as G
     if not a.keep:
         G._TUNE.clear()
+    for op in filter(None, a.drop.split(",")):
+        for k in [k for k in G._TUNE if k.split("|")[0] == op]:
+            del G._TUNE[k]
     for spec in a.models.split(","):
         name, b = spec.split(":")
         b = int(b)

@@ -555,13 +555,17 @@ void launch_t(const Operand &A, const Operand &B, const Epilogue &E, int groups,
 
 // Tile ids (BM x BN, waves along M x N):
 //   0: 128x128 (2x2)   1: 64x64 (2x2)   2: 64x128 (1x4)   3: 32x128 (1x4)
-//   4: 96x128 (1x4)    5: 128x64 (2x2)
+//   4: 96x128 (1x4)    5: 128x64 (2x2)   6: 128x96 (2x2)   7: 128x32 (4x1)
+// (6 / 7: weight-grad tiles for 96- / 16..32-output-channel convs -- AlexNet conv1, GoogLeNet's
+//  96/192/288-channel and 5x5-reduce layers -- whose j rows padded to 128 / 64 idled MFMA rows)
 #define CXN_T0(AM, BMo, VA, VB, EPI) launch_t<128, 128, 2, AM, BMo, VA, VB, EPI>
 #define CXN_T1(AM, BMo, VA, VB, EPI) launch_t<64, 64, 2, AM, BMo, VA, VB, EPI>
 #define CXN_T2(AM, BMo, VA, VB, EPI) launch_t<64, 128, 1, AM, BMo, VA, VB, EPI>
 #define CXN_T3(AM, BMo, VA, VB, EPI) launch_t<32, 128, 1, AM, BMo, VA, VB, EPI>
 #define CXN_T4(AM, BMo, VA, VB, EPI) launch_t<96, 128, 1, AM, BMo, VA, VB, EPI>
 #define CXN_T5(AM, BMo, VA, VB, EPI) launch_t<128, 64, 2, AM, BMo, VA, VB, EPI>
+#define CXN_T6(AM, BMo, VA, VB, EPI) launch_t<128, 96, 2, AM, BMo, VA, VB, EPI>
+#define CXN_T7(AM, BMo, VA, VB, EPI) launch_t<128, 32, 4, AM, BMo, VA, VB, EPI>
 
 #define CXN_CASE(AM, BMo, VA, VB, EPI, TID)                                                         \
   if (g.amode == AM && g.bmode == BMo && g.va == VA && g.vb == VB && g.epi == EPI && g.tile == TID) { \
@@ -601,6 +605,14 @@ int dispatch(const GemmArgs &g, const Operand &A, const Operand &B, const Epilog
   CXN_CASE(GATHER_MN, DIRECT_MN, 8, 8, EPI_F32_ATOMIC, 5)
   CXN_CASE(GATHER_MN, DIRECT_MN, 4, 8, EPI_F32_ATOMIC, 0)
   CXN_CASE(GATHER_MN, DIRECT_MN, 4, 8, EPI_F32_ATOMIC, 5)
+  CXN_CASE(GATHER_MN, DIRECT_MN, 8, 8, EPI_F32, 6)
+  CXN_CASE(GATHER_MN, DIRECT_MN, 4, 8, EPI_F32, 6)
+  CXN_CASE(GATHER_MN, DIRECT_MN, 8, 8, EPI_F32_ATOMIC, 6)
+  CXN_CASE(GATHER_MN, DIRECT_MN, 4, 8, EPI_F32_ATOMIC, 6)
+  CXN_CASE(GATHER_MN, DIRECT_MN, 8, 8, EPI_F32, 7)
+  CXN_CASE(GATHER_MN, DIRECT_MN, 4, 8, EPI_F32, 7)
+  CXN_CASE(GATHER_MN, DIRECT_MN, 8, 8, EPI_F32_ATOMIC, 7)
+  CXN_CASE(GATHER_MN, DIRECT_MN, 4, 8, EPI_F32_ATOMIC, 7)
   return -1;
 }
 #undef CXN_CASE

@@ -81,10 +81,11 @@ def _op(t, gstride=0, ld=0, rows=0, kdim=0, **geo):
 
 
 # tile id -> (BM, BN); must match TILES in gemm_mfma.hip
-TILES = {0: (128, 128), 1: (64, 64), 2: (64, 128), 3: (32, 128), 4: (96, 128), 5: (128, 64)}
+TILES = {0: (128, 128), 1: (64, 64), 2: (64, 128), 3: (32, 128), 4: (96, 128), 5: (128, 64), 6: (128, 96),
+         7: (128, 32)}
 CONV_FWD_TILES = (0, 4, 2, 3, 1)
 CONV_FWD_TILES_V4 = (0, 4, 2, 3)
-WGRAD_TILES = (0, 5)
+WGRAD_TILES = (0, 5, 6, 7)
 FC_TILES = (0, 5, 1)
 
 

@@ -163,3 +163,26 @@ def test_tuner_rejects_a_wrong_fast_tile(monkeypatch):
     assert t != 15
     assert any(k == "test-reject|1" and tl == 15 for k, tl, _ in gemm.TUNE_REJECTED)
     gemm._TUNE.pop("test-reject|1", None)
+
+
+@pytest.mark.parametrize("tile", gemm.WGRAD_TILES)
+@pytest.mark.parametrize("sig", [
+    (4, 27, 27, 96, 96, 5, 5, 1, 2, 2, 1),     # 96 output channels: tile 6's exact fit
+    (4, 14, 14, 480, 16, 1, 1, 1, 0, 0, 1),    # GoogLeNet 5x5-reduce: 16 channels (tile 7)
+    (2, 28, 28, 32, 32, 5, 5, 1, 2, 2, 1),     # 32 channels, 5x5
+    (2, 55, 55, 96, 256, 5, 5, 1, 2, 2, 2),    # grouped, 128 per group
+])
+def test_register_wgrad_tiles(tile, sig):
+    """Every register-kernel weight-grad tile (split-K fp32 atomics) at a forced (tile, split)
+    against torch, through the per-shape "cws" table entry the op looks up."""
+    key = "|".join(["cws"] + [str(v) for v in sig])
+    saved = gemm._TUNE.get(key)
+    gemm._TUNE[key] = tile * 100000 + 3
+    try:
+        err = check_conv("cw", sig)
+    finally:
+        if saved is None:
+            gemm._TUNE.pop(key, None)
+        else:
+            gemm._TUNE[key] = saved
+    assert err < 1e-2, (tile, sig, err)
