@@ -549,6 +549,157 @@ __global__ void pool_bwd_rows(const bf16_t *__restrict__ x, const uint8_t *__res
   *reinterpret_cast<uint4 *>(dx + idx) = pack8(g);
 }
 
+// Stride-1 3x3 max pooling (GoogLeNet's inception pool branches) on strips of R output rows per
+// thread: each input row of the strip is read once as a 3-tap row maximum (value + kw), and every
+// output row takes the row maxima of its three input rows -- (R + 2) * 3 loads per R outputs
+// instead of 9 per output.  Same first-max order (kh, then kw) and relu flags as pool_fwd_rows.
+template <int R>
+__global__ void pool_fwd_s1k3(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, uint8_t *__restrict__ arg,
+                              int H, int W, int C, int Ho, int Wo, int P, int relu, FastDiv fd_cv, FastDiv fd_row,
+                              FastDiv fd_hs, uint32_t total) {
+  const int CV = C / 8, HS = (Ho + R - 1) / R;
+  const uint32_t idx = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int row = static_cast<int>(fdiv(idx, fd_row));  // n * HS + strip
+  const int e = static_cast<int>(idx) - row * (Wo * CV);
+  const int n = static_cast<int>(fdiv(static_cast<uint32_t>(row), fd_hs)), st = row - n * HS;
+  const int wo = static_cast<int>(fdiv(static_cast<uint32_t>(e), fd_cv));
+  const int cv = e - wo * CV;
+  const int ho0 = st * R, h0 = ho0 - P, ws = wo - P;
+  const bf16_t *xb = x + static_cast<long>(n) * H * W * C + cv * 8;
+  float acc[R][8];
+  uint32_t am[R][8];
+#pragma unroll
+  for (int o = 0; o < R; ++o)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      acc[o][q] = -INFINITY;
+      am[o][q] = 0;
+    }
+#pragma unroll
+  for (int r = 0; r < R + 2; ++r) {
+    const int h = h0 + r;
+    if (h < 0 || h >= H) continue;
+    uint4 raw[3];
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int w = min(max(ws + kw, 0), W - 1);
+      raw[kw] = *reinterpret_cast<const uint4 *>(xb + (static_cast<long>(h) * W + w) * C);
+    }
+    float hm[8];
+    uint32_t hk[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      hm[q] = -INFINITY;
+      hk[q] = 0;
+    }
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      if (ws + kw < 0 || ws + kw >= W) continue;
+      float v[8];
+      unpack8(raw[kw], v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float a = (relu & 1) ? fmaxf(v[q], 0.f) : v[q];
+        if (a > hm[q]) {
+          hm[q] = a;
+          hk[q] = kw;
+        }
+      }
+    }
+    // output rows o of the strip whose window holds input row r at kh = r - o
+#pragma unroll
+    for (int o = 0; o < R; ++o) {
+      const int kh = r - o;
+      if (kh < 0 || kh > 2) continue;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (hm[q] > acc[o][q]) {
+          acc[o][q] = hm[q];
+          am[o][q] = static_cast<uint32_t>(kh * 3) + hk[q];
+        }
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < R; ++o) {
+    const int ho = ho0 + o;
+    if (ho >= Ho) break;
+    if (relu & 2)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) am[o][q] |= acc[o][q] > 0.f ? 0u : 0x80u;
+    const long off = ((static_cast<long>(n) * Ho + ho) * Wo + wo) * C + cv * 8;
+    *reinterpret_cast<uint4 *>(y + off) = pack8(acc[o]);
+    if (arg)
+      *reinterpret_cast<uint2 *>(arg + off) =
+          make_uint2(am[o][0] | am[o][1] << 8 | am[o][2] << 16 | am[o][3] << 24,
+                     am[o][4] | am[o][5] << 8 | am[o][6] << 16 | am[o][7] << 24);
+  }
+}
+
+// Backward of pool_fwd_s1k3 (max mode) on strips of R input rows: the (R + 2) x 3 windows that
+// cover the strip are read once each (dy + recorded offset) and routed to the strip's rows;
+// contributions arrive in (ho, wo) order as in pool_bwd_rows.  relu 1: times relu'(x); relu 2:
+// relu' is in the offsets' bit 7 (a marked window matches no tap).
+template <int R>
+__global__ void pool_bwd_s1k3(const bf16_t *__restrict__ x, const uint8_t *__restrict__ arg,
+                              const bf16_t *__restrict__ dy, bf16_t *__restrict__ dx, int H, int W, int C, int Ho,
+                              int Wo, int P, int relu, FastDiv fd_cv, FastDiv fd_row, FastDiv fd_hs, uint32_t total) {
+  const int CV = C / 8, HS = (H + R - 1) / R;
+  const uint32_t idx = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int row = static_cast<int>(fdiv(idx, fd_row));  // n * HS + strip
+  const int e = static_cast<int>(idx) - row * (W * CV);
+  const int n = static_cast<int>(fdiv(static_cast<uint32_t>(row), fd_hs)), st = row - n * HS;
+  const int w = static_cast<int>(fdiv(static_cast<uint32_t>(e), fd_cv));
+  const int cv = e - w * CV;
+  const int h0 = st * R;
+  float g[R][8];
+#pragma unroll
+  for (int o = 0; o < R; ++o)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) g[o][q] = 0.f;
+  // window rows ho = h + P - kh for the strip's rows h0..h0+R-1: ho0 = h0 + P - 2 .. h0 + R - 1 + P
+  const int hob = h0 + P - 2;
+#pragma unroll
+  for (int t = 0; t < R + 2; ++t) {
+    const int ho = hob + t;
+    if (ho < 0 || ho >= Ho) continue;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int wo = w + P - 2 + j;  // kw = w - (wo - P) = 2 - j
+      if (wo < 0 || wo >= Wo) continue;
+      const long o = ((static_cast<long>(n) * Ho + ho) * Wo + wo) * C + cv * 8;
+      float gv[8];
+      unpack8(*reinterpret_cast<const uint4 *>(dy + o), gv);
+      const uint2 a2 = *reinterpret_cast<const uint2 *>(arg + o);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int kh = (h0 + r) - (ho - P);  // the input row's tap in window row ho
+        if (kh < 0 || kh > 2) continue;
+        const uint32_t off = static_cast<uint32_t>(kh * 3 + (2 - j));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          g[r][q] += (((a2.x >> (8 * q)) & 0xff) == off) ? gv[q] : 0.f;
+          g[r][q + 4] += (((a2.y >> (8 * q)) & 0xff) == off) ? gv[q + 4] : 0.f;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int h = h0 + r;
+    if (h >= H) break;
+    const long idx8 = ((static_cast<long>(n) * H + h) * W + w) * C + cv * 8;
+    if (relu == 1) {
+      float xv[8];
+      unpack8(*reinterpret_cast<const uint4 *>(x + idx8), xv);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) g[r][q] = xv[q] > 0.f ? g[r][q] : 0.f;
+    }
+    *reinterpret_cast<uint4 *>(dx + idx8) = pack8(g[r]);
+  }
+}
+
 // ------------------------------------------------------------------ LRN
 // norm[c] = knorm + alpha/n * sum_{c' in [c-h, c+h] clipped} x[c']^2 ; y = x * norm^-beta
 // One thread per (pixel, 8 channels); halo of up to 8 channels each side via three 16-B loads.
@@ -1471,6 +1622,13 @@ CXN_API int cxn_conv_weight_flip_multi(const void *const *ws, void *const *wts, 
   }
   RET;
 }
+// stride-1 3x3 max pooling on row strips (pool_fwd_s1k3 / pool_bwd_s1k3); CXXNET_POOL_STRIPS=0 keeps
+// the one-output-per-thread kernels (A/B)
+static const int pool_strips = [] {
+  const char *e = getenv("CXXNET_POOL_STRIPS");
+  return (e && e[0] == '0') ? 0 : 1;
+}();
+
 CXN_API int cxn_pool_fwd(const void *x, void *y, void *arg, int N, int H, int W, int C, int Ho, int Wo, int KH, int KW, int S,
                          int P, int mode, int relu, void *stream) {
   if (C % 8 == 0) {
@@ -1482,7 +1640,15 @@ CXN_API int cxn_pool_fwd(const void *x, void *y, void *arg, int N, int H, int W,
       make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(Wo * (C / 8))),        \
       make_fastdiv(static_cast<uint32_t>(Ho)), static_cast<uint32_t>(total))
     const int sq = KH == KW ? KH : 0;
-    if (S == 2 && sq == 3) CXN_POOL_FWD(2, 3);
+    if (S == 1 && sq == 3 && mode == 0 && P <= 2 && pool_strips) {
+      constexpr int R = 4;
+      const int HS = (Ho + R - 1) / R;
+      const long tot = static_cast<long>(N) * HS * Wo * (C / 8);
+      pool_fwd_s1k3<R><<<cdiv(tot, NT), NT, 0, S_>>>(
+          (const bf16_t *)x, (bf16_t *)y, (uint8_t *)arg, H, W, C, Ho, Wo, P, relu,
+          make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(Wo * (C / 8))),
+          make_fastdiv(static_cast<uint32_t>(HS)), static_cast<uint32_t>(tot));
+    } else if (S == 2 && sq == 3) CXN_POOL_FWD(2, 3);
     else if (S == 1 && sq == 3) CXN_POOL_FWD(1, 3);
     else if (S == 2 && sq == 2) CXN_POOL_FWD(2, 2);
     else CXN_POOL_FWD(0, 0);
@@ -1512,7 +1678,15 @@ CXN_API int cxn_pool_bwd(const void *x, const void *arg, const void *dy, void *d
       relu, make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(W * (C / 8))),          \
       make_fastdiv(static_cast<uint32_t>(H)), static_cast<uint32_t>(total))
     const int sq = KH == KW ? KH : 0;
-    if (S == 2 && sq == 3) CXN_POOL_BWD(2, 3);
+    if (S == 1 && sq == 3 && mode == 0 && P <= 2 && pool_strips) {
+      constexpr int R = 4;
+      const int HS = (H + R - 1) / R;
+      const long tot = static_cast<long>(N) * HS * W * (C / 8);
+      pool_bwd_s1k3<R><<<cdiv(tot, NT), NT, 0, S_>>>(
+          (const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, H, W, C, Ho, Wo, P, relu,
+          make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(W * (C / 8))),
+          make_fastdiv(static_cast<uint32_t>(HS)), static_cast<uint32_t>(tot));
+    } else if (S == 2 && sq == 3) CXN_POOL_BWD(2, 3);
     else if (S == 1 && sq == 3) CXN_POOL_BWD(1, 3);
     else if (S == 2 && sq == 2) CXN_POOL_BWD(2, 2);
     else CXN_POOL_BWD(0, 0);

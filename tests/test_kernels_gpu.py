@@ -558,3 +558,35 @@ def test_conv_weight_flip_multi_matches_single():
     torch.cuda.synchronize()
     for (_, wt, _), ref in zip(items, refs):
         assert torch.equal(wt, ref)
+
+
+@pytest.mark.parametrize("H,p", [(28, 1), (14, 1), (7, 1), (9, 0), (13, 1), (6, 2)])
+@pytest.mark.parametrize("relu", [0, 1, 2])
+def test_pool_stride1_3x3_strips(H, p, relu):
+    """Stride-1 3x3 max pooling on row strips (pool_fwd_s1k3 / pool_bwd_s1k3, GoogLeNet's
+    inception pool branches): outputs, first-max offsets (on data with many exact ties) and
+    data-gradients against the CPU executor, for strip-ragged heights, pads 0-2 and the three
+    relu modes (2 = relu' from the offsets' bit 7)."""
+    N, C, k, s = 3, 24, 3, 1
+    g = torch.Generator().manual_seed(100 * H + p + relu)
+    x = torch.randint(-3, 4, (N, H, H + 1, C), generator=g).float() * 0.25
+    if relu == 2:
+        x = x.clamp_min(0)  # fused conv -> relu producer
+    Ho = ops.pool_out_size(H, k, s, p)
+    Wo = ops.pool_out_size(H + 1, k, s, p)
+    dy = rnd(N, Ho, Wo, C, seed=H)
+    y_ref = torch.empty(N, Ho, Wo, C)
+    st_ref = torch.empty(N, Ho, Wo, C, dtype=torch.uint8)
+    ops.pool_forward(x, y_ref, st_ref, k, k, s, p, "max", relu == 1)
+    dx_ref = torch.empty_like(x)
+    ops.pool_backward(x, st_ref, dy, dx_ref, k, k, s, p, "max", relu > 0)
+    xd = x.to(DEV, torch.bfloat16)
+    y = torch.empty(N, Ho, Wo, C, dtype=torch.bfloat16, device=DEV)
+    st = torch.empty(N, Ho, Wo, C, dtype=torch.uint8, device=DEV)
+    ops.pool_forward(xd, y, st, k, k, s, p, "max", relu == 1, mark_mask=relu == 2)
+    dx = torch.empty_like(xd)
+    ops.pool_backward(xd, st, dy.to(DEV, torch.bfloat16), dx, k, k, s, p, "max", relu)
+    torch.cuda.synchronize()
+    assert torch.equal(y.float().cpu(), y_ref)
+    assert torch.equal(st.cpu() & 0x7F, st_ref)
+    assert relerr(dx, dx_ref) < 1e-2
