@@ -1013,6 +1013,7 @@ void launch_pp(const GOperand &A, const GOperand &B, const GEpi &E, int groups, 
     CXG_TP(37, 64, 128, 1, 4, 2, 3) CXG_TP(38, 128, 256, 2, 4, 2, 3) CXG_TP(39, 64, 256, 2, 4, 3, 3)      \
     CXG_TP(70, 96, 256, 1, 4, 2, 3) CXG_TP(71, 96, 128, 1, 4, 2, 3) CXG_TP(72, 96, 128, 2, 2, 2, 0)       \
     CXG_TP(73, 160, 128, 1, 4, 2, 0) CXG_TP(74, 128, 96, 2, 2, 2, 0) CXG_TP(75, 64, 96, 2, 2, 2, 0)       \
+    CXG_T(76, 32, 128, 1, 4, 2) CXG_T(77, 32, 64, 1, 4, 3) CXG_T(78, 32, 256, 1, 4, 2)                    \
     default: return -1;                                                                                   \
   }
 #define CXG_MK_TILES  /* A MN-major (BM = 128), B K-major */                                              \
