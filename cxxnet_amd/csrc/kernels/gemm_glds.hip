@@ -298,13 +298,17 @@ __device__ __forceinline__ bf16x8 frag(const char *tile, int base, int kk, int l
 //             barriers instead of spreading it among the DMA issue -- cdna guide T5);
 // PIPE bit 1: both k-steps' fragments are read before the first MFMA (the k=32 reads are in
 //             flight under the k=0 MFMAs).
-template <int BM, int BN, int WGM, int WGN, int STAGES, int AMODE, int BMODE, int EPI, int PIPE = 0>
+// BMC (<= BM): A rows COMPUTED per block when it differs from the BM rows staged in LDS -- a
+// 48-row tile stages 64 rows (the DMA granularity is 8 rows x waves) but runs MFMAs and the
+// epilogue on 48 and steps i by 48 (AlexNet conv2's data-gradient onto 48 channels per group).
+template <int BM, int BN, int WGM, int WGN, int STAGES, int AMODE, int BMODE, int EPI, int PIPE = 0, int BMC = BM>
 __global__ void __launch_bounds__(64 * WGM * WGN, 1)
 gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_tiles, int ktiles_total) {
   constexpr int NW = WGM * WGN;  // 4 waves, or 8 (two per SIMD) for the large tiles
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows: a multiple of 8 rows per DMA x waves");
-  constexpr int WM = BM / WGM, WN = BN / WGN;
+  static_assert(BMC <= BM && BMC % (16 * WGM) == 0, "computed rows: whole 16-row fragments per wave");
+  constexpr int WM = BMC / WGM, WN = BN / WGN;
   static_assert(WM % 16 == 0 && WN % 16 == 0, "wave tile must be a multiple of 16");
   constexpr int MR = WM / 16, NR = WN / 16;
   using OA = Op<AMODE, BM, NW>;
@@ -321,7 +325,7 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
   const int g = wb.g;
   const uint32_t tile = wb.tile;
   const int ti = tile % tiles_i, tj = tile / tiles_i;  // i fastest: neighbours share the B panel
-  const int i0 = ti * BM, j0 = tj * BN;
+  const int i0 = ti * BMC, j0 = tj * BN;
   const int kt_beg = wb.slice * ksplit_tiles;
   const int kt_end = min(kt_beg + ksplit_tiles, ktiles_total);
   if (kt_beg >= kt_end) return;
@@ -551,15 +555,15 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, int STAGES, int AMODE, int BMODE, int EPI, int PIPE = 0>
+template <int BM, int BN, int WGM, int WGN, int STAGES, int AMODE, int BMODE, int EPI, int PIPE = 0, int BMC = BM>
 void launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int ksplit, hipStream_t s) {
-  const int ti = cdiv(A.rows, BM), tj = cdiv(B.rows, BN);
+  const int ti = cdiv(A.rows, BMC), tj = cdiv(B.rows, BN);
   const int ktiles = cdiv(A.kdim, BK);
   ksplit = ksplit < 1 ? 1 : (ksplit > ktiles ? ktiles : ksplit);
   const int per = cdiv(ktiles, ksplit);
   ksplit = cdiv(ktiles, per);
   dim3 grid(ti * tj, ksplit, groups);
-  hipLaunchKernelGGL((gemm_glds<BM, BN, WGM, WGN, STAGES, AMODE, BMODE, EPI, PIPE>), grid, dim3(64 * WGM * WGN), 0, s,
+  hipLaunchKernelGGL((gemm_glds<BM, BN, WGM, WGN, STAGES, AMODE, BMODE, EPI, PIPE, BMC>), grid, dim3(64 * WGM * WGN), 0, s,
                      A, B, E, ti, tj, per, ktiles);
 }
 
@@ -1003,6 +1007,8 @@ void launch_pp(const GOperand &A, const GOperand &B, const GEpi &E, int groups, 
   case ID: launch<BM, BN, WGM, WGN, ST, AM, BMo, EP>(A, B, E, groups, ksplit, s); return 0;
 #define CXG_TP(ID, BM, BN, WGM, WGN, ST, PIPE) \
   case ID: launch<BM, BN, WGM, WGN, ST, AM, BMo, EP, PIPE>(A, B, E, groups, ksplit, s); return 0;
+#define CXG_TC(ID, BM, BMC, BN, WGM, WGN, ST) \
+  case ID: launch<BM, BN, WGM, WGN, ST, AM, BMo, EP, 0, BMC>(A, B, E, groups, ksplit, s); return 0;
 #define CXG_KK_TILES                                                                                      \
   switch (tile) {                                                                                         \
     CXG_T(0, 128, 256, 1, 4, 3) CXG_T(1, 128, 128, 1, 4, 2) CXG_T(2, 128, 128, 2, 2, 3)                   \
@@ -1014,6 +1020,7 @@ void launch_pp(const GOperand &A, const GOperand &B, const GEpi &E, int groups, 
     CXG_TP(70, 96, 256, 1, 4, 2, 3) CXG_TP(71, 96, 128, 1, 4, 2, 3) CXG_TP(72, 96, 128, 2, 2, 2, 0)       \
     CXG_TP(73, 160, 128, 1, 4, 2, 0) CXG_TP(74, 128, 96, 2, 2, 2, 0) CXG_TP(75, 64, 96, 2, 2, 2, 0)       \
     CXG_T(76, 32, 128, 1, 4, 2) CXG_T(77, 32, 64, 1, 4, 3) CXG_T(78, 32, 256, 1, 4, 2)                    \
+    CXG_TC(79, 64, 48, 128, 1, 4, 2) CXG_TC(80, 64, 48, 256, 1, 4, 2) CXG_TC(81, 64, 48, 64, 1, 4, 3)     \
     default: return -1;                                                                                   \
   }
 #define CXG_MK_TILES  /* A MN-major (BM = 128), B K-major */                                              \
@@ -1081,6 +1088,7 @@ int dispatch(int amode, int bmode, int epi, int tile, const GOperand &A, const G
 #undef CXG_MK_TILES
 #undef CXG_KK_TILES
 #undef CXG_T
+#undef CXG_TC
 #undef CXG_TP
 
 }  // namespace

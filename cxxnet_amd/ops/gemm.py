@@ -124,7 +124,9 @@ GLDS_TILES = {0: (128, 256), 1: (128, 128), 2: (128, 128), 4: (192, 256), 5: (64
               70: (96, 256), 71: (96, 128), 72: (96, 128), 73: (160, 128), 74: (128, 96), 75: (64, 96),
               # 32-row tiles (K-major A): convs with 16..48 output channels (GoogLeNet's 5x5-reduce and
               # pool-projection layers) and their data-gradients onto 16..48 input channels
-              76: (32, 128), 77: (32, 64), 78: (32, 256)}
+              76: (32, 128), 77: (32, 64), 78: (32, 256),
+              # 48 computed rows on 64 staged (AlexNet conv2's data-gradient: 48 channels per group)
+              79: (48, 128), 80: (48, 256), 81: (48, 64)}
 # operand loaders of gemm_glds.hip
 GL_K, GL_KG, GL_MN, GL_MNG, GL_KR = 0, 1, 2, 3, 4  # K_DIRECT, K_GATHER, MN_DIRECT, MN_GATHER, K_ROWGATHER
 EPI_F32_ACC_G, EPI_F32_ATOMIC_G = 2, 3
@@ -143,7 +145,8 @@ _glds_cfg = {"on": os.environ.get("CXXNET_GEMM_GLDS", "1") != "0",
 # AlexNet shape (profiles/r14_glds_tiles.jsonl); 2 and 0 cover wide-i GEMMs (fc); the 8-wave
 # 128x256 / 64x256 tiles and the pipelined variants (30-41) win conv2/conv3 forward, fc6 forward
 # and several VGG shapes (profiles/r2_sweep_tiles.jsonl).
-GLDS_CANDS = (1, 7, 10, 15, 2, 0, 13, 17, 21, 25, 30, 31, 34, 37, 38, 39, 40, 41, 50, 51, 72, 76, 77, 78)
+GLDS_CANDS = (1, 7, 10, 15, 2, 0, 13, 17, 21, 25, 30, 31, 34, 37, 38, 39, 40, 41, 50, 51, 72, 76, 77, 78, 79, 80,
+              81)
 # conv weight-grad shapes missing from the shipped table are timed on first use too (else the
 # register kernel runs them)
 _CW_TUNE = os.environ.get("CXXNET_CW_TUNE", "0") == "1"
