@@ -93,7 +93,11 @@ class LayerContext:
 
     def __init__(self, device: torch.device, seed: int = 0):
         self.device = torch.device(device)
-        self.is_gpu = self.device.type == "cuda"
+        # is_gpu: the HIP-kernel (bf16) path; a GPU context in reference precision (fp32) runs the
+        # CPU path's torch formulas on device tensors (ops.mode)
+        from ..ops.mode import reference_precision
+        self.on_device = self.device.type == "cuda"
+        self.is_gpu = self.on_device and not reference_precision()
         self.act_dtype = torch.bfloat16 if self.is_gpu else torch.float32
         self.seed = seed
         # set by the trainer around an update step's backprop: the arena updater when the fc
@@ -115,7 +119,7 @@ class LayerContext:
     def bias_grad(self, dy2d, db, mask=None):
         """db += column sums of dy2d (mask: see ops.bias_grad), now or (deferred) at the end
         of the backward pass."""
-        if self.deferred_bias is not None and dy2d.is_cuda:
+        if self.deferred_bias is not None and self.is_gpu:
             self.deferred_bias.append((dy2d, db, mask))
             return
         from .. import ops

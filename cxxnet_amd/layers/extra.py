@@ -39,7 +39,7 @@ class BiasLayer(Layer):
 
     def forward(self, is_train, nodes_in, nodes_out):
         m = nodes_in[0].mat()
-        if m.is_cuda:  # y = 1*x + b on the BN affine kernel: mean 0, inv 1, slope 1
+        if self.ctx.is_gpu:  # y = 1*x + b on the BN affine kernel: mean 0, inv 1, slope 1
             st = self._affine(m.shape[1], m.device)
             L.affine_forward(m, m, st.mean, st.inv, self._ones, self.params[0].w)
         else:

@@ -99,7 +99,7 @@ class FullConnectLayer(Layer):
         which the weight-gradient still needs, lives where it goes); the scratch is copied
         back (with relu' when fused) after the update."""
         upd = getattr(self.ctx, "sgd_fuse", None)
-        if upd is None or not (getattr(self.ctx, "grad_overwrite", False) and self.w.overwrite) or not x.is_cuda:
+        if upd is None or not (getattr(self.ctx, "grad_overwrite", False) and self.w.overwrite) or not self.ctx.is_gpu:
             return False
         spec = self.w
         lr, wd, mom, clip = upd.hyper(spec, self.ctx.epoch)
@@ -271,7 +271,7 @@ class ConvolutionLayer(Layer):
         zero-bordered copy of x with a pad-0 geometry.  refresh=False reuses the forward's copy
         (x is unchanged until this layer's own backprop writes its gradient)."""
         g = self.geo
-        if not (self._prepad_on and x.is_cuda):
+        if not (self._prepad_on and self.ctx.is_gpu):
             return x, g
         N = x.shape[0]
         H2, W2 = g.H + 2 * g.pad_y, g.W + 2 * g.pad_x
@@ -450,7 +450,7 @@ class PoolingLayer(Layer):
         if relu and self._mask_in_state():
             relu = 2  # relu' of the argmax was recorded by the forward: no read of x
         conv = self.bias_of
-        if conv is not None and conv.b is not None and relu in (0, 2) and x.is_cuda and not deterministic():
+        if conv is not None and conv.b is not None and relu in (0, 2) and self.ctx.is_gpu and not deterministic():
             # the conv's bias gradient from this pool's output gradient (before it is consumed)
             dy = nodes_out[0].data
             self.ctx.bias_grad(dy.view(-1, dy.shape[-1]), conv.b.g,

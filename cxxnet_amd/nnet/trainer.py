@@ -80,6 +80,8 @@ class NetTrainer:
         self.check_nonfinite = 0
         self._nf_flag = None
         self.deterministic = int(os.environ.get("CXXNET_DETERMINISTIC", "0"))
+        # "bf16": HIP kernels; "fp32": the reference formulas in fp32 on the GPU (ops.mode)
+        self.precision = os.environ.get("CXXNET_PRECISION", "bf16")
         # observability: HIP-event timers around forward / backward+reduce / optimizer
         self.profile_step = 0
         self.trace_layers = int(os.environ.get("CXXNET_TRACE_LAYERS", "0"))  # roctx range per layer
@@ -131,6 +133,10 @@ class NetTrainer:
             self.overlap_update = int(val)
         elif name == "cuda_graph":
             self.cuda_graph = int(val)
+        elif name == "precision":
+            if val not in ("bf16", "fp32"):
+                raise ValueError(f"precision must be bf16 or fp32, not {val}")
+            self.precision = val
         elif name == "check_nonfinite":
             self.check_nonfinite = int(val)
         elif name == "deterministic":
@@ -178,6 +184,8 @@ class NetTrainer:
         return self._device().type == "cuda" and (self.world > 1 or bool(self.dp_force)) and not gather
 
     def _apply_modes(self):
+        from ..ops.mode import set_reference_precision
+        set_reference_precision(self._device().type == "cuda" and self.precision == "fp32")
         if self._device().type == "cuda":
             from ..ops import gemm
             if self.deterministic or gemm.deterministic():
@@ -484,7 +492,7 @@ class NetTrainer:
 
     def _graph_eligible(self) -> bool:
         net, red = self.net, self.reducer
-        if not (self.cuda_graph != 0 and net.device.type == "cuda" and self.update_period == 1 and red is not None):
+        if not (self.cuda_graph != 0 and net.ctx.is_gpu and self.update_period == 1 and red is not None):
             return False
         if self.cuda_graph < 0:
             return red.handles_update and self._local_batch() <= 64

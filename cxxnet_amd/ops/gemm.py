@@ -21,6 +21,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import native
+from .mode import native as _native_t
 
 DIRECT_K, DIRECT_MN, GATHER_K, GATHER_MN = 0, 1, 2, 3
 EPI_BF16, EPI_F32, EPI_F32_ACC, EPI_F32_ATOMIC = 0, 1, 2, 3
@@ -459,7 +460,7 @@ def _wgrad_pad_buf(cout, kr, device):
 
 def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
     """y = conv(x, w) + bias (optionally relu).  x/y NHWC."""
-    if not x.is_cuda:
+    if not _native_t(x):
         xn = x.permute(0, 3, 1, 2)
         out = F.conv2d(xn, _w_nchw(w), bias, stride=g.stride, padding=(g.pad_y, g.pad_x), groups=g.groups)
         if relu:
@@ -506,7 +507,7 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
 def conv_weight_flip_multi(items):
     """wt = w with (Cout, Cin) swapped and the taps reversed (the data-gradient GEMM's weight
     operand), for every (w, wt, geometry) of `items` in one launch."""
-    items = [it for it in items if it[0].is_cuda]
+    items = [it for it in items if _native_t(it[0])]
     if not items:
         return
     n = len(items)
@@ -523,7 +524,7 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False, wt_
     """dx = conv_transpose(dy, w); dx overwritten.  mask_relu: dx holds relu(z) on entry
     (fused producer->relu) and the result is multiplied by relu'(z).  wt_ready: wt_buf already
     holds the flipped weights (conv_weight_flip_multi at the start of the backward pass)."""
-    if not dy.is_cuda:
+    if not _native_t(dy):
         dyn = dy.permute(0, 3, 1, 2)
         out = torch.nn.grad.conv2d_input((g.N, g.C, g.H, g.W), _w_nchw(w), dyn, stride=g.stride,
                                          padding=(g.pad_y, g.pad_x), groups=g.groups).permute(0, 2, 3, 1)
@@ -564,7 +565,7 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
     (Folding the bias gradient into this GEMM was measured a wash on GoogLeNet and its
     extra registers slowed every weight-grad kernel by 5-25%: profiles/r2_inception_bias_fold.md,
     profiles/r2_ab_bias_fold_regression.md.)"""
-    if not x.is_cuda:
+    if not _native_t(x):
         xn = x.permute(0, 3, 1, 2)
         dyn = dy.permute(0, 3, 1, 2)
         gw = torch.nn.grad.conv2d_weight(xn, (g.Cout, g.cg_in, g.KH, g.KW), dyn, stride=g.stride,
@@ -644,7 +645,7 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
 # ----------------------------------------------------------------------------- fully connected
 def fc_forward(x, w, bias, y, relu=False, out_fp32=False):
     """y[B][nout] = x[B][nin] . w[nout][nin]^T + bias."""
-    if not x.is_cuda:
+    if not _native_t(x):
         out = x @ w.t()
         if bias is not None:
             out = out + bias
@@ -664,7 +665,7 @@ def fc_forward(x, w, bias, y, relu=False, out_fp32=False):
 
 def fc_backward_data(dy, w, dx, mask_relu=False):
     """dx[B][nin] = dy[B][nout] . w[nout][nin]  (mask_relu: see conv_backward_data)."""
-    if not dy.is_cuda:
+    if not _native_t(dy):
         out = dy @ w
         if mask_relu:
             out = out * (dx > 0).to(out.dtype)
@@ -684,7 +685,7 @@ def fc_backward_weight_sgd(x, dy, w, m, wb, lr, wd, mom, clip) -> bool:
     gradient never goes to memory.  Same arithmetic as the fused optimizer, so the
     result is bitwise the unfused one.  False when the LDS-DMA kernel does not cover the
     shape (the caller then takes the unfused path)."""
-    if not (x.is_cuda and _glds_cfg["on"] and _use("fw")):
+    if not (_native_t(x) and _glds_cfg["on"] and _use("fw")):
         return False
     Bn, nin = x.shape
     nout = dy.shape[1]
@@ -701,7 +702,7 @@ def fc_backward_weight_sgd(x, dy, w, m, wb, lr, wd, mom, clip) -> bool:
 
 def fc_backward_weight(x, dy, dw, overwrite=False):
     """dw[nout][nin] += dy^T . x  (fp32 accumulate; overwrite=True stores instead)."""
-    if not x.is_cuda:
+    if not _native_t(x):
         if overwrite:
             dw.copy_(dy.t() @ x)
         else:

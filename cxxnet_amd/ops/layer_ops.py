@@ -9,6 +9,7 @@ from __future__ import annotations
 import torch
 
 from .. import native
+from .mode import native as _native_t
 from .gemm import _stream
 from .nn import _hash_u32, effective_seed
 
@@ -35,7 +36,7 @@ def rand_fill(t: torch.Tensor, seed: int, dist: str, a: float, b: float):
     n = t.numel()
     d = 0 if dist == "uniform" else 1
     seed &= 0xFFFFFFFF
-    if t.is_cuda:
+    if t.is_cuda:  # fp32 kernel: also in reference-precision mode
         native.check(_k().cxn_rand_fill(t.data_ptr(), n, seed, d, float(a), float(b), _stream()), "rand_fill")
         return t
     flat = t.view(-1)
@@ -71,7 +72,7 @@ def bn_forward(x2d, y2d, slope, bias, eps, st: BNState, is_train: bool):
     train AND test; in training the input node is overwritten with x-hat and a copy of x is
     kept for backward."""
     rows, C = x2d.shape
-    if not x2d.is_cuda:
+    if not _native_t(x2d):
         x = x2d.float()
         mean = x.mean(0)
         var = ((x - mean) ** 2).mean(0)
@@ -108,7 +109,7 @@ def affine_forward(x2d, y2d, mean, inv, slope, bias):
 def bn_backward(g2d, dx2d, slope, gslope, gbias, st: BNState, prop_grad: bool):
     """Reference BatchNormLayer::Backprop (batch_norm_layer-inl.hpp:138-179)."""
     rows, C = g2d.shape
-    if not g2d.is_cuda:
+    if not _native_t(g2d):
         x = st.xsave.float()
         g = g2d.float()
         mean, inv = st.mean, st.inv
@@ -143,7 +144,7 @@ def _prelu_mask_ref(x2d, slope, seed, counter, rnd):
 def prelu_forward(x2d, y2d, slope, seed, counter, rnd):
     """y = x > 0 ? x : x * clamp(slope * noise, 0, 1)   (reference prelu_layer-inl.hpp:111-135)."""
     rows, C = x2d.shape
-    if not x2d.is_cuda:
+    if not _native_t(x2d):
         x = x2d.float()
         y2d.copy_(torch.where(x > 0, x, x * _prelu_mask_ref(x2d, slope, seed, counter, rnd)))
         return
@@ -154,7 +155,7 @@ def prelu_forward(x2d, y2d, slope, seed, counter, rnd):
 def prelu_backward(x2d, g2d, dx2d, slope, gslope, seed, counter, rnd, prop_grad, ws=None):
     """gslope += sum min(x, 0) * g; dx = x > 0 ? g : g * mask  (reference :137-152).  dx may alias x."""
     rows, C = x2d.shape
-    if not x2d.is_cuda:
+    if not _native_t(x2d):
         x, g = x2d.float(), g2d.float()
         gslope.add_((torch.clamp(x, max=0) * g).sum(0))
         if prop_grad:
@@ -181,7 +182,7 @@ def _insanity_div_ref(n, lb, ub, train, seed, counter, device):
 
 def insanity_forward(x, y, y2, lb, ub, train, seed, counter):
     """y (and y2) = x > 0 ? x : x / U[lb, ub)  (test: / ((lb + ub) / 2))."""
-    if not x.is_cuda:
+    if not _native_t(x):
         d = _insanity_div_ref(x.numel(), lb, ub, train, seed, counter, x.device).view_as(x)
         xf = x.float()
         out = torch.where(xf > 0, xf, xf / d)
@@ -196,7 +197,7 @@ def insanity_forward(x, y, y2, lb, ub, train, seed, counter):
 
 def insanity_backward(y, g, dx, lb, ub, train, seed, counter):
     """dx = y > 0 ? g : g / d with forward's draws (dx may alias y)."""
-    if not y.is_cuda:
+    if not _native_t(y):
         d = _insanity_div_ref(y.numel(), lb, ub, train, seed, counter, y.device).view_as(y)
         yf, gf = y.float(), g.float()
         dx.copy_(torch.where(yf > 0, gf, gf / d))
@@ -224,9 +225,9 @@ def _shift_ref(N, H, W, C, keep, seed, counter, device):
 def ins_pool_forward(x, y, ysave, K, S, keep, seed, counter):
     N, H, W, C = x.shape
     Ho, Wo = y.shape[1], y.shape[2]
-    if not x.is_cuda:
+    if not _native_t(x):
         src = x.reshape(-1)[_shift_ref(N, H, W, C, keep, seed, counter, x.device)].float()  # shifted image
-        out = torch.full((N, Ho, Wo, C), float("-inf"))
+        out = torch.full((N, Ho, Wo, C), float("-inf"), device=x.device)
         for py in range(Ho):
             for px in range(Wo):
                 win = src[:, py * S:min(py * S + K, H), px * S:min(px * S + K, W), :]
@@ -244,9 +245,9 @@ def ins_pool_backward(x, ypool, gy, dx, K, S, keep, seed, counter):
     """dx must not alias x."""
     N, H, W, C = x.shape
     Ho, Wo = gy.shape[1], gy.shape[2]
-    if not x.is_cuda:
+    if not _native_t(x):
         vsrc = x.reshape(-1)[_shift_ref(N, H, W, C, keep, seed, counter, x.device)].float()
-        out = torch.zeros(N, H, W, C)
+        out = torch.zeros(N, H, W, C, device=x.device)
         yp, g = ypool.float(), gy.float()
         for py in range(Ho):
             for px in range(Wo):

@@ -1,0 +1,24 @@
+"""Precision mode of the GPU executor.
+
+bf16 (default): activations bf16, every op on the HIP kernels (fp32 accumulation, fp32 master
+weights and optimizer state).  fp32 ("precision = fp32" in a conf, or set_reference_precision):
+the GPU runs the executor's fp32 reference formulas -- the torch code the CPU path uses -- on
+device tensors, the reference's own precision (cxxnet's real_t = float).  It is a parity oracle
+at production batch sizes (tests/test_fp32_mode_gpu.py compares the bf16 kernels against it on
+the real AlexNet graph), not a fast path."""
+import torch
+
+_REF = {"on": False}
+
+
+def set_reference_precision(on: bool = True):
+    _REF["on"] = bool(on)
+
+
+def reference_precision() -> bool:
+    return _REF["on"]
+
+
+def native(t: torch.Tensor) -> bool:
+    """Whether an op on tensor t runs its HIP kernel (GPU tensor, bf16 mode)."""
+    return t.is_cuda and not _REF["on"]

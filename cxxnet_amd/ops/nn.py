@@ -12,6 +12,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import native
+from .mode import native as _native_t
 from .gemm import _stream
 
 ACT_KIND = {"relu": 0, "sigmoid": 1, "tanh": 2, "xelu": 3}
@@ -26,7 +27,7 @@ def input_to_nhwc(x_nchw: torch.Tensor, out: torch.Tensor, scale: float = 1.0):
     """NCHW fp32 batch -> NHWC node (bf16 on GPU), zero-padding extra channels."""
     N, C, H, W = x_nchw.shape
     Cp = out.shape[-1]
-    if not out.is_cuda:
+    if not _native_t(out):
         out.zero_()
         out[..., :C].copy_(x_nchw.permute(0, 2, 3, 1) * scale)
         return
@@ -38,7 +39,7 @@ def input_to_nhwc(x_nchw: torch.Tensor, out: torch.Tensor, scale: float = 1.0):
 def image_to_nhwc(img, out: torch.Tensor):
     """U8Images batch -> NHWC input node with the augmenter arithmetic fused
     (GPU: one kernel over uint8 pixels; CPU: the fp32 reference)."""
-    if not out.is_cuda:
+    if not _native_t(out):
         input_to_nhwc(img.to_float(), out)
         return
     B, C, h, w = img.shape
@@ -67,7 +68,7 @@ def image_to_nhwc(img, out: torch.Tensor):
 def nhwc_to_nchw(x: torch.Tensor, C: int) -> torch.Tensor:
     """NHWC node (any dtype) -> NCHW fp32 tensor with C logical channels."""
     N, H, W, Cp = x.shape
-    if not x.is_cuda:
+    if not _native_t(x):
         return x[..., :C].permute(0, 3, 1, 2).float().contiguous()
     out = torch.empty((N, C, H, W), dtype=torch.float32, device=x.device)
     native.check(_k().cxn_nhwc_bf16_to_nchw_f32(x.data_ptr(), out.data_ptr(), N, C, H, W, Cp, _stream()),
@@ -77,7 +78,7 @@ def nhwc_to_nchw(x: torch.Tensor, C: int) -> torch.Tensor:
 
 def transpose(x: torch.Tensor, y: torch.Tensor, B: int, R: int, Cc: int):
     """y[b][Cc][R] = x[b][R][Cc]."""
-    if not x.is_cuda:
+    if not _native_t(x):
         y.view(B, Cc, R).copy_(x.view(B, R, Cc).transpose(1, 2))
         return
     native.check(_k().cxn_transpose(x.data_ptr(), y.data_ptr(), B, R, Cc, _stream()), "transpose")
@@ -110,8 +111,8 @@ def _pool_ref(x, KH, KW, S, P, mode, relu, Ho, Wo):
         out, ind = out[:, :, :Ho, :Wo], ind[:, :, :Ho, :Wo]
         Wp = xp.shape[3]
         ih, iw = ind // Wp, ind % Wp
-        ho = torch.arange(Ho).view(1, 1, Ho, 1) * S
-        wo = torch.arange(Wo).view(1, 1, 1, Wo) * S
+        ho = torch.arange(Ho, device=x.device).view(1, 1, Ho, 1) * S
+        wo = torch.arange(Wo, device=x.device).view(1, 1, 1, Wo) * S
         arg = ((ih - ho) * KW + (iw - wo)).to(torch.uint8).permute(0, 2, 3, 1)
     else:
         out = F.avg_pool2d(xp, (KH, KW), S) * (KH * KW)
@@ -130,7 +131,7 @@ def pool_forward(x, y, state, KH, KW, S, P, mode: str, relu=False, mark_mask=Fal
     m = POOL_MODE[mode]
     if m == 0 and KH * KW > 255:
         raise ValueError("max pooling window larger than 255 elements is not supported")
-    if not x.is_cuda:
+    if not _native_t(x):
         out, arg = _pool_ref(x, KH, KW, S, P, m, relu, Ho, Wo)
         y.copy_(out)
         if state is not None and arg is not None:
@@ -156,7 +157,7 @@ def pool_backward(x, state, dy, dx, KH, KW, S, P, mode: str, relu=False, dbias=N
     N, H, W, C = x.shape
     Ho, Wo = dy.shape[1], dy.shape[2]
     m = POOL_MODE[mode]
-    if not x.is_cuda:
+    if not _native_t(x):
         g = torch.zeros_like(dy.new_empty(N, H + 2 * P + KH + S, W + 2 * P + KW + S, C))
         for ho in range(Ho):
             hs = ho * S
@@ -198,9 +199,9 @@ def pool_backward_tie_all(x, y, dy, dx, KH, KW, S, P, relu=False):
     gradient masked by relu'(x).  y: the saved pooled output."""
     N, H, W, C = x.shape
     Ho, Wo = dy.shape[1], dy.shape[2]
-    if not x.is_cuda:
+    if not _native_t(x):
         xv = x.clamp_min(0) if relu else x
-        g = torch.zeros((N, H + 2 * P + KH + S, W + 2 * P + KW + S, C), dtype=dy.dtype)
+        g = torch.zeros((N, H + 2 * P + KH + S, W + 2 * P + KW + S, C), dtype=dy.dtype, device=dy.device)
         xp = torch.full_like(g, float("nan"))  # padding never equals a max
         xp[:, P:P + H, P:P + W, :] = xv
         for ho in range(Ho):
@@ -230,7 +231,7 @@ def _lrn_norm(x, nsize, alpha, knorm):
 
 
 def lrn_forward(x, y, nsize, alpha, beta, knorm):
-    if not x.is_cuda:
+    if not _native_t(x):
         y.copy_(x * _lrn_norm(x, nsize, alpha, knorm).pow(-beta))
         return
     N, H, W, C = x.shape
@@ -241,7 +242,7 @@ def lrn_forward(x, y, nsize, alpha, beta, knorm):
 def lrn_backward(x, dy, dx, nsize, alpha, beta, knorm, mask_relu=False):
     """dx = d LRN / dx (dx may alias x; it must not alias dy).  mask_relu: x is relu(z) of a
     fused producer, so dx is also multiplied by relu'(z) = (x > 0)."""
-    if not x.is_cuda:
+    if not _native_t(x):
         norm = _lrn_norm(x, nsize, alpha, knorm)
         t = dy * x * norm.pow(-beta - 1)
         C = x.shape[-1]
@@ -281,7 +282,7 @@ def _act_grad_ref(kind, y, b):
 
 def act_forward(kind, x, y, y2=None, b=5.0):
     """y = f(x); when y2 is given it also receives f(x) (in-place write of the input node)."""
-    if not x.is_cuda:
+    if not _native_t(x):
         out = _act_ref(kind, x, b)
         y.copy_(out)
         if y2 is not None:
@@ -293,7 +294,7 @@ def act_forward(kind, x, y, y2=None, b=5.0):
 
 def act_backward(kind, y, dy, dx, b=5.0):
     """dx = dy * f'(y) (gradient in terms of the forward output)."""
-    if not y.is_cuda:
+    if not _native_t(y):
         dx.copy_(dy * _act_grad_ref(kind, y, b))
         return
     native.check(_k().cxn_act_bwd(y.data_ptr(), dy.data_ptr(), dx.data_ptr(), y.numel(), ACT_KIND[kind], float(b),
@@ -330,8 +331,8 @@ def dropout_apply(x, y, seed: int, pkeep: float, counter=None):
     counter: optional int32 device tensor; the mask seed is hash(counter, seed), read on
     device, so a captured HIP graph draws a new mask on every replay.
     """
-    if not x.is_cuda:
-        m = dropout_mask_ref(x.numel(), effective_seed(seed, counter), pkeep).view_as(x).to(x.dtype)
+    if not _native_t(x):
+        m = dropout_mask_ref(x.numel(), effective_seed(seed, counter), pkeep, x.device).view_as(x).to(x.dtype)
         y.copy_(x * m)
         return
     native.check(_k().cxn_dropout(x.data_ptr(), y.data_ptr(), x.numel(), seed & 0xFFFFFFFF,
@@ -342,7 +343,7 @@ def dropout_apply(x, y, seed: int, pkeep: float, counter=None):
 # ----------------------------------------------------------------------------- softmax / losses
 def softmax_forward(x, y, p32=None):
     """Row softmax of x[rows][K] into y (and the fp32 copy p32)."""
-    if not x.is_cuda:
+    if not _native_t(x):
         p = torch.softmax(x.float(), dim=1)
         y.copy_(p)
         if p32 is not None:
@@ -360,7 +361,7 @@ def loss_grad(kind: str, node, label, scale: float, p32=None):
     """node <- (pred - target) * scale, pred = p32 if given else node.  label fp32 [rows][lw]."""
     rows, K = node.shape
     lw = label.shape[1]
-    if not node.is_cuda:
+    if not _native_t(node):
         p = p32 if p32 is not None else node
         if kind == "softmax":
             oh = torch.zeros_like(p)
@@ -393,7 +394,7 @@ def bias_grad(dy2d, db, mask=None):
     offsets recorded with relu' in bit 7 (pool_forward(mark_mask=True)); an entry whose bit 7
     is set counts as zero -- dy2d is then a max-pool's output gradient and the sum is the
     bias gradient of the conv in front of the pool (see colsum_multi)."""
-    if not dy2d.is_cuda:
+    if not _native_t(dy2d):
         if mask is not None:
             dy2d = dy2d * (mask < 128).to(dy2d.dtype)
         db.add_(dy2d.float().sum(0))
@@ -417,7 +418,7 @@ def _det() -> bool:
 
 def bias_fast_ok(d, m=None) -> bool:
     """Served by the one-launch colsum_multi kernel (no workspace, no temporaries)."""
-    return d.is_cuda and d.shape[1] % 8 == 0 and d.is_contiguous() and (m is None or m.is_contiguous())
+    return _native_t(d) and d.shape[1] % 8 == 0 and d.is_contiguous() and (m is None or m.is_contiguous())
 
 
 def bias_grad_multi(items):
@@ -427,7 +428,7 @@ def bias_grad_multi(items):
     fast = [it for it in items if bias_fast_ok(it[0], it[2])]
     for d, b, m in items:
         if not bias_fast_ok(d, m):
-            if m is not None and d.is_cuda:
+            if m is not None and _native_t(d):
                 bias_grad(d * (m < 128).to(d.dtype), b)
             else:
                 bias_grad(d, b, m)
@@ -448,14 +449,14 @@ def bias_grad_multi(items):
 
 
 def cast_to_bf16(src_f32, dst_bf16):
-    if not src_f32.is_cuda:
+    if not _native_t(src_f32):
         dst_bf16.copy_(src_f32)
         return
     native.check(_k().cxn_cast_f32_bf16(src_f32.data_ptr(), dst_bf16.data_ptr(), src_f32.numel(), _stream()), "cast")
 
 
 def add(a, b, y):
-    if not a.is_cuda:
+    if not _native_t(a):
         torch.add(a, b, out=y)
         return
     native.check(_k().cxn_add_bf16(a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), _stream()), "add")
@@ -468,7 +469,7 @@ def _vec8(*ts):
 
 def fanout_copy(src, dsts):
     """dst[k] = src for every dst (split forward): the source is read once per 4 copies."""
-    if not src.is_cuda or not _vec8(src, *dsts):
+    if not _native_t(src) or not _vec8(src, *dsts):
         for d in dsts:
             d.copy_(src)
         return
@@ -485,7 +486,7 @@ def sum_into(y, srcs):
         if y.data_ptr() != srcs[0].data_ptr():
             y.copy_(srcs[0])
         return
-    if not y.is_cuda or not _vec8(y, *srcs):
+    if not _native_t(y) or not _vec8(y, *srcs):
         acc = srcs[0].float()
         for t in srcs[1:]:
             acc = acc + t.float()
@@ -504,7 +505,7 @@ def concat_channels(ins, out, backward=False, mask=()):
     """NHWC channel concat of `ins` into `out` (forward) or the gradient slices of `out` back
     into `ins` (backward; relu' for the input indices in `mask`), one launch on the GPU.
     Returns False when the kernel does not cover the shapes (the caller copies per input)."""
-    if not out.is_cuda or len(ins) > 4:
+    if not _native_t(out) or len(ins) > 4:
         return False
     n = len(ins)
     Ct = out.shape[-1]
@@ -528,7 +529,7 @@ def channel_copy(src, soff, dst, doff, cc, accumulate=False, mask_relu=False):
     mask_relu: dst holds relu(z) on entry; the copy keeps src only where dst > 0 (relu')."""
     Cs, Cd = src.shape[-1], dst.shape[-1]
     npix = src.numel() // Cs
-    if not src.is_cuda:
+    if not _native_t(src):
         d = dst.view(npix, Cd)[:, doff:doff + cc]
         s = src.view(npix, Cs)[:, soff:soff + cc]
         if accumulate:
