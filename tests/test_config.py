@@ -114,3 +114,17 @@ def test_layer_param_pod():
     q = rt().LayerParam.from_bytes(p.to_bytes())
     assert (q.kernel_height, q.kernel_width, q.pad_x, q.pad_y, q.random_type) == (5, 5, 2, 2, 1)
     assert q.temp_col_max == 64 << 18 and q.init_uniform == -1.0
+
+
+def test_precision_key():
+    """`precision` accepts bf16 / fp32; on the CPU it changes nothing (the CPU path is fp32)."""
+    import pytest as _pytest
+    from cxxnet_amd.nnet import NetTrainer
+    from cxxnet_amd.ops.mode import reference_precision
+    tr = NetTrainer()
+    tr.set_param("precision", "fp32")
+    assert tr.precision == "fp32"
+    with _pytest.raises(ValueError):
+        tr.set_param("precision", "fp16")
+    tr._apply_modes()
+    assert not reference_precision()  # no GPU device: the host executor is fp32 already
