@@ -48,7 +48,13 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef __attribute__((address_space(3))) void lds_void;
 
 enum { K_DIRECT = 0, K_GATHER = 1, MN_DIRECT = 2, MN_GATHER = 3, K_ROWGATHER = 4 };
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_ACC = 2, EPI_F32_ATOMIC = 3, EPI_F32_SGD = 4 };
+// EPI_BF16_DB: the bf16 epilogue that also sums its stored output per column i -- a conv
+// data-gradient that writes the gradient of the conv below it (through a fused relu) hands over
+// that conv's bias gradient, so that gradient is never re-read.  Each wave writes its column sums
+// as one row of a partials workspace (row = j-tile x wave column, no atomics: one fp32 atomic per
+// column per wave put ~10^5 adders on each of VGG conv1_1's 64 addresses and ran 3.7x slower),
+// and db_partials_reduce adds the rows into dbias.
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_ACC = 2, EPI_F32_ATOMIC = 3, EPI_F32_SGD = 4, EPI_BF16_DB = 5 };
 
 struct GOperand {
   const bf16_t *ptr;
@@ -75,6 +81,10 @@ struct GEpi {
   float *sgd_w, *sgd_m;
   bf16_t *sgd_wb;
   float lr, wd, mom, clip;
+  float *dbias;  // EPI_BF16_DB: partials workspace [tiles_j * WGN][part_ld] (column g * bias_gstride + i)
+  int part_ld;
+  long part_elems;     // workspace capacity
+  float *dbias_final;  // += the workspace's column sums (db_partials_reduce)
 };
 
 __device__ __forceinline__ float sgd_step(const GEpi &E, float g, float &m, float w) {
@@ -439,8 +449,11 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
   // are loaded once here instead of once per output row
   constexpr int LPR_B = WM / 8;  // lanes per output row (8 bf16 per lane)
   const int il_b = (lane % LPR_B) * 8;
-  float bias8[8];
-  if constexpr (EPI == EPI_BF16) {
+  constexpr bool BF = EPI == EPI_BF16 || EPI == EPI_BF16_DB;
+  float bias8[8], bsum[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bsum[e] = 0.f;
+  if constexpr (BF) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) bias8[e] = (bias && ibase + il_b + e < Mi) ? bias[ibase + il_b + e] : 0.f;
   }
@@ -452,7 +465,7 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     constexpr bool kPartialLanes = (64 / (WM / 8)) * (WM / 8) < 64 || (64 / (WM / 4)) * (WM / 4) < 64;
     wave_lds_handoff<kPartialLanes>();
-    if constexpr (EPI == EPI_BF16) {
+    if constexpr (BF) {
       bf16_t *out = reinterpret_cast<bf16_t *>(E.out) + g * E.gstride;
       constexpr int LPR = LPR_B;
       constexpr int RPI = 64 / LPR;  // rows per pass
@@ -479,11 +492,19 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
 #pragma unroll
               for (int e = 0; e < 8; ++e) f[e] = old[e] > 0.f ? f[e] : 0.f;
             }
-            *reinterpret_cast<uint4 *>(dst) = pack8(f);
+            const uint4 packed = pack8(f);
+            *reinterpret_cast<uint4 *>(dst) = packed;
+            if constexpr (EPI == EPI_BF16_DB) {  // sum what was stored (bf16), as a separate pass would
+              float r[8];
+              unpack8(packed, r);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) bsum[e] += r[e];
+            }
           } else {
             for (int e = 0; e < 8 && i + e < Mi; ++e) {
               if (E.mask_relu && !(bf2f(dst[e]) > 0.f)) f[e] = 0.f;
               dst[e] = f2bf(f[e]);
+              if constexpr (EPI == EPI_BF16_DB) bsum[e] += bf2f(dst[e]);
             }
           }
         }
@@ -553,18 +574,71 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
     __builtin_amdgcn_s_waitcnt(0xc07f);
     wave_lds_handoff<kPartialLanes>();
   }
+  if constexpr (EPI == EPI_BF16_DB) {
+    // lanes l and l + k * LPR_B served the same 8 columns: their sums meet in this wave's (now
+    // free) staging area, then one fp32 atomic per column per wave
+    static_assert(16 * (WM + 4) >= 64 * 9, "staging area holds the lane sums");
+    constexpr int RPI_B = 64 / LPR_B;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ep[lane * 9 + e] = bsum[e];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    wave_lds_handoff<true>();
+    if (lane < LPR_B) {
+      float *row = E.dbias + static_cast<long>(tj * WGN + wj_) * E.part_ld + g * E.bias_gstride;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < RPI_B; ++q) t += ep[(lane + q * LPR_B) * 9 + e];
+        const int i = ibase + lane * 8 + e;
+        if (i < Mi) row[i] = t;
+      }
+    }
+  }
+}
+
+// db[c] += sum_r part[r][c] (r < nrows, row stride ld): 32 columns x 8 row groups per block over
+// one chunk of rows, one atomic per column per chunk (~10^3 adders per address at most)
+__global__ void db_partials_reduce(const float *__restrict__ part, int nrows, int ld, float *__restrict__ db) {
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const int rg = threadIdx.x >> 5;
+  const int per = (nrows + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * per, r1 = min(nrows, r0 + per);
+  float acc = 0.f;
+  if (c < ld)
+    for (int r = r0 + rg; r < r1; r += 8) acc += part[static_cast<long>(r) * ld + c];
+  __shared__ float red[8][33];
+  red[rg][threadIdx.x & 31] = acc;
+  __syncthreads();
+  if (rg == 0 && c < ld) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t += red[q][threadIdx.x & 31];
+    atomicAdd(db + c, t);
+  }
 }
 
 template <int BM, int BN, int WGM, int WGN, int STAGES, int AMODE, int BMODE, int EPI, int PIPE = 0, int BMC = BM>
-void launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int ksplit, hipStream_t s) {
+int launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int ksplit, hipStream_t s) {
   const int ti = cdiv(A.rows, BMC), tj = cdiv(B.rows, BN);
   const int ktiles = cdiv(A.kdim, BK);
   ksplit = ksplit < 1 ? 1 : (ksplit > ktiles ? ktiles : ksplit);
   const int per = cdiv(ktiles, ksplit);
   ksplit = cdiv(ktiles, per);
   dim3 grid(ti * tj, ksplit, groups);
+  if constexpr (EPI == EPI_BF16_DB) {
+    const long rows = static_cast<long>(tj) * WGN;
+    if (rows * E.part_ld > E.part_elems) return -1;  // workspace too small: the caller sums dx itself
+  }
   hipLaunchKernelGGL((gemm_glds<BM, BN, WGM, WGN, STAGES, AMODE, BMODE, EPI, PIPE, BMC>), grid, dim3(64 * WGM * WGN), 0, s,
                      A, B, E, ti, tj, per, ktiles);
+  if constexpr (EPI == EPI_BF16_DB) {
+    const int rows = tj * WGN;
+    const int chunks = (rows + 255) / 256;  // 256 rows per block: <= ~10^3 adders per address
+    hipLaunchKernelGGL(db_partials_reduce, dim3((E.part_ld + 31) / 32, chunks), dim3(256), 0, s, E.dbias, rows,
+                       E.part_ld, E.dbias_final);
+  }
+  return 0;
 }
 
 
@@ -1004,11 +1078,11 @@ void launch_pp(const GOperand &A, const GOperand &B, const GEpi &E, int groups, 
 // the epilogue's intra-wave LDS hand-off was unfenced (wave_lds_handoff); fixed, they are correct
 // and 72 ties the 128-row tile on AlexNet conv1 (the row gather, not the idle MFMA rows, bounds it).
 #define CXG_T(ID, BM, BN, WGM, WGN, ST) \
-  case ID: launch<BM, BN, WGM, WGN, ST, AM, BMo, EP>(A, B, E, groups, ksplit, s); return 0;
+  case ID: return launch<BM, BN, WGM, WGN, ST, AM, BMo, EP>(A, B, E, groups, ksplit, s);
 #define CXG_TP(ID, BM, BN, WGM, WGN, ST, PIPE) \
-  case ID: launch<BM, BN, WGM, WGN, ST, AM, BMo, EP, PIPE>(A, B, E, groups, ksplit, s); return 0;
+  case ID: return launch<BM, BN, WGM, WGN, ST, AM, BMo, EP, PIPE>(A, B, E, groups, ksplit, s);
 #define CXG_TC(ID, BM, BMC, BN, WGM, WGN, ST) \
-  case ID: launch<BM, BN, WGM, WGN, ST, AM, BMo, EP, 0, BMC>(A, B, E, groups, ksplit, s); return 0;
+  case ID: return launch<BM, BN, WGM, WGN, ST, AM, BMo, EP, 0, BMC>(A, B, E, groups, ksplit, s);
 #define CXG_KK_TILES                                                                                      \
   switch (tile) {                                                                                         \
     CXG_T(0, 128, 256, 1, 4, 3) CXG_T(1, 128, 128, 1, 4, 2) CXG_T(2, 128, 128, 2, 2, 3)                   \
@@ -1072,6 +1146,7 @@ int dispatch(int amode, int bmode, int epi, int tile, const GOperand &A, const G
   }
 #undef CXG_PP
   CXG_CASE(K_DIRECT, K_GATHER, EPI_BF16, CXG_KK_TILES)    // conv fwd / dgrad
+  CXG_CASE(K_DIRECT, K_GATHER, EPI_BF16_DB, CXG_KK_TILES)  // conv dgrad + the lower conv's bias gradient
   CXG_CASE(K_DIRECT, K_ROWGATHER, EPI_BF16, CXG_KK_TILES)  // conv fwd, few input channels (conv1)
   CXG_CASE(K_DIRECT, K_DIRECT, EPI_BF16, CXG_KK_TILES)    // fc fwd
   CXG_CASE(K_DIRECT, K_DIRECT, EPI_F32, CXG_KK_TILES)     // fc fwd split-K
@@ -1145,8 +1220,10 @@ void fill(GOperand &r, const CxnOperandG *o, int mode) {
 // gathers: Cg % 8 == 0 and dil == 1; every buffer < 2 GiB.
 CXN_API int cxn_gemm_glds(const CxnOperandG *a, const CxnOperandG *b, int amode, int bmode, void *out,
                           long out_gstride, int ldc, float alpha, const float *bias, long bias_gstride, int relu,
-                          int mask_relu, int epi, int tile, int groups, int ksplit, long kstride, void *stream) {
+                          int mask_relu, int epi, int tile, int groups, int ksplit, long kstride, float *dbias,
+                          float *dws, long dws_elems, int dws_ld, void *stream) {
   if (a->kdim != b->kdim) return -1;
+  if (epi == EPI_BF16_DB && (dbias == nullptr || dws == nullptr || ksplit > 1 || bias != nullptr)) return -1;
   if ((kmajor(amode) || kmajor(bmode)) && a->kdim % 8 != 0) return -1;
   if (!supported(a, amode) || !supported(b, bmode)) return -1;
   if (a->rows <= 0 || b->rows <= 0 || a->kdim <= 0) return 0;
@@ -1155,7 +1232,7 @@ CXN_API int cxn_gemm_glds(const CxnOperandG *a, const CxnOperandG *b, int amode,
   fill(B, b, bmode);
   if (epi == EPI_F32_SGD) return -1;  // only through cxn_gemm_glds_sgd
   GEpi E{out, out_gstride, ldc, alpha, bias, bias_gstride, relu, mask_relu, kstride,
-         nullptr, nullptr, nullptr, 0.f, 0.f, 0.f, 0.f};
+         nullptr, nullptr, nullptr, 0.f, 0.f, 0.f, 0.f, dws, dws_ld, dws_elems, dbias};
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int rc = dispatch(amode, bmode, epi, tile, A, B, E, groups < 1 ? 1 : groups, ksplit < 1 ? 1 : ksplit, s);
   if (rc != 0) return rc;
@@ -1177,7 +1254,7 @@ CXN_API int cxn_gemm_glds_sgd(const CxnOperandG *a, const CxnOperandG *b, int ld
   GOperand A{}, B{};
   fill(A, a, MN_DIRECT);
   fill(B, b, MN_DIRECT);
-  GEpi E{nullptr, 0, ldc, alpha, nullptr, 0, 0, 0, 0, w, m, static_cast<bf16_t *>(wb), lr, wd, mom, clip};
+  GEpi E{nullptr, 0, ldc, alpha, nullptr, 0, 0, 0, 0, w, m, static_cast<bf16_t *>(wb), lr, wd, mom, clip, nullptr, 0, 0, nullptr};
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int rc = dispatch(MN_DIRECT, MN_DIRECT, EPI_F32_SGD, tile, A, B, E, 1, 1, s);
   if (rc != 0) return rc;

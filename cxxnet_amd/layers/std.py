@@ -200,6 +200,9 @@ class ConvolutionLayer(Layer):
         self._xpad = None
         self._prepad_on = False
         self.bias_done = False  # set by a fused max-pool backward that already summed the bias gradient
+        # the conv below whose bias gradient this conv's data-gradient epilogue sums
+        # (NeuralNet._fuse_dgrad_bias); None = not fused
+        self.bias_below = None
 
     def init_connection(self, nodes_in, nodes_out):
         _check(len(nodes_in) == 1 and len(nodes_out) == 1, "ConvolutionLayer: only support 1-1 connection")
@@ -300,8 +303,13 @@ class ConvolutionLayer(Layer):
             self.ctx.bias_grad(dy.view(-1, dy.shape[-1]), self.b.g)
         if prop_grad:
             ready = self.ctx.flipped is not None and id(self) in self.ctx.flipped
-            ops.conv_backward_data(dy, self.w.wb, nodes_in[0].gdst, self.geo, self.flip_target()[1],
-                                   mask_relu=self.grad_mask_relu, wt_ready=ready)
+            below = self.bias_below
+            db = None
+            if below is not None and below.b is not None and self.ctx.is_gpu and not deterministic():
+                db = below.b.g
+            if ops.conv_backward_data(dy, self.w.wb, nodes_in[0].gdst, self.geo, self.flip_target()[1],
+                                      mask_relu=self.grad_mask_relu, wt_ready=ready, dbias=db):
+                below.bias_done = True
 
     def flip_target(self):
         """(weights, flipped-weights buffer, geometry) of the data-gradient GEMM."""

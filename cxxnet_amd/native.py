@@ -70,7 +70,7 @@ _SIGS = {
     "cxn_gemm_glds_sgd": [ctypes.POINTER(CxnOperand), ctypes.POINTER(CxnOperand), _I, _F, _P, _P, _P, _F, _F, _F, _F,
                           _I, _P],
     "cxn_gemm_glds": [ctypes.POINTER(CxnOperand), ctypes.POINTER(CxnOperand), _I, _I, _P, _L, _I, _F, _P, _L, _I,
-                      _I, _I, _I, _I, _I, _L, _P],
+                      _I, _I, _I, _I, _I, _L, _P, _P, _L, _I, _P],
     "cxn_pad_rows": [_P, _P, _L, _I, _I, _P],
     "cxn_chan_reduce": [_P, _P, _P, _P, _L, _I, _I, _P],
     "cxn_bn_stats": [_P, _P, _P, _P, _L, _I, _F, _P],

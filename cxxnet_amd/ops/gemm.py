@@ -130,7 +130,7 @@ GLDS_TILES = {0: (128, 256), 1: (128, 128), 2: (128, 128), 4: (192, 256), 5: (64
               79: (48, 128), 80: (48, 256), 81: (48, 64)}
 # operand loaders of gemm_glds.hip
 GL_K, GL_KG, GL_MN, GL_MNG, GL_KR = 0, 1, 2, 3, 4  # K_DIRECT, K_GATHER, MN_DIRECT, MN_GATHER, K_ROWGATHER
-EPI_F32_ACC_G, EPI_F32_ATOMIC_G = 2, 3
+EPI_F32_ACC_G, EPI_F32_ATOMIC_G, EPI_BF16_DB_G = 2, 3, 5
 _glds_cfg = {"on": os.environ.get("CXXNET_GEMM_GLDS", "1") != "0",
              "tile": int(os.environ.get("CXXNET_GLDS_TILE", "-1")),
              "tune": os.environ.get("CXXNET_GEMM_TUNE", "1") != "0",
@@ -294,7 +294,8 @@ def _pick_glds(rows_i, rows_j, groups, nblocks_target=NUM_CU):
 
 
 def _glds(a, b, amode, bmode, out, out_gstride, ldc, *, alpha=1.0, bias=None, bias_gstride=0, relu=False,
-          mask_relu=False, epi=EPI_BF16, groups=1, ksplit=1, kstride=0, tile=None) -> bool:
+          mask_relu=False, epi=EPI_BF16, groups=1, ksplit=1, kstride=0, tile=None, dbias=None, dws=None,
+          dws_ld=0) -> bool:
     """Run the LDS-DMA kernel; False when it does not support the operands (caller falls back)."""
     if not _glds_cfg["on"]:
         return False
@@ -303,7 +304,8 @@ def _glds(a, b, amode, bmode, out, out_gstride, ldc, *, alpha=1.0, bias=None, bi
     rc = native.kernels().cxn_gemm_glds(
         a, b, amode, bmode, out.data_ptr(), out_gstride, ldc, float(alpha),
         bias.data_ptr() if bias is not None else None, bias_gstride, int(relu), int(mask_relu), epi, tile, groups,
-        ksplit, kstride, _stream())
+        ksplit, kstride, dbias.data_ptr() if dbias is not None else None,
+        dws.data_ptr() if dws is not None else None, dws.numel() if dws is not None else 0, int(dws_ld), _stream())
     if rc == -1:
         return False
     native.check(rc, "gemm_glds")
@@ -520,10 +522,13 @@ def conv_weight_flip_multi(items):
                  "conv_weight_flip_multi")
 
 
-def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False, wt_ready=False):
+def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False, wt_ready=False, dbias=None) -> bool:
     """dx = conv_transpose(dy, w); dx overwritten.  mask_relu: dx holds relu(z) on entry
     (fused producer->relu) and the result is multiplied by relu'(z).  wt_ready: wt_buf already
-    holds the flipped weights (conv_weight_flip_multi at the start of the backward pass)."""
+    holds the flipped weights (conv_weight_flip_multi at the start of the backward pass).
+    dbias (fp32 [C], optional): += column sums of the stored dx -- the bias gradient of the conv
+    that produced x -- inside the GEMM epilogue (EPI_BF16_DB).  Returns True when dbias was
+    accumulated; False when the chosen kernel has no such epilogue (the caller sums dx itself)."""
     if not _native_t(dy):
         dyn = dy.permute(0, 3, 1, 2)
         out = torch.nn.grad.conv2d_input((g.N, g.C, g.H, g.W), _w_nchw(w), dyn, stride=g.stride,
@@ -531,7 +536,7 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False, wt_
         if mask_relu:
             out = out * (dx > 0).to(out.dtype)
         dx.copy_(out)
-        return
+        return False
     cg_in, cg_out = g.cg_in, g.cg_out
     if cg_out % 8:
         raise ValueError("conv dgrad: output channels per group must be a multiple of 8 on the GPU path")
@@ -555,9 +560,17 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False, wt_
                 return reg(o)
             return _glds(A, B, GL_K, GL_KG, o, cg_in, g.C, groups=g.groups, mask_relu=mask_relu, tile=t)
         key = ("cd", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
-        if run(_tuned_tile(key, run, dx, lambda: _pick_glds(A.rows, B.rows, g.groups), extra=(REG,)), dx):
-            return
+        t = _tuned_tile(key, run, dx, lambda: _pick_glds(A.rows, B.rows, g.groups), extra=(REG,))
+        if dbias is not None and t != REG:
+            from .nn import _workspace
+            ws = _workspace((-(-B.rows // 16) + 8) * g.C, dx.device)  # >= tiles_j * waves_j rows
+            if _glds(A, B, GL_K, GL_KG, dx, cg_in, g.C, groups=g.groups, mask_relu=mask_relu, tile=t,
+                     epi=EPI_BF16_DB_G, bias_gstride=cg_in, dbias=dbias, dws=ws, dws_ld=g.C):
+                return True
+        if run(t, dx):
+            return False
     reg(dx)
+    return False
 
 
 def conv_backward_weight(x, dy, dw, g: ConvGeom):

@@ -590,3 +590,60 @@ def test_pool_stride1_3x3_strips(H, p, relu):
     assert torch.equal(y.float().cpu(), y_ref)
     assert torch.equal(st.cpu() & 0x7F, st_ref)
     assert relerr(dx, dx_ref) < 1e-2
+
+
+@pytest.mark.parametrize("geo_args,mask", [((4, 13, 13, 384, 13, 13, 384, 3, 3, 1, 1, 1, 2), True),
+                                           ((2, 28, 28, 64, 28, 28, 96, 3, 3, 1, 1, 1, 1), False),
+                                           ((2, 14, 14, 48, 14, 14, 64, 5, 5, 1, 2, 2, 1), True)])
+def test_conv_dgrad_epilogue_bias_sum(geo_args, mask):
+    """The data-gradient GEMM's EPI_BF16_DB epilogue: dx as the plain epilogue writes it, and
+    dbias += column sums of the stored (relu'-masked) dx."""
+    from cxxnet_amd.ops.gemm import ConvGeom
+    g = ConvGeom(*geo_args)
+    dy = rnd(g.N, g.Ho, g.Wo, g.Cout, seed=7).to(DEV, torch.bfloat16)
+    w = (rnd(g.Cout, g.KH, g.KW, g.cg_in, seed=8) * 0.05).to(DEV, torch.bfloat16)
+    z = rnd(g.N, g.H, g.W, g.C, seed=9).to(DEV, torch.bfloat16)
+    dx_ref = z.clone() if mask else torch.empty_like(z)
+    ops.conv_backward_data(dy, w, dx_ref, g, mask_relu=mask)
+    dx = z.clone() if mask else torch.empty_like(z)
+    db = torch.full((g.C,), 0.25, device=DEV)
+    fused = ops.conv_backward_data(dy, w, dx, g, mask_relu=mask, dbias=db)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dx_ref)
+    ref = 0.25 + dx_ref.float().reshape(-1, g.C).sum(0)
+    if fused:
+        assert relerr(db, ref) < 1e-3
+    else:
+        assert torch.equal(db, torch.full_like(db, 0.25))
+
+
+def test_dgrad_fused_bias_grads_match_unfused(monkeypatch):
+    """conv -> relu -> conv: the lower conv's bias gradient from the upper conv's data-gradient
+    epilogue (NeuralNet._fuse_dgrad_bias) equals the column-sum pass, on AlexNet (conv3, conv4)."""
+    from cxxnet_amd.io.data import DataBatch
+    from cxxnet_amd.models import load_conf
+    from cxxnet_amd.nnet import NetTrainer
+
+    grads = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("CXXNET_DGRAD_BIAS", fused)  # the fusion is opt-in
+        pairs = load_conf("alexnet", [("batch_size", "16"), ("dev", "gpu"), ("eval_train", "0"), ("silent", "1"),
+                                      ("update_period", "2")])
+        tr = NetTrainer()
+        for k, v in pairs:
+            if not k.startswith("metric"):
+                tr.set_param(k, v)
+        tr.init_model()
+        below = [c.layer.bias_below for c in tr.net.connections if getattr(c.layer, "bias_below", None) is not None]
+        assert len(below) == (2 if fused == "1" else 0)
+        c, h, w = tr.net_cfg.input_shape
+        g = torch.Generator().manual_seed(6)
+        x = torch.randn(16, c, h, w, generator=g).to(DEV)
+        y = torch.randint(0, 1000, (16, 1), generator=g).float().to(DEV)
+        tr.update(DataBatch(x, y))
+        torch.cuda.synchronize()
+        grads.append([cn.layer.b.g.clone() for cn in tr.net.connections
+                      if type(cn.layer).__name__ == "ConvolutionLayer" and cn.layer.b is not None])
+    for a, b in zip(*grads):
+        assert b.abs().max().item() > 0
+        assert relerr(a, b) < 1e-2, relerr(a, b)
