@@ -213,6 +213,8 @@ def _use(op: str) -> bool:
     return _glds_cfg["on"] and op in _glds_cfg["ops"]
 
 
+# CXXNET_TUNE_LOG=1: report every signature timed on first use (a table miss) on stderr
+_TUNE_LOG = os.environ.get("CXXNET_TUNE_LOG", "0") == "1"
 TUNE_REJECTED = []  # (signature, tile, relative error) of candidates that failed the output check
 
 
@@ -246,6 +248,9 @@ def _tuned_tile(key, run, out, default, extra=(), tune=True, cands=None):
         return t
     if not (tune and _glds_cfg["tune"]) or torch.cuda.is_current_stream_capturing():
         return default()
+    if _TUNE_LOG:
+        import sys
+        print(f"gemm tune: timing {key} (not in the tile table)", file=sys.stderr, flush=True)
     init = out.clone()
     ref = init.clone()
     dflt = default()
