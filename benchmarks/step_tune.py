@@ -82,7 +82,7 @@ def main():
         op = key.split("|")[0]
         if op in ("cf", "cd", "cr", "fc"):
             cands = list(SHORT if a.short else KK) + ([G.REG] if op in ("cf", "cd") else [])
-        elif op == "fw":
+        elif op in ("fw", "fws"):
             cands = list(MM)
         elif op == "cws":
             N, H, W, C, Co, KH, KW, st, py, px, g = (int(v) for v in key.split("|")[1:])

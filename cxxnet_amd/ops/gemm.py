@@ -709,7 +709,12 @@ def fc_backward_weight_sgd(x, dy, w, m, wb, lr, wd, mom, clip) -> bool:
     nout = dy.shape[1]
     A = _op(x, 0, nin, nin, Bn)
     Bo = _op(dy, 0, nout, nout, Bn)
-    tile = _TUNE.get(f"fw|{nin}|{nout}|{Bn}", 1) if _glds_cfg["tile"] < 0 else _glds_cfg["tile"]
+    # the SGD epilogue streams w / m / wb: its own tile entry ("fws"), else the plain weight-grad one
+    tile = _glds_cfg["tile"]
+    if tile < 0:
+        tile = _TUNE.get(f"fws|{nin}|{nout}|{Bn}")
+        if tile is None:
+            tile = _TUNE.get(f"fw|{nin}|{nout}|{Bn}", 1)
     rc = native.kernels().cxn_gemm_glds_sgd(A, Bo, nin, 1.0, w.data_ptr(), m.data_ptr(), wb.data_ptr(), float(lr),
                                             float(wd), float(mom), float(clip), tile, _stream())
     if rc == -1:

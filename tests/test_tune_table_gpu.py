@@ -116,10 +116,29 @@ def test_shipped_table_entry(op, sig):
     elif op == "fc":
         _, nout, B, nin, _ = sig  # amode, a.rows = nout, b.rows = B, kdim = nin, ldc
         err = check_fc("fc", nin, nout, B)
+    elif op == "fws":
+        nin, nout, B = sig
+        err = check_fc_sgd(nin, nout, B)
     else:
         nin, nout, B = sig
         err = check_fc("fw", nin, nout, B)
     assert err < 1e-2, (op, sig, gemm._TUNE.get("|".join([op] + [str(v) for v in sig])), err)
+
+
+def check_fc_sgd(nin, nout, B):
+    """The fc weight-gradient fused with the SGD step (table key "fws") against torch:
+    m' = mom m - lr (dy^T x + wd w), w' = w + m'; returns the worse relative error of m' and w'."""
+    x = _rnd((B, nin), 1.0, 11)
+    dy = _rnd((B, nout), 1.0, 12)
+    w = torch.randn(nout, nin, device=DEV) * 0.02
+    m = torch.randn(nout, nin, device=DEV) * 0.01
+    wb = w.to(torch.bfloat16)
+    lr, wd, mom = 0.01, 5e-4, 0.9
+    g = dy.float().t() @ x.float()
+    m_ref = mom * m - lr * (g + wd * w)
+    w_ref = w + m_ref
+    assert ops.fc_backward_weight_sgd(x, dy, w, m, wb, lr, wd, mom, 0.0)
+    return max(_relnorm(m, m_ref), _relnorm(w, w_ref), _relnorm(wb.float(), w_ref))
 
 
 # one representative (non-table) shape per op class; each candidate tile is forced
