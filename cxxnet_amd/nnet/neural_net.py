@@ -399,7 +399,7 @@ class NeuralNet:
                 with self._range(i, "fwd"):
                     conn.layer.forward(is_train, conn.nodes_in, conn.nodes_out)
 
-    def backprop(self, prop_to_input: bool = False, hook=None, first: bool = False):
+    def backprop(self, prop_to_input: bool = False, hook=None, first: bool = False, hook_due=None):
         """Reverse pass.  hook(layer_index) runs after each layer's backprop (used by the
         data-parallel bucketer to launch reductions as soon as gradients are final).
 
@@ -410,11 +410,12 @@ class NeuralNet:
         self.ctx.grad_overwrite = bool(first)
         if first:
             self.arena.zero_accumulated_grads()
-        # without a per-layer hook (data-parallel buckets need every gradient of a layer when
-        # it returns) the bias gradients are queued and summed in ONE launch at the end: the
-        # dy buffers they read are not rewritten later in the pass
+        # the bias gradients are queued and summed in one multi-tensor launch: at the end of the
+        # pass, or -- with a data-parallel bucket hook -- right before the hook that launches a
+        # bucket (hook_due(i): the hook would launch one after layer i), since a bucket needs every
+        # gradient of its layers.  The dy buffers they read are not rewritten later in the pass.
         from ..ops.gemm import deterministic
-        defer = hook is None and self.ctx.is_gpu and not deterministic()
+        defer = self.ctx.is_gpu and not deterministic()
         self.ctx.deferred_bias = [] if defer else None
         if self.ctx.is_gpu:
             # every conv data-gradient's flipped weights in one launch (weights do not change
@@ -428,13 +429,15 @@ class NeuralNet:
             from ..ops.gemm import conv_weight_flip_multi
             conv_weight_flip_multi(flips)
             self.ctx.flipped = seen
-        side = self._bias_stream() if defer else None
+        side = self._bias_stream() if defer and hook is None else None
         with _BatchView(self):
             for i in range(len(self.connections) - 1, -1, -1):
                 conn = self.connections[i]
                 with self._range(i, "bwd"):
                     conn.layer.backprop(i != 0 or prop_to_input, conn.nodes_in, conn.nodes_out)
                 if hook is not None:
+                    if self.ctx.deferred_bias and (hook_due is None or hook_due(i)):
+                        self._flush_bias(None)
                     hook(i)
                 if side is not None and self._pending_bias_bytes() >= _BIAS_FLUSH_BYTES:
                     self._flush_bias(side)

@@ -367,7 +367,7 @@ class NetTrainer:
             red = self.reducer
             hook = red.hook if (red.active or red.update_fn is not None) else None
             try:
-                net.backprop(False, hook=hook, first=first)
+                net.backprop(False, hook=hook, first=first, hook_due=red.due if hook is not None else None)
             finally:
                 net.ctx.sgd_fuse = None
             self.reducer.finish()
@@ -538,6 +538,9 @@ class NetTrainer:
                 waited.update(new)
                 cut(functools.partial(red.before_forward, li))
 
+        def bwd_due(li):
+            return any(bi not in ready and li <= b.li_min for bi, b in enumerate(red.buckets))
+
         def bwd_hook(li):
             bs = [bi for bi, b in enumerate(red.buckets) if bi not in ready and li <= b.li_min]
             if bs:
@@ -550,7 +553,7 @@ class NetTrainer:
             net.forward(True, pre_hook=fwd_hook if dp else None)
             end()
             begin(bwd)
-            net.backprop(False, hook=bwd_hook if dp else None, first=True)
+            net.backprop(False, hook=bwd_hook if dp else None, first=True, hook_due=bwd_due if dp else None)
             end()
         torch.cuda.synchronize()
         return fwd, bwd

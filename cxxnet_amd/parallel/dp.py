@@ -285,6 +285,13 @@ class GradReducer:
             if not b.ready:
                 self._ready(b)
 
+    def due(self, layer_index: int) -> bool:
+        """Whether hook(layer_index) launches a bucket (the executor flushes queued gradient
+        work of the pass before it)."""
+        if not self.overlap or not (self.active or self.update_fn is not None):
+            return False
+        return any(not b.ready and layer_index <= b.li_min for b in self.buckets)
+
     def hook(self, layer_index: int):
         """Called after each layer's backprop (reverse order)."""
         if not self.overlap or not (self.active or self.update_fn is not None):
