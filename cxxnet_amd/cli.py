@@ -430,8 +430,14 @@ def _maybe_spawn_ranks(argv: List[str]) -> Optional[int]:
     env = dict(os.environ)
     env["HIP_VISIBLE_DEVICES"] = ",".join(str(i) for i in ids)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    port = env.get("CXXNET_MASTER_PORT")
+    if not port:  # a free local port: a fixed default collides with any other job on the host
+        import socket
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = str(s.getsockname()[1])
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={len(ids)}",
-           "--master-addr", "127.0.0.1", "--master-port", env.get("CXXNET_MASTER_PORT", "29517"),
+           "--master-addr", "127.0.0.1", "--master-port", port,
            "-m", "cxxnet_amd"] + argv
     return subprocess.call(cmd, env=env)
 

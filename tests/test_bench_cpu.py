@@ -45,8 +45,12 @@ def test_bench_strong_scaling_splits_global_batch():
 
 
 def test_bench_rank_mismatch_fails():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = str(s.getsockname()[1])
     r = _run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr", "127.0.0.1",
-              "--master-port", "29561", "bench.py", "--gpus", "2", "--device", "cpu", "--model", "mnist_mlp",
+              "--master-port", port, "bench.py", "--gpus", "2", "--device", "cpu", "--model", "mnist_mlp",
               "--batch", "8", "--steps", "1", "--warmup", "0"])
     assert r.returncode != 0
     assert "process group holds 1" in r.stderr
