@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--margin", type=float, default=0.004)
     ap.add_argument("--out", required=True)
     ap.add_argument("--short", action="store_true", help="shortlist of LDS-DMA tiles (models with many signatures)")
+    ap.add_argument("--ops", default="", help="only these op classes (comma list, e.g. fw)")
     a = ap.parse_args()
     from cxxnet_amd.io.data import DataBatch
     from cxxnet_amd.models import load_conf
@@ -52,6 +53,9 @@ def main():
     from cxxnet_amd.ops import gemm as G
     from cxxnet_amd.ops.gemm import conv_out_size
 
+    if os.environ.get("CXXNET_DIST_FORCE", "0") == "1":  # the data-parallel step (RCCL at world 1)
+        from cxxnet_amd.parallel import init_distributed
+        init_distributed()
     G._TUNE = LogDict(G._TUNE)
     pairs = load_conf(a.model, [("batch_size", str(a.batch)), ("eval_train", "0"), ("dev", "gpu"), ("silent", "1")])
     tr = NetTrainer()
@@ -80,6 +84,8 @@ def main():
     log = []
     for key in keys:
         op = key.split("|")[0]
+        if a.ops and op not in a.ops.split(","):
+            continue
         if op in ("cf", "cd", "cr", "fc"):
             cands = list(SHORT if a.short else KK) + ([G.REG] if op in ("cf", "cd") else [])
         elif op in ("fw", "fws"):
