@@ -189,16 +189,19 @@ class LearnTask:
         self.start_counter += 1
         if self.save_period == 0 or self.start_counter % self.save_period != 0:
             return
+        # collective on EVERY rank (sharded data parallelism gathers the fp32 masters and the
+        # optimizer state here); rank 0 then writes without entering another collective
+        self.trainer.prepare_save(opt_state=bool(self.save_opt_state))
         if self.rank != 0:
             return
         os.makedirs(self.name_model_dir, exist_ok=True)
-        blob = self.trainer.save_model()
+        blob = self.trainer.save_model(sync=False)
         with open(path + ".tmp", "wb") as f:
             f.write(struct.pack("<i", self.net_type))
             f.write(blob)
         os.replace(path + ".tmp", path)
         if self.save_opt_state:
-            self.trainer.save_optimizer_state(path + ".state.tmp")
+            self.trainer.save_optimizer_state(path + ".state.tmp", sync=False)
             os.replace(path + ".state.tmp", path + ".state")
 
     def init(self):
@@ -411,21 +414,34 @@ def _maybe_spawn_ranks(argv: List[str]) -> Optional[int]:
     if "WORLD_SIZE" in os.environ:
         return None
     dev = None
+    batch = None
     try:
         from . import native
         for k, v in native.rt().parse_config_file(argv[0]):
             if k == "dev":
                 dev = v
+            elif k == "batch_size":
+                batch = int(v)
     except Exception:
         return None
     for a in argv[1:]:
         if a.startswith("dev="):
             dev = a.split("=", 1)[1]
+        elif a.startswith("batch_size="):
+            batch = int(a.split("=", 1)[1])
     if not dev or not dev.startswith("gpu") or ":" not in dev:
         return None
-    from .nnet.trainer import parse_devices
+    from .nnet.trainer import parse_devices, prune_devices
     _, ids = parse_devices(dev)
-    if len(ids) <= 1:
+    if batch is not None and len(ids) > 1:
+        # the reference drops the devices a batch cannot cover (nnet_impl-inl.hpp:344-354)
+        n = prune_devices(batch, len(ids))
+        if n < len(ids):
+            step = max((batch + len(ids) - 1) // len(ids), 1)
+            print(f"Warning: The number of devices is induce mini-batch={step}\n"
+                  f"We can equally use {n} devices to cover the batch_size")
+            ids = ids[:n]
+    if len(ids) <= 1:  # one device (possibly after pruning): this process runs on device ids[0]
         return None
     env = dict(os.environ)
     env["HIP_VISIBLE_DEVICES"] = ",".join(str(i) for i in ids)

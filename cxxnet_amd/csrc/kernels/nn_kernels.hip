@@ -1483,8 +1483,10 @@ __global__ void pool_bwd_tie_all(const bf16_t *__restrict__ x, const bf16_t *__r
 // instance row of fp32 scores p[B][K] against labels lab[B][lw]:
 //   kind 0 error   : first-max argmax != label[0]   (K == 1: score > 0 is class 1)
 //   kind 1 logloss : -log(clamp(p[label[0]], 1e-15, 1 - 1e-15))   (K == 1: binary form)
-//   kind 2 rec@n   : (#distinct labels whose score has fewer than n strictly larger scores) / lw
-// (the reference breaks exact ties at random; here tied scores count as not larger).
+//   kind 2 rec@n   : (#distinct labels ranked within the top n) / lw, where a label's rank
+//                    counts the scores that are larger, or equal at a lower index (the
+//                    reference breaks exact ties at random; here the lowest index ranks first,
+//                    so at most n labels can hit).
 // Each block writes the sums over its rows to part[block][metric]; metric_accum adds the
 // block partials, in block order, into a float64 accumulator (deterministic, no atomics).
 struct MetricSpec {
@@ -1545,7 +1547,7 @@ __global__ void __launch_bounds__(256) metric_rows(const float *__restrict__ p, 
           if (dup || lc < 0 || lc >= K) continue;
           const float sl = pr[lc];
           float cnt = 0.f;
-          for (int j = lane; j < K; j += 64) cnt += pr[j] > sl ? 1.f : 0.f;
+          for (int j = lane; j < K; j += 64) cnt += (pr[j] > sl || (pr[j] == sl && j < lc)) ? 1.f : 0.f;
           cnt = wave_sum(cnt);
           hits += cnt < static_cast<float>(n) ? 1 : 0;
         }

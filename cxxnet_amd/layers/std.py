@@ -616,7 +616,8 @@ class LossLayerBase(Layer):
     def backprop(self, prop_grad, nodes_in, nodes_out):
         label = self.ctx.label_fields[self.target]
         bs = self.batch_size if self.batch_size > 0 else nodes_in[0].batch
-        scale = self.grad_scale / (bs * self.update_period)
+        # loss_weight 0: an idle data-parallel rank (trainer.active_ranks) adds zero gradients
+        scale = self.grad_scale / (bs * self.update_period) * getattr(self.ctx, "loss_weight", 1.0)
         node = nodes_in[0].mat()
         ops.loss_grad(self.kind, node, label[: node.shape[0]], scale, self.p32)
 

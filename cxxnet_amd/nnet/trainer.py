@@ -27,6 +27,15 @@ from ..utils.metric import DeviceMetricSet, MetricSet
 from .neural_net import NeuralNet
 
 
+def prune_devices(batch_size: int, ndev: int) -> int:
+    """Number of devices that cover a batch (reference nnet_impl-inl.hpp:344-354)."""
+    ndev = max(int(ndev), 1)
+    step = max((batch_size + ndev - 1) // ndev, 1)
+    while ndev > 1 and step * (ndev - 1) >= batch_size:
+        ndev -= 1
+    return ndev
+
+
 def parse_devices(val: str):
     """'gpu', 'gpu:0-3', 'gpu:0,1', 'cpu' -> (kind, [ids])."""
     kind = val.split(":")[0]
@@ -57,8 +66,9 @@ class NetTrainer:
         self.bucket_mb = 64.0
         self.comm_dtype = "fp32"
         self.shard_update = 0
-        # data-parallel reduction: auto = sharded (reduce-scatter / sliced update /
-        # all-gather) on the GPU, replicated all-reduce elsewhere or with fullc_gather
+        # data-parallel reduction: auto = replicated all-reduce (the path every backend runs
+        # the same way); shard = reduce-scatter / sliced update / all-gather (opt-in, also
+        # update_on_server = 1)
         self.dp_mode = "auto"
         self.dp_force = int(os.environ.get("CXXNET_DIST_FORCE", "0"))
         self.test_on_server = 0
@@ -96,6 +106,7 @@ class NetTrainer:
         self.net: Optional[NeuralNet] = None
         self.reducer: Optional[GradReducer] = None
         self.rank, self.world = world_info()
+        self._rows = 0  # rows of the current batch that belong to this rank (0: idle rank)
 
     # ------------------------------------------------------------------ configuration
     def set_param(self, name: str, val: str):
@@ -175,13 +186,22 @@ class NetTrainer:
         step = max((self.batch_size + self.world - 1) // self.world, 1)
         return step
 
+    def active_ranks(self) -> int:
+        """Ranks that hold rows of the global batch: the reference drops devices while
+        step * (ndev - 1) >= batch_size, keeping step = ceil(batch / ndev_requested)
+        (src/nnet/nnet_impl-inl.hpp:344-354).  The launchers start only that many ranks;
+        a rank beyond it (torchrun started with more) is IDLE: it runs the same schedule on
+        stand-in rows with a zero loss weight, so it joins every collective and adds zero."""
+        return prune_devices(self.batch_size, self.world)
+
+    @property
+    def idle(self) -> bool:
+        return self.rank >= self.active_ranks()
+
     def _use_shard(self) -> bool:
         if self.shard_update or self.dp_mode == "shard":
             return True
-        if self.dp_mode == "allreduce":
-            return False
-        gather = any(k == "fullc_gather" and v.strip() not in ("", "0") for k, v in self.cfg)
-        return self._device().type == "cuda" and (self.world > 1 or bool(self.dp_force)) and not gather
+        return False
 
     def _apply_modes(self):
         from ..ops.mode import set_reference_precision
@@ -248,9 +268,16 @@ class NetTrainer:
         self._post_init()
 
     # ------------------------------------------------------------------ model io
-    def save_model(self) -> bytes:
+    def prepare_save(self, opt_state: bool = False):
+        """Collective part of a save: every rank calls it (sharded mode gathers the fp32
+        masters and, with opt_state, the optimizer state), then rank 0 serialises with
+        save_model(sync=False) / save_optimizer_state(sync=False)."""
         if self.reducer is not None:
-            self.reducer.sync_master()
+            self.reducer.sync_master(opt_state=opt_state)
+
+    def save_model(self, sync: bool = True) -> bytes:
+        if sync:
+            self.prepare_save()
         fo = BinWriter()
         self.net.save_model(fo)
         blob = fo.getvalue()
@@ -335,14 +362,26 @@ class NetTrainer:
 
     def _set_batch(self, batch, local=False):
         b = batch.batch_size
+        self.net.ctx.loss_weight = 1.0
         if local:  # batch already holds this rank's rows
             data, extra, label = batch.data, batch.extra_data, batch.label
+        elif self.world > 1 and self.idle:
+            # idle rank (more ranks than the batch needs): the first rows of the batch stand in,
+            # with a zero loss weight -- every gradient is zero, every collective is joined
+            n = min(self._local_batch(), b)
+            data, extra, label = batch.data[:n], [e[:n] for e in batch.extra_data], batch.label[:n]
+            self.net.ctx.loss_weight = 0.0
+            self._rows = 0
+            self.net.set_input(data, extra)
+            self.net.set_labels(label)
+            return n
         else:
             data = self._slice(batch.data, b)
             extra = [self._slice(e, b) for e in batch.extra_data]
             label = self._slice(batch.label, b)
         self.net.set_input(data, extra)
         self.net.set_labels(label)
+        self._rows = data.shape[0]
         return data.shape[0]
 
     def update(self, batch, local=False):
@@ -454,11 +493,11 @@ class NetTrainer:
                                      f"(check_nonfinite = {self.check_nonfinite})")
 
     # ------------------------------------------------------------------ optimizer state sidecar
-    def save_optimizer_state(self, path: str):
+    def save_optimizer_state(self, path: str, sync: bool = True):
         """Momentum / second moment and counters next to a model file (the model file itself
         stays byte-compatible with the reference layout, which has no optimizer state)."""
-        if self.reducer is not None:
-            self.reducer.sync_master()
+        if sync:
+            self.prepare_save(opt_state=True)
         a = self.net.arena
         state = {"m1": a.m1.detach().cpu(), "epoch_counter": torch.tensor([self.epoch_counter]),
                  "step_counter": self.net.ctx.step_counter.detach().cpu()}
@@ -644,7 +683,7 @@ class NetTrainer:
         if not self.eval_train or not self.eval_ids:
             return None
         if self.device_metrics:
-            self.train_metric.add_eval(self._eval_scores(), self.net.ctx.label_fields)
+            self.train_metric.add_eval(self._eval_scores(), self.net.ctx.label_fields, rows=self._rows)
             return None
         return self._collect_eval()
 
@@ -671,7 +710,7 @@ class NetTrainer:
     def _collect_eval(self) -> List[np.ndarray]:
         out = []
         for nid in self.eval_ids:
-            t = self._gather(self._node_output(nid).reshape(self.net.cur_batch, -1).float())
+            t = self._gather(self._node_output(nid).reshape(self.net.cur_batch, -1)[: self._rows].float())
             out.append(t.cpu().numpy())
         return out
 
@@ -689,7 +728,8 @@ class NetTrainer:
         self.reducer.sync()
         self._set_batch(batch)
         self.net.forward(False)
-        return [self._gather(self._node_output(n).contiguous().float()).cpu().numpy() for n in node_ids]
+        return [self._gather(self._node_output(n)[: self._rows].contiguous().float()).cpu().numpy()
+                for n in node_ids]
 
     def predict(self, batch) -> np.ndarray:
         out = self.forward_to([len(self.net.nodes) - 1], batch)[0]

@@ -18,8 +18,8 @@ Replaces the reference's mshadow-ps "local"/"dist" parameter server
 Two reduction modes:
   * replicated (``dp_mode = allreduce``): fp32 all-reduce of each bucket, every rank
     runs the optimizer on the whole bucket.  8 B/param on the wire.
-  * sharded (``dp_mode = shard``, default on the GPU under data parallelism; also
-    ``update_on_server = 1``).  This maps the reference's parameter server
+  * sharded (``dp_mode = shard``, opt-in; also ``update_on_server = 1``; ``dp_mode = auto``
+    stays on the replicated all-reduce).  This maps the reference's parameter server
     (nnet_ps_server.cpp:54-89: each server owns some keys, workers push gradients and
     pull updated weights) onto collectives: each bucket is REDUCE-SCATTERED (fp32), rank
     r updates the fp32 master / optimizer state of its 1/N slice only, and the bf16
@@ -94,8 +94,10 @@ class GradReducer:
         self.extra_ranges = []     # fullc_gather segments: updated after backward
         # RCCL runs reduce-scatter / all-gather IN PLACE (output = this rank's chunk of the
         # input): no staging buffers and no copies; gloo gets separate buffers
+        # (CXXNET_DP_INPLACE=1 takes the in-place path on gloo too: the CPU tests exercise RCCL's
+        # aliasing layout -- gloo honours the same in-place semantics)
         self.inplace = (self.comm_dtype == torch.float32 and dist.is_available() and dist.is_initialized()
-                        and dist.get_backend(group) == "nccl")
+                        and (dist.get_backend(group) == "nccl" or os.environ.get("CXXNET_DP_INPLACE") == "1"))
         if self.shard:
             self._shard_buckets(limit)
         else:
@@ -369,16 +371,27 @@ class GradReducer:
         for w in works:
             w.wait()
 
-    def sync_master(self):
-        """Sharded mode: gather the fp32 master weights (for save / get_weight)."""
+    def sync_master(self, opt_state: bool = False):
+        """Sharded mode: gather the fp32 master weights (for save / get_weight) and, with
+        opt_state, the optimizer state (momentum, Adam's second moment) -- each rank updates
+        only its owned slices of them.  A COLLECTIVE: every rank must call it (the CLI does
+        so before rank 0 serialises the model)."""
         self.sync()
-        if not self.shard or self.arena.wb is None:
+        if not self.shard:
             return
         a = self.arena
-        for b in self.buckets:
-            lo, hi = b.own(self.rank, self.world)
-            src = a.w[lo:hi].clone()
-            dist.all_gather_into_tensor(a.w[b.start:b.end], src, group=self.group)
+        tensors = []
+        if a.wb is not None:  # without a shadow the compute weights ARE the masters: gathered every step
+            tensors.append(a.w)
+        if opt_state:
+            tensors.append(a.m1)
+            if a.m2 is not None:
+                tensors.append(a.m2)
+        for t in tensors:
+            for b in self.buckets:
+                lo, hi = b.own(self.rank, self.world)
+                src = t[lo:hi].clone()
+                dist.all_gather_into_tensor(t[b.start:b.end], src, group=self.group)
 
     def check_consistency(self) -> float:
         """Max |w - w_rank0| over the compute weights of every replica (the
@@ -418,7 +431,11 @@ def init_distributed(backend: Optional[str] = None):
         backend = os.environ.get("CXXNET_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if ws <= 1:
-        os.environ.setdefault("MASTER_PORT", "29531")
+        if "MASTER_PORT" not in os.environ:  # a free local port: a fixed one collides across jobs
+            import socket
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(s.getsockname()[1])
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
     kw = {}

@@ -57,8 +57,9 @@ class DeviceMetricSet:
     accumulator; nothing is copied to the host until print(), which (under data
     parallelism) all-reduces the sums and counts once.  The reference instead copies every
     eval node to the host every step and reduces there (nnet_impl-inl.hpp:174-180).
-    Deviation: rec@n breaks exact score ties by the lowest index (torch.topk) where the
-    reference shuffles before sorting; ties between float softmax scores are measure-zero."""
+    Deviation: rec@n breaks exact score ties by the lowest index (kernel and fallback alike)
+    where the reference shuffles before sorting; ties between float softmax scores are
+    measure-zero."""
 
     KINDS = ("error", "logloss", "rmse")
 
@@ -138,9 +139,19 @@ class DeviceMetricSet:
         if K < n:
             raise ValueError(f"it is meaningless to take rec@n for list shorter than n, evaluating rec@{n}, "
                              f"list={K}")
-        top = p.topk(n, dim=1).indices                                   # (B, n)
-        # a top-n entry counts once if it equals any of the instance's labels
-        hit = (top.unsqueeze(2) == lab.long().unsqueeze(1)).any(2)       # (B, n)
+        # rank of each distinct label: scores larger, or equal at a lower index (the kernel's
+        # tie rule, so at most n labels hit); hit if rank < n
+        L = lab.long()
+        valid = (L >= 0) & (L < K)
+        Lc = L.clamp(0, K - 1)
+        s = p.gather(1, Lc)                                              # (B, lw)
+        idx = torch.arange(K, device=p.device).view(1, 1, K)
+        pe = p.unsqueeze(1)                                              # (B, 1, K)
+        rank = ((pe > s.unsqueeze(2)) | ((pe == s.unsqueeze(2)) & (idx < Lc.unsqueeze(2)))).sum(2)
+        first = torch.ones_like(valid)
+        for c in range(1, L.shape[1]):                                   # duplicates count once
+            first[:, c] = (L[:, :c] != L[:, c:c + 1]).all(1)
+        hit = (rank < n) & valid & first
         return hit.float().sum() / lab.shape[1]
 
     def add_eval(self, preds: List[torch.Tensor], label_fields: Dict[str, torch.Tensor], rows: int = None):

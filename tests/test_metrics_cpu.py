@@ -62,3 +62,21 @@ def test_rmse_and_field_label():
     assert dev.print("test") == host.print("test")
     dev.clear()
     assert "nan" in dev.print("test")
+
+
+def test_rec_at_n_fallback_ties():
+    """rec@n fallback rule: a label's rank counts larger scores and equal scores at a lower
+    index, so with all scores tied exactly the n lowest indices hit."""
+    import torch
+    from cxxnet_amd.utils.metric import DeviceMetricSet
+    p = torch.zeros(1, 6)
+    lab = torch.tensor([[0.0, 1.0, 4.0]])
+    # rec@2: labels 0 and 1 rank 0 and 1 (hit), label 4 ranks 4 (miss) -> 2/3
+    assert abs(DeviceMetricSet._one("rec@2", p, lab).item() - 2 / 3) < 1e-6
+    # duplicate labels count once
+    lab2 = torch.tensor([[0.0, 0.0, 5.0]])
+    assert abs(DeviceMetricSet._one("rec@1", p, lab2).item() - 1 / 3) < 1e-6
+    # larger scores outrank
+    p3 = torch.tensor([[0.1, 0.9, 0.5, 0.5, 0.0, 0.2]])
+    assert abs(DeviceMetricSet._one("rec@2", p3, torch.tensor([[2.0]])).item() - 1.0) < 1e-6
+    assert abs(DeviceMetricSet._one("rec@2", p3, torch.tensor([[3.0]])).item() - 0.0) < 1e-6

@@ -33,3 +33,18 @@ def test_metric_kernel_matches_host(K, L, B):
         host.add_eval([p[:b].numpy()] * len(names), {"label": lab[:b].numpy()})
     hv = [float(x.split(":")[1]) for x in host.print("t").split("\t")[1:]]
     assert np.allclose(hv, dev.values(), rtol=1e-4, atol=1e-6), (hv, dev.values())
+
+
+def test_rec_at_n_ties_lowest_index_first():
+    """Tied scores: the kernel ranks the lowest index first (at most n labels hit), exactly as
+    the torch fallback (DeviceMetricSet._one) -- the metric no longer depends on the path."""
+    B, K = 64, 12
+    g = torch.Generator().manual_seed(5)
+    p = torch.randint(0, 3, (B, K), generator=g).float() / 4.0  # many exact ties
+    lab = torch.randint(0, K, (B, 3), generator=g).float()
+    for n in ("rec@1", "rec@2", "rec@5"):
+        dev = DeviceMetricSet()
+        dev.add_metric(n)
+        dev.add_eval([p.cuda()], {"label": lab.cuda()})
+        ref = DeviceMetricSet._one(n, p, lab).item() / B
+        assert abs(dev.values()[0] - ref) < 1e-6, (n, dev.values()[0], ref)
