@@ -1,0 +1,176 @@
+// One-wave-per-SIMD bf16 MFMA GEMM tiles for gfx950: 4 waves, each owning a (BM/2) x (BN/2)
+// block of the output (256 x 256 tile: 128 x 128 per wave, 256 accumulator registers), with
+// the fragment reads of the next k-step and the LDS-DMA of the K-tile after next issued in the
+// shadow of the current k-step's MFMAs.
+//
+// Same contract and operand loaders as gemm_glds.hip (C[j][i] (+)= alpha * sum_k A(i,k) B(j,k),
+// K-major A and B); tile ids 92-97.
+//
+// Why this shape: PMC on 8192^3 (profiles/r3_pmc_square_gemm.md) shows hipBLASLt's
+// MT256x256x64 kernel at 86 % MFMA utilisation with waves parked 5 % of their cycles, against
+// 57 % / 36 % for our 8-wave (two per SIMD) 256 x 256 tile: two co-resident waves that meet at
+// every barrier leave the SIMD's matrix pipe idle while both wait.  With one wave per SIMD the
+// wave's own instruction stream has to hide every latency, so the loop is software-pipelined:
+//   iteration t (K-tile t in LDS buffer t & 1; fragments F0 = k-step 0 of tile t in registers):
+//     [A]  ds_read F1 = k-step 1 of tile t           | 64 (MR x NR) MFMAs on F0
+//          lgkmcnt(0) (F1 read, so buffer t & 1 is free for this wave), vmcnt(0) (tile t+1's
+//          DMAs, issued one half-iteration ago, have landed), s_barrier
+//     [B]  ds_read F0 = k-step 0 of tile t+1 (buffer (t+1) & 1)
+//          LDS-DMA of tile t+2 into buffer t & 1   | MFMAs on F1
+//   so one barrier per K-tile, no wait on an LDS read in front of an MFMA, and a DMA has
+//   [B] + [A] (two k-steps of MFMAs) to land.  Past the K slice the DMAs are all-OOB dummies.
+// SCHED = 1 pins the interleave with sched_group_barrier (one memory op between MFMAs).
+// Reference: src/layer/convolution_layer-inl.hpp:70-155, src/layer/fullc_layer-inl.hpp:101-130.
+#include "gemm_glds_common.h"
+
+using namespace cxg;
+
+namespace {
+
+template <int BM, int BN, int AMODE, int BMODE, int EPI, int SCHED>
+__global__ void __launch_bounds__(256, 1)
+gemm_4w(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_tiles, int ktiles_total) {
+  constexpr int NW = 4, WM = BM / 2, WN = BN / 2, MR = WM / 16, NR = WN / 16;
+  using OA = Op<AMODE, BM, NW>;
+  using OB = Op<BMODE, BN, NW>;
+  constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
+  static_assert(NW * 16 * (WM + 4) * 4 <= 2 * STAGE, "epilogue staging fits");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const uint32_t ntile = static_cast<uint32_t>(tiles_i) * tiles_j;
+  const GemmBlock wb = gemm_block(ntile);
+  const int g = wb.g;
+  const uint32_t tile = wb.tile;
+  const int ti = tile % tiles_i, tj = tile / tiles_i;
+  const int i0 = ti * BM, j0 = tj * BN;
+  const int kt_beg = wb.slice * ksplit_tiles;
+  const int kt_end = min(kt_beg + ksplit_tiles, ktiles_total);
+  if (kt_beg >= kt_end) return;
+  const int nt = kt_end - kt_beg;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const rsrc_t rA = make_rsrc(A.ptr, A.nbytes);
+  const rsrc_t rB = make_rsrc(B.ptr, B.nbytes);
+  const uint32_t goA = static_cast<uint32_t>(g * A.gstride) * 2u;
+  const uint32_t goB = static_cast<uint32_t>(g * B.gstride) * 2u;
+  OA oa;
+  OB ob;
+  oa.init(A, i0, goA, wave, lane);
+  ob.init(B, j0, goB, wave, lane);
+
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    const int kt = kt_beg + t;
+    char *sa = smem + (t & 1) * STAGE;
+    const typename OA::Prep pa = oa.prep(A, kt, kt_end, goA);
+    const typename OB::Prep pb = ob.prep(B, kt, kt_end, goB);
+    static_for<OA::NI>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void *)(sa + (wave + NW * s) * 1024), 16,
+                                               oa.template offset<s>(A, pa, wave, lane), 0, 0, 0);
+    });
+    static_for<OB::NI>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void *)(sa + A_BYTES + (wave + NW * s) * 1024), 16,
+                                               ob.template offset<s>(B, pb, wave, lane), 0, 0, 0);
+    });
+  };
+
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 a0[MR], b0[NR], a1[MR], b1[NR];
+  auto read = [&](int t, int kk, bf16x8 (&fa)[MR], bf16x8 (&fb)[NR]) __attribute__((always_inline)) {
+    const char *sa = smem + (t & 1) * STAGE;
+#pragma unroll
+    for (int m = 0; m < MR; ++m) fa[m] = frag<K_DIRECT>(sa, wr * WM + m * 16, kk, lane);
+#pragma unroll
+    for (int n = 0; n < NR; ++n) fb[n] = frag<K_DIRECT>(sa + A_BYTES, wc * WN + n * 16, kk, lane);
+  };
+  auto mfma = [&](const bf16x8 (&fa)[MR], const bf16x8 (&fb)[NR]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+#pragma unroll
+      for (int n = 0; n < NR; ++n)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
+  };
+
+  // prologue: tiles 0 and 1 in flight, tile 0 landed for every wave, F0 of tile 0 read
+  issue(0);
+  issue(1);
+  wait_vmcnt<OA::NI + OB::NI>();
+  block_barrier();
+  read(0, 0, a0, b0);
+
+  for (int t = 0; t < nt; ++t) {
+    // [A] k-step 1 fragments of tile t under the k-step 0 MFMAs
+    read(t, 32, a1, b1);
+    mfma(a0, b0);
+    if constexpr (SCHED) {
+#pragma unroll
+      for (int q = 0; q < MR + NR; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, MR * NR / (MR + NR), 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                      // DS read
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of buffer t & 1 are done
+    wait_vmcnt<0>();                     // tile t + 1 has landed (this wave's DMAs)
+    block_barrier();
+    // [B] k-step 0 fragments of tile t+1, DMAs of tile t+2 into buffer t & 1, k-step 1 MFMAs
+    read(t + 1, 0, a0, b0);
+    issue(t + 2);
+    mfma(a1, b1);
+    if constexpr (SCHED) {
+#pragma unroll
+      for (int q = 0; q < MR + NR; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, MR * NR / (2 * (MR + NR)), 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                            // DS read
+        __builtin_amdgcn_sched_group_barrier(0x008, MR * NR / (2 * (MR + NR)), 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x020, (OA::NI + OB::NI) / (MR + NR), 0);  // VMEM (LDS-DMA)
+      }
+    }
+  }
+  wait_vmcnt<0>();
+  __syncthreads();  // the epilogue reuses the stage buffers
+
+  seg_epilogue<EPI, MR, NR, WM>(acc, smem, E, g, wb.slice, A.rows, B.rows, i0 + wr * WM, j0 + wc * WN, wave, lane);
+}
+
+template <int BM, int BN, int AMODE, int BMODE, int EPI, int SCHED>
+void launch_4w(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int ksplit, hipStream_t s) {
+  const int ti = cdiv(A.rows, BM), tj = cdiv(B.rows, BN);
+  const int ktiles = cdiv(A.kdim, BK);
+  ksplit = ksplit < 1 ? 1 : (ksplit > ktiles ? ktiles : ksplit);
+  const int per = cdiv(ktiles, ksplit);
+  ksplit = cdiv(ktiles, per);
+  dim3 grid(ti * tj, ksplit, groups);
+  hipLaunchKernelGGL((gemm_4w<BM, BN, AMODE, BMODE, EPI, SCHED>), grid, dim3(256), 0, s, A, B, E, ti, tj, per, ktiles);
+}
+
+}  // namespace
+
+namespace cxg {
+// 92: 256x256, 93: 256x256 + sched_group_barrier interleave, 94: 128x256, 95: 256x128
+int dispatch_4w(int amode, int bmode, int epi, int tile, const GOperand &A, const GOperand &B, const GEpi &E,
+                int groups, int ksplit, hipStream_t s) {
+#define CX4(AMV, BMV, EPV)                                                                                 \
+  if (amode == AMV && bmode == BMV && epi == EPV) {                                                        \
+    switch (tile) {                                                                                        \
+      case 92: launch_4w<256, 256, AMV, BMV, EPV, 0>(A, B, E, groups, ksplit, s); return 0;                \
+      case 93: launch_4w<256, 256, AMV, BMV, EPV, 1>(A, B, E, groups, ksplit, s); return 0;                \
+      case 94: launch_4w<128, 256, AMV, BMV, EPV, 0>(A, B, E, groups, ksplit, s); return 0;                \
+      case 95: launch_4w<256, 128, AMV, BMV, EPV, 0>(A, B, E, groups, ksplit, s); return 0;                \
+      default: return -1;                                                                                  \
+    }                                                                                                      \
+  }
+  CX4(K_DIRECT, K_GATHER, EPI_BF16)  // conv fwd / dgrad
+  CX4(K_DIRECT, K_DIRECT, EPI_BF16)  // fc fwd, square GEMMs
+  CX4(K_DIRECT, K_DIRECT, EPI_F32)   // fc fwd split-K
+#undef CX4
+  return -1;
+}
+}  // namespace cxg

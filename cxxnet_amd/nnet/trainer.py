@@ -425,10 +425,24 @@ class NetTrainer:
         self._after_step(ev)
         if evals is not None:
             self.train_metric.add_eval(evals, self._label_fields(batch))
+        self._sync_tiles()
         self.sample_counter += 1
         if self.sample_counter >= self.update_period:
             self.sample_counter = 0
             self.epoch_counter += 1
+
+    def _sync_tiles(self):
+        """Data parallelism: after each of the first two updates (the eager step that times
+        the GEMM tile-table misses, and the step after it), every rank adopts the same tile
+        choice for every signature any rank timed (ops.gemm.sync_tune_table) -- a fixed point
+        in the schedule, so every rank enters the collective."""
+        if self.world <= 1 or not self.net.ctx.is_gpu:
+            return
+        self._tile_syncs = getattr(self, "_tile_syncs", 0)
+        if self._tile_syncs < 2:
+            self._tile_syncs += 1
+            from ..ops import gemm
+            gemm.sync_tune_table()
 
     # ------------------------------------------------------------------ step instrumentation
     def _events(self):

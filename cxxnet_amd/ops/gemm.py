@@ -127,7 +127,11 @@ GLDS_TILES = {0: (128, 256), 1: (128, 128), 2: (128, 128), 4: (192, 256), 5: (64
               # pool-projection layers) and their data-gradients onto 16..48 input channels
               76: (32, 128), 77: (32, 64), 78: (32, 256),
               # 48 computed rows on 64 staged (AlexNet conv2's data-gradient: 48 channels per group)
-              79: (48, 128), 80: (48, 256), 81: (48, 64)}
+              79: (48, 128), 80: (48, 256), 81: (48, 64),
+              # 8-phase 256x256 pipeline (gemm_8p.hip): 90 = two barriers per phase, 91 = one
+              90: (256, 256), 91: (256, 256),
+              # one wave per SIMD, software-pipelined (gemm_4w.hip): 92/93 256x256, 94 128x256, 95 256x128
+              92: (256, 256), 93: (256, 256), 94: (128, 256), 95: (256, 128)}
 # operand loaders of gemm_glds.hip
 GL_K, GL_KG, GL_MN, GL_MNG, GL_KR = 0, 1, 2, 3, 4  # K_DIRECT, K_GATHER, MN_DIRECT, MN_GATHER, K_ROWGATHER
 EPI_F32_ACC_G, EPI_F32_ATOMIC_G, EPI_BF16_DB_G = 2, 3, 5
@@ -263,6 +267,7 @@ def _tuned_tile(key, run, out, default, extra=(), tune=True, cands=None):
     scratch = torch.empty_like(out)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     best, best_ms = None, float("inf")
+    timed = {}
     for tile in (GLDS_CANDS if cands is None else tuple(cands)) + tuple(extra):
         scratch.copy_(init)
         if not run(tile, scratch):
@@ -280,10 +285,56 @@ def _tuned_tile(key, run, out, default, extra=(), tune=True, cands=None):
             e.synchronize()
             ts.append(s.elapsed_time(e))
         ms = sorted(ts)[1]
+        timed[tile] = ms
         if ms < best_ms:
             best, best_ms = tile, ms
     _TUNE[key] = best if best is not None else dflt
+    if timed:
+        TUNED_HERE[key] = timed
     return _TUNE[key]
+
+
+# Signatures timed by THIS process (table misses): {signature: {tile: ms}}.  Under data
+# parallelism each rank times its misses on its own, so two ranks could settle on different
+# tiles and the slower pick would hold every step of the job; sync_tune_table() makes the
+# choice rank-consistent.
+TUNED_HERE = {}
+
+
+def merge_tune_timings(per_rank):
+    """Rank-consistent tile choice from every rank's timings ([{signature: {tile: ms}}] in rank
+    order): per signature, the tile with the smallest summed time over the ranks that timed it
+    (a tile some rank rejected or could not run is not eligible); ties go to the lower tile id."""
+    out = {}
+    keys = set()
+    for d in per_rank:
+        keys.update(d)
+    for k in sorted(keys):
+        have = [d[k] for d in per_rank if k in d]
+        common = set(have[0])
+        for h in have[1:]:
+            common &= set(h)
+        if not common:  # no tile every timing rank could run: the lowest rank's pick
+            h = have[0]
+            out[k] = min(h, key=lambda t: (h[t], t))
+            continue
+        out[k] = min(common, key=lambda t: (sum(h[t] for h in have), t))
+    return out
+
+
+def sync_tune_table(group=None):
+    """Collective (every data-parallel rank calls it at the same point): exchange the tile
+    timings of this process's table misses and adopt the merged choice on every rank."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return {}
+    objs = [None] * dist.get_world_size(group)
+    dist.all_gather_object(objs, {k: dict(v) for k, v in TUNED_HERE.items()}, group=group)
+    merged = merge_tune_timings(objs)
+    for k, t in merged.items():
+        _TUNE[k] = int(t)
+    TUNED_HERE.clear()
+    return merged
 
 
 def _pick_glds(rows_i, rows_j, groups, nblocks_target=NUM_CU):

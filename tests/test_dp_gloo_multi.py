@@ -139,3 +139,37 @@ def test_cli_launcher_prunes_devices(tmp_path, monkeypatch):
     assert seen["env"]["HIP_VISIBLE_DEVICES"] == "0,1,2,3,4"
     # batch 1 over 8 devices: one device, no launcher
     assert cli._maybe_spawn_ranks([str(conf), "batch_size=1"]) is None
+
+
+def test_merge_tune_timings():
+    from cxxnet_amd.ops.gemm import merge_tune_timings
+    r0 = {"cf|a": {1: 10.0, 7: 9.0}, "cf|b": {1: 5.0}}
+    r1 = {"cf|a": {1: 8.0, 7: 12.0}, "cd|c": {10: 3.0, 15: 2.0}}
+    m = merge_tune_timings([r0, r1])
+    assert m == {"cf|a": 1, "cf|b": 1, "cd|c": 15}  # cf|a: 18 vs 21 summed
+    # a tile only one rank could run is not eligible when the ranks share another
+    m2 = merge_tune_timings([{"k": {1: 5.0, 2: 1.0}}, {"k": {1: 6.0}}])
+    assert m2 == {"k": 1}
+
+
+def _tune_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from cxxnet_amd.ops import gemm
+    # mocked per-rank timings: each rank alone would pick a different tile
+    gemm.TUNED_HERE.clear()
+    gemm.TUNED_HERE["cf|x"] = {1: 1.0 + rank, 7: 2.5 - rank}
+    gemm._TUNE["cf|x"] = min(gemm.TUNED_HERE["cf|x"], key=gemm.TUNED_HERE["cf|x"].get)
+    local = gemm._TUNE["cf|x"]
+    gemm.sync_tune_table()
+    torch.save({"local": local, "synced": gemm._TUNE["cf|x"]}, f"{out}.r{rank}")
+    dist.destroy_process_group()
+
+
+def test_tile_choice_is_rank_consistent(tmp_path):
+    """Ranks whose own timings disagree adopt one tile (sum of times over the ranks)."""
+    out = str(tmp_path / "tune")
+    mp.spawn(_tune_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    r = [torch.load(f"{out}.r{i}", weights_only=True) for i in range(2)]
+    assert r[0]["local"] != r[1]["local"]
+    assert r[0]["synced"] == r[1]["synced"] == 1  # 1.0 + 2.0 = 3.0 < 2.5 + 1.5 = 4.0
