@@ -19,13 +19,28 @@
 //          LDS-DMA of tile t+2 into buffer t & 1   | MFMAs on F1
 //   so one barrier per K-tile, no wait on an LDS read in front of an MFMA, and a DMA has
 //   [B] + [A] (two k-steps of MFMAs) to land.  Past the K slice the DMAs are all-OOB dummies.
-// SCHED = 1 pins the interleave with sched_group_barrier (one memory op between MFMAs).
+// The order is pinned with sched_barrier (hipcc otherwise sinks the reads and DMAs to the end of
+// each k-step, where their latency is exposed).  SCHED = 0: [B] issues the fragment reads first;
+// SCHED = 1: they are spread over [B]'s MFMA chunks like the DMAs.
 // Reference: src/layer/convolution_layer-inl.hpp:70-155, src/layer/fullc_layer-inl.hpp:101-130.
 #include "gemm_glds_common.h"
 
 using namespace cxg;
 
 namespace {
+
+// One MFMA row (8 accumulators) as inline asm: with the builtin, hipcc rotated the 256 loop-carried
+// accumulators through other AGPRs / VGPRs (352 v_accvgpr_* per 128 MFMAs); the "+a" operand pins
+// each accumulator in place.  Hazards hipcc no longer pads (cdna guide 5.7 item 2): the chain
+// MFMA D -> next MFMA's C needs none; the A/B operands are written only by ds_read (the loop is
+// audited for VALU writes of them: benchmarks/asm_audit.py); the reads of D after the main loop
+// are padded there.
+template <int NR>
+__device__ __forceinline__ void mfma_row_asm(f32x4 (&acc)[NR], const bf16x8 &a, const bf16x8 (&fb)[NR]) {
+#pragma unroll
+  for (int n = 0; n < NR; ++n)
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[n]) : "v"(a), "v"(fb[n]));
+}
 
 template <int BM, int BN, int AMODE, int BMODE, int EPI, int SCHED>
 __global__ void __launch_bounds__(256, 1)
@@ -34,6 +49,7 @@ gemm_4w(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
   using OA = Op<AMODE, BM, NW>;
   using OB = Op<BMODE, BN, NW>;
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
+  constexpr int NPT = OA::NI + OB::NI;  // DMA instructions per wave per K-tile
   static_assert(NW * 16 * (WM + 4) * 4 <= 2 * STAGE, "epilogue staging fits");
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
 
@@ -59,22 +75,52 @@ gemm_4w(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
   OB ob;
   oa.init(A, i0, goA, wave, lane);
   ob.init(B, j0, goB, wave, lane);
+  // K_DIRECT operands: DMA s reads rows 32 s further than DMA 0 -- one base register and a
+  // stride instead of one row offset per DMA (rows past the operand read zeros (outside the
+  // buffer) or rows of the next group, which only feed output rows the epilogue never stores)
+  const uint32_t rsA = 32u * static_cast<uint32_t>(A.ld) * 2u, rsB = 32u * static_cast<uint32_t>(B.ld) * 2u;
+  const uint32_t baseA = goA + static_cast<uint32_t>((i0 + 8 * wave + (lane >> 3)) * A.ld) * 2u;
+  const uint32_t baseB = goB + static_cast<uint32_t>((j0 + 8 * wave + (lane >> 3)) * B.ld) * 2u;
+  auto offA = [&](auto sc, const typename OA::Prep &p) __attribute__((always_inline)) -> uint32_t {
+    constexpr int s = decltype(sc)::value;
+    if constexpr (AMODE == K_DIRECT) {
+      uint32_t off = p.kin ? baseA + static_cast<uint32_t>(p.k) * 2u + s * rsA : OOB;
+      asm volatile("" : "+v"(off));
+      return off;
+    } else {
+      return oa.template offset<s>(A, p, wave, lane);
+    }
+  };
+  auto offB = [&](auto sc, const typename OB::Prep &p) __attribute__((always_inline)) -> uint32_t {
+    constexpr int s = decltype(sc)::value;
+    if constexpr (BMODE == K_DIRECT) {
+      uint32_t off = p.kin ? baseB + static_cast<uint32_t>(p.k) * 2u + s * rsB : OOB;
+      asm volatile("" : "+v"(off));
+      return off;
+    } else {
+      return ob.template offset<s>(B, p, wave, lane);
+    }
+  };
 
+  // DMA instruction q (0 .. NPT-1) of K-tile t into buffer t & 1: A's NI first, then B's
+  auto dma = [&](auto qc, int t, const typename OA::Prep &pa, const typename OB::Prep &pb)
+      __attribute__((always_inline)) -> void {
+    constexpr int q = decltype(qc)::value;
+    char *sa = smem + (t & 1) * STAGE;
+    if constexpr (q < OA::NI) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void *)(sa + (wave + NW * q) * 1024), 16,
+                                               offA(std::integral_constant<int, q>{}, pa), 0, 0, 0);
+    } else {
+      constexpr int s = q - OA::NI;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void *)(sa + A_BYTES + (wave + NW * s) * 1024), 16,
+                                               offB(std::integral_constant<int, s>{}, pb), 0, 0, 0);
+    }
+  };
   auto issue = [&](int t) __attribute__((always_inline)) {
     const int kt = kt_beg + t;
-    char *sa = smem + (t & 1) * STAGE;
     const typename OA::Prep pa = oa.prep(A, kt, kt_end, goA);
     const typename OB::Prep pb = ob.prep(B, kt, kt_end, goB);
-    static_for<OA::NI>([&](auto sc) {
-      constexpr int s = decltype(sc)::value;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void *)(sa + (wave + NW * s) * 1024), 16,
-                                               oa.template offset<s>(A, pa, wave, lane), 0, 0, 0);
-    });
-    static_for<OB::NI>([&](auto sc) {
-      constexpr int s = decltype(sc)::value;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void *)(sa + A_BYTES + (wave + NW * s) * 1024), 16,
-                                               ob.template offset<s>(B, pb, wave, lane), 0, 0, 0);
-    });
+    static_for<NPT>([&](auto qc) { dma(qc, t, pa, pb); });
   };
 
   f32x4 acc[MR][NR];
@@ -83,57 +129,77 @@ gemm_4w(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
 #pragma unroll
     for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 a0[MR], b0[NR], a1[MR], b1[NR];
-  auto read = [&](int t, int kk, bf16x8 (&fa)[MR], bf16x8 (&fb)[NR]) __attribute__((always_inline)) {
-    const char *sa = smem + (t & 1) * STAGE;
-#pragma unroll
-    for (int m = 0; m < MR; ++m) fa[m] = frag<K_DIRECT>(sa, wr * WM + m * 16, kk, lane);
-#pragma unroll
-    for (int n = 0; n < NR; ++n) fb[n] = frag<K_DIRECT>(sa + A_BYTES, wc * WN + n * 16, kk, lane);
+  // Fragment registers: one A set, refilled row by row right behind its last MFMA, and two B
+  // sets that alternate between k-steps (B fragments are used by every MFMA row, so the next
+  // k-step's B needs registers of its own): 96 fragment VGPRs next to the 256 accumulators.
+  bf16x8 fa[MR], fb0[NR], fb1[NR];
+  auto read_a = [&](auto mc, int t, int kk) __attribute__((always_inline)) -> void {
+    constexpr int m = decltype(mc)::value;
+    fa[m] = frag<K_DIRECT>(smem + (t & 1) * STAGE, wr * WM + m * 16, kk, lane);
   };
-  auto mfma = [&](const bf16x8 (&fa)[MR], const bf16x8 (&fb)[NR]) __attribute__((always_inline)) {
+  auto read_b = [&](int t, int kk, bf16x8 (&fb)[NR]) __attribute__((always_inline)) -> void {
+    const char *sb = smem + (t & 1) * STAGE + A_BYTES;
 #pragma unroll
-    for (int m = 0; m < MR; ++m)
-#pragma unroll
-      for (int n = 0; n < NR; ++n)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
+    for (int n = 0; n < NR; ++n) fb[n] = frag<K_DIRECT>(sb, wc * WN + n * 16, kk, lane);
+  };
+  auto mfma_row = [&](auto mc, const bf16x8 (&fb)[NR]) __attribute__((always_inline)) -> void {
+    constexpr int m = decltype(mc)::value;
+    mfma_row_asm<NR>(acc[m], fa[m], fb);
   };
 
-  // prologue: tiles 0 and 1 in flight, tile 0 landed for every wave, F0 of tile 0 read
+  // prologue: tiles 0 and 1 in flight, tile 0 landed for every wave, k-step 0 of tile 0 read
   issue(0);
   issue(1);
-  wait_vmcnt<OA::NI + OB::NI>();
+  wait_vmcnt<NPT>();
   block_barrier();
-  read(0, 0, a0, b0);
+  static_for<MR>([&](auto mc) { read_a(mc, 0, 0); });
+  read_b(0, 0, fb0);
 
   for (int t = 0; t < nt; ++t) {
-    // [A] k-step 1 fragments of tile t under the k-step 0 MFMAs
-    read(t, 32, a1, b1);
-    mfma(a0, b0);
-    if constexpr (SCHED) {
-#pragma unroll
-      for (int q = 0; q < MR + NR; ++q) {
-        __builtin_amdgcn_sched_group_barrier(0x008, MR * NR / (MR + NR), 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                      // DS read
-      }
-    }
+    // [A] k-step 0 of tile t (fa, fb0); reads of k-step 1: fb1 first, fa row by row
+    read_b(t, 32, fb1);
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<MR>([&](auto mc) {
+      mfma_row(mc, fb0);
+      read_a(mc, t, 32);
+      __builtin_amdgcn_sched_barrier(0);
+    });
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of buffer t & 1 are done
     wait_vmcnt<0>();                     // tile t + 1 has landed (this wave's DMAs)
     block_barrier();
-    // [B] k-step 0 fragments of tile t+1, DMAs of tile t+2 into buffer t & 1, k-step 1 MFMAs
-    read(t + 1, 0, a0, b0);
-    issue(t + 2);
-    mfma(a1, b1);
-    if constexpr (SCHED) {
-#pragma unroll
-      for (int q = 0; q < MR + NR; ++q) {
-        __builtin_amdgcn_sched_group_barrier(0x008, MR * NR / (2 * (MR + NR)), 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                            // DS read
-        __builtin_amdgcn_sched_group_barrier(0x008, MR * NR / (2 * (MR + NR)), 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x020, (OA::NI + OB::NI) / (MR + NR), 0);  // VMEM (LDS-DMA)
-      }
+    // [B] k-step 1 of tile t (fa, fb1); reads of k-step 0 of tile t+1 (fb0, then fa row by row)
+    // and the DMAs of tile t+2 into buffer t & 1, spread over the MFMA rows
+    read_b(t + 1, 0, fb0);
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      const int kt = kt_beg + t + 2;
+      const typename OA::Prep pa = oa.prep(A, kt, kt_end, goA);
+      const typename OB::Prep pb = ob.prep(B, kt, kt_end, goB);
+      static_for<MR>([&](auto mc) {
+        constexpr int m = decltype(mc)::value;
+        constexpr int qlo = m * NPT / MR, qhi = (m + 1) * NPT / MR;
+        static_for<qhi - qlo>([&](auto dc) {
+          constexpr int q = qlo + decltype(dc)::value;
+          char *sa = smem + (t & 1) * STAGE;
+          if constexpr (q < OA::NI) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void *)(sa + (wave + NW * q) * 1024), 16,
+                                                     offA(std::integral_constant<int, q>{}, pa), 0, 0, 0);
+          } else {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void *)(sa + A_BYTES + (wave + NW * (q - OA::NI)) * 1024),
+                                                     16, offB(std::integral_constant<int, q - OA::NI>{}, pb), 0, 0, 0);
+          }
+        });
+        mfma_row(mc, fb1);
+        read_a(mc, t + 1, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      });
     }
+    // retire tile t+1's k-step 0 reads behind [B]'s MFMAs: the next [A] then waits on nothing
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_sched_barrier(0);
   }
+  // the last MFMAs' results are read by compiler code below: 8-pass XDL -> 12 wait states
+  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
   wait_vmcnt<0>();
   __syncthreads();  // the epilogue reuses the stage buffers
 
