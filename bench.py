@@ -203,7 +203,8 @@ def main():
             "per_rank_ms_per_step": [round(x / a.steps * 1000.0, 3) for x in per_rank],
             "dp": {"mode": ("shard" if red.shard else "allreduce") if red.active else "none",
                    "buckets": len(red.buckets) if red.active else 0,
-                   "comm_bytes_per_step_per_rank": red.comm_bytes_per_step(),
+                   "comm_bytes_per_step_per_rank": tr.comm_bytes_per_step(),
+                   "fullc_gather": any(getattr(c.layer, "fullc_gather", 0) for c in tr.net.connections),
                    "overlapped_update": red.handles_update},
             "baseline": (f"torch eager {a.model} {base:.0f} img/s per GPU x {world} (BASELINE.json measured)"
                          if base else None),

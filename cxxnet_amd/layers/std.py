@@ -82,7 +82,8 @@ class FullConnectLayer(Layer):
         B x (nin + nout) activations/gradients of every rank and form the global
         gradient locally.  Active only under plain (non-sharded) data parallelism."""
         from ..parallel.dp import world_info
-        return bool(self.fullc_gather) and world_info()[1] > 1 and not getattr(self.ctx, "dp_shard", False)
+        # (dp_force: a one-rank process group runs the gather too -- the RCCL path on one GPU)
+        return bool(self.fullc_gather) and (world_info()[1] > 1 or bool(getattr(self.ctx, "dp_force", False)))
 
     def forward(self, is_train, nodes_in, nodes_out):
         bias = self.b.w if self.b is not None else None
@@ -92,15 +93,19 @@ class FullConnectLayer(Layer):
             self._x_all = _all_gather_rows(x, nodes_in[0].shape[0])
         ops.fc_forward(x, self.w.wb, bias, nodes_out[0].mat(), relu=self.fuse_relu)
 
-    def _fused_sgd(self, x, dy, prop_grad, nodes_in) -> bool:
-        """Single-GPU SGD step of the weights fused into the weight-gradient GEMM
-        (ctx.sgd_fuse = the arena updater, set by the trainer when eligible).  The data
-        gradient reads the OLD shadow weights, so it runs first, into a scratch buffer (x,
-        which the weight-gradient still needs, lives where it goes); the scratch is copied
-        back (with relu' when fused) after the update."""
+    def _fused_sgd(self, x, dy, prop_grad, nodes_in, xw=None, dyw=None) -> bool:
+        """SGD step of the weights fused into the weight-gradient GEMM (ctx.sgd_fuse = the
+        arena updater, set by the trainer when eligible): one GPU, or -- under data
+        parallelism -- a fullc_gather layer, whose gradient is formed from the all-gathered
+        rows (xw, dyw) and is the same global gradient on every rank.  The data gradient reads
+        the OLD shadow weights, so it runs first, into a scratch buffer (x, which the
+        weight-gradient still needs, lives where it goes); the scratch is copied back (with
+        relu' when fused) after the update."""
         upd = getattr(self.ctx, "sgd_fuse", None)
         if upd is None or not (getattr(self.ctx, "grad_overwrite", False) and self.w.overwrite) or not self.ctx.is_gpu:
             return False
+        if getattr(self.ctx, "dp_active", False) and xw is None:
+            return False  # a reduced gradient: the step must follow the reduction
         spec = self.w
         lr, wd, mom, clip = upd.hyper(spec, self.ctx.epoch)
         a = upd.arena
@@ -111,10 +116,11 @@ class FullConnectLayer(Layer):
                 self._dx = torch.empty_like(x)
             gx = self._dx[:x.shape[0]]
             ops.fc_backward_data(dy, spec.wb, gx)
-        if ops.fc_backward_weight_sgd(x, dy, spec.w, m, spec.wb, lr, wd, mom, clip):
+        xg, dyg = (x, dy) if xw is None else (xw, dyw)
+        if ops.fc_backward_weight_sgd(xg, dyg, spec.w, m, spec.wb, lr, wd, mom, clip):
             upd.fused_offsets.add(spec.offset)
         else:  # the kernel does not cover this shape: plain gradient, updated by the updater
-            ops.fc_backward_weight(x, dy, spec.g, overwrite=True)
+            ops.fc_backward_weight(xg, dyg, spec.g, overwrite=True)
         if gx is not None:
             dst = nodes_in[0].gmat()
             ops.channel_copy(gx, 0, dst, 0, dst.shape[1], mask_relu=self.grad_mask_relu)
@@ -130,8 +136,13 @@ class FullConnectLayer(Layer):
         if self._gathering():
             dy_all = _all_gather_rows(dy, nodes_out[0].shape[0])
             x_all = self._x_all.wait()
-            ops.fc_backward_weight(x_all, dy_all.wait(), self.w.g, overwrite=overwrite)
             self._x_all = None
+            dyw = dy_all.wait()
+            if self._fused_sgd(x, dy, prop_grad, nodes_in, xw=x_all, dyw=dyw):
+                if self.b is not None:
+                    self.ctx.bias_grad(dy, self.b.g)
+                return
+            ops.fc_backward_weight(x_all, dyw, self.w.g, overwrite=overwrite)
         else:
             ops.fc_backward_weight(x, dy, self.w.g, overwrite=overwrite)
         if self.b is not None:

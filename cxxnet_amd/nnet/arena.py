@@ -30,17 +30,24 @@ class ParamArena:
 
     def build(self, layer_specs: Sequence[tuple]):
         """layer_specs: [(layer_index, [ParamSpec, ...]), ...] in forward order."""
+        from ..parallel.dp import world_info
+        # a multiple of world*ALIGN, so that sharded buckets split into equal,
+        # aligned per-rank chunks (parallel/dp.py, update_on_server); a segment whose gradient
+        # is not reduced (fullc_gather) starts and ends on such a boundary, so the reduced runs
+        # between them split evenly too
+        q = ALIGN * world_info()[1]
         off = 0
         self.specs = []
         for li, specs in sorted(layer_specs, key=lambda t: -t[0]):
             for s in specs:
+                nr = getattr(s, "no_reduce", False)
+                if nr:
+                    off = (off + q - 1) // q * q
                 s.offset = off
                 self.specs.append((li, s))
                 off += (s.numel + ALIGN - 1) // ALIGN * ALIGN
-        # a multiple of world*ALIGN, so that sharded buckets split into equal,
-        # aligned per-rank chunks (parallel/dp.py, update_on_server)
-        from ..parallel.dp import world_info
-        q = ALIGN * world_info()[1]
+                if nr:
+                    off = (off + q - 1) // q * q
         self.total = max((off + q - 1) // q * q, q)
         dev = self.device
         self.w = torch.zeros(self.total, dtype=torch.float32, device=dev)

@@ -27,6 +27,11 @@ from ..utils.metric import DeviceMetricSet, MetricSet
 from .neural_net import NeuralNet
 
 
+def _dist_ready() -> bool:
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
 def prune_devices(batch_size: int, ndev: int) -> int:
     """Number of devices that cover a batch (reference nnet_impl-inl.hpp:344-354)."""
     ndev = max(int(ndev), 1)
@@ -215,6 +220,7 @@ class NetTrainer:
         self._apply_modes()
         net = NeuralNet(self.net_cfg, self._local_batch(), self._device(), seed=self.seed)
         net.ctx.dp_shard = self._use_shard()
+        net.ctx.dp_force = bool(self.dp_force) and self.world == 1 and _dist_ready()
         return net
 
     def _forward_global_params(self, net: NeuralNet):
@@ -389,6 +395,8 @@ class NetTrainer:
         rank's rows directly when local=True."""
         need_update = (self.sample_counter + 1) % self.update_period == 0
         first = self.sample_counter % self.update_period == 0
+        if self.net.updater is not None:  # offsets of fc steps fused into this step's GEMMs
+            self.net.updater.fused_offsets.clear()
         self._set_batch(batch, local)
         net = self.net
         self._cur_batch = batch
@@ -402,6 +410,7 @@ class NetTrainer:
         if need_update:
             self.reducer.start_step()
             net.ctx.sgd_fuse = self._sgd_fuse_target()
+            net.ctx.dp_active = self.reducer.active
             net.ctx.epoch = self.epoch_counter
             red = self.reducer
             hook = red.hook if (red.active or red.update_fn is not None) else None
@@ -443,6 +452,23 @@ class NetTrainer:
             self._tile_syncs += 1
             from ..ops import gemm
             gemm.sync_tune_table()
+
+    def comm_bytes_per_step(self) -> int:
+        """Bytes handed to collectives per update step on this rank: the gradient buckets
+        (GradReducer.comm_bytes_per_step) plus, for every fullc_gather layer, the all-gathered
+        [in | out-grad] rows (bf16, world x local rows each)."""
+        red = self.reducer
+        tot = red.comm_bytes_per_step() if red is not None else 0
+        if self.world > 1 or (red is not None and red.active):
+            for conn in self.net.connections:
+                lay = conn.layer
+                if getattr(lay, "_gathering", None) is not None and lay._gathering():
+                    rows = conn.nodes_in[0].shape[0]
+                    nin = lay.lp.num_input_node
+                    nout = lay.lp.num_hidden
+                    esz = 2 if self.net.ctx.is_gpu else 4
+                    tot += rows * (nin + nout) * esz * max(self.world, 1)
+        return tot
 
     # ------------------------------------------------------------------ step instrumentation
     def _events(self):
@@ -532,14 +558,17 @@ class NetTrainer:
 
     def _sgd_fuse_target(self):
         """The arena updater when the fc weight steps may run inside the weight-gradient
-        GEMM (FullConnectLayer._fused_sgd): one GPU, SGD, one micro-batch per update, no
-        non-finite check (the gradient never reaches memory).  Under data parallelism the
-        gradients must be reduced before the step, so it stays separate."""
+        GEMM (FullConnectLayer._fused_sgd): SGD, one micro-batch per update, no non-finite
+        check (the gradient never reaches memory).  One GPU: every fc layer; under data
+        parallelism only fullc_gather layers (ctx.dp_active), whose all-gathered gradient is
+        already global -- a reduced gradient must be reduced before its step."""
         net, red = self.net, self.reducer
         if not _FUSE_FC_SGD or net.device.type != "cuda" or self.update_period != 1 or self.check_nonfinite:
             return None
         upd = net.updater
-        if upd is None or upd.algo != "sgd" or red is None or red.active or red.handles_update:
+        if upd is None or upd.algo != "sgd" or red is None:
+            return None
+        if not red.active and red.handles_update:
             return None
         return upd
 

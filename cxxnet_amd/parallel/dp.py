@@ -133,18 +133,34 @@ class GradReducer:
         q = ALIGN * max(self.world, 1)
         total = self.arena.total
         assert total % q == 0, "arena must be padded to world*ALIGN"
-        segs = [(spec.offset, spec.offset + spec.numel, li) for li, spec in self.arena.specs]
-        start = 0
-        while start < total:
-            end = min(total, start + max(q, (limit + q - 1) // q * q))
-            # extend to the end of the segment that the cut falls into, rounded up to q
-            for a, b, _ in segs:
-                if a < end < b:
-                    end = min(total, (b + q - 1) // q * q)
-                    break
-            lis = [li for a, b, li in segs if a < end and b > start]
-            self.buckets.append(Bucket(start, end, min(lis) if lis else -1))
-            start = end
+        segs = [(spec.offset, spec.offset + spec.numel, li) for li, spec in self.arena.specs
+                if not getattr(spec, "no_reduce", False)]
+        # fullc_gather segments (q-aligned by the arena) hold a global gradient: every rank
+        # updates them whole, they are cut out of the reduced runs
+        runs, pos = [], 0
+        for li, spec in self.arena.specs:
+            if getattr(spec, "no_reduce", False):
+                lo, hi = spec.offset, (spec.offset + spec.numel + q - 1) // q * q
+                assert lo % q == 0, "fullc_gather segment not aligned to world*ALIGN"
+                self.extra_ranges.append((spec.offset, spec.offset + spec.numel))
+                if lo > pos:
+                    runs.append((pos, lo))
+                pos = hi
+        if total > pos:
+            runs.append((pos, total))
+        for r0, r1 in runs:
+            start = r0
+            while start < r1:
+                end = min(r1, start + max(q, (limit + q - 1) // q * q))
+                # extend to the end of the segment that the cut falls into, rounded up to q
+                for a, b, _ in segs:
+                    if a < end < b:
+                        end = min(r1, (b + q - 1) // q * q)
+                        break
+                lis = [li for a, b, li in segs if a < end and b > start]
+                if lis:
+                    self.buckets.append(Bucket(start, end, min(lis)))
+                start = end
         if self.inplace:
             return
         for b in self.buckets:
@@ -163,8 +179,9 @@ class GradReducer:
                     self.layer_buckets.setdefault(li, []).append(bi)
 
     def owned_ranges(self):
-        """[start, end) arena ranges this rank updates (sharded mode)."""
-        return [b.own(self.rank, self.world) for b in self.buckets]
+        """[start, end) arena ranges this rank updates (sharded mode): its slice of every
+        bucket, plus the fullc_gather segments, which every rank updates whole."""
+        return [b.own(self.rank, self.world) for b in self.buckets] + list(self.extra_ranges)
 
     @property
     def active(self):

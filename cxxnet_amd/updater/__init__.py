@@ -112,7 +112,8 @@ class ArenaUpdater:
         self.arena = arena
         self.entries = []  # (ParamSpec, UpdaterParam)
         # arena offsets whose SGD step already ran this step inside the fc weight-gradient
-        # GEMM (ops.fc_backward_weight_sgd); update() skips them once, then clears the set
+        # GEMM (ops.fc_backward_weight_sgd); update() skips them (every call of the step: the
+        # overlapped update calls it once per bucket); the trainer clears the set per step
         self.fused_offsets = set()
         self.beta1 = 0.1
         self.beta2 = 0.001
@@ -172,9 +173,8 @@ class ArenaUpdater:
             self._segs = self.segments(epoch)
             self._seg_epoch = epoch
         segs = self._segs
-        if self.fused_offsets:
+        if self.fused_offsets:  # cleared by the trainer at the start of each step
             segs = [sg for sg in segs if sg[0] not in self.fused_offsets]
-            self.fused_offsets = set()
         if ranges is not None:
             segs = _clip_segments(segs, ranges)
         # gradients are reset by the next cycle's first backprop (NeuralNet.backprop(first=True))

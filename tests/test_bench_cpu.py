@@ -54,3 +54,25 @@ def test_bench_rank_mismatch_fails():
               "--batch", "8", "--steps", "1", "--warmup", "0"])
     assert r.returncode != 0
     assert "process group holds 1" in r.stderr
+
+
+def test_bench_8_ranks_weak():
+    r = _run(["bench.py", "--gpus", "8", "--device", "cpu", "--model", "mnist_mlp", "--batch", "8",
+              "--steps", "2", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _json(r.stdout)
+    assert out["n_gpus"] == 8 and out["world_size"] == 8 and len(out["per_rank_ms_per_step"]) == 8
+    assert out["config"]["global_batch"] == 64 and out["dp"]["mode"] == "allreduce"
+
+
+def test_bench_8_ranks_strong_alexnet_fullc_gather():
+    """AlexNet at the strong-scaling split (256 over 8 ranks = 32 rows each) with fullc_gather:
+    the fc layers all-gather [in | out-grad] rows instead of reducing their 58.6 M gradient
+    values, so a rank hands <= 40 MB per step to collectives (fp32 here; the GPU gathers bf16)
+    against 244 MB of fp32 gradients without it."""
+    r = _run(["bench.py", "--gpus", "8", "--device", "cpu", "--model", "alexnet", "--batch", "256",
+              "--scaling", "strong", "--set", "fullc_gather=1", "--steps", "1", "--warmup", "0"], timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _json(r.stdout)
+    assert out["config"]["per_gpu_batch"] == 32 and out["dp"]["fullc_gather"]
+    assert out["dp"]["comm_bytes_per_step_per_rank"] <= 40e6, out["dp"]

@@ -83,10 +83,9 @@ def _worker(rank, world, port, steps, out, update_period, shard=0, B=8):
     assert tr.reducer.check_consistency() == 0.0
     line = tr.evaluate(None, "train")
     tr.reducer.sync_master()
-    if rank == 0:
-        torch.save({"w": tr.net.arena.w.clone(), "line": line}, out)
-    else:
-        torch.save({"w": tr.net.arena.w.clone(), "line": line}, out + ".r1")
+    params = [tr.net.arena.w[sp.offset:sp.offset + sp.numel].clone() for _, sp in tr.net.arena.specs]
+    rec = {"w": tr.net.arena.w.clone(), "line": line, "params": params}
+    torch.save(rec, out if rank == 0 else out + ".r1")
     dist.destroy_process_group()
 
 
@@ -108,8 +107,12 @@ def test_dp_two_ranks_equals_single_process(tmp_path, update_period, shard, B):
     x, y = _data(B)
     for _ in range(steps):
         tr.update(DataBatch(x, y))
-    n = tr.net.arena.total  # the 2-rank arena may carry extra zero padding
-    assert torch.allclose(r0["w"][:n], tr.net.arena.w, rtol=1e-4, atol=1e-6)
+    # per parameter: the 2-rank arena carries extra padding (fullc_gather segments sit on
+    # world*ALIGN boundaries)
+    single = [tr.net.arena.w[sp.offset:sp.offset + sp.numel] for _, sp in tr.net.arena.specs]
+    assert len(single) == len(r0["params"])
+    for a, b in zip(r0["params"], single):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-6)
     assert r0["line"] == tr.evaluate(None, "train")
 
 

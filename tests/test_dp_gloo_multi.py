@@ -35,10 +35,14 @@ def _worker(rank, world, port, steps, out, mode, update_period, B, save_dir):
         extra += [("dp_mode", "shard")]
     elif mode == "gather":
         extra += [("fullc_gather", "1")]
+    elif mode == "shard_gather":  # sharded conv buckets + all-gathered fc layers
+        extra += [("fullc_gather", "1"), ("dp_mode", "shard")]
     else:
         extra += [("dp_mode", "allreduce")]
     tr = _make(B, extra)
-    assert tr.reducer.shard == (mode in ("shard", "shard_inplace"))
+    assert tr.reducer.shard == (mode in ("shard", "shard_inplace", "shard_gather"))
+    if "gather" in mode:
+        assert len(tr.reducer.extra_ranges) == 2  # both fc weight matrices
     if mode == "shard_inplace":
         assert tr.reducer.inplace
     x, y = _data(B)
@@ -51,9 +55,30 @@ def _worker(rank, world, port, steps, out, mode, update_period, B, save_dir):
     blob = tr.save_model(sync=False) if rank == 0 else None
     if rank == 0:
         tr.save_optimizer_state(os.path.join(save_dir, "opt.state"), sync=False)
-    torch.save({"w": tr.net.arena.w.clone(), "m1": tr.net.arena.m1.clone(), "line": line,
-                "blob": blob, "idle": tr.idle, "active": tr.active_ranks()}, f"{out}.r{rank}")
+    a = tr.net.arena
+    if rank == 0:
+        torch.save([(sp.offset, sp.numel) for _, sp in a.specs], os.path.join(save_dir, "layout.pt"))
+    torch.save({"w": a.w.clone(), "m1": a.m1.clone(), "line": line, "params": _params(tr), "blob": blob,
+                "idle": tr.idle, "active": tr.active_ranks()}, f"{out}.r{rank}")
     dist.destroy_process_group()
+
+
+def _params(tr):
+    """Per-parameter fp32 master weights (the arena layout differs between world sizes:
+    fullc_gather segments sit on world*ALIGN boundaries)."""
+    return [tr.net.arena.w[s.offset:s.offset + s.numel].clone() for _, s in tr.net.arena.specs]
+
+
+def _opt_params(tr, m1):
+    return [m1[s.offset:s.offset + s.numel] for _, s in tr.net.arena.specs]
+
+
+def _make_world_layout(tmp_path, world):
+    return torch.load(str(tmp_path / "layout.pt"), weights_only=True)
+
+
+def _close(a, b):
+    return len(a) == len(b) and all(torch.allclose(x, y, rtol=1e-4, atol=1e-6) for x, y in zip(a, b))
 
 
 def _run(tmp_path, world, mode, update_period, B, steps=3):
@@ -79,21 +104,22 @@ def _single(B, update_period, steps=3):
     (8, "shard_inplace", 1, 16),  # RCCL's in-place reduce-scatter / all-gather layout, on gloo
     (8, "allreduce", 2, 17),      # ceil split 3*5+2, update_period 2
     (8, "gather", 1, 16),
+    (4, "shard_gather", 1, 10),   # fullc_gather composed with the sharded update
+    (8, "shard_gather", 2, 16),
 ])
 def test_dp_multi_rank_equals_single_process(tmp_path, world, mode, update_period, B):
     rs = _run(tmp_path, world, mode, update_period, B)
     for r in rs[1:]:
         assert torch.equal(rs[0]["w"], r["w"]), "replicas diverged"
     tr = _single(B, update_period)
-    n = tr.net.arena.total
-    assert torch.allclose(rs[0]["w"][:n], tr.net.arena.w, rtol=1e-4, atol=1e-6)
+    assert _close(rs[0]["params"], _params(tr))
     assert rs[0]["line"] == tr.evaluate(None, "train")
-    # the saved model (rank 0, after the all-rank gather) equals the single-process model's
-    # bytes up to float rounding of the weights: compare through a reload
     assert rs[0]["blob"] is not None
-    # optimizer state: sharded mode gathers every rank's momentum slice before the save
+    # optimizer state: sharded mode gathers every rank's momentum slice before the save; the
+    # saved state is in the multi-rank arena layout, compared per parameter
     m1 = torch.load(str(tmp_path / "opt.state"), weights_only=True)["m1"]
-    assert torch.allclose(m1[:n], tr.net.arena.m1, rtol=1e-4, atol=1e-6)
+    trw = _make_world_layout(tmp_path, world)
+    assert _close([m1[o:o + n] for o, n in trw], _opt_params(tr, tr.net.arena.m1))
 
 
 def test_device_pruning_rule():
@@ -117,8 +143,7 @@ def test_idle_ranks_batch10_world8(tmp_path):
     for r in rs[1:]:
         assert torch.equal(rs[0]["w"], r["w"])
     tr = _single(10, 1)
-    n = tr.net.arena.total
-    assert torch.allclose(rs[0]["w"][:n], tr.net.arena.w, rtol=1e-4, atol=1e-6)
+    assert _close(rs[0]["params"], _params(tr))
     assert rs[0]["line"] == tr.evaluate(None, "train")
 
 

@@ -59,6 +59,9 @@ def _worker(rank, world, port, steps, out, extra, backend="gloo"):
         assert tr._graphs, "the data-parallel step did not run as graph segments"
         fwd, bwd = next(iter(tr._graphs.values()))
         assert sum(callable(i) and not isinstance(i, torch.cuda.CUDAGraph) for i in fwd + bwd) > 0
+    if any(k == "fullc_gather" for k, _ in extra):
+        # the gathered fc layers ran their SGD step inside the weight-gradient GEMM
+        assert tr.net.ctx.dp_active and len(tr.net.updater.fused_offsets) == 2, tr.net.updater.fused_offsets
     tr.reducer.sync_master()  # sharded: each rank updated only its slice of the fp32 masters
     torch.save(tr.net.arena.w.cpu(), out + f".r{rank}")
     dist.destroy_process_group()
@@ -107,4 +110,25 @@ def test_rccl_single_rank_forced_is_exact(tmp_path, mode, graph):
     for _ in range(steps):
         tr.update(DataBatch(x.cuda(), y.cuda()))
     torch.cuda.synchronize()
+    assert torch.equal(r0[: tr.net.arena.total], tr.net.arena.w.cpu())
+
+
+@pytest.mark.parametrize("mode", ["shard", "allreduce"])
+def test_rccl_forced_fullc_gather_fused_sgd(tmp_path, mode):
+    """fullc_gather under data parallelism (RCCL, world 1 forced): the fc layers all-gather
+    [in | out-grad] rows and -- their gradient being global -- take the SGD step inside the
+    weight-gradient GEMM (EPI_F32_SGD), as the single-GPU path does; the conv layers' buckets
+    are reduced (sharded or all-reduced).  Bit-exact against the single-GPU run."""
+    steps = 4
+    out = str(tmp_path / "w")
+    extra = [("dp_mode", mode), ("dp_bucket_mb", "0.002"), ("fullc_gather", "1")]
+    mp.spawn(_worker, args=(1, _free_port(), steps, out, extra, "nccl"), nprocs=1, join=True)
+    r0 = torch.load(out + ".r0", weights_only=True)
+    from cxxnet_amd.io.data import DataBatch
+    tr = _make(8, [])
+    x, y = _data(8)
+    for _ in range(steps):
+        tr.update(DataBatch(x.cuda(), y.cuda()))
+    torch.cuda.synchronize()
+    assert len(tr.net.updater.fused_offsets) == 2  # the single-GPU run fuses both fc steps too
     assert torch.equal(r0[: tr.net.arena.total], tr.net.arena.w.cpu())
