@@ -20,8 +20,8 @@
 //   so one barrier per K-tile, no wait on an LDS read in front of an MFMA, and a DMA has
 //   [B] + [A] (two k-steps of MFMAs) to land.  Past the K slice the DMAs are all-OOB dummies.
 // The order is pinned with sched_barrier (hipcc otherwise sinks the reads and DMAs to the end of
-// each k-step, where their latency is exposed).  SCHED = 0: [B] issues the fragment reads first;
-// SCHED = 1: they are spread over [B]'s MFMA chunks like the DMAs.
+// each k-step, where their latency is exposed).  SCHED = 0: [B]'s DMAs are spread evenly over its
+// MFMAs; SCHED = 1: one in front of each of the first MFMAs (a burst: more time to land).
 // Reference: src/layer/convolution_layer-inl.hpp:70-155, src/layer/fullc_layer-inl.hpp:101-130.
 #include "gemm_glds_common.h"
 
@@ -35,6 +35,10 @@ namespace {
 // MFMA D -> next MFMA's C needs none; the A/B operands are written only by ds_read (the loop is
 // audited for VALU writes of them: benchmarks/asm_audit.py); the reads of D after the main loop
 // are padded there.
+__device__ __forceinline__ void mfma_asm(f32x4 &acc, const bf16x8 &a, const bf16x8 &b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
 template <int NR>
 __device__ __forceinline__ void mfma_row_asm(f32x4 (&acc)[NR], const bf16x8 &a, const bf16x8 (&fb)[NR]) {
 #pragma unroll
@@ -50,6 +54,7 @@ gemm_4w(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
   using OB = Op<BMODE, BN, NW>;
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
   constexpr int NPT = OA::NI + OB::NI;  // DMA instructions per wave per K-tile
+  static_assert(NPT <= (MR - 1) * NR, "every DMA gets an MFMA slot in rows 1.. of [B]");
   static_assert(NW * 16 * (WM + 4) * 4 <= 2 * STAGE, "epilogue staging fits");
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
 
@@ -142,6 +147,10 @@ gemm_4w(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
 #pragma unroll
     for (int n = 0; n < NR; ++n) fb[n] = frag<K_DIRECT>(sb, wc * WN + n * 16, kk, lane);
   };
+  auto read_b1 = [&](auto nc, int t, int kk, bf16x8 (&fb)[NR]) __attribute__((always_inline)) -> void {
+    constexpr int n = decltype(nc)::value;
+    fb[n] = frag<K_DIRECT>(smem + (t & 1) * STAGE + A_BYTES, wc * WN + n * 16, kk, lane);
+  };
   auto mfma_row = [&](auto mc, const bf16x8 (&fb)[NR]) __attribute__((always_inline)) -> void {
     constexpr int m = decltype(mc)::value;
     mfma_row_asm<NR>(acc[m], fa[m], fb);
@@ -154,42 +163,60 @@ gemm_4w(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
   block_barrier();
   static_for<MR>([&](auto mc) { read_a(mc, 0, 0); });
   read_b(0, 0, fb0);
+  // retire them here: left pending into the loop, hipcc's wait for them lands in front of the
+  // first MFMA of EVERY iteration (it merges the loop-entry state at the header)
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_sched_barrier(0);
 
   for (int t = 0; t < nt; ++t) {
     // [A] k-step 0 of tile t (fa, fb0); reads of k-step 1: fb1 first, fa row by row
-    read_b(t, 32, fb1);
-    __builtin_amdgcn_sched_barrier(0);
+    // [A] k-step 0 of tile t (fa, fb0); reads of k-step 1: fb1 one per MFMA of row 0, fa row by
+    // row behind each row's last MFMA
     static_for<MR>([&](auto mc) {
-      mfma_row(mc, fb0);
+      constexpr int m = decltype(mc)::value;
+      static_for<NR>([&](auto nc) {
+        constexpr int n = decltype(nc)::value;
+        mfma_asm(acc[m][n], fa[m], fb0[n]);
+        if constexpr (m == 0) read_b1(nc, t, 32, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+      });
       read_a(mc, t, 32);
       __builtin_amdgcn_sched_barrier(0);
     });
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of buffer t & 1 are done
     wait_vmcnt<0>();                     // tile t + 1 has landed (this wave's DMAs)
     block_barrier();
-    // [B] k-step 1 of tile t (fa, fb1); reads of k-step 0 of tile t+1 (fb0, then fa row by row)
-    // and the DMAs of tile t+2 into buffer t & 1, spread over the MFMA rows
-    read_b(t + 1, 0, fb0);
-    __builtin_amdgcn_sched_barrier(0);
+    // [B] k-step 1 of tile t (fa, fb1); reads of k-step 0 of tile t+1 (fb0 one per MFMA of row 0,
+    // fa row by row) and the DMAs of tile t+2 into buffer t & 1 over the remaining MFMAs
     {
       const int kt = kt_beg + t + 2;
       const typename OA::Prep pa = oa.prep(A, kt, kt_end, goA);
       const typename OB::Prep pb = ob.prep(B, kt, kt_end, goB);
+      // DMA q goes in front of MFMA number slot(q) of [B] (rows 1..MR-1): spread evenly
+      // (SCHED 0) or one per MFMA from the first (SCHED 1)
       static_for<MR>([&](auto mc) {
         constexpr int m = decltype(mc)::value;
-        constexpr int qlo = m * NPT / MR, qhi = (m + 1) * NPT / MR;
-        static_for<qhi - qlo>([&](auto dc) {
-          constexpr int q = qlo + decltype(dc)::value;
-          char *sa = smem + (t & 1) * STAGE;
-          if constexpr (q < OA::NI) {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void *)(sa + (wave + NW * q) * 1024), 16,
-                                                     offA(std::integral_constant<int, q>{}, pa), 0, 0, 0);
-          } else {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void *)(sa + A_BYTES + (wave + NW * (q - OA::NI)) * 1024),
-                                                     16, offB(std::integral_constant<int, q - OA::NI>{}, pb), 0, 0, 0);
-          }
+        static_for<NR>([&](auto nc) {
+          constexpr int n = decltype(nc)::value, u = m * NR + n;
+          static_for<NPT>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            constexpr int slot = NR + (SCHED == 1 ? q : q * ((MR - 1) * NR) / NPT);
+            if constexpr (slot == u) {
+              char *sa = smem + (t & 1) * STAGE;
+              if constexpr (q < OA::NI) {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void *)(sa + (wave + NW * q) * 1024), 16,
+                                                         offA(std::integral_constant<int, q>{}, pa), 0, 0, 0);
+              } else {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rB, (lds_void *)(sa + A_BYTES + (wave + NW * (q - OA::NI)) * 1024), 16,
+                    offB(std::integral_constant<int, q - OA::NI>{}, pb), 0, 0, 0);
+              }
+            }
+          });
+          mfma_asm(acc[m][n], fa[m], fb1[n]);
+          if constexpr (m == 0) read_b1(nc, t + 1, 0, fb0);
+          __builtin_amdgcn_sched_barrier(0);
         });
-        mfma_row(mc, fb1);
         read_a(mc, t + 1, 0);
         __builtin_amdgcn_sched_barrier(0);
       });
@@ -220,7 +247,8 @@ void launch_4w(const GOperand &A, const GOperand &B, const GEpi &E, int groups, 
 }  // namespace
 
 namespace cxg {
-// 92: 256x256, 93: 256x256 + sched_group_barrier interleave, 94: 128x256, 95: 256x128
+// 92: 256x256, 94: 128x256, 95: 256x128, 98: 96x256 (DMAs spread over [B]); 93 / 96 / 97 / 100: the same
+// with the DMAs in a burst
 int dispatch_4w(int amode, int bmode, int epi, int tile, const GOperand &A, const GOperand &B, const GEpi &E,
                 int groups, int ksplit, hipStream_t s) {
 #define CX4(AMV, BMV, EPV)                                                                                 \
@@ -230,10 +258,15 @@ int dispatch_4w(int amode, int bmode, int epi, int tile, const GOperand &A, cons
       case 93: launch_4w<256, 256, AMV, BMV, EPV, 1>(A, B, E, groups, ksplit, s); return 0;                \
       case 94: launch_4w<128, 256, AMV, BMV, EPV, 0>(A, B, E, groups, ksplit, s); return 0;                \
       case 95: launch_4w<256, 128, AMV, BMV, EPV, 0>(A, B, E, groups, ksplit, s); return 0;                \
+      case 96: launch_4w<128, 256, AMV, BMV, EPV, 1>(A, B, E, groups, ksplit, s); return 0;                \
+      case 97: launch_4w<256, 128, AMV, BMV, EPV, 1>(A, B, E, groups, ksplit, s); return 0;                \
+      case 98: launch_4w<96, 256, AMV, BMV, EPV, 0>(A, B, E, groups, ksplit, s); return 0;                 \
+      case 100: launch_4w<96, 256, AMV, BMV, EPV, 1>(A, B, E, groups, ksplit, s); return 0;                \
       default: return -1;                                                                                  \
     }                                                                                                      \
   }
-  CX4(K_DIRECT, K_GATHER, EPI_BF16)  // conv fwd / dgrad
+  CX4(K_DIRECT, K_GATHER, EPI_BF16)     // conv fwd / dgrad
+  CX4(K_DIRECT, K_ROWGATHER, EPI_BF16)  // conv fwd, few input channels (AlexNet conv1)
   CX4(K_DIRECT, K_DIRECT, EPI_BF16)  // fc fwd, square GEMMs
   CX4(K_DIRECT, K_DIRECT, EPI_F32)   // fc fwd split-K
 #undef CX4

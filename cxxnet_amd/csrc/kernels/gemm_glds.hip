@@ -693,7 +693,8 @@ int dispatch(int amode, int bmode, int epi, int tile, const GOperand &A, const G
     if (tile == 50) { launch_seg<256, 256, AMV, BMV, EPV>(A, B, E, groups, ksplit, s); return 0; }  \
     if (tile == 51) { launch_seg<128, 256, AMV, BMV, EPV>(A, B, E, groups, ksplit, s); return 0; }  \
   }
-  if (tile >= 92 && tile <= 97) return cxg::dispatch_4w(amode, bmode, epi, tile, A, B, E, groups, ksplit, s);
+  // (99 is the Python-side pseudo-tile of the register kernel, never passed here)
+  if ((tile >= 92 && tile <= 98) || (tile >= 100 && tile <= 109)) return cxg::dispatch_4w(amode, bmode, epi, tile, A, B, E, groups, ksplit, s);
   if (tile >= 90 && tile <= 99) return cxg::dispatch_8p(amode, bmode, epi, tile, A, B, E, groups, ksplit, s);
   if (tile >= 50 && tile <= 51) {
     CXG_SEG(K_DIRECT, K_GATHER, EPI_BF16)

@@ -60,8 +60,9 @@ def _worker(rank, world, port, steps, out, extra, backend="gloo"):
         fwd, bwd = next(iter(tr._graphs.values()))
         assert sum(callable(i) and not isinstance(i, torch.cuda.CUDAGraph) for i in fwd + bwd) > 0
     if any(k == "fullc_gather" for k, _ in extra):
-        # the gathered fc layers ran their SGD step inside the weight-gradient GEMM
-        assert tr.net.ctx.dp_active and len(tr.net.updater.fused_offsets) == 2, tr.net.updater.fused_offsets
+        # the gathered fc layer the kernel covers (f1: 16 x 128; f2's 5 outputs are not a multiple
+        # of 8) ran its SGD step inside the weight-gradient GEMM
+        assert tr.net.ctx.dp_active and len(tr.net.updater.fused_offsets) == 1, tr.net.updater.fused_offsets
     tr.reducer.sync_master()  # sharded: each rank updated only its slice of the fp32 masters
     torch.save(tr.net.arena.w.cpu(), out + f".r{rank}")
     dist.destroy_process_group()
@@ -130,5 +131,5 @@ def test_rccl_forced_fullc_gather_fused_sgd(tmp_path, mode):
     for _ in range(steps):
         tr.update(DataBatch(x.cuda(), y.cuda()))
     torch.cuda.synchronize()
-    assert len(tr.net.updater.fused_offsets) == 2  # the single-GPU run fuses both fc steps too
+    assert len(tr.net.updater.fused_offsets) == 1  # the single-GPU run fuses the same fc step
     assert torch.equal(r0[: tr.net.arena.total], tr.net.arena.w.cpu())
