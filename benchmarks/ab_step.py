@@ -4,7 +4,8 @@ configurations (per guide rule: perf deltas come from interleaved rounds in ONE 
   python benchmarks/ab_step.py --configs "all:cf,cd,cw,fc,fw" "no_cw:cf,cd,fc,fw" --rounds 5
 Each config is `name:glds-op-classes[:ov][:db=path]` ("none" = register-staged kernel everywhere;
 ":ov" runs the optimizer per gradient bucket on a side stream, overlapped with the rest of backward;
-":db=path" lays a tile table written by benchmarks/tune_db.py over the shipped one).
+":db=path" lays a tile table written by benchmarks/tune_db.py over the shipped one; ":g=N" sets the
+GEMM tile-order group, ops.gemm.set_tile_group).
 Prints one JSON line per config: median / min ms per step over the rounds.
 """
 import argparse
@@ -52,18 +53,22 @@ def main():
     for spec in a.configs:
         name, ops, *flags = spec.split(":")
         db = {}
+        grp = 0
         for f in flags:
+            if f.startswith("g="):
+                grp = int(f[2:])
             if f.startswith("db="):
                 db = G._load_tune_db(f[3:])
                 assert db, f"empty or unreadable tile table {f[3:]}"
-        cfgs.append((name, [] if ops == "none" else ops.split(","), "ov" in flags, db))
+        cfgs.append((name, [] if ops == "none" else ops.split(","), "ov" in flags, db, grp))
     shipped = dict(G._TUNE)
     net = tr.net
     ov_fn = lambda ranges: net.update(tr.epoch_counter, ranges)  # noqa: E731
     times = {n: [] for n, *_ in cfgs}
     for r in range(a.rounds):
-        for name, ops, ov, db in cfgs:
+        for name, ops, ov, db, grp in cfgs:
             G.set_glds(on=bool(ops), ops=ops)
+            G.set_tile_group(grp)
             G._TUNE.clear()
             G._TUNE.update(shipped)
             G._TUNE.update(db)

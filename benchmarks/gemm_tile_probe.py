@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--tiles", default="21,90,91")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--groups", default="0", help="tile-order groups to A/B (ops.gemm.set_tile_group), e.g. 0,8")
     a = ap.parse_args()
     tiles = [int(t) for t in a.tiles.split(",")]
     for name in a.ops.split(","):
@@ -46,13 +47,17 @@ def main():
         ref = out.float().clone()
         arms = {}
         errs = {}
+        groups = [int(x) for x in a.groups.split(",")]
         for t in tiles:
-            G.set_glds(True, t)
-            out.zero_()
-            run()
-            torch.cuda.synchronize()
-            errs[t] = ((out.float() - ref).norm() / ref.norm().clamp_min(1e-6)).item()
-            arms[f"t{t}"] = (lambda t=t: (G.set_glds(True, t), run()))
+            for gi in groups:
+                G.set_glds(True, t)
+                G.set_tile_group(gi)
+                out.zero_()
+                run()
+                torch.cuda.synchronize()
+                tag = f"t{t}" + (f"g{gi}" if len(groups) > 1 else "")
+                errs[tag] = ((out.float() - ref).norm() / ref.norm().clamp_min(1e-6)).item()
+                arms[tag] = (lambda t=t, gi=gi: (G.set_glds(True, t), G.set_tile_group(gi), run()))
         if name.startswith("sq"):
             n = int(name[2:].split("_")[0])
             g = torch.Generator(device="cuda").manual_seed(1)
@@ -68,8 +73,9 @@ def main():
             us = statistics.median(v)
             rec[f"{k}_us"] = round(us, 1)
             rec[f"{k}_tflops"] = round(flops / us / 1e6, 1)
-        rec["err"] = {f"t{t}": round(e, 5) for t, e in errs.items()}
+        rec["err"] = {t: round(e, 5) for t, e in errs.items()}
         G.set_glds(True, -1)
+        G.set_tile_group(0)
         print(json.dumps(rec), flush=True)
 
 

@@ -77,6 +77,26 @@ __device__ __forceinline__ GemmBlock gemm_block(uint32_t ntile) {
   return {r - rt * ntile, static_cast<int>(rt % ny), static_cast<int>(rt / ny)};
 }
 
+// Tile (ti, tj) of a work item.  group_i <= 0 or tiles_i <= group_i: i fastest over all i-tiles
+// (neighbouring items share the B panel).  Otherwise i fastest inside groups of group_i i-tiles:
+// the ~32 items an XCD runs together then cover a group_i x (32 / group_i) patch of the output,
+// re-reading group_i A panels and 32 / group_i B panels from the XCD's L2 instead of 32 A panels
+// and one B panel (square / fc GEMMs, where tiles_i is large).  Speed-only.
+__device__ __forceinline__ void tile_ij(uint32_t tile, int tiles_i, int tiles_j, int group_i, int &ti, int &tj) {
+  if (group_i <= 0 || tiles_i <= group_i) {
+    ti = static_cast<int>(tile % static_cast<uint32_t>(tiles_i));
+    tj = static_cast<int>(tile / static_cast<uint32_t>(tiles_i));
+    return;
+  }
+  const uint32_t per = static_cast<uint32_t>(group_i) * static_cast<uint32_t>(tiles_j);
+  const uint32_t grp = tile / per;
+  const int first = static_cast<int>(grp) * group_i;
+  const int gm = min(tiles_i - first, group_i);
+  const uint32_t r = tile - grp * per;
+  ti = first + static_cast<int>(r % static_cast<uint32_t>(gm));
+  tj = static_cast<int>(r / static_cast<uint32_t>(gm));
+}
+
 static inline int cdiv(long a, long b) { return static_cast<int>((a + b - 1) / b); }
 
 // Deterministic mode (cxn_set_deterministic): reductions that would combine partial sums with

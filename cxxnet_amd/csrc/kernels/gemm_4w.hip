@@ -62,7 +62,8 @@ gemm_4w(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
   const GemmBlock wb = gemm_block(ntile);
   const int g = wb.g;
   const uint32_t tile = wb.tile;
-  const int ti = tile % tiles_i, tj = tile / tiles_i;
+  int ti, tj;
+  tile_ij(tile, tiles_i, tiles_j, E.group_i, ti, tj);
   const int i0 = ti * BM, j0 = tj * BN;
   const int kt_beg = wb.slice * ksplit_tiles;
   const int kt_end = min(kt_beg + ksplit_tiles, ktiles_total);

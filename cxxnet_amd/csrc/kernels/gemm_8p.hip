@@ -46,7 +46,8 @@ gemm_8p(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
   const GemmBlock wb = gemm_block(ntile);
   const int g = wb.g;
   const uint32_t tile = wb.tile;
-  const int ti = tile % tiles_i, tj = tile / tiles_i;
+  int ti, tj;
+  tile_ij(tile, tiles_i, tiles_j, E.group_i, ti, tj);
   const int i0 = ti * 256, j0 = tj * 256;
   const int kt_beg = wb.slice * ksplit_tiles;
   const int kt_end = min(kt_beg + ksplit_tiles, ktiles_total);

@@ -75,7 +75,8 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
   const GemmBlock wb = gemm_block(ntile);
   const int g = wb.g;
   const uint32_t tile = wb.tile;
-  const int ti = tile % tiles_i, tj = tile / tiles_i;  // i fastest: neighbours share the B panel
+  int ti, tj;
+  tile_ij(tile, tiles_i, tiles_j, E.group_i, ti, tj);
   const int i0 = ti * BMC, j0 = tj * BN;
   const int kt_beg = wb.slice * ksplit_tiles;
   const int kt_end = min(kt_beg + ksplit_tiles, ktiles_total);
@@ -404,7 +405,8 @@ gemm_seg(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_ti
   const GemmBlock wb = gemm_block(ntile);
   const int g = wb.g;
   const uint32_t tile = wb.tile;
-  const int ti = tile % tiles_i, tj = tile / tiles_i;
+  int ti, tj;
+  tile_ij(tile, tiles_i, tiles_j, E.group_i, ti, tj);
   const int i0 = ti * BM, j0 = tj * BN;
   const int kt_beg = wb.slice * ksplit_tiles;
   const int kt_end = min(kt_beg + ksplit_tiles, ktiles_total);
@@ -528,7 +530,8 @@ gemm_pp(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
   const GemmBlock wb = gemm_block(ntile);
   const int g = wb.g;
   const uint32_t tile = wb.tile;
-  const int ti = tile % tiles_i, tj = tile / tiles_i;
+  int ti, tj;
+  tile_ij(tile, tiles_i, tiles_j, E.group_i, ti, tj);
   const int i0 = ti * BM, j0 = tj * BN;
   const int kt_beg = wb.slice * ksplit_tiles;
   const int kt_end = min(kt_beg + ksplit_tiles, ktiles_total);
@@ -739,6 +742,16 @@ int dispatch(int amode, int bmode, int epi, int tile, const GOperand &A, const G
 
 }  // namespace
 
+int cxg::g_gemm_group_i = 8;  // +7 % on 8192^3 (profiles/r3_gemm_tile_order.jsonl), neutral on the model steps
+
+// Tile order of the LDS-DMA GEMM kernels: 0 = i fastest over all i-tiles; n > 0 = i fastest in
+// groups of n i-tiles (common.h tile_ij).  Returns the previous setting.
+CXN_API int cxn_gemm_set_group(int group_i) {
+  const int old = cxg::g_gemm_group_i;
+  cxg::g_gemm_group_i = group_i < 0 ? 0 : group_i;
+  return old;
+}
+
 // Same operand record as cxn_gemm (gemm_mfma.hip).
 struct CxnOperandG {
   const void *ptr;
@@ -803,7 +816,7 @@ CXN_API int cxn_gemm_glds(const CxnOperandG *a, const CxnOperandG *b, int amode,
   fill(B, b, bmode);
   if (epi == EPI_F32_SGD) return -1;  // only through cxn_gemm_glds_sgd
   GEpi E{out, out_gstride, ldc, alpha, bias, bias_gstride, relu, mask_relu, kstride,
-         nullptr, nullptr, nullptr, 0.f, 0.f, 0.f, 0.f, dws, dws_ld, dws_elems, dbias};
+         nullptr, nullptr, nullptr, 0.f, 0.f, 0.f, 0.f, dws, dws_ld, dws_elems, dbias, g_gemm_group_i};
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int rc = dispatch(amode, bmode, epi, tile, A, B, E, groups < 1 ? 1 : groups, ksplit < 1 ? 1 : ksplit, s);
   if (rc != 0) return rc;
@@ -825,7 +838,8 @@ CXN_API int cxn_gemm_glds_sgd(const CxnOperandG *a, const CxnOperandG *b, int ld
   GOperand A{}, B{};
   fill(A, a, MN_DIRECT);
   fill(B, b, MN_DIRECT);
-  GEpi E{nullptr, 0, ldc, alpha, nullptr, 0, 0, 0, 0, w, m, static_cast<bf16_t *>(wb), lr, wd, mom, clip, nullptr, 0, 0, nullptr};
+  GEpi E{nullptr, 0, ldc, alpha, nullptr, 0, 0, 0, 0, w, m, static_cast<bf16_t *>(wb), lr, wd, mom, clip, nullptr, 0, 0, nullptr,
+         g_gemm_group_i};
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int rc = dispatch(MN_DIRECT, MN_DIRECT, EPI_F32_SGD, tile, A, B, E, 1, 1, s);
   if (rc != 0) return rc;

@@ -49,7 +49,13 @@ struct GEpi {
   int part_ld;
   long part_elems;     // workspace capacity
   float *dbias_final;  // += the workspace's column sums (db_partials_reduce)
+  int group_i;         // tile order (common.h tile_ij); set at launch from cxn_gemm_set_group
 };
+
+}  // namespace cxg
+namespace cxg {
+// host-side tile-order setting copied into every GEpi at launch (cxn_gemm_set_group)
+extern int g_gemm_group_i;
 
 __device__ __forceinline__ float sgd_step(const GEpi &E, float g, float &m, float w) {
   if (E.clip != 0.f) g = (g != g) ? 0.f : fminf(fmaxf(g, -E.clip), E.clip);

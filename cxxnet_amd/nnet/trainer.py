@@ -576,6 +576,10 @@ class NetTrainer:
         net, red = self.net, self.reducer
         if not (self.cuda_graph != 0 and net.ctx.is_gpu and self.update_period == 1 and red is not None):
             return False
+        # fullc_gather layers run their all-gathers inside forward / backward: a collective
+        # cannot be captured (RCCL refuses to join a capturing stream), so those steps stay eager
+        if any(getattr(c.layer, "_gathering", None) is not None and c.layer._gathering() for c in net.connections):
+            return False
         if self.cuda_graph < 0:
             return red.handles_update and self._local_batch() <= 64
         if red.handles_update:  # data parallel: segmented graphs around the collectives

@@ -206,6 +206,12 @@ def deterministic() -> bool:
     return _DET["on"]
 
 
+def set_tile_group(group_i: int) -> int:
+    """Tile order of the LDS-DMA kernels (csrc/kernels/common.h tile_ij): 0 = i fastest over all
+    i-tiles, n = i fastest in groups of n i-tiles.  Returns the previous setting."""
+    return int(native.kernels().cxn_gemm_set_group(int(group_i)))
+
+
 def set_glds(on: bool = True, tile: int = -1, tune: bool = True, ops=None):
     """Enable/disable the LDS-DMA GEMM path, force its tile, turn autotuning off, or pick
     the op classes it serves (subset of cf, cd, cw, fc, fw)."""

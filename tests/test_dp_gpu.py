@@ -55,7 +55,7 @@ def _worker(rank, world, port, steps, out, extra, backend="gloo"):
         tr.update(DataBatch(x.cuda(), y.cuda()))
     torch.cuda.synchronize()
     assert tr.reducer.check_consistency() == 0.0
-    if any(k == "cuda_graph" and v == "1" for k, v in extra):
+    if any(k == "cuda_graph" and v == "1" for k, v in extra) and not any(k == "fullc_gather" for k, _ in extra):
         assert tr._graphs, "the data-parallel step did not run as graph segments"
         fwd, bwd = next(iter(tr._graphs.values()))
         assert sum(callable(i) and not isinstance(i, torch.cuda.CUDAGraph) for i in fwd + bwd) > 0
@@ -132,4 +132,21 @@ def test_rccl_forced_fullc_gather_fused_sgd(tmp_path, mode):
         tr.update(DataBatch(x.cuda(), y.cuda()))
     torch.cuda.synchronize()
     assert len(tr.net.updater.fused_offsets) == 1  # the single-GPU run fuses the same fc step
+    assert torch.equal(r0[: tr.net.arena.total], tr.net.arena.w.cpu())
+
+
+def test_rccl_forced_fullc_gather_graph_stays_eager(tmp_path):
+    """cuda_graph = 1 with fullc_gather under RCCL: the gathers cannot be captured, so the step
+    runs eagerly (it used to abort with hipErrorStreamCaptureImplicit) and stays exact."""
+    steps = 3
+    out = str(tmp_path / "w")
+    extra = [("dp_mode", "allreduce"), ("fullc_gather", "1"), ("cuda_graph", "1")]
+    mp.spawn(_worker, args=(1, _free_port(), steps, out, extra, "nccl"), nprocs=1, join=True)
+    r0 = torch.load(out + ".r0", weights_only=True)
+    from cxxnet_amd.io.data import DataBatch
+    tr = _make(8, [])
+    x, y = _data(8)
+    for _ in range(steps):
+        tr.update(DataBatch(x.cuda(), y.cuda()))
+    torch.cuda.synchronize()
     assert torch.equal(r0[: tr.net.arena.total], tr.net.arena.w.cpu())
