@@ -715,6 +715,75 @@ __global__ void pool_bwd_s1k3(const bf16_t *__restrict__ x, const uint8_t *__res
   }
 }
 
+// Backward of the 3x3 stride-2 max pool (AlexNet's pools) on 2x2 input cells.  In padded
+// coordinates hp = h + P, window ho covers hp in [2ho, 2ho + 2], so input rows 2i and 2i + 1 are
+// covered by window rows {i - 1, i} and {i}: the 4 windows (i-1..i) x (j-1..j) hold every
+// contribution to the cell's 4 pixels.  pool_bwd_rows loads up to 4 windows per PIXEL (16 per
+// cell, 9 distinct), all from L2; here each window is loaded once (4 per cell) and the cell's
+// 4 outputs are written -- the kernel becomes write-bound.  Contributions are summed in
+// (ho, wo) order as in pool_bwd_rows, so both give the same bits.  relu as pool_bwd_s1k3.
+__global__ void pool_bwd_s2k3(const bf16_t *__restrict__ x, const uint8_t *__restrict__ arg,
+                              const bf16_t *__restrict__ dy, bf16_t *__restrict__ dx, int H, int W, int C, int Ho,
+                              int Wo, int P, int relu, int i0, int j0, int WC, FastDiv fd_cv, FastDiv fd_row,
+                              FastDiv fd_hc, uint32_t total) {
+  const int CV = C / 8;
+  const uint32_t idx = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int row = static_cast<int>(fdiv(idx, fd_row));  // n * HC + cell row
+  const int e = static_cast<int>(idx) - row * (WC * CV);
+  const int n = static_cast<int>(fdiv(static_cast<uint32_t>(row), fd_hc));
+  const int i = row - n * static_cast<int>(fd_hc.d) + i0;
+  const int cj = static_cast<int>(fdiv(static_cast<uint32_t>(e), fd_cv));
+  const int cv = e - cj * CV, j = cj + j0;
+  uint4 d[2][2];
+  uint2 a[2][2];
+  bool ok[2][2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int ho = i - 1 + p, wo = j - 1 + q;
+      ok[p][q] = ho >= 0 && ho < Ho && wo >= 0 && wo < Wo;
+      const long o = ((static_cast<long>(n) * Ho + min(max(ho, 0), Ho - 1)) * Wo + min(max(wo, 0), Wo - 1)) * C +
+                     cv * 8;
+      d[p][q] = *reinterpret_cast<const uint4 *>(dy + o);
+      a[p][q] = *reinterpret_cast<const uint2 *>(arg + o);
+    }
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int h = 2 * i + r - P, w = 2 * j + s - P;
+      if (h < 0 || h >= H || w < 0 || w >= W) continue;
+      float g[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = 0.f;
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int kh = 2 + r - 2 * p, kw = 2 + s - 2 * q;  // tap of (h, w) in window (i-1+p, j-1+q)
+          if (kh > 2 || kw > 2 || !ok[p][q]) continue;
+          const uint32_t off = static_cast<uint32_t>(kh * 3 + kw);
+          float gv[8];
+          unpack8(d[p][q], gv);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            g[k] += (((a[p][q].x >> (8 * k)) & 0xff) == off) ? gv[k] : 0.f;
+            g[k + 4] += (((a[p][q].y >> (8 * k)) & 0xff) == off) ? gv[k + 4] : 0.f;
+          }
+        }
+      const long o = ((static_cast<long>(n) * H + h) * W + w) * C + cv * 8;
+      if (relu == 1) {
+        float xv[8];
+        unpack8(*reinterpret_cast<const uint4 *>(x + o), xv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[k] = xv[k] > 0.f ? g[k] : 0.f;
+      }
+      *reinterpret_cast<uint4 *>(dx + o) = pack8(g);
+    }
+}
+
 // ------------------------------------------------------------------ LRN
 // norm[c] = knorm + alpha/n * sum_{c' in [c-h, c+h] clipped} x[c']^2 ; y = x * norm^-beta
 // One thread per (pixel, 8 channels); halo of up to 8 channels each side via three 16-B loads.
@@ -1156,7 +1225,7 @@ struct ColsumSeg {
   const uint8_t *mask;  // nullable: max-pool offsets [rows][C]; entries with bit 7 set count as 0
   float *db;
   long rows;
-  int C, rpb, nblk;
+  int C, rpb, nblk, nchunk;
 };
 struct ColsumTable {
   ColsumSeg s[COLSUM_MAXSEG];
@@ -1174,11 +1243,15 @@ __global__ void colsum_multi(ColsumTable tab) {
   const int blk = bx - tab.b0[si];
   const int CV = sg.C / 8;
   const int t = threadIdx.x;
-  const long r0 = static_cast<long>(blk) * sg.rpb;
+  // nchunk > 1: each block owns one chunk of 64 column vectors (wide fc segments would
+  // otherwise leave one block walking all 4096 columns); 1: the block walks every chunk
+  const int rb = blk / sg.nchunk, chunk = blk - rb * sg.nchunk;
+  const int cbeg = sg.nchunk > 1 ? chunk * 64 : 0, cend = sg.nchunk > 1 ? min(CV, cbeg + 64) : CV;
+  const long r0 = static_cast<long>(rb) * sg.rpb;
   const long r1 = min(sg.rows, r0 + sg.rpb);
   __shared__ float red[NT][9];
-  for (int cb = 0; cb < CV; cb += 64) {
-    const int CB = min(CV - cb, 64);
+  for (int cb = cbeg; cb < cend; cb += 64) {
+    const int CB = min(cend - cb, 64);
     const int RG = NT / CB;
     const int cvl = t % CB, rg = t / CB;
     const int cv = cb + cvl;
@@ -1645,6 +1718,16 @@ static const int pool_strips = [] {
   const char *e = getenv("CXXNET_POOL_STRIPS");
   return (e && e[0] == '0') ? 0 : 1;
 }();
+// kernel variants kept for A/B (benchmarks/small_kernels.py): 0 pool_bwd_s2k3 cells,
+// 1 colsum_multi column-chunk split
+static int pool_cells = 1;
+static int colsum_split = 1;
+CXN_API int cxn_set_kernel_variant(int which, int v) {
+  if (which == 0) pool_cells = v;
+  else if (which == 1) colsum_split = v;
+  else return -1;
+  return 0;
+}
 
 CXN_API int cxn_pool_fwd(const void *x, void *y, void *arg, int N, int H, int W, int C, int Ho, int Wo, int KH, int KW, int S,
                          int P, int mode, int relu, void *stream) {
@@ -1703,6 +1786,14 @@ CXN_API int cxn_pool_bwd(const void *x, const void *arg, const void *dy, void *d
           (const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, H, W, C, Ho, Wo, P, relu,
           make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(W * (C / 8))),
           make_fastdiv(static_cast<uint32_t>(HS)), static_cast<uint32_t>(tot));
+    } else if (S == 2 && sq == 3 && mode == 0 && pool_cells) {
+      const int i0 = P / 2, j0 = P / 2;
+      const int HC = (P + H - 1) / 2 - i0 + 1, WC = (P + W - 1) / 2 - j0 + 1;
+      const long tot = static_cast<long>(N) * HC * WC * (C / 8);
+      pool_bwd_s2k3<<<cdiv(tot, NT), NT, 0, S_>>>(
+          (const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, H, W, C, Ho, Wo, P, relu, i0,
+          j0, WC, make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(WC * (C / 8))),
+          make_fastdiv(static_cast<uint32_t>(HC)), static_cast<uint32_t>(tot));
     } else if (S == 2 && sq == 3) CXN_POOL_BWD(2, 3);
     else if (S == 1 && sq == 3) CXN_POOL_BWD(1, 3);
     else if (S == 2 && sq == 2) CXN_POOL_BWD(2, 2);
@@ -1869,16 +1960,30 @@ CXN_API int cxn_colsum_multi(const void *const *dys, float *const *dbs, const lo
       // <= 1024 blocks (adders per channel) per segment, >= 256 rows per block: the largest
       // segment (AlexNet conv1: 774k rows) needs ~4 blocks per CU to keep HBM busy
       long nb = cdiv(rows[j], 256L);
+      int nchunk = 1;
+      if (colsum_split) {
+        // one block per (rows, chunk of <= 64 column vectors) reading ~96 KiB, >= 8 rows per
+        // thread (one round of the 8-deep load batch): fc6 (256 x 4096) gets 24 blocks, not 1
+        const int CV = Cs[j] / 8;
+        nchunk = (CV + 63) / 64;
+        const int CB = CV < 64 ? CV : 64;
+        const long bpr = static_cast<long>(CB) * 8 * (masks && masks[j] ? 3 : 2);
+        long want = 98304 / bpr;
+        const long minr = (NT / CB) * 8L;
+        if (want < minr) want = minr;
+        nb = cdiv(rows[j], want);
+      }
       if (nb > 1024) nb = 1024;
       if (nb < 1) nb = 1;
-      const int rpb = static_cast<int>(cdiv(rows[j], nb));
+      const int rpb = rows[j] > 0 ? static_cast<int>(cdiv(rows[j], nb)) : 1;
+      const int nrb = static_cast<int>(cdiv(rows[j], static_cast<long>(rpb)));
       tab.s[i] = ColsumSeg{static_cast<const bf16_t *>(dys[j]),
                            masks ? static_cast<const uint8_t *>(masks[j]) : nullptr, dbs[j], rows[j], Cs[j], rpb,
-                           static_cast<int>(cdiv(rows[j], static_cast<long>(rpb)))};
+                           nrb * nchunk, nchunk};
       tab.b0[i] = nblk;
       nblk += tab.s[i].nblk;
     }
-    colsum_multi<<<nblk, NT, 0, S_>>>(tab);
+    if (nblk > 0) colsum_multi<<<nblk, NT, 0, S_>>>(tab);
   }
   RET;
 }

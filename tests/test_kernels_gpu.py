@@ -592,6 +592,42 @@ def test_pool_stride1_3x3_strips(H, p, relu):
     assert relerr(dx, dx_ref) < 1e-2
 
 
+@pytest.mark.parametrize("H,W,p", [(55, 55, 0), (27, 27, 0), (13, 14, 0), (28, 28, 1), (9, 8, 1), (7, 7, 2)])
+@pytest.mark.parametrize("relu", [0, 1, 2])
+def test_pool_bwd_stride2_3x3_cells(H, W, p, relu):
+    """3x3 stride-2 max-unpool on 2x2 input cells (pool_bwd_s2k3, AlexNet / GoogLeNet pools):
+    against the CPU executor for odd / even / non-square sizes, pads 0-2 and the three relu
+    modes, and bitwise against the one-pixel-per-thread kernel (kernel variant 0)."""
+    from cxxnet_amd import native
+    N, C, k, s = 2, 40, 3, 2
+    g = torch.Generator().manual_seed(10 * H + W + p + relu)
+    x = torch.randint(-3, 4, (N, H, W, C), generator=g).float() * 0.25
+    if relu == 2:
+        x = x.clamp_min(0)
+    Ho, Wo = ops.pool_out_size(H, k, s, p), ops.pool_out_size(W, k, s, p)
+    dy = rnd(N, Ho, Wo, C, seed=H + W)
+    y_ref = torch.empty(N, Ho, Wo, C)
+    st_ref = torch.empty(N, Ho, Wo, C, dtype=torch.uint8)
+    ops.pool_forward(x, y_ref, st_ref, k, k, s, p, "max", relu == 1)
+    dx_ref = torch.empty_like(x)
+    ops.pool_backward(x, st_ref, dy, dx_ref, k, k, s, p, "max", relu > 0)
+    xd = x.to(DEV, torch.bfloat16)
+    y = torch.empty(N, Ho, Wo, C, dtype=torch.bfloat16, device=DEV)
+    st = torch.empty(N, Ho, Wo, C, dtype=torch.uint8, device=DEV)
+    ops.pool_forward(xd, y, st, k, k, s, p, "max", relu == 1, mark_mask=relu == 2)
+    dyd = dy.to(DEV, torch.bfloat16)
+    out = []
+    for v in (1, 0):
+        native.check(native.kernels().cxn_set_kernel_variant(0, v), "variant")
+        dx = torch.full_like(xd, 7.0)  # every pixel must be written
+        ops.pool_backward(xd, st, dyd, dx, k, k, s, p, "max", relu)
+        out.append(dx)
+    native.check(native.kernels().cxn_set_kernel_variant(0, 1), "variant")
+    torch.cuda.synchronize()
+    assert torch.equal(out[0], out[1])
+    assert relerr(out[0], dx_ref) < 1e-2
+
+
 @pytest.mark.parametrize("geo_args,mask", [((4, 13, 13, 384, 13, 13, 384, 3, 3, 1, 1, 1, 2), True),
                                            ((2, 28, 28, 64, 28, 28, 96, 3, 3, 1, 1, 1, 1), False),
                                            ((2, 14, 14, 48, 14, 14, 64, 5, 5, 1, 2, 2, 1), True)])
