@@ -104,14 +104,38 @@ def colsum_case(iters, out):
     return ok
 
 
+def image_case(iters, out):
+    """u8 [B][227][227][3] -> bf16 node: NHWC4 (image_u8c3_nhwc4) vs 3 channels on 228-pixel rows
+    (image_u8c3_nhwc3p), mean subtraction (mode 1)."""
+    from cxxnet_amd.io.data import U8Images
+    B, h, w = 256, 227, 227
+    pix = torch.randint(0, 256, (B, h, w, 3), dtype=torch.uint8, device="cuda")
+    cm = torch.ones(B, 2, device="cuda")
+    cm[:, 1] = 0
+    img = U8Images(pix, torch.zeros(B, 4, dtype=torch.int32, device="cuda"), cm,
+                   torch.tensor([120.0, 110.0, 100.0], device="cuda"), 1, 1.0)
+    for cp, wp in ((4, 227), (3, 228)):
+        node = torch.zeros(B, h, wp, cp, dtype=torch.bfloat16, device="cuda")
+        us = timeit(lambda: nn.image_to_nhwc(img, node), iters)
+        byts = pix.numel() + node.numel() * 2
+        rec = {"case": f"image_u8 -> nhwc{cp} row {wp}", "us": round(us, 2), "TBps": round(byts / us / 1e6, 2)}
+        print(json.dumps(rec), flush=True)
+        out.write(json.dumps(rec) + "\n")
+    return True
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--out", default="gpurun_out/small_kernels.jsonl")
+    ap.add_argument("--only-image", action="store_true")
     a = ap.parse_args()
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     ok = True
     with open(a.out, "w") as out:
+        ok &= image_case(a.iters, out)
+        if a.only_image:
+            return 0 if ok else 1
         ok &= pool_case(256, 55, 96, a.iters, out)
         ok &= pool_case(256, 27, 256, a.iters, out)
         ok &= pool_case(256, 13, 256, a.iters, out)

@@ -37,6 +37,7 @@
 //   * epilogues staged per wave through LDS so every global access is a contiguous row
 //     segment: bf16 (+bias, relu, relu'-mask of the old value), fp32 split-K slab, fp32 +=,
 //     fp32 atomics.
+#include <cstdlib>
 #include "gemm_glds_common.h"
 
 using namespace cxg;
@@ -762,16 +763,28 @@ struct CxnOperandG {
 };
 
 namespace {
+// Byte alignment the kernel-row runs of the row gathers need (their 16-byte DMAs start at a
+// pixel's first element): every image row (W*C*2 bytes) and every output-pixel step
+// (stride*C*2) must be a multiple of it.  8: NHWC4 input (C = 4); CXXNET_ROWRUN_ALIGN overrides
+// for probing (benchmarks/conv1_c3_probe.py).
+static const int g_rowrun_align = [] {
+  const char *e = getenv("CXXNET_ROWRUN_ALIGN");
+  const int v = e ? atoi(e) : 8;
+  return v > 0 ? v : 8;
+}();
+bool rowrun_aligned(const CxnOperandG *o) {
+  return (o->W * o->C * 2) % g_rowrun_align == 0 && (o->stride * o->C * 2) % g_rowrun_align == 0;
+}
 bool supported(const CxnOperandG *o, int mode) {
   if (o->nbytes >= (1L << 31) || (reinterpret_cast<uintptr_t>(o->ptr) & 15) || o->gstride % 8 != 0) return false;
   if (mode == K_DIRECT || mode == MN_DIRECT) return o->ld % 8 == 0 && (mode == K_DIRECT || o->rows % 8 == 0);
-  if (mode == K_ROWGATHER)  // whole kernel rows read as runs: no padding, one group, 8-byte aligned pixels
-    return o->pad_h == 0 && o->pad_w == 0 && o->Cg == o->C && o->C % 4 == 0 && o->dil <= 1 &&
+  if (mode == K_ROWGATHER)  // whole kernel rows read as runs: no padding, one group, aligned pixels
+    return o->pad_h == 0 && o->pad_w == 0 && o->Cg == o->C && rowrun_aligned(o) && o->dil <= 1 &&
            o->kdim == o->KH * ((o->KW * o->C + 7) / 8) * 8;
   if (o->Cg % 8 != 0 || o->dil > 1) return false;
   // MN gather over whole kernel rows (few-channel weight-grad, conv1): KW = 1 and Cg = a kernel row's
-  // KW*C elements padded to 8, so a 16-byte chunk runs across pixels; with C % 8 == 4 it is 8-byte aligned
-  const bool row_runs = mode == MN_GATHER && o->KW == 1 && o->pad_h == 0 && o->pad_w == 0 && o->C % 4 == 0;
+  // KW*C elements padded to 8, so a 16-byte chunk runs across pixels (aligned as the runs above)
+  const bool row_runs = mode == MN_GATHER && o->KW == 1 && o->pad_h == 0 && o->pad_w == 0 && rowrun_aligned(o);
   if (o->C % 8 != 0 && !row_runs) return false;
   return mode == K_GATHER || o->rows % 8 == 0;
 }

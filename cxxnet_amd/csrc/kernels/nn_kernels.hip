@@ -24,15 +24,17 @@ static inline int nblocks(long n, int per_block = NT, int cap = 256 * 16) {
 }
 
 // ------------------------------------------------------------------ layout
-// x: NCHW fp32 [N][C][H][W] -> y: NHWC bf16 [N][H][W][Cp] (channels >= C zero-filled)
+// x: NCHW fp32 [N][C][H][W] -> y: NHWC bf16 [N][H][Wp][Cp] (channels >= C zero-filled; columns
+// >= W of a row-padded node are left as they are)
 __global__ void nchw_f32_to_nhwc_bf16(const float *__restrict__ x, bf16_t *__restrict__ y, int N, int C, int H,
-                                      int W, int Cp, float scale) {
+                                      int W, int Cp, int Wp, float scale) {
   const long total = static_cast<long>(N) * H * W;
   for (long pix = grid_stride_start(); pix < total; pix += grid_stride()) {
     const long n = pix / (static_cast<long>(H) * W);
     const long hw = pix - n * H * W;
     const float *src = x + n * C * H * W + hw;
-    bf16_t *dst = y + pix * Cp;
+    const long row = pix / W;
+    bf16_t *dst = y + (row * Wp + (pix - row * W)) * Cp;
     if (Cp == 4) {
       float v[4];
 #pragma unroll
@@ -58,7 +60,7 @@ __global__ void nchw_f32_to_nhwc_bf16(const float *__restrict__ x, bf16_t *__res
 //        3: mean image [C][h][w] of the crop size
 __global__ void image_u8_to_nhwc_bf16(const uint8_t *__restrict__ pix, const int *__restrict__ prm,
                                       const float *__restrict__ cm, const float *__restrict__ mean, int B, int h,
-                                      int w, int C, int Cp, int Hm, int Wm, int mode, float scale,
+                                      int w, int C, int Cp, int Wp, int Hm, int Wm, int mode, float scale,
                                       bf16_t *__restrict__ y) {
   // grid: x over blockIdx.x*NT + tid, one image row (b, r) per blockIdx.y: no per-pixel division
   const int row = blockIdx.y;
@@ -90,7 +92,7 @@ __global__ void image_u8_to_nhwc_bf16(const uint8_t *__restrict__ pix, const int
       }
     }
   }
-  bf16_t *dst = y + p * Cp;
+  bf16_t *dst = y + (static_cast<long>(row) * Wp + x) * Cp;
   if (Cp == 4) {  // one 8-byte store per pixel
     *reinterpret_cast<uint2 *>(dst) = make_uint2(static_cast<uint32_t>(f2bf(v[0])) | static_cast<uint32_t>(f2bf(v[1])) << 16,
                                                  static_cast<uint32_t>(f2bf(v[2])) | static_cast<uint32_t>(f2bf(v[3])) << 16);
@@ -130,9 +132,58 @@ __global__ void image_u8c3_nhwc4(const uint32_t *__restrict__ pix, const float *
   }
 }
 
-// x: NHWC bf16 [N][H][W][Cp] -> y: NCHW fp32 [N][C][H][W]
+// Fast path for the row-padded 3-channel node of a first conv on kernel-row runs
+// (NeuralNet._pad_input_channels: AlexNet conv1 reads [B][h][Wp][3] with Wp % 4 == 0, so every
+// image row and every 4-pixel group starts 8-byte aligned): one thread per 4 output pixels of a
+// padded row, three 8-byte stores; the pad columns (x >= w) get zeros.  mode 0/1.  The 12 source
+// bytes of a group start at any byte (rows of w*3 bytes): 4 aligned dword loads + alignbyte.
+__global__ void image_u8c3_nhwc3p(const uint32_t *__restrict__ pix, long ndw, const float *__restrict__ cm,
+                                  const float *__restrict__ mean, FastDiv fd_qpr, FastDiv fd_h, int w, int Wp,
+                                  int mode, float scale, uint32_t total, uint2 *__restrict__ y) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= total) return;
+  const uint32_t row = fdiv(q, fd_qpr);
+  const int x0 = static_cast<int>(q - row * fd_qpr.d) * 4;
+  float ct = 1.f, il = 0.f;
+  if (mode == 1) {
+    const uint32_t b = fdiv(row, fd_h);
+    ct = cm[2 * b];
+    il = cm[2 * b + 1];
+  }
+  const long start = (static_cast<long>(row) * w + x0) * 3;
+  const long d0 = start >> 2;
+  const uint32_t sh = static_cast<uint32_t>(start & 3) * 8;
+  uint32_t d[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) d[t] = pix[min(d0 + t, ndw - 1)];
+  // bytes start .. start + 11 of the image batch as three dwords
+  const uint32_t e[3] = {__builtin_amdgcn_alignbyte(d[1], d[0], sh >> 3), __builtin_amdgcn_alignbyte(d[2], d[1], sh >> 3),
+                         __builtin_amdgcn_alignbyte(d[3], d[2], sh >> 3)};
+  float out[12];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int byte = 3 * k + c;
+      float v = 0.f;
+      if (x0 + k < w) {
+        const float dv = static_cast<float>((e[byte >> 2] >> (8 * (byte & 3))) & 0xffu);
+        v = mode == 1 ? ((dv - mean[c]) * ct + il) * scale : dv * scale;
+      }
+      out[3 * k + c] = v;
+    }
+  {
+    uint2 *dst = y + (static_cast<long>(row) * Wp + x0) * 3 / 4;  // 4 pixels = 24 bytes = three uint2
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+      dst[t] = make_uint2(static_cast<uint32_t>(f2bf(out[4 * t])) | static_cast<uint32_t>(f2bf(out[4 * t + 1])) << 16,
+                          static_cast<uint32_t>(f2bf(out[4 * t + 2])) | static_cast<uint32_t>(f2bf(out[4 * t + 3])) << 16);
+  }
+}
+
+// x: NHWC bf16 [N][H][Wp][Cp] -> y: NCHW fp32 [N][C][H][W]
 __global__ void nhwc_bf16_to_nchw_f32(const bf16_t *__restrict__ x, float *__restrict__ y, int N, int C, int H,
-                                      int W, int Cp) {
+                                      int W, int Cp, int Wp) {
   const long total = static_cast<long>(N) * C * H * W;
   for (long i = grid_stride_start(); i < total; i += grid_stride()) {
     const long w = i % W;
@@ -141,7 +192,7 @@ __global__ void nhwc_bf16_to_nchw_f32(const bf16_t *__restrict__ x, float *__res
     t /= H;
     const long c = t % C;
     const long n = t / C;
-    y[i] = bf2f(x[((n * H + h) * W + w) * Cp + c]);
+    y[i] = bf2f(x[((n * H + h) * Wp + w) * Cp + c]);
   }
 }
 
@@ -1653,19 +1704,32 @@ __global__ void metric_accum(const float *__restrict__ part, int nb, int nm, dou
 #define S_ static_cast<hipStream_t>(stream)
 #define RET return hipGetLastError() == hipSuccess ? 0 : -3
 
-CXN_API int cxn_nchw_f32_to_nhwc_bf16(const float *x, void *y, int N, int C, int H, int W, int Cp, float scale,
-                                      void *stream) {
-  nchw_f32_to_nhwc_bf16<<<nblocks(static_cast<long>(N) * H * W), NT, 0, S_>>>(x, (bf16_t *)y, N, C, H, W, Cp, scale);
+// Wp: the node's physical row width (>= W; row-padded first-conv input, see image_u8c3_nhwc3p)
+CXN_API int cxn_nchw_f32_to_nhwc_bf16(const float *x, void *y, int N, int C, int H, int W, int Cp, int Wp,
+                                      float scale, void *stream) {
+  if (Wp < W) return -2;
+  nchw_f32_to_nhwc_bf16<<<nblocks(static_cast<long>(N) * H * W), NT, 0, S_>>>(x, (bf16_t *)y, N, C, H, W, Cp, Wp,
+                                                                              scale);
   RET;
 }
 CXN_API int cxn_image_u8_to_nhwc_bf16(const void *pix, const int *prm, const float *cm, const float *mean, int B,
-                                      int h, int w, int C, int Cp, int Hm, int Wm, int mode, float scale, void *y,
-                                      void *stream) {
-  if (Cp < C || (mode != 0 && cm == nullptr) || (mode >= 1 && mean == nullptr) || (mode == 2 && prm == nullptr))
+                                      int h, int w, int C, int Cp, int Wp, int Hm, int Wm, int mode, float scale,
+                                      void *y, void *stream) {
+  if (Cp < C || Wp < w || (mode != 0 && cm == nullptr) || (mode >= 1 && mean == nullptr) ||
+      (mode == 2 && prm == nullptr))
     return -2;
   if (C > 8) return -2;
   const long npix = static_cast<long>(B) * h * w;
-  if (C == 3 && Cp == 4 && mode <= 1 && npix % 4 == 0 && npix < (1L << 32) &&
+  const long nq = static_cast<long>(B) * h * (Wp / 4);
+  if (C == 3 && Cp == 3 && mode <= 1 && Wp % 4 == 0 && reinterpret_cast<uintptr_t>(y) % 8 == 0 &&
+      reinterpret_cast<uintptr_t>(pix) % 4 == 0 && npix * 3 >= 16 && nq < (1L << 31)) {
+    image_u8c3_nhwc3p<<<cdiv(nq, NT), NT, 0, S_>>>((const uint32_t *)pix, (npix * 3 + 3) / 4, cm, mean,
+                                                    make_fastdiv(static_cast<uint32_t>(Wp / 4)),
+                                                    make_fastdiv(static_cast<uint32_t>(h)), w, Wp, mode, scale,
+                                                    static_cast<uint32_t>(nq), (uint2 *)y);
+    RET;
+  }
+  if (C == 3 && Cp == 4 && Wp == w && mode <= 1 && npix % 4 == 0 && npix < (1L << 32) &&
       reinterpret_cast<uintptr_t>(pix) % 4 == 0) {
     image_u8c3_nhwc4<<<nblocks(npix / 4), NT, 0, S_>>>((const uint32_t *)pix, cm, mean, npix / 4,
                                                         make_fastdiv(static_cast<uint32_t>(h * w)), mode, scale,
@@ -1673,12 +1737,14 @@ CXN_API int cxn_image_u8_to_nhwc_bf16(const void *pix, const int *prm, const flo
     RET;
   }
   dim3 grid(cdiv(w, NT), B * h);
-  image_u8_to_nhwc_bf16<<<grid, NT, 0, S_>>>((const uint8_t *)pix, prm, cm, mean, B, h, w, C, Cp, Hm, Wm, mode, scale,
-                                             (bf16_t *)y);
+  image_u8_to_nhwc_bf16<<<grid, NT, 0, S_>>>((const uint8_t *)pix, prm, cm, mean, B, h, w, C, Cp, Wp, Hm, Wm, mode,
+                                             scale, (bf16_t *)y);
   RET;
 }
-CXN_API int cxn_nhwc_bf16_to_nchw_f32(const void *x, float *y, int N, int C, int H, int W, int Cp, void *stream) {
-  nhwc_bf16_to_nchw_f32<<<nblocks(static_cast<long>(N) * C * H * W), NT, 0, S_>>>((const bf16_t *)x, y, N, C, H, W, Cp);
+CXN_API int cxn_nhwc_bf16_to_nchw_f32(const void *x, float *y, int N, int C, int H, int W, int Cp, int Wp,
+                                      void *stream) {
+  nhwc_bf16_to_nchw_f32<<<nblocks(static_cast<long>(N) * C * H * W), NT, 0, S_>>>((const bf16_t *)x, y, N, C, H, W, Cp,
+                                                                                  Wp);
   RET;
 }
 CXN_API int cxn_transpose(const void *x, void *y, int B, int R, int Cc, void *stream) {

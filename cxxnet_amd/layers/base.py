@@ -25,6 +25,7 @@ class Node:
         self.name = name
         self.shape: Tuple[int, int, int, int] = (0, 0, 0, 0)  # (b, c, h, w)
         self.cp = 0
+        self.wp = 0  # physical row width when > w (row-padded first-conv input, NeuralNet._pad_input_channels)
         self.data: Optional[torch.Tensor] = None
         self.fp32_view: Optional[torch.Tensor] = None  # loss layers expose fp32 predictions here
         # zero-copy split outputs: `data` aliases the split input (read-only in forward) and the
@@ -43,6 +44,7 @@ class Node:
     def set_shape(self, b, c, h, w, cp=None):
         self.shape = (int(b), int(c), int(h), int(w))
         self.cp = int(cp if cp is not None else c)
+        self.wp = int(w)
 
     @property
     def batch(self):
@@ -54,7 +56,7 @@ class Node:
 
     def alloc(self, device, dtype):
         b, c, h, w = self.shape
-        self.data = torch.zeros((b, h, w, self.cp), device=device, dtype=dtype)
+        self.data = torch.zeros((b, h, max(w, self.wp), self.cp), device=device, dtype=dtype)
 
     def mat(self) -> torch.Tensor:
         """(batch, c*h*w) view (reference Node::mat); physical order is NHWC."""
@@ -62,7 +64,7 @@ class Node:
 
     def to_nchw(self) -> torch.Tensor:
         from ..ops import nhwc_to_nchw
-        return nhwc_to_nchw(self.data, self.shape[1])
+        return nhwc_to_nchw(self.data, self.shape[1], self.shape[3])
 
 
 @dataclass

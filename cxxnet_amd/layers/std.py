@@ -233,8 +233,9 @@ class ConvolutionLayer(Layer):
         Ho, Wo = conv_out_size(h, w, lp.kernel_height, lp.kernel_width, lp.stride, lp.pad_y, lp.pad_x)
         nodes_out[0].set_shape(b, lp.num_channel, Ho, Wo)
         self.cin_phys = x.cp
-        self.geo = ConvGeom(b, h, w, x.cp, Ho, Wo, lp.num_channel, lp.kernel_height, lp.kernel_width, lp.stride,
-                            lp.pad_y, lp.pad_x, G)
+        # physical row width: the row-padded 3-channel input (NeuralNet._pad_input_channels)
+        self.geo = ConvGeom(b, h, max(w, x.wp), x.cp, Ho, Wo, lp.num_channel, lp.kernel_height, lp.kernel_width,
+                            lp.stride, lp.pad_y, lp.pad_x, G)
         cg_l, cg_p = c // G, x.cp // G
         kh, kw, co = lp.kernel_height, lp.kernel_width, lp.num_channel
         # few input channels with padding (VGG's 3x3 pad-1 first conv on 4 channels): forward and

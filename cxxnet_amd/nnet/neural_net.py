@@ -98,20 +98,37 @@ class NeuralNet:
                 layer.layer_index = i
                 self.connections.append(Connection(layer, info.type, nin, nout))
                 self.connections[-1].owner = i
-        self._pad_input_channels()
         for i, c_ in enumerate(self.connections):
             if not c_.shared:
                 self._configure_layer(i, c_.layer)
+        self._pad_input_channels()
 
     def _pad_input_channels(self):
         """First-layer conv on the GPU: pad input channels to a multiple of 4 so the
-        implicit-GEMM gather can use 8-byte vector loads (weights get zero columns)."""
+        implicit-GEMM gather can use 8-byte vector loads (weights get zero columns).
+
+        Exception, the 3-channel strided pad-0 conv that is the input's only reader (AlexNet
+        conv1, 11x11 / 4): its GEMMs read whole kernel-row runs (ops.gemm.rowrun_ok), and with
+        3 channels a run is 33 elements -- 5 16-byte chunks, K = 11 x 40 = 440 -- against 44
+        (6 chunks, K = 528) with a zero 4th channel.  The node then keeps 3 channels and pads
+        each image row to a multiple of 4 pixels instead, so that every row and every 4-pixel
+        output step starts 8-byte aligned (forward 165 -> 120 us at batch 256,
+        profiles/r3_conv1_c3_probe.jsonl).  CXXNET_CONV1_C3=0 keeps the 4-channel layout."""
         if not self.ctx.is_gpu:
             return
         n0 = self.nodes[0]
         b, c, h, w = n0.shape
-        for conn in self.connections:
+        readers = [conn for conn in self.connections if any(n is n0 for n in conn.nodes_in)]
+        for conn in readers:
             if conn.type == K_CONV and conn.nodes_in[0] is n0 and c % 8 != 0:
+                lp = conn.layer.lp
+                wp = (w + 3) // 4 * 4
+                if (c == 3 and len(readers) == 1 and lp.num_group == 1 and lp.pad_y == 0 and lp.pad_x == 0
+                        and (lp.stride * c * 2) % 8 == 0 and lp.kernel_width <= w
+                        and (wp - lp.kernel_width) // lp.stride == (w - lp.kernel_width) // lp.stride
+                        and os.environ.get("CXXNET_CONV1_C3", "1") != "0" and not ops.gemm.deterministic()):
+                    n0.cp, n0.wp = 3, wp
+                    return
                 n0.cp = (c + 3) // 4 * 4
                 return
 

@@ -706,7 +706,7 @@ class NetTrainer:
             return out.view(out.shape[0], *node.shape[1:])
         with_data = node.data[: self.net.cur_batch]
         from ..ops import nhwc_to_nchw
-        return nhwc_to_nchw(with_data, node.shape[1])
+        return nhwc_to_nchw(with_data, node.shape[1], node.shape[3])
 
     def _gather(self, t: torch.Tensor) -> torch.Tensor:
         if self.world == 1:

@@ -481,6 +481,17 @@ def conv_out_size(H, W, KH, KW, stride, pad_y, pad_x):
     return (H + 2 * pad_y - KH) // stride + 1, (W + 2 * pad_x - KW) // stride + 1
 
 
+ROWRUN_ALIGN = int(os.environ.get("CXXNET_ROWRUN_ALIGN", "8") or 8)  # as gemm_glds.hip g_rowrun_align
+
+
+def rowrun_ok(g: ConvGeom) -> bool:
+    """Few-channel conv served by the kernel-row-run GEMMs (K_ROWGATHER forward, row-run MN
+    gather weight-grad): pad 0, one group, and every image row and output-pixel step of x at
+    ROWRUN_ALIGN bytes (the runs' 16-byte DMAs start at a pixel)."""
+    return (g.groups == 1 and g.pad_y == 0 and g.pad_x == 0 and g.C % 8 != 0 and
+            (g.W * g.C * 2) % ROWRUN_ALIGN == 0 and (g.stride * g.C * 2) % ROWRUN_ALIGN == 0)
+
+
 def _w_nchw(w: torch.Tensor) -> torch.Tensor:
     # [Cout][KH][KW][Cg] -> [Cout][Cg][KH][KW]
     return w.permute(0, 3, 1, 2).contiguous()
@@ -534,7 +545,7 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
         return
     cg = g.cg_in
     va = 8 if cg % 8 == 0 else 4
-    if cg % va:
+    if cg % va and not rowrun_ok(g):
         raise ValueError(f"conv: channels per group ({cg}) must be a multiple of 4 on the GPU path")
     kd = g.kdim
     A = _op(w, g.cg_out * kd, kd, g.cg_out, kd)
@@ -554,7 +565,7 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
         key = ("cf", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
         if run(_tuned_tile(key, run, y, lambda: _pick_glds(A.rows, B.rows, g.groups), extra=(REG,)), y):
             return
-    if va != 8 and g.groups == 1 and g.pad_y == 0 and g.pad_x == 0 and g.C % 4 == 0 and _use("cr"):
+    if va != 8 and rowrun_ok(g) and (_use("cr") or g.C % 4):
         # few input channels (conv1: 11x11 taps of 4 channels): each kernel row's KW*C
         # elements are contiguous in NHWC; the GEMM reads them as zero-padded runs
         wp, lp = _row_padded_weights(w, g)
@@ -566,6 +577,8 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
         key = ("cr", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride)
         if run(_tuned_tile(key, run, y, lambda: 1), y):
             return
+    if cg % va:
+        raise RuntimeError(f"conv: no GPU kernel for {cg} channels per group ({g})")
     reg(y)
 
 
@@ -695,7 +708,7 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
         # wins shapes where it loses inside the step (conv2/conv3 above)
         if run(_tuned_tile(key, run, dw, lambda: REG, extra=(REG,), tune=_CW_TUNE), dw):
             return
-    if va != 8 and g.groups == 1 and g.pad_y == 0 and g.pad_x == 0 and g.C % 4 == 0 and _use("cwr"):
+    if va != 8 and rowrun_ok(g) and (_use("cwr") or g.C % 4):
         # few input channels (conv1): the KW*C im2col rows of one kernel row are one contiguous run
         # of x, so the transposed gather reads each run as Cg = roundup(KW*C, 8) "channels" of a
         # 1-wide kernel; the result lands in a row-padded fp32 buffer whose pad columns are dropped
@@ -715,6 +728,8 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
             L = g.KW * g.C
             dw.view(g.Cout, g.KH, L).add_(ws.view(g.Cout, g.KH, lp)[:, :, :L])
             return
+    if cg % va:
+        raise RuntimeError(f"conv weight-grad: no GPU kernel for {cg} channels per group ({g})")
     reg(dw)
 
 

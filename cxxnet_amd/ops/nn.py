@@ -24,15 +24,18 @@ def _k():
 
 # ----------------------------------------------------------------------------- layout
 def input_to_nhwc(x_nchw: torch.Tensor, out: torch.Tensor, scale: float = 1.0):
-    """NCHW fp32 batch -> NHWC node (bf16 on GPU), zero-padding extra channels."""
+    """NCHW fp32 batch -> NHWC node (bf16 on GPU), zero-padding extra channels (and, for a
+    row-padded node of physical width out.shape[2] > W, leaving the pad columns zero)."""
     N, C, H, W = x_nchw.shape
-    Cp = out.shape[-1]
+    Cp, Wp = out.shape[-1], out.shape[2]
+    if Wp < W:
+        raise ValueError(f"input batch {tuple(x_nchw.shape)} does not fit node {tuple(out.shape)}")
     if not _native_t(out):
         out.zero_()
-        out[..., :C].copy_(x_nchw.permute(0, 2, 3, 1) * scale)
+        out[:, :, :W, :C].copy_(x_nchw.permute(0, 2, 3, 1) * scale)
         return
     x = x_nchw.contiguous().float()
-    native.check(_k().cxn_nchw_f32_to_nhwc_bf16(x.data_ptr(), out.data_ptr(), N, C, H, W, Cp, float(scale),
+    native.check(_k().cxn_nchw_f32_to_nhwc_bf16(x.data_ptr(), out.data_ptr(), N, C, H, W, Cp, Wp, float(scale),
                                                 _stream()), "nchw_to_nhwc")
 
 
@@ -43,8 +46,8 @@ def image_to_nhwc(img, out: torch.Tensor):
         input_to_nhwc(img.to_float(), out)
         return
     B, C, h, w = img.shape
-    Cp = out.shape[-1]
-    if tuple(out.shape[:3]) != (B, h, w) or Cp < C:
+    Cp, Wp = out.shape[-1], out.shape[2]
+    if tuple(out.shape[:2]) != (B, h) or Wp < w or Cp < C:
         raise ValueError(f"image batch {tuple(img.shape)} does not fit input node {tuple(out.shape)}")
     dev = out.device
     pix = img.pix.to(dev, non_blocking=True).contiguous()
@@ -62,16 +65,18 @@ def image_to_nhwc(img, out: torch.Tensor):
         raise ValueError("mean_value needs one value per channel")
     native.check(_k().cxn_image_u8_to_nhwc_bf16(
         pix.data_ptr(), prm.data_ptr(), cm.data_ptr(), mean.data_ptr() if mean is not None else None,
-        B, h, w, C, Cp, Hm, Wm, int(img.mode), float(img.scale), out.data_ptr(), _stream()), "image_to_nhwc")
+        B, h, w, C, Cp, Wp, Hm, Wm, int(img.mode), float(img.scale), out.data_ptr(), _stream()), "image_to_nhwc")
 
 
-def nhwc_to_nchw(x: torch.Tensor, C: int) -> torch.Tensor:
-    """NHWC node (any dtype) -> NCHW fp32 tensor with C logical channels."""
-    N, H, W, Cp = x.shape
+def nhwc_to_nchw(x: torch.Tensor, C: int, W: int = 0) -> torch.Tensor:
+    """NHWC node (any dtype) -> NCHW fp32 tensor with C logical channels (and W logical
+    columns of a row-padded node; 0 = all)."""
+    N, H, Wp, Cp = x.shape
+    W = W or Wp
     if not _native_t(x):
-        return x[..., :C].permute(0, 3, 1, 2).float().contiguous()
+        return x[:, :, :W, :C].permute(0, 3, 1, 2).float().contiguous()
     out = torch.empty((N, C, H, W), dtype=torch.float32, device=x.device)
-    native.check(_k().cxn_nhwc_bf16_to_nchw_f32(x.data_ptr(), out.data_ptr(), N, C, H, W, Cp, _stream()),
+    native.check(_k().cxn_nhwc_bf16_to_nchw_f32(x.data_ptr(), out.data_ptr(), N, C, H, W, Cp, Wp, _stream()),
                  "nhwc_to_nchw")
     return out
 

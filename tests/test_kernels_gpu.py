@@ -361,6 +361,118 @@ def test_image_u8_fast_path(mode):
     assert got[..., 3].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("w", [7, 13, 227])
+def test_image_u8_row_padded_c3(mode, w):
+    """3-channel node with rows padded to a multiple of 4 pixels (the first-conv row-run layout,
+    NeuralNet._pad_input_channels): image_u8c3_nhwc3p (modes 0/1) and the generic kernel (mode 2)
+    write the logical columns, the pad columns stay zero; input_to_nhwc / nhwc_to_nchw honour the
+    pitch too."""
+    from cxxnet_amd.io.data import U8Images
+    g = torch.Generator().manual_seed(11 * w + mode)
+    B, h = 3, 5
+    wp = (w + 3) // 4 * 4 + (4 if w == 13 else 0)  # one case with more than the minimal pad
+    pix = torch.randint(0, 256, (B, h, w, 3), generator=g, dtype=torch.uint8)
+    prm = torch.zeros((B, 4), dtype=torch.int32)
+    cm = torch.stack([torch.rand(B, generator=g) + 0.5, torch.rand(B, generator=g) * 10 - 5], 1)
+    mean = {0: None, 1: torch.tensor([100.0, 110.0, 120.0]), 2: torch.rand((3, h + 2, w + 3), generator=g) * 255}[mode]
+    if mode == 2:
+        prm[:, 0], prm[:, 1], prm[:, 2] = 1, 2, torch.tensor([0, 1, 0])
+    img = U8Images(pix, prm, cm, mean, mode, 1.0 / 64)
+    ref = img.to_float().permute(0, 2, 3, 1)
+    out = torch.zeros((B, h, wp, 3), dtype=torch.bfloat16, device=DEV)
+    ops.image_to_nhwc(img, out)
+    got = out.float().cpu()
+    assert relerr(got[:, :, :w], ref) < 1e-2
+    assert got[:, :, w:].abs().max().item() == 0
+    back = ops.nhwc_to_nchw(out, 3, w)
+    x = torch.randn(B, 3, h, w)
+    node = torch.zeros((B, h, wp, 3), dtype=torch.bfloat16, device=DEV)
+    ops.input_to_nhwc(x.to(DEV), node)
+    torch.cuda.synchronize()
+    assert relerr(back.cpu(), ref.permute(0, 3, 1, 2)) < 1e-2
+    assert relerr(ops.nhwc_to_nchw(node, 3, w).cpu(), x) < 1e-2
+    assert node[:, :, w:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("N", [2, 16])
+def test_conv1_three_channel_row_runs(N):
+    """AlexNet conv1 (11x11 / 4, 96 outputs) on the 3-channel row-padded node: forward (K_ROWGATHER,
+    K = 11 x 40) and weight-gradient (row-run MN gather) against fp32 torch on the same bf16 values."""
+    import torch.nn.functional as F
+    from cxxnet_amd.ops import gemm as G
+    torch.manual_seed(N)
+    H = W = 227
+    x3 = torch.randn(N, 3, H, W, device=DEV).to(torch.bfloat16).float()
+    w3 = (torch.randn(96, 3, 11, 11, device=DEV) * 0.05).to(torch.bfloat16).float()
+    dy = torch.randn(N, 96, 55, 55, device=DEV).to(torch.bfloat16).float()
+    y_ref = F.conv2d(x3, w3, stride=4) + 0.5
+    dw_ref = torch.nn.grad.conv2d_weight(x3, w3.shape, dy, stride=4)
+    x = torch.zeros(N, H, 228, 3, device=DEV, dtype=torch.bfloat16)
+    x[:, :, :W] = x3.permute(0, 2, 3, 1).to(torch.bfloat16)
+    w = w3.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    g = ConvGeom(N, H, 228, 3, 55, 55, 96, 11, 11, 4, 0, 0, 1)
+    assert G.rowrun_ok(g)
+    y = torch.empty(N, 55, 55, 96, device=DEV, dtype=torch.bfloat16)
+    ops.conv_forward(x, w, torch.full((96,), 0.5, device=DEV), y, g)
+    dw = torch.full((96, 11, 11, 3), 0.25, device=DEV)
+    ops.conv_backward_weight(x, dy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16), dw, g)
+    torch.cuda.synchronize()
+    assert relerr(y.permute(0, 3, 1, 2), y_ref) < 1e-2
+    assert relerr(dw.permute(0, 3, 1, 2) - 0.25, dw_ref) < 1e-2
+
+
+def test_alexnet_input_node_three_channels(monkeypatch):
+    """The GPU net keeps AlexNet's input at 3 channels on 228-pixel rows and a training step
+    matches the 4-channel layout's (CXXNET_CONV1_C3=0) loss and conv1 weight-gradient."""
+    from cxxnet_amd.io.data import DataBatch
+    from cxxnet_amd.models import load_conf
+    from cxxnet_amd.nnet import NetTrainer
+    out = []
+    trs = []
+    for c3 in ("1", "0"):
+        monkeypatch.setenv("CXXNET_CONV1_C3", c3)
+        pairs = load_conf("alexnet", [("batch_size", "8"), ("dev", "gpu"), ("eval_train", "0"), ("silent", "1"),
+                                      ("update_period", "2")])
+        tr = NetTrainer()
+        for k, v in pairs:
+            if not k.startswith("metric"):
+                tr.set_param(k, v)
+        tr.init_model()
+        n0 = tr.net.nodes[0]
+        assert (n0.cp, n0.data.shape[2]) == ((3, 228) if c3 == "1" else (4, 227))
+        trs.append(tr)
+    # same weights in both nets (the arenas differ in conv1's channel count)
+    for ca, cb in zip(trs[0].net.connections, trs[1].net.connections):
+        if ca.shared:
+            continue
+        for pa, pb in zip(ca.layer.params, cb.layer.params):
+            if pa.shape == pb.shape:
+                pb.w.copy_(pa.w.view(pb.w.shape))
+            else:  # conv1 wmat [96][11][11][3] -> [96][11][11][4]
+                pb.w.view(pb.shape).zero_()
+                pb.w.view(pb.shape)[..., :3].copy_(pa.w.view(pa.shape))
+    trs[1].net.arena.sync_shadow()
+    for tr in trs:
+        c, h, w = tr.net_cfg.input_shape
+        g = torch.Generator().manual_seed(3)
+        x = torch.randn(8, c, h, w, generator=g).to(DEV)
+        y = torch.randint(0, 1000, (8, 1), generator=g).float().to(DEV)
+        tr.net.set_input(x)
+        tr.net.forward(False)
+        torch.cuda.synchronize()
+        fwd = (tr.net.nodes[1].data.float().clone(), tr.net.nodes[-1].data.float().clone())
+        tr.update(DataBatch(x, y))
+        torch.cuda.synchronize()
+        conv1 = tr.net.connections[0].layer
+        out.append(fwd + (conv1.w.g.view(96, 11, 11, -1)[..., :3].clone(),))
+    # conv1's output agrees to bf16 rounding; the softmax output and conv1's weight-gradient pass
+    # through 7 more bf16 layers each way and differ by their summation orders only
+    # (test_conv1_three_channel_row_runs pins the kernels against fp32 torch)
+    errs = [relerr(a, b) for a, b in zip(out[0], out[1])]
+    assert errs[0] < 1e-2 and errs[1] < 6e-2 and errs[2] < 1e-1, errs
+
+
 @pytest.fixture
 def register_kernel_only():
     """Route every GEMM to the register-staged kernel (gemm_mfma.hip), whose MN-major tiles
