@@ -1276,6 +1276,7 @@ struct ColsumSeg {
   const uint8_t *mask;  // nullable: max-pool offsets [rows][C]; entries with bit 7 set count as 0
   float *db;
   long rows;
+  long ld;  // dy row stride in elements (>= C: a channel slice of a wider NHWC buffer); mask rows are C
   int C, rpb, nblk, nchunk;
 };
 struct ColsumTable {
@@ -1311,8 +1312,8 @@ __global__ void colsum_multi(ColsumTable tab) {
       // 8 rows in flight per thread; whole groups of 8 without bounds checks
       constexpr int U = 8;
       const long e0 = (r0 + rg) * sg.C + cv * 8;
-      const bf16_t *p = sg.dy + e0;
-      const long step = static_cast<long>(RG) * sg.C;
+      const bf16_t *p = sg.dy + (r0 + rg) * sg.ld + cv * 8;
+      const long step = static_cast<long>(RG) * sg.ld;  // masked segments have ld == C
       long r = r0 + rg;
       if (sg.mask == nullptr) {
         for (; r + (U - 1) * RG < r1; r += RG * U, p += U * step) {
@@ -1464,10 +1465,13 @@ __global__ void fanout_bf16(const uint4 *__restrict__ src, uint4 *d0, uint4 *d1,
   }
 }
 // split backward: y = s0 + s1 (+ s2 + s3) in fp32, rounded once (y may alias s0)
+// mask: y holds relu(z) on entry and the sum is kept only where y > 0 (relu') -- the backward
+// of a split whose input is a zero-copy ch_concat of fused conv+relu branches
 __global__ void sum_bf16(const uint4 *s0, const uint4 *s1, const uint4 *s2, const uint4 *s3, int ns, uint4 *y,
-                         long n8) {
+                         long n8, int mask) {
   for (long i = grid_stride_start(); i < n8; i += grid_stride()) {
-    float a[8], b[8];
+    float a[8], b[8], z[8];
+    if (mask) unpack8(y[i], z);
     unpack8(s0[i], a);
     unpack8(s1[i], b);
 #pragma unroll
@@ -1481,6 +1485,10 @@ __global__ void sum_bf16(const uint4 *s0, const uint4 *s1, const uint4 *s2, cons
       unpack8(s3[i], b);
 #pragma unroll
       for (int e = 0; e < 8; ++e) a[e] += b[e];
+    }
+    if (mask) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] = z[e] > 0.f ? a[e] : 0.f;
     }
     y[i] = pack8(a);
   }
@@ -2014,7 +2022,7 @@ CXN_API int cxn_colsum(const void *dy, float *db, long rows, int C, float *ws, l
 // dys / dbs / rows / Cs: n deferred bias gradients (C % 8 == 0 each); masks: nullable array of
 // nullable max-pool offset tensors (masked segments, see colsum_multi)
 CXN_API int cxn_colsum_multi(const void *const *dys, float *const *dbs, const long *rows, const int *Cs,
-                             const void *const *masks, int n, void *stream) {
+                             const void *const *masks, int n, void *stream, const long *lds) {
   for (int base = 0; base < n; base += COLSUM_MAXSEG) {
     ColsumTable tab;
     const int cnt = n - base < COLSUM_MAXSEG ? n - base : COLSUM_MAXSEG;
@@ -2023,6 +2031,8 @@ CXN_API int cxn_colsum_multi(const void *const *dys, float *const *dbs, const lo
     for (int i = 0; i < cnt; ++i) {
       const int j = base + i;
       if (Cs[j] % 8) return -1;
+      const long ld = lds ? lds[j] : Cs[j];
+      if (ld % 8 || ld < Cs[j] || (masks && masks[j] && ld != Cs[j])) return -1;
       // <= 1024 blocks (adders per channel) per segment, >= 256 rows per block: the largest
       // segment (AlexNet conv1: 774k rows) needs ~4 blocks per CU to keep HBM busy
       long nb = cdiv(rows[j], 256L);
@@ -2044,7 +2054,7 @@ CXN_API int cxn_colsum_multi(const void *const *dys, float *const *dbs, const lo
       const int rpb = rows[j] > 0 ? static_cast<int>(cdiv(rows[j], nb)) : 1;
       const int nrb = static_cast<int>(cdiv(rows[j], static_cast<long>(rpb)));
       tab.s[i] = ColsumSeg{static_cast<const bf16_t *>(dys[j]),
-                           masks ? static_cast<const uint8_t *>(masks[j]) : nullptr, dbs[j], rows[j], Cs[j], rpb,
+                           masks ? static_cast<const uint8_t *>(masks[j]) : nullptr, dbs[j], rows[j], ld, Cs[j], rpb,
                            nrb * nchunk, nchunk};
       tab.b0[i] = nblk;
       nblk += tab.s[i].nblk;
@@ -2091,11 +2101,11 @@ CXN_API int cxn_fanout_bf16(const void *src, void *d0, void *d1, void *d2, void 
   RET;
 }
 CXN_API int cxn_sum_bf16(const void *s0, const void *s1, const void *s2, const void *s3, int ns, void *y, long n,
-                         void *stream) {
+                         void *stream, int mask) {
   if (ns < 2 || ns > 4 || (n & 7) != 0) return -2;
   const long n8 = n / 8;
   sum_bf16<<<nblocks(n8), NT, 0, S_>>>((const uint4 *)s0, (const uint4 *)s1, (const uint4 *)s2, (const uint4 *)s3, ns,
-                                       (uint4 *)y, n8);
+                                       (uint4 *)y, n8, mask);
   RET;
 }
 // ins[k] (NHWC, cs[k] channels, k < n <= 4) <-> out (Ct channels), npix pixels; bwd: out -> ins

@@ -91,8 +91,9 @@ class SplitLayer(Layer):
     def backprop(self, prop_grad, nodes_in, nodes_out):
         if not prop_grad:
             return
-        # the output gradients summed in one pass (fp32 accumulation, one rounding)
-        ops.sum_into(nodes_in[0].gdst, [o.gdst for o in nodes_out])
+        # the output gradients summed in one pass (fp32 accumulation, one rounding); masked by
+        # relu' when the input is a zero-copy concat of relu outputs (NeuralNet._fuse_concat)
+        ops.sum_into(nodes_in[0].gdst, [o.gdst for o in nodes_out], mask_relu=self.grad_mask_relu)
 
 
 class ConcatLayer(Layer):
@@ -106,6 +107,8 @@ class ConcatLayer(Layer):
         # inputs that hold relu(z) of a fused conv/fullc -> relu producer: the gradient slice
         # copied back into them is masked by relu'(z) (the activation they still hold)
         self.grad_mask_inputs = set()
+        # the inputs are channel slices of the output buffer (NeuralNet._fuse_concat): no copies
+        self.zero_copy = False
 
     def init_connection(self, nodes_in, nodes_out):
         _check(len(nodes_in) > 1 and len(nodes_out) == 1, "Concat layer only support n-1 connection")
@@ -136,6 +139,8 @@ class ConcatLayer(Layer):
                 off += n.shape[3]
 
     def forward(self, is_train, nodes_in, nodes_out):
+        if self.zero_copy:
+            return
         if self.dim == 1:
             if ops.concat_channels([n.data for n in nodes_in], nodes_out[0].data):
                 return
@@ -152,7 +157,7 @@ class ConcatLayer(Layer):
                 off += wi
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
-        if not prop_grad:
+        if not prop_grad or self.zero_copy:
             return
         if self.dim == 1:
             if ops.concat_channels([n.gdst for n in nodes_in], nodes_out[0].data, backward=True,

@@ -194,6 +194,15 @@ def _all_gather_rows(t: torch.Tensor, rows: int) -> _Gathered:
 
 
 # ============================================================================ conv
+def _pixel_rows(t: torch.Tensor) -> torch.Tensor:
+    """[pixels][C] view of an NHWC activation; a channel slice of a zero-copy ch_concat buffer
+    (NeuralNet._fuse_concat) keeps the full buffer's pixel stride as its row stride."""
+    if t.is_contiguous():
+        return t.view(-1, t.shape[-1])
+    n, h, w, c = t.shape
+    return t.as_strided((n * h * w, c), (t.stride(2), 1))
+
+
 class ConvolutionLayer(Layer):
     """`conv` -- reference src/layer/convolution_layer-inl.hpp:12-228.
 
@@ -312,7 +321,7 @@ class ConvolutionLayer(Layer):
         if self.bias_done:  # summed by the max-pool behind this conv (NeuralNet._fuse_pool_bias)
             self.bias_done = False
         elif self.b is not None:
-            self.ctx.bias_grad(dy.view(-1, dy.shape[-1]), self.b.g)
+            self.ctx.bias_grad(_pixel_rows(dy), self.b.g)
         if prop_grad:
             ready = self.ctx.flipped is not None and id(self) in self.ctx.flipped
             below = self.bias_below

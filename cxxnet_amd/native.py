@@ -104,12 +104,12 @@ _SIGS = {
     "cxn_softmax": [_P, _P, _P, _I, _I, _P],
     "cxn_loss_grad": [_P, _P, _P, _I, _I, _I, _F, _I, _P],
     "cxn_colsum": [_P, _P, _L, _I, _P, _L, _P],
-    "cxn_colsum_multi": [_P, _P, _P, _P, _P, _I, _P],
+    "cxn_colsum_multi": [_P, _P, _P, _P, _P, _I, _P, _P],
     "cxn_concat": [_P, _P, _I, _P, _I, _L, _I, _I, _P],
     "cxn_cast_f32_bf16": [_P, _P, _L, _P],
     "cxn_add_bf16": [_P, _P, _P, _L, _P],
     "cxn_fanout_bf16": [_P, _P, _P, _P, _P, _I, _L, _P],
-    "cxn_sum_bf16": [_P, _P, _P, _P, _I, _P, _L, _P],
+    "cxn_sum_bf16": [_P, _P, _P, _P, _I, _P, _L, _P, _I],
     "cxn_channel_copy": [_P, _I, _I, _P, _I, _I, _I, _L, _I, _P],
     "cxn_fused_update": [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _F, _F, _P],
     "cxn_nonfinite_check": [_P, _L, _P, _P],

@@ -59,7 +59,10 @@ class NeuralNet:
         self.ctx.label_name_map = dict(cfg.label_name_map)
         self.ctx.step_counter = torch.zeros(1, dtype=torch.int32, device=self.device)
         if fuse is None:
-            fuse = self.ctx.is_gpu and os.environ.get("CXXNET_FUSE", "1") != "0"
+            # CXXNET_FUSE=0: no graph fusion; 2: fusion on the CPU executor too (the fp32 torch
+            # path implements every fused epilogue, so CPU tests can check the fused graph)
+            mode = os.environ.get("CXXNET_FUSE", "1")
+            fuse = mode == "2" or (self.ctx.is_gpu and mode != "0")
         self.fuse = fuse
         self.nodes: List[Node] = []
         self.connections: List[Connection] = []
@@ -185,6 +188,7 @@ class NeuralNet:
             conn.layer.fused_into_producer = True
             cj.layer.grad_mask_relu = True
             self.aliases[id(b)] = a
+        self._fuse_concat(producers, consumers)
         self._fuse_split(producers, consumers)
         self._fuse_pool_bias(producers, consumers)
         self._fuse_dgrad_bias(producers, consumers)
@@ -240,6 +244,53 @@ class NeuralNet:
                 continue
             lay.bias_of = p.layer
 
+    def _fuse_concat(self, producers, consumers):
+        """Zero-copy ch_concat (reference src/layer/concat_layer-inl.hpp:38-76 copies): when
+        every input is the fused relu output of its own conv, read by the concat alone, each
+        conv writes relu(z) straight into its channel slice of the concat output (the GEMM
+        epilogue's row stride is the full channel count) and reads its output gradient from
+        that slice in backward -- the concat moves no bytes either way.
+        relu' of the slices is applied by the layer that writes the concat output's gradient
+        (its single consumer: split, or a pooling layer, gets grad_mask_relu), since every
+        channel of the output is a relu output and still holds it at that point.
+        CXXNET_CONCAT_ZC=0 keeps the copying concat."""
+        self.concat_views = {}
+        if os.environ.get("CXXNET_CONCAT_ZC", "1") == "0":
+            return
+        for i, conn in enumerate(self.connections):
+            if conn.type != K_CHCONCAT or conn.shared or conn.layer.dim != 1:
+                continue
+            out = conn.nodes_out[0]
+            cons = consumers.get(id(out), [])
+            if len(cons) != 1 or cons[0][1]:
+                continue
+            cj = self.connections[cons[0][0]]
+            if cj.shared or len(cj.nodes_in) != 1 or cj.type not in (K_SPLIT, K_MAXPOOL, K_AVGPOOL, K_SUMPOOL):
+                continue
+            if cj.type != K_SPLIT and getattr(cj.layer, "tie_all", False):
+                continue
+            views, off, ok = {}, 0, True
+            for b in conn.nodes_in:
+                a = self.aliases.get(id(b))  # b = fused relu(a)
+                prod = producers.get(id(a), []) if a is not None else []
+                c = b.shape[1]
+                if (a is None or len(prod) != 1 or len(consumers.get(id(b), [])) != 1 or id(a) in views
+                        or c % 8 or off % 8 or a.cp != c):
+                    ok = False
+                    break
+                p = self.connections[prod[0]]
+                if p.type != K_CONV or p.shared or not p.layer.fuse_relu:
+                    ok = False
+                    break
+                views[id(a)] = (a, out, off, c)
+                off += c
+            if not ok or off != out.shape[1] or out.cp != off:
+                continue
+            conn.layer.zero_copy = True
+            conn.layer.grad_mask_inputs.clear()
+            cj.layer.grad_mask_relu = True
+            self.concat_views.update(views)
+
     def _fuse_split(self, producers, consumers):
         """Zero-copy split: when the split is its input's only reader and every output feeds
         exactly one read-only-in-forward layer, the outputs alias the input buffer and each
@@ -274,9 +325,12 @@ class NeuralNet:
         aliases = dict(getattr(self, "aliases", {}))
         splits = getattr(self, "split_alias", {})
         aliases.update(splits)
+        views = getattr(self, "concat_views", {})
         for n in self.nodes:
-            if id(n) not in aliases:
+            if id(n) not in aliases and id(n) not in views:
                 n.alloc(self.device, dt)
+        for a, out, off, c in views.values():  # conv outputs that are channel slices of a concat
+            a.data = out.data[..., off:off + c]
         pending = [n for n in self.nodes if id(n) in aliases]
         for _ in range(len(pending) + 1):  # resolve chains (split of a relu alias, ...)
             left = []
@@ -552,7 +606,7 @@ class _BatchView:
         self.saved = [(n, n.data, n.grad_buf) for n in net.nodes]
         seen = {}
         for n, d, g in self.saved:
-            key = d.data_ptr()
+            key = (d.data_ptr(), tuple(d.shape), tuple(d.stride()))  # a concat slice may share a base pointer
             if key not in seen:
                 seen[key] = d[: net.cur_batch]
             n.data = seen[key]

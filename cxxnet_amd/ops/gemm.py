@@ -65,10 +65,34 @@ class ConvGeom:
         return self.KH * self.KW * self.cg_in
 
 
+def _span_bytes(t) -> int:
+    """Bytes from t's first element to one past its last: numel * size for a contiguous tensor;
+    for a strided view (a channel slice of a zero-copy ch_concat buffer) the span its elements
+    cover, so the kernel's buffer descriptor still ends at the view's last element."""
+    if t.is_contiguous() or t.numel() == 0:
+        return t.numel() * t.element_size()
+    return (sum((n - 1) * st for n, st in zip(t.shape, t.stride())) + 1) * t.element_size()
+
+
+def _pix(t) -> int:
+    """Pixel stride (elements) of an NHWC activation: its channel count when contiguous, the
+    full buffer's channel count for a channel slice."""
+    return t.shape[-1] if t.is_contiguous() else t.stride(-2)
+
+
+def _like(t) -> torch.Tensor:
+    """Uninitialised tensor with t's shape AND strides (tuning scratch for a strided output:
+    the kernel is launched with the output's row stride)."""
+    if t.is_contiguous():
+        return torch.empty_like(t)
+    base = torch.empty(_span_bytes(t) // t.element_size(), dtype=t.dtype, device=t.device)
+    return base.as_strided(t.shape, t.stride())
+
+
 def _op(t, gstride=0, ld=0, rows=0, kdim=0, **geo):
     o = native.CxnOperand()
     o.ptr = t.data_ptr()
-    o.nbytes = t.numel() * t.element_size()  # bound of the kernel's buffer descriptor
+    o.nbytes = _span_bytes(t)  # bound of the kernel's buffer descriptor
     o.gstride = gstride
     o.ld = ld
     o.rows = rows
@@ -262,8 +286,10 @@ def _tuned_tile(key, run, out, default, extra=(), tune=True, cands=None):
     if _TUNE_LOG:
         import sys
         print(f"gemm tune: timing {key} (not in the tile table)", file=sys.stderr, flush=True)
-    init = out.clone()
-    ref = init.clone()
+    init = _like(out)
+    init.copy_(out)
+    ref = _like(out)
+    ref.copy_(init)
     dflt = default()
     ref_tile = dflt
     have_ref = bool(run(dflt, ref))
@@ -271,7 +297,7 @@ def _tuned_tile(key, run, out, default, extra=(), tune=True, cands=None):
         ref.copy_(init)
         ref_tile = REG
         have_ref = bool(run(REG, ref))
-    scratch = torch.empty_like(out)
+    scratch = _like(out)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     best, best_ms = None, float("inf")
     timed = {}
@@ -553,14 +579,14 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
             stride=g.stride, pad_h=g.pad_y, pad_w=g.pad_x, dil=1, Cg=cg)
     def reg(o):
         tile = _pick(CONV_FWD_TILES if va == 8 else CONV_FWD_TILES_V4, g.cg_out, g.N * g.Ho * g.Wo, g.groups)
-        _gemm(A, B, DIRECT_K, GATHER_K, va, va, o, g.cg_out, g.Cout, bias=bias, bias_gstride=g.cg_out, relu=relu,
+        _gemm(A, B, DIRECT_K, GATHER_K, va, va, o, g.cg_out, _pix(o), bias=bias, bias_gstride=g.cg_out, relu=relu,
               tile=tile, epi=EPI_BF16, groups=g.groups)
         return True
     if va == 8 and _use("cf"):
         def run(t, o):
             if t == REG:
                 return reg(o)
-            return _glds(A, B, GL_K, GL_KG, o, g.cg_out, g.Cout, bias=bias, bias_gstride=g.cg_out, relu=relu,
+            return _glds(A, B, GL_K, GL_KG, o, g.cg_out, _pix(o), bias=bias, bias_gstride=g.cg_out, relu=relu,
                          groups=g.groups, tile=t)
         key = ("cf", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
         if run(_tuned_tile(key, run, y, lambda: _pick_glds(A.rows, B.rows, g.groups), extra=(REG,)), y):
@@ -573,7 +599,7 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
         Ar = _op(wp, 0, kr, g.Cout, kr)
         Br = _op(x, 0, 0, g.N * g.Ho * g.Wo, kr, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW,
                  stride=g.stride, pad_h=0, pad_w=0, dil=1, Cg=g.C)
-        run = lambda t, o: _glds(Ar, Br, GL_K, GL_KR, o, 0, g.Cout, bias=bias, relu=relu, tile=t)  # noqa: E731
+        run = lambda t, o: _glds(Ar, Br, GL_K, GL_KR, o, 0, _pix(o), bias=bias, relu=relu, tile=t)  # noqa: E731
         key = ("cr", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride)
         if run(_tuned_tile(key, run, y, lambda: 1), y):
             return
@@ -623,7 +649,7 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False, wt_
                                                            g.KW, cg_in, _stream()), "conv_weight_flip")
     kd = g.KH * g.KW * cg_out
     A = _op(wt_buf, cg_in * kd, kd, cg_in, kd)
-    B = _op(dy, cg_out, 0, g.N * g.H * g.W, kd, H=g.Ho, W=g.Wo, C=g.Cout, Ho=g.H, Wo=g.W, KH=g.KH,
+    B = _op(dy, cg_out, 0, g.N * g.H * g.W, kd, H=g.Ho, W=g.Wo, C=_pix(dy), Ho=g.H, Wo=g.W, KH=g.KH,
             KW=g.KW, stride=1, pad_h=g.KH - 1 - g.pad_y, pad_w=g.KW - 1 - g.pad_x, dil=g.stride, Cg=cg_out)
     def reg(o):
         tile = _pick(CONV_FWD_TILES, cg_in, g.N * g.H * g.W, g.groups)
@@ -667,7 +693,7 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
     P = g.N * g.Ho * g.Wo
     A = _op(x, cg, 0, kd, P, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW, stride=g.stride,
             pad_h=g.pad_y, pad_w=g.pad_x, dil=1, Cg=cg)
-    B = _op(dy, g.cg_out, g.Cout, g.cg_out, P)
+    B = _op(dy, g.cg_out, _pix(dy), g.cg_out, P)
 
     def reg_run(code, o):
         _gemm(A, B, GATHER_MN, DIRECT_MN, va, 8, o, g.cg_out * kd, kd, epi=EPI_F32_ATOMIC, groups=g.groups,

@@ -75,6 +75,8 @@ def nhwc_to_nchw(x: torch.Tensor, C: int, W: int = 0) -> torch.Tensor:
     W = W or Wp
     if not _native_t(x):
         return x[:, :, :W, :C].permute(0, 3, 1, 2).float().contiguous()
+    if not x.is_contiguous():  # a channel slice of a zero-copy ch_concat buffer
+        x = x.contiguous()
     out = torch.empty((N, C, H, W), dtype=torch.float32, device=x.device)
     native.check(_k().cxn_nhwc_bf16_to_nchw_f32(x.data_ptr(), out.data_ptr(), N, C, H, W, Cp, Wp, _stream()),
                  "nhwc_to_nchw")
@@ -409,6 +411,8 @@ def bias_grad(dy2d, db, mask=None):
         # colsum below keeps a fixed summation order for deterministic mode
         bias_grad_multi([(dy2d, db, mask)])
         return
+    if not dy2d.is_contiguous():  # a channel slice of a zero-copy ch_concat output
+        dy2d = dy2d.contiguous()
     rows, C = dy2d.shape
     n = max(4096, -(-rows // 512)) * C
     ws = _workspace(n, dy2d.device)
@@ -421,9 +425,17 @@ def _det() -> bool:
     return deterministic()
 
 
+def _rows_ok(d) -> bool:
+    """[rows][C] with unit column stride and a row stride that is a multiple of 8 elements
+    (contiguous, or a channel slice of a wider NHWC buffer), 16-byte aligned."""
+    return d.dim() == 2 and d.stride(1) == 1 and (d.stride(0) % 8 == 0 or d.shape[0] == 1) and \
+        d.stride(0) >= d.shape[1] and d.data_ptr() % 16 == 0
+
+
 def bias_fast_ok(d, m=None) -> bool:
     """Served by the one-launch colsum_multi kernel (no workspace, no temporaries)."""
-    return _native_t(d) and d.shape[1] % 8 == 0 and d.is_contiguous() and (m is None or m.is_contiguous())
+    return _native_t(d) and d.shape[1] % 8 == 0 and _rows_ok(d) and \
+        (m is None or (m.is_contiguous() and d.is_contiguous()))
 
 
 def bias_grad_multi(items):
@@ -444,13 +456,14 @@ def bias_grad_multi(items):
     dbs = (ctypes.c_void_p * n)(*[b.data_ptr() for _, b, _ in fast])
     rows = (ctypes.c_long * n)(*[d.shape[0] for d, _, _ in fast])
     cs = (ctypes.c_int * n)(*[d.shape[1] for d, _, _ in fast])
+    lds = (ctypes.c_long * n)(*[d.stride(0) if d.shape[0] > 1 else d.shape[1] for d, _, _ in fast])
     masks = None
     if any(m is not None for _, _, m in fast):
         masks = (ctypes.c_void_p * n)(*[m.data_ptr() if m is not None else None for _, _, m in fast])
     native.check(_k().cxn_colsum_multi(ctypes.cast(dys, ctypes.c_void_p), ctypes.cast(dbs, ctypes.c_void_p),
                                        ctypes.cast(rows, ctypes.c_void_p), ctypes.cast(cs, ctypes.c_void_p),
                                        ctypes.cast(masks, ctypes.c_void_p) if masks is not None else None, n,
-                                       _stream()), "colsum_multi")
+                                       _stream(), ctypes.cast(lds, ctypes.c_void_p)), "colsum_multi")
 
 
 def cast_to_bf16(src_f32, dst_bf16):
@@ -484,17 +497,23 @@ def fanout_copy(src, dsts):
         native.check(_k().cxn_fanout_bf16(src.data_ptr(), *ptr, len(ds), src.numel(), _stream()), "fanout")
 
 
-def sum_into(y, srcs):
+def sum_into(y, srcs, mask_relu=False):
     """y = sum(srcs) (split backward), accumulated in fp32 and rounded once per 4 terms;
-    y may alias srcs[0]."""
+    y may alias srcs[0].  mask_relu: y holds relu(z) on entry (a zero-copy ch_concat of fused
+    conv+relu branches, NeuralNet._fuse_concat) and the sum is kept only where y > 0."""
     if len(srcs) == 1:
-        if y.data_ptr() != srcs[0].data_ptr():
+        if mask_relu:
+            C = y.shape[-1]
+            channel_copy(srcs[0], 0, y, 0, C, mask_relu=True)
+        elif y.data_ptr() != srcs[0].data_ptr():
             y.copy_(srcs[0])
         return
-    if not _native_t(y) or not _vec8(y, *srcs):
+    if not _native_t(y) or not _vec8(y, *srcs) or (mask_relu and len(srcs) > 4):
         acc = srcs[0].float()
         for t in srcs[1:]:
             acc = acc + t.float()
+        if mask_relu:
+            acc = torch.where(y > 0, acc, torch.zeros_like(acc))
         y.copy_(acc)
         return
     first, rest = srcs[0], list(srcs[1:])
@@ -502,7 +521,7 @@ def sum_into(y, srcs):
         part = [first] + rest[:3]
         rest = rest[3:]
         ptr = [t.data_ptr() for t in part] + [None] * (4 - len(part))
-        native.check(_k().cxn_sum_bf16(*ptr, len(part), y.data_ptr(), y.numel(), _stream()), "sum")
+        native.check(_k().cxn_sum_bf16(*ptr, len(part), y.data_ptr(), y.numel(), _stream(), int(mask_relu)), "sum")
         first = y
 
 

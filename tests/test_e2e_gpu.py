@@ -185,19 +185,28 @@ def test_device_metrics_match_host_metrics():
     assert line.count("train-") == 3 and "nan" not in line
 
 
-def test_zero_copy_split_and_concat_relu_fusion_match_unfused(monkeypatch):
+@pytest.mark.parametrize("zc", ["1", "0"])
+def test_zero_copy_split_and_concat_relu_fusion_match_unfused(monkeypatch, zc):
     """GoogLeNet graph: zero-copy split (outputs alias the input, data-grads go to private
-    grad buffers) and relu fused into the conv epilogue in front of ch_concat (relu'-masked
-    gradient copy) must compute what the unfused executor computes."""
+    grad buffers) and relu fused into the conv epilogue in front of ch_concat -- with zc=1 the
+    zero-copy concat (branch convs write into channel slices of the concat output, strided
+    GEMM epilogues / gradient reads / bias sums, relu' applied by the split sum and the pools),
+    with zc=0 the relu'-masked gradient copy -- must compute what the unfused executor computes."""
     batch = 4
     pairs = _pairs("inception_v1", batch)
+    monkeypatch.setenv("CXXNET_CONCAT_ZC", zc)
     fused = _trainer(pairs, "gpu")
     monkeypatch.setenv("CXXNET_FUSE", "0")
     plain = _trainer(pairs, "gpu")
     monkeypatch.delenv("CXXNET_FUSE")
     net = fused.net
     assert any(getattr(c.layer, "alias", False) for c in net.connections), "no split was aliased"
-    assert any(getattr(c.layer, "grad_mask_inputs", None) for c in net.connections), "no concat relu fusion"
+    nzc = sum(bool(getattr(c.layer, "zero_copy", False)) for c in net.connections)
+    if zc == "1":
+        assert nzc == 9, nzc  # every inception concat
+    else:
+        assert nzc == 0
+        assert any(getattr(c.layer, "grad_mask_inputs", None) for c in net.connections), "no concat relu fusion"
     assert not any(getattr(c.layer, "alias", False) for c in plain.net.connections)
     plain.net.arena.w.copy_(fused.net.arena.w)
     plain.net.arena.sync_shadow()
