@@ -64,7 +64,7 @@ def build_runtime(verbose=False, force=False) -> str:
         cmd = ["g++", "-O1" if _san["on"] else "-O2", "-std=c++17", "-shared", "-fPIC", "-Wall",
                "-Wno-unused-result", "-fvisibility=hidden"] + (SAN_FLAGS if _san["on"] else []) + [
                "-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"],
-               src, "-o", target + ".tmp", "-lz", "-lpthread"]
+               src, "-o", target + ".tmp", "-lz", "-lpthread", "-ldl"]
         _run(cmd, verbose)
         os.replace(target + ".tmp", target)
     return target

@@ -10,6 +10,7 @@
 
 #include "config_reader.h"
 #include "data_io.h"
+#include "jpeg_decode.h"
 #include "layer_param.h"
 #include "layer_types.h"
 #include "metric.h"
@@ -163,6 +164,73 @@ PYBIND11_MODULE(_cxxnet_rt, m) {
         for (auto &o : objs) out.append(py::bytes(o));
         return out;
       });
+
+  py::class_<JpegDecodePool>(m, "JpegDecodePool")
+      .def(py::init<int>(), py::arg("threads"))
+      .def_property_readonly("threads", &JpegDecodePool::threads)
+      .def_static("available", [] { return jpg::api().ok; })
+      .def_static("error", [] { return jpg::api().error; })
+      .def(
+          "decode",
+          [](JpegDecodePool &pool, py::list items, py::tuple cfg, py::array_t<uint8_t> out, py::array_t<int32_t> prm,
+             py::array_t<float> cm) {
+            // items: [(row, payload bytes-like or path str, seed)]; cfg: (out_h, out_w, channels,
+            // rand_crop, rand_mirror, mirror, crop_y_start, crop_x_start, max_random_contrast,
+            // max_random_illumination, mean_mode)
+            CropConfig c;
+            c.out_h = cfg[0].cast<int>();
+            c.out_w = cfg[1].cast<int>();
+            c.channels = cfg[2].cast<int>();
+            c.rand_crop = cfg[3].cast<int>();
+            c.rand_mirror = cfg[4].cast<int>();
+            c.mirror = cfg[5].cast<int>();
+            c.crop_y_start = cfg[6].cast<int>();
+            c.crop_x_start = cfg[7].cast<int>();
+            c.max_random_contrast = cfg[8].cast<float>();
+            c.max_random_illumination = cfg[9].cast<float>();
+            c.mean_mode = cfg[10].cast<int>();
+            if (c.channels < 1 || c.channels > 3) throw std::runtime_error("JpegDecodePool: 1-3 channels");
+            if (out.ndim() != 4 || out.shape(1) != c.out_h || out.shape(2) != c.out_w || out.shape(3) != c.channels ||
+                !(out.flags() & py::array::c_style))
+              throw std::runtime_error("JpegDecodePool: out must be a C-contiguous [B][h][w][C] uint8 array");
+            const long B = out.shape(0);
+            if (prm.ndim() != 2 || prm.shape(0) != B || prm.shape(1) != 4 || cm.ndim() != 2 || cm.shape(0) != B ||
+                cm.shape(1) != 2 || !(prm.flags() & py::array::c_style) || !(cm.flags() & py::array::c_style))
+              throw std::runtime_error("JpegDecodePool: prm [B][4] int32 / cm [B][2] float32 expected");
+            std::vector<DecodeItem> its;
+            std::vector<py::buffer_info> keep;  // buffer views stay valid while the GIL is released
+            its.reserve(items.size());
+            keep.reserve(items.size());
+            for (auto h : items) {
+              py::tuple t = h.cast<py::tuple>();
+              DecodeItem d;
+              d.row = t[0].cast<int>();
+              if (d.row < 0 || d.row >= B) throw std::runtime_error("JpegDecodePool: row out of range");
+              d.seed = t[2].cast<uint64_t>();
+              py::handle pl = t[1];
+              if (py::isinstance<py::str>(pl)) {
+                d.data = nullptr;
+                d.size = 0;
+                d.path = pl.cast<std::string>();
+              } else {
+                keep.push_back(py::reinterpret_borrow<py::buffer>(pl).request());
+                d.data = static_cast<const unsigned char *>(keep.back().ptr);
+                d.size = static_cast<size_t>(keep.back().size * keep.back().itemsize);
+              }
+              its.push_back(std::move(d));
+            }
+            uint8_t *o = out.mutable_data();
+            int32_t *pp = prm.mutable_data();
+            float *cp = cm.mutable_data();
+            std::vector<int> failed;
+            {
+              py::gil_scoped_release rel;
+              failed = pool.Run(its, c, o, pp, cp);
+            }
+            return failed;
+          },
+          "Decode + crop/mirror every (row, payload, seed) into out[row]; returns the rows it could not "
+          "decode (non-JPEG or unsupported JPEG: use the Pillow path for those)");
 
   py::class_<ImageListEntry>(m, "ImageListEntry")
       .def_readonly("index", &ImageListEntry::index)

@@ -17,9 +17,13 @@ MI355X-first design:
   * The page reader is native (``_cxxnet_rt.ImageBinReader``: a C++ thread streams
     64 MB pages ahead of the consumer).
   * Records are pulled serially (deterministic order and RNG), then decoded and
-    geometrically augmented by worker processes that write straight into a shared
-    batch buffer (io/augment.py; a thread pool when decode_process = 0).  The batch
-    lands in page-locked memory for a straight host-to-device DMA.
+    geometrically augmented by the native decode pool (``_cxxnet_rt.JpegDecodePool``,
+    csrc/runtime/jpeg_decode.h: C++ threads over libjpeg-turbo, crop-window-only decode,
+    no interpreter per image) straight into the page-locked batch buffer -- the
+    reference's decode thread (iter_thread_imbin_x-inl.hpp:150-388, utils/decoder.h).
+    Affine augmentation and non-JPEG records take the Pillow path: worker processes
+    writing into a shared batch buffer (io/augment.py; a thread pool when
+    decode_process = 0).
   * A batch leaves the host as uint8 (``U8Images``).  Mean subtraction, contrast,
     illumination, scale and the NHWC-bf16 conversion happen on the GPU in one fused
     kernel (``ops.image_to_nhwc``).  That is 4x less PCIe traffic than fp32 and
@@ -247,12 +251,16 @@ def _dist_rows(batch_size: int) -> Tuple[int, int]:
 class ImageBatchIterator(DataIterator):
     """BatchAdaptIterator(AugmentIterator(<source>)) with a parallel decode stage.
 
-    Extra keys (new): decode_process (default min(16, host cores) when there are at
-    least 4, else 0: decode in that many worker processes, io/augment.py, writing into
-    a shared-memory batch; 0 = use threads), decode_thread (threads when decode_process
-    is 0; default min(8, cpus)), shard_decode (default 1: under torch.distributed each
-    rank decodes only its own rows of the batch).  Results do not depend on either
-    setting: every record's augmentation RNG is seeded from the iterator's stream."""
+    Extra keys (new): decode_native (default 1: JPEG records without affine augmentation
+    are decoded by the native C++ pool of decode_native_threads threads, default
+    min(16, host cores)), decode_process (default min(16, host cores) when there are at
+    least 4, else 0: the Pillow path decodes in that many worker processes, io/augment.py,
+    writing into a shared-memory batch; 0 = use threads), decode_thread (threads when
+    decode_process is 0; default min(8, cpus)), shard_decode (default 1: under
+    torch.distributed each rank decodes only its own rows of the batch).  Results do not
+    depend on the worker counts: every record's augmentation draws are seeded from the
+    iterator's stream (the native and Pillow paths draw crops from different generators, so
+    switching decode_native changes which crops a seed picks, not their distribution)."""
 
     fresh_batches = True  # every next() returns newly allocated tensors
 
@@ -270,6 +278,9 @@ class ImageBatchIterator(DataIterator):
         self._shm_fin = None
         self._procs = None
         self.shard_decode = 1
+        self.decode_native = 1
+        self.decode_native_threads = 0
+        self._jpeg = None
         self._pool: Optional[ThreadPoolExecutor] = None
         self.mean: Optional[torch.Tensor] = None
         self.mean_mode = 0
@@ -298,6 +309,10 @@ class ImageBatchIterator(DataIterator):
             self.decode_process = int(val)
         elif name == "shard_decode":
             self.shard_decode = int(val)
+        elif name == "decode_native":
+            self.decode_native = int(val)
+        elif name == "decode_native_threads":
+            self.decode_native_threads = int(val)
 
     # ------------------------------------------------------------------ setup
     def init(self):
@@ -309,6 +324,13 @@ class ImageBatchIterator(DataIterator):
         if not shm_available():
             self.decode_process = 0
         C, h, w = self.aug.shape
+        if self.decode_native and h > 1 and C <= 3 and not self.aug.need_affine():
+            rt = native.rt()
+            if rt.JpegDecodePool.available():
+                n = self.decode_native_threads or default_decode_process() or (os.cpu_count() or 1)
+                self._jpeg = rt.JpegDecodePool(n)
+            elif not self.silent:
+                print(f"native JPEG decoder unavailable ({rt.JpegDecodePool.error()}): decoding with Pillow")
         if self.aug.mean_value is not None and any(v > 0 for v in self.aug.mean_value):
             # the reference subtracts mean_value[i] from channel i (iter_augment_proc-inl.hpp:64-67,128)
             self.mean = torch.tensor(self.aug.mean_value, dtype=torch.float32)
@@ -421,7 +443,9 @@ class ImageBatchIterator(DataIterator):
         prm = np.zeros((B, 4), dtype=np.int32)
         cm = np.zeros((B, 2), dtype=np.float32)
         cm[:, 0] = 1.0
-        if self.decode_process > 0 and h > 1:
+        if self._jpeg is not None:
+            pix = self._decode_native(rows, seeds, (B, h, w, C), prm, cm)
+        elif self.decode_process > 0 and h > 1:
             pix = self._decode_procs(rows, seeds, (B, h, w, C), prm, cm)
         else:
             pix = self._decode_threads(rows, seeds, (B, h, w, C), prm, cm)
@@ -449,6 +473,28 @@ class ImageBatchIterator(DataIterator):
             prm[i, :3] = p
             cm[i] = c
             done[i] = True
+        pix[~done] = 0  # padding rows / other ranks' rows
+        return dst
+
+    def _decode_native(self, rows, seeds, shape, prm, cm) -> torch.Tensor:
+        """Every row through the native pool (GIL released, crops written in place); the rows it
+        reports back (non-JPEG / CMYK / corrupt) through Pillow with the same seed."""
+        B, h, w, C = shape
+        dst = self._host_buffer(shape)
+        pix = dst.numpy()
+        a = self.aug
+        cfg = (h, w, C, a.rand_crop, a.rand_mirror, a.mirror, a.crop_y_start, a.crop_x_start,
+               a.max_random_contrast, a.max_random_illumination, self.mean_mode)
+        items = [(i, r.payload, seeds[i]) for i, r in rows]
+        failed = set(self._jpeg.decode(items, cfg, pix, prm, cm)) if items else set()
+        for i, r in rows:
+            if i in failed:
+                img, p, c = _augment_one(r.payload, a, seeds[i], self.mean_mode)
+                pix[i] = img[..., :C]
+                prm[i, :3] = p
+                cm[i] = c
+        done = np.zeros(B, dtype=bool)
+        done[[i for i, _ in rows]] = True
         pix[~done] = 0  # padding rows / other ranks' rows
         return dst
 

@@ -133,7 +133,7 @@ def test_process_and_thread_decode_agree(imgset, kind):
     runs = {}
     for mode in ("thread", "process"):
         kw = dict(rand_crop=1, rand_mirror=1, seed_data=5, max_random_contrast=0.2, mean_value="1,2,3",
-                  decode_process=(0 if mode == "thread" else 2), round_batch=1)
+                  decode_process=(0 if mode == "thread" else 2), round_batch=1, decode_native=0)
         cfg = _cfg(kind, d, **kw)
         cfg.insert(-1, ("iter", "threadbuffer"))
         it = create_iterator(cfg)
@@ -245,3 +245,103 @@ model_dir = {tmp_path}/models
 """)
     rc = LearnTask().run([str(conf)])
     assert rc == 0
+
+
+# ----------------------------------------------------------------------------- native JPEG decode
+@pytest.fixture(scope="module")
+def jpegset(tmp_path_factory):
+    """JPEGs of assorted sizes: 4:4:4, 4:2:0 and grayscale, plus one PNG (fallback path)."""
+    d = tmp_path_factory.mktemp("jpgs")
+    rng = np.random.default_rng(1)
+    lines, raw = [], {}
+    for i in range(12):
+        h, w = int(rng.integers(40, 90)), int(rng.integers(40, 90))
+        yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+        a = np.stack([(yy * (k + 1) * 3 + xx * (5 - k) * 2) % 256 for k in range(3)], -1)
+        a = np.clip(a + rng.normal(0, 20, a.shape), 0, 255).astype(np.uint8)
+        if i == 11:
+            name = f"im{i}.png"
+            Image.fromarray(a).save(d / name)
+        elif i % 4 == 3:
+            name = f"im{i}.jpg"
+            Image.fromarray(a[..., 0]).save(d / name, quality=85)  # grayscale JPEG
+        else:
+            name = f"im{i}.jpg"
+            Image.fromarray(a).save(d / name, quality=90, subsampling=(0 if i % 2 else 2))
+        raw[200 + i] = (d / name).read_bytes()
+        lines.append(f"{200 + i}\t{i % 5}\t{name}\n")
+    (d / "all.lst").write_text("".join(lines))
+    im2bin.main([str(d / "all.lst"), str(d) + "/", str(d / "all.bin")])
+    return d, raw
+
+
+def test_native_jpeg_crops_match_pillow_decode(jpegset):
+    """The native pool's crop (crop-window-only libjpeg-turbo decode) is bit-identical to
+    Pillow decoding the whole image and cropping / mirroring it at the reported position."""
+    import io as _io
+    from cxxnet_amd import native
+    rt = native.rt()
+    if not rt.JpegDecodePool.available():
+        pytest.skip(rt.JpegDecodePool.error())
+    d, raw = jpegset
+    keys = sorted(raw)
+    B = len(keys)
+    items = [(i, raw[k], 1000 + 7 * i) for i, k in enumerate(keys)]
+    out = np.zeros((B, 32, 32, 3), np.uint8)
+    prm = np.zeros((B, 4), np.int32)
+    cm = np.zeros((B, 2), np.float32)
+    cfg = (32, 32, 3, 1, 1, 0, -1, -1, 0.3, 0.1, 1)
+    failed = rt.JpegDecodePool(3).decode(items, cfg, out, prm, cm)
+    assert failed == [B - 1]  # the PNG
+    seen_mirror = set()
+    for i, k in enumerate(keys[:-1]):
+        full = np.asarray(Image.open(_io.BytesIO(raw[k])).convert("RGB"))
+        y, x, m = (int(v) for v in prm[i, :3])
+        assert 0 <= y <= full.shape[0] - 32 and 0 <= x <= full.shape[1] - 32
+        ref = full[y:y + 32, x:x + 32]
+        if m:
+            ref = ref[:, ::-1]
+        seen_mirror.add(m)
+        assert np.array_equal(out[i], ref), (k, y, x, m)
+        assert 0.7 <= cm[i, 0] <= 1.3 and -0.1 <= cm[i, 1] <= 0.1
+    assert seen_mirror == {0, 1}
+    # thread count does not change anything
+    out2, prm2, cm2 = np.zeros_like(out), np.zeros_like(prm), np.zeros_like(cm)
+    rt.JpegDecodePool(1).decode(items, cfg, out2, prm2, cm2)
+    assert np.array_equal(out[:-1], out2[:-1]) and np.array_equal(prm[:-1], prm2[:-1])
+    assert np.array_equal(cm[:-1], cm2[:-1])
+
+
+@pytest.mark.parametrize("kind", ["imgbin", "img"])
+def test_native_decode_iterator_matches_its_crop_params(jpegset, kind):
+    """iter = imgbin / img with decode_native = 1: every row is the Pillow decode of its record
+    cropped at the batch's own crop parameters (the PNG row goes through the Pillow path),
+    and the batches do not depend on the native thread count."""
+    import io as _io
+    from cxxnet_amd import native
+    if not native.rt().JpegDecodePool.available():
+        pytest.skip("no libjpeg")
+    d, raw = jpegset
+    runs = []
+    for nt in (1, 4):
+        it = create_iterator(_cfg(kind, d, rand_crop=1, rand_mirror=1, seed_data=2, mean_value="1,2,3",
+                                  decode_native=1, decode_native_threads=nt, round_batch=1))
+        it.init()
+        assert it._jpeg is not None and it._jpeg.threads == nt
+        batches = []
+        while it.next():
+            b = it.value()
+            batches.append((b.data.pix.clone(), b.data.prm.clone(), b.inst_index.copy(), b.num_batch_padd))
+        runs.append(batches)
+        it.close()
+    assert len(runs[0]) == 3
+    for (p0, q0, i0, _), (p1, q1, i1, _) in zip(*runs):
+        assert torch.equal(p0, p1) and torch.equal(q0, q1) and (i0 == i1).all()
+    for pix, prm, idx, padd in runs[0]:
+        for r in range(4):
+            full = np.asarray(Image.open(_io.BytesIO(raw[int(idx[r])])).convert("RGB"))
+            y, x, m = (int(v) for v in prm[r, :3])
+            ref = full[y:y + 32, x:x + 32]
+            if m:
+                ref = ref[:, ::-1]
+            assert np.array_equal(pix[r].numpy(), ref)
