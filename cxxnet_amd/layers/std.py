@@ -310,13 +310,21 @@ class ConvolutionLayer(Layer):
     def forward(self, is_train, nodes_in, nodes_out):
         self.geo.N = nodes_in[0].data.shape[0]
         bias = self.b.w if self.b is not None else None
+        # few-channel first layers (VGG conv1_1, GoogLeNet conv1): the direct kernel pads on the
+        # fly; the zero-bordered copy is then built by the weight-gradient pass that needs it
+        if ops.gemm.conv_forward_fewc(nodes_in[0].data, self.w.wb, bias, nodes_out[0].data, self.geo,
+                                      relu=self.fuse_relu):
+            self._xpad_stale = True
+            return
         x, geo = self._padded(nodes_in[0].data, True)
+        self._xpad_stale = False
         ops.conv_forward(x, self.w.wb, bias, nodes_out[0].data, geo, relu=self.fuse_relu)
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
         x, dy = nodes_in[0].data, nodes_out[0].data
         self.geo.N = x.shape[0]
-        xw, geo = self._padded(x, False)
+        xw, geo = self._padded(x, getattr(self, "_xpad_stale", False))
+        self._xpad_stale = False
         ops.conv_backward_weight(xw, dy, self.w.g, geo)
         if self.bias_done:  # summed by the max-pool behind this conv (NeuralNet._fuse_pool_bias)
             self.bias_done = False

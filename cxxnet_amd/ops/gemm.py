@@ -560,6 +560,29 @@ def _wgrad_pad_buf(cout, kr, device):
     return buf
 
 
+_FEWC = os.environ.get("CXXNET_FEWC", "1") != "0"
+
+
+def fewc_ok(x, g: ConvGeom) -> bool:
+    """Few-channel first-layer forward kernel (conv_fewc.hip): 4-channel NHWC input, one group,
+    16..128 output channels (multiple of 16), at most 64 taps, any stride / padding."""
+    return (_FEWC and _native_t(x) and g.C == 4 and g.groups == 1 and g.Cout % 16 == 0 and g.Cout <= 128
+            and g.KH * g.KW <= 64 and g.pad_y == g.pad_x and x.is_contiguous() and g.W == x.shape[2])
+
+
+def conv_forward_fewc(x, w, bias, y, g: ConvGeom, relu=False) -> bool:
+    """y = relu?(conv(x, w) + bias) on the few-channel kernel; False when it does not serve the shape."""
+    if not fewc_ok(x, g):
+        return False
+    rc = native.kernels().cxn_conv_fewc_fwd(x.data_ptr(), w.data_ptr(), bias.data_ptr() if bias is not None else None,
+                                           y.data_ptr(), g.N, g.H, g.W, g.Ho, g.Wo, g.Cout, g.KH, g.KW, g.stride,
+                                           g.pad_y, _pix(y), int(relu), _stream())
+    if rc == -1:
+        return False
+    native.check(rc, "conv_fewc_fwd")
+    return True
+
+
 def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
     """y = conv(x, w) + bias (optionally relu).  x/y NHWC."""
     if not _native_t(x):

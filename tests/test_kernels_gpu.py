@@ -795,3 +795,35 @@ def test_dgrad_fused_bias_grads_match_unfused(monkeypatch):
     for a, b in zip(*grads):
         assert b.abs().max().item() > 0
         assert relerr(a, b) < 1e-2, relerr(a, b)
+
+
+FEWC_CASES = [
+    # N, H, W, Cout, K, stride, pad, relu, bias, ldc_extra
+    (2, 224, 224, 64, 3, 1, 1, True, True, 0),    # VGG conv1_1
+    (2, 224, 224, 64, 7, 2, 3, True, True, 0),    # GoogLeNet conv1
+    (3, 37, 53, 48, 5, 1, 2, False, True, 0),     # ragged width (last 16-pixel column partial)
+    (2, 300, 300, 16, 3, 2, 0, True, False, 0),   # Wo > 256: two passes; no bias
+    (1, 19, 23, 128, 8, 3, 1, True, True, 0),     # even kernel, stride 3, 128 channels
+    (2, 33, 31, 32, 3, 1, 1, True, True, 64),     # channel slice of a wider buffer (ldc 96)
+]
+
+
+@pytest.mark.parametrize("case", FEWC_CASES)
+def test_conv_fewc_forward(case):
+    """Few-channel first-layer kernel (conv_fewc.hip) against the fp32 torch conv."""
+    N, H, W, Cout, K, s, p, relu, use_b, extra = case
+    geo = _geom(N, 4, H, W, Cout, K, s, p, 1)
+    x = rnd(N, H, W, 4, seed=1)
+    w = rnd(Cout, K, K, 4, scale=0.05, seed=2)
+    b = rnd(Cout, scale=0.1, seed=3) if use_b else None
+    y_ref = torch.empty(N, geo.Ho, geo.Wo, Cout)
+    ops.conv_forward(x, w, b, y_ref, geo, relu=relu)
+    full = torch.full((N, geo.Ho, geo.Wo, Cout + extra), 7.0, dtype=torch.bfloat16, device=DEV)
+    y = full[..., :Cout]
+    ran = ops.gemm.conv_forward_fewc(x.to(DEV, torch.bfloat16), w.to(DEV, torch.bfloat16),
+                                     b.to(DEV) if b is not None else None, y, geo, relu=relu)
+    torch.cuda.synchronize()
+    assert ran, "the few-channel kernel did not take the shape"
+    assert relerr(y, y_ref) < 2e-2
+    if extra:
+        assert bool((full[..., Cout:] == 7.0).all()), "wrote outside its channel slice"
