@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--model", default="alexnet", choices=["alexnet", "vgg16"])
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--no-lib", action="store_true")
+    ap.add_argument("--fc-only", action="store_true")
     a = ap.parse_args()
     global N, CONVS, FCS
     if a.model == "vgg16":
@@ -57,7 +58,7 @@ def main():
         N = a.batch
     bf = torch.bfloat16
     dev = "cuda"
-    for name, (C, H, Cout, K, s, p, g) in CONVS.items():
+    for name, (C, H, Cout, K, s, p, g) in ({} if a.fc_only else CONVS).items():
         Ho, Wo = conv_out_size(H, H, K, K, s, p, p)
         geo = ConvGeom(N, H, H, C, Ho, Wo, Cout, K, K, s, p, p, g)
         x = torch.randn(N, H, H, C, device=dev).to(bf)

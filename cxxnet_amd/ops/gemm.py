@@ -732,7 +732,8 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
             return reg_run(reg_default(), o)
         key = ("cws", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
         return reg_run(_tuned_tile(key, reg_run, o, reg_default, cands=_wgrad_cands(kd, g.cg_out, g.groups, P)), o)
-    if _DET["on"]:
+    rowrun = va != 8 and rowrun_ok(g)
+    if _DET["on"] and not (rowrun and cg % va):
         # one fp32 slab per K slice, summed in slice order into dw: bitwise reproducible
         tile = _pick(WGRAD_TILES, kd, g.cg_out, g.groups, min_blocks=1)
         split = _effective_split(P, _auto_split(kd, g.cg_out, g.groups, P, tile))
@@ -757,7 +758,7 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
         # wins shapes where it loses inside the step (conv2/conv3 above)
         if run(_tuned_tile(key, run, dw, lambda: REG, extra=(REG,), tune=_CW_TUNE), dw):
             return
-    if va != 8 and rowrun_ok(g) and (_use("cwr") or g.C % 4):
+    if rowrun and (_use("cwr") or g.C % 4 or _DET["on"]):
         # few input channels (conv1): the KW*C im2col rows of one kernel row are one contiguous run
         # of x, so the transposed gather reads each run as Cg = roundup(KW*C, 8) "channels" of a
         # 1-wide kernel; the result lands in a row-padded fp32 buffer whose pad columns are dropped
@@ -770,6 +771,8 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
         def run(t, o):
             bm, bn = GLDS_TILES[t]
             split = max(1, min(2 * NUM_CU // max(_cdiv(kr, bm) * _cdiv(g.Cout, bn), 1), _cdiv(P, 64) // 16))
+            if _DET["on"]:  # one K slice: each output is one atomic add onto zero, bitwise reproducible
+                split = 1
             return _glds(Ar, B, GL_MNG, GL_MN, o, 0, kr, epi=EPI_F32_ATOMIC_G, ksplit=split, tile=t)
         key = ("cwr", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride)
         ws.zero_()

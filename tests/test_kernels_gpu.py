@@ -422,6 +422,27 @@ def test_conv1_three_channel_row_runs(N):
     assert relerr(dw.permute(0, 3, 1, 2) - 0.25, dw_ref) < 1e-2
 
 
+def test_conv1_three_channel_row_runs_deterministic():
+    """Deterministic mode (left on by a trainer with deterministic = 1) keeps the 3-channel
+    row-run weight-gradient: one K slice, bitwise equal on a repeat, and still exact."""
+    from cxxnet_amd.ops import gemm as G
+    G.set_deterministic(True)
+    test_conv1_three_channel_row_runs(2)
+    torch.manual_seed(5)
+    N = 2
+    x = torch.zeros(N, 227, 228, 3, device=DEV, dtype=torch.bfloat16)
+    x[:, :, :227] = torch.randn(N, 227, 227, 3, device=DEV).to(torch.bfloat16)
+    dy = torch.randn(N, 55, 55, 96, device=DEV).to(torch.bfloat16)
+    g = ConvGeom(N, 227, 228, 3, 55, 55, 96, 11, 11, 4, 0, 0, 1)
+    outs = []
+    for _ in range(2):
+        dw = torch.zeros(96, 11, 11, 3, device=DEV)
+        ops.conv_backward_weight(x, dy, dw, g)
+        outs.append(dw)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_alexnet_input_node_three_channels(monkeypatch):
     """The GPU net keeps AlexNet's input at 3 channels on 228-pixel rows and a training step
     matches the 4-channel layout's (CXXNET_CONV1_C3=0) loss and conv1 weight-gradient."""

@@ -3,8 +3,8 @@
 set -o pipefail
 OUT=gpurun_out/full
 mkdir -p $OUT
-timeout -k 10 1000 python -u -m pytest tests/ -q -m gpu --timeout 150 --timeout-method thread -p no:cacheprovider > $OUT/tests.log 2>&1
-rc=$?; echo "tests rc=$rc"; tail -15 $OUT/tests.log | grep -E "passed|failed|FAILED|error" | head -20
+timeout -k 10 1000 python -u -m pytest tests/ -q -rfE -m gpu --timeout 150 --timeout-method thread -p no:cacheprovider > $OUT/tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -40 $OUT/tests.log | grep -E "passed|failed|FAILED|error" | head -20
 if [ $rc -gt 1 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 || { echo smoke failed; tail -20 $OUT/smoke.log; exit 1; }
 tail -1 $OUT/smoke.log
