@@ -40,6 +40,20 @@ def run_fc(layer, kind, iters):
 
 def run(name, iters=5):
     n = N
+    if name.startswith("conv1c3_"):  # AlexNet conv1 on the 3-channel 228-pixel-row input node
+        kind = name.split("_")[1]
+        geo = ConvGeom(n, 227, 228, 3, 55, 55, 96, 11, 11, 4, 0, 0, 1)
+        x = torch.randn(n, 227, 228, 3, device="cuda").to(torch.bfloat16)
+        w = (torch.randn(96, 11, 11, 3, device="cuda") * 0.05).to(torch.bfloat16)
+        y = torch.randn(n, 55, 55, 96, device="cuda").to(torch.bfloat16)
+        dw = torch.zeros(96, 11, 11, 3, device="cuda")
+        for _ in range(iters):
+            if kind == "fwd":
+                ops.conv_forward(x, w, None, y, geo, relu=True)
+            else:
+                ops.conv_backward_weight(x, y, dw, geo)
+        torch.cuda.synchronize()
+        return
     if name.startswith("conv:"):  # generic: conv:C:H:Cout:K:stride:pad:groups:N_kind
         layer, kind = name.rsplit("_", 1)
         C, H, Cout, K, s, p, g, n = (int(v) for v in layer.split(":")[1:])

@@ -310,10 +310,10 @@ class ConvolutionLayer(Layer):
     def forward(self, is_train, nodes_in, nodes_out):
         self.geo.N = nodes_in[0].data.shape[0]
         bias = self.b.w if self.b is not None else None
-        # few-channel first layers (VGG conv1_1, GoogLeNet conv1): the direct kernel pads on the
+        # few-channel stride-1 first layers (VGG conv1_1): the direct kernel pads on the
         # fly; the zero-bordered copy is then built by the weight-gradient pass that needs it
-        if ops.gemm.conv_forward_fewc(nodes_in[0].data, self.w.wb, bias, nodes_out[0].data, self.geo,
-                                      relu=self.fuse_relu):
+        if ops.gemm.fewc_preferred(self.geo) and ops.gemm.conv_forward_fewc(
+                nodes_in[0].data, self.w.wb, bias, nodes_out[0].data, self.geo, relu=self.fuse_relu):
             self._xpad_stale = True
             return
         x, geo = self._padded(nodes_in[0].data, True)

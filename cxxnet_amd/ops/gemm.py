@@ -561,6 +561,9 @@ def _wgrad_pad_buf(cout, kr, device):
 
 
 _FEWC = os.environ.get("CXXNET_FEWC", "1") != "0"
+# direct row-run forward (conv_rowrun.hip: input rows staged once per 4 output rows) for the
+# few-channel pad-0 first layer (AlexNet conv1) instead of the K_ROWGATHER GEMM
+_ROWRUN_DIRECT = os.environ.get("CXXNET_ROWRUN_DIRECT", "1") != "0"
 
 
 def fewc_ok(x, g: ConvGeom) -> bool:
@@ -568,6 +571,13 @@ def fewc_ok(x, g: ConvGeom) -> bool:
     16..128 output channels (multiple of 16), at most 64 taps, any stride / padding."""
     return (_FEWC and _native_t(x) and g.C == 4 and g.groups == 1 and g.Cout % 16 == 0 and g.Cout <= 128
             and g.KH * g.KW <= 64 and g.pad_y == g.pad_x and x.is_contiguous() and g.W == x.shape[2])
+
+
+def fewc_preferred(g: ConvGeom) -> bool:
+    """Where the few-channel kernel beats the GEMM inside the training step: stride 1 (VGG-16
+    conv1_1: 9.47 -> 9.44 ms/step); on GoogLeNet's 7x7 / 2 conv1 it lost, 5.78 -> 5.90 ms
+    (profiles/r3_ab_fewc.jsonl)."""
+    return g.stride == 1
 
 
 def conv_forward_fewc(x, w, bias, y, g: ConvGeom, relu=False) -> bool:
@@ -618,6 +628,14 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
         # few input channels (conv1: 11x11 taps of 4 channels): each kernel row's KW*C
         # elements are contiguous in NHWC; the GEMM reads them as zero-padded runs
         wp, lp = _row_padded_weights(w, g)
+        if _ROWRUN_DIRECT and x.is_contiguous() and y.shape[-1] == _pix(y):
+            rc = native.kernels().cxn_conv_rowrun_fwd(
+                x.data_ptr(), x.numel() * x.element_size(), wp.data_ptr(), bias.data_ptr() if bias is not None else None,
+                y.data_ptr(), g.N, g.H, g.W, g.C, g.Ho, g.Wo, g.Cout, g.KH, lp, g.stride, _pix(y), int(relu), _stream())
+            if rc == 0:
+                return
+            if rc != -1:
+                native.check(rc, "conv_rowrun_fwd")
         kr = g.KH * lp
         Ar = _op(wp, 0, kr, g.Cout, kr)
         Br = _op(x, 0, 0, g.N * g.Ho * g.Wo, kr, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW,

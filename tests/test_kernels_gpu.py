@@ -422,6 +422,34 @@ def test_conv1_three_channel_row_runs(N):
     assert relerr(dw.permute(0, 3, 1, 2) - 0.25, dw_ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W,C,Cout,K,S,relu", [(2, 227, 228, 3, 96, 11, 4, True), (3, 227, 228, 3, 96, 11, 4, False),
+                                                   (2, 35, 35, 4, 32, 5, 2, True), (2, 43, 44, 3, 128, 7, 4, False),
+                                                   (5, 30, 32, 3, 64, 3, 4, True)])
+def test_conv_rowrun_direct_forward(N, H, W, C, Cout, K, S, relu):
+    """conv_rowrun.hip (input rows staged once per 4 output rows, LDS-DMA double buffer) called
+    directly -- it must serve the shape (rc 0, no GEMM fallback) -- against fp32 torch."""
+    import torch.nn.functional as F
+    from cxxnet_amd import native
+    from cxxnet_amd.ops import gemm as G
+    torch.manual_seed(N * 7 + K)
+    x = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(Cout, K, K, C, device=DEV) * 0.05).to(torch.bfloat16)
+    b = torch.randn(Cout, device=DEV)
+    Ho, Wo = (H - K) // S + 1, (W - K) // S + 1
+    g = ConvGeom(N, H, W, C, Ho, Wo, Cout, K, K, S, 0, 0, 1)
+    wp, lp = G._row_padded_weights(w, g)
+    y = torch.full((N, Ho, Wo, Cout), 7.0, device=DEV, dtype=torch.bfloat16)
+    rc = native.kernels().cxn_conv_rowrun_fwd(x.data_ptr(), x.numel() * 2, wp.data_ptr(), b.data_ptr(), y.data_ptr(),
+                                              N, H, W, C, Ho, Wo, Cout, K, lp, S, Cout, int(relu),
+                                              torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, stride=S)
+    if relu:
+        ref = ref.clamp_min(0)
+    assert relerr(y.permute(0, 3, 1, 2), ref) < 1e-2
+
+
 def test_conv1_three_channel_row_runs_deterministic():
     """Deterministic mode (left on by a trainer with deterministic = 1) keeps the 3-channel
     row-run weight-gradient: one K slice, bitwise equal on a repeat, and still exact."""
