@@ -75,6 +75,7 @@ _SIGS = {
                       _I, _I, _I, _I, _I, _L, _P, _P, _L, _I, _P],
     "cxn_pad_rows": [_P, _P, _L, _I, _I, _P],
     "cxn_conv_rowrun_fwd": [_P, _L, _P, _P, _P] + [_I] * 12 + [_P],
+    "cxn_conv_rowrun_wgrad": [_P, _L, _P, _L, _P] + [_I] * 10 + [_P],
     "cxn_conv_fewc_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "cxn_chan_reduce": [_P, _P, _P, _P, _L, _I, _I, _P],
     "cxn_bn_stats": [_P, _P, _P, _P, _L, _I, _F, _P],

@@ -1,5 +1,5 @@
 #!/bin/bash
-# 8-wave direct row-run conv1 forward: numerics, AlexNet A/B, kernel profile
+# direct row-run conv1 forward + weight-grad: numerics, AlexNet A/B, kernel profile
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/r3h
