@@ -242,8 +242,11 @@ conv_rowrun_wgrad(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__re
                   int XB, int ndma_x, int DB, int ndma_d) {
   constexpr int COUT = 32 * CFH;
   constexpr int NWV = NT / 64;
-  constexpr int DCH = COUT / 8 + 1;     // 16-byte chunks per dy slot (one pad chunk)
-  constexpr int DPB = DCH * 16;         // dy slot pitch (bytes)
+  // dy slot pitch: 32 * odd bytes (COUT/8 data chunks + 2), so the 8 consecutive slots a 32-lane
+  // half reads land on 8 distinct 8-dword bank ranges (conflict-free transposed reads)
+  constexpr int DCH = COUT / 8 + 2;
+  constexpr int DPB = DCH * 16;
+  static_assert((DPB / 32) % 2 == 1, "slot pitch 32 * odd bytes");
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int pitch = W * C * 2;
   const int pxs = S * C * 2;
@@ -279,7 +282,7 @@ conv_rowrun_wgrad(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__re
       const int r = slot / WS, wo = slot - r * WS;
       const int ho = grp * WR + r;
       uint32_t o = 0x80000000u;
-      if (live && q < ndma_d && part < DCH - 1 && wo < Wo && r < WR && ho < Ho)
+      if (live && q < ndma_d && part < DCH - 2 && wo < Wo && r < WR && ho < Ho)
         o = static_cast<uint32_t>((((static_cast<long>(n) * Ho + ho) * Wo + wo) * COUT) * 2 + part * 16);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rd, (lds_void *)(q < ndma_d ? dd + q * 1024 : scratch), 16, o, 0, 0, 0);
     }
@@ -298,8 +301,11 @@ conv_rowrun_wgrad(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__re
     const int kh = quad / qpr, jj = 4 * (quad - kh * qpr);
     qoff[kf] = kh * pitch + jj * 2;
   }
-  // per k-step s (32 slots = half an output row): the lane's pixel rows 8*g4 + q4 (lo) and +4 (hi)
-  const int w_lo = 8 * g4 + q4;
+  // per k-step s (32 slots = half an output row) the lane's 8 K values are pixels 4*g4 + q4 (lo
+  // read) and + 16 (hi read): each read instruction's 32-lane half takes 8 consecutive pixels,
+  // whose x runs (24-byte steps) span < 256 bytes (shared words broadcast) and whose dy slots
+  // fall on distinct banks
+  const int w_lo = 4 * g4 + q4;
   f32x4 acc[CFH][KF];
 #pragma unroll
   for (int cf = 0; cf < CFH; ++cf)
@@ -317,9 +323,9 @@ conv_rowrun_wgrad(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__re
       bf16x8 a[CFH], b[KF];
       const int r = s / (WS / 32), w0 = (s % (WS / 32)) * 32 + w_lo;
       const char *xlo = sx + r * S * pitch + w0 * pxs;
-      const char *xhi = xlo + 4 * pxs;
+      const char *xhi = xlo + 16 * pxs;
       const char *dlo = sd + (s * 32 + w_lo) * DPB + 8 * p4;
-      const char *dhi = dlo + 4 * DPB;
+      const char *dhi = dlo + 16 * DPB;
       typedef short s16x8 __attribute__((ext_vector_type(8)));
 #pragma unroll
       for (int cf = 0; cf < CFH; ++cf) {
@@ -366,7 +372,7 @@ int launch_wgrad(const bf16_t *x, long x_bytes, const bf16_t *dy, long dy_bytes,
   const long span = static_cast<long>(S * (WR - 1) + KH) * W * C * 2 + 16;
   const int ndma_x = static_cast<int>((span + 1023) / 1024);
   const int XB = ndma_x * 1024;
-  const int dch = 32 * CFH / 8 + 1;
+  const int dch = 32 * CFH / 8 + 2;
   const int ndma_d = (WR * WS * dch + 63) / 64;
   const int DB = ndma_d * 1024;
   const long lds = 3L * (XB + DB) + 1024;
