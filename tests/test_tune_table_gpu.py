@@ -113,6 +113,8 @@ def test_shipped_table_entry(op, sig):
         if op == "cr":  # key: N, H, W, C, Cout, KH, KW, stride (no pad, one group)
             sig = sig + (0, 0, 1)
         err = check_conv(op, sig)
+    elif op == "cwr":  # row-run weight-grad (few channels, conv1): key as "cr"
+        err = check_conv("cw", sig + (0, 0, 1))
     elif op == "fc":
         _, nout, B, nin, _ = sig  # amode, a.rows = nout, b.rows = B, kdim = nin, ldc
         err = check_fc("fc", nin, nout, B)
