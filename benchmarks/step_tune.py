@@ -88,7 +88,7 @@ def main():
             continue
         if op in ("cf", "cd", "cr", "fc"):
             cands = list(SHORT if a.short else KK) + ([G.REG] if op in ("cf", "cd") else [])
-        elif op in ("fw", "fws"):
+        elif op in ("fw", "fws", "cwr"):
             cands = list(MM)
         elif op == "cws":
             N, H, W, C, Co, KH, KW, st, py, px, g = (int(v) for v in key.split("|")[1:])
