@@ -20,7 +20,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 KK = (0, 1, 2, 7, 10, 15, 20, 21, 25, 30, 31, 33, 34, 35, 36, 37, 38, 39, 50, 51, 70, 71, 72, 73, 74, 75, 76, 77,
-      78, 79, 80, 81)
+      78, 79, 80, 81, 82, 83)
 MM = (1, 2, 13, 17, 23, 36, 40, 41)
 SHORT = (0, 1, 2, 7, 10, 15, 34, 37, 38, 75, 76, 77, 78, 79, 80, 81)
 
@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--short", action="store_true", help="shortlist of LDS-DMA tiles (models with many signatures)")
     ap.add_argument("--ops", default="", help="only these op classes (comma list, e.g. fw)")
+    ap.add_argument("--cands", default="", help="only these candidate tiles (comma list; the current entry is kept)")
     a = ap.parse_args()
     from cxxnet_amd.io.data import DataBatch
     from cxxnet_amd.models import load_conf
@@ -96,6 +97,8 @@ def main():
             cands = list(G._wgrad_cands(KH * KW * (C // g), Co // g, g, N * Ho * Wo))
         else:
             continue
+        if a.cands:
+            cands = [int(t) for t in a.cands.split(",")]
         cur = G._TUNE[key]
         if cur not in cands:
             cands.append(cur)

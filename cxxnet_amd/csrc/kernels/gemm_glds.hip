@@ -667,6 +667,7 @@ void launch_pp(const GOperand &A, const GOperand &B, const GEpi &E, int groups, 
     CXG_TP(73, 160, 128, 1, 4, 2, 0) CXG_TP(74, 128, 96, 2, 2, 2, 0) CXG_TP(75, 64, 96, 2, 2, 2, 0)       \
     CXG_T(76, 32, 128, 1, 4, 2) CXG_T(77, 32, 64, 1, 4, 3) CXG_T(78, 32, 256, 1, 4, 2)                    \
     CXG_TC(79, 64, 48, 128, 1, 4, 2) CXG_TC(80, 64, 48, 256, 1, 4, 2) CXG_TC(81, 64, 48, 64, 1, 4, 3)     \
+    CXG_TP(82, 256, 192, 2, 4, 2, 3) CXG_TP(83, 192, 256, 2, 4, 2, 3)                                     \
     default: return -1;                                                                                   \
   }
 #define CXG_MK_TILES  /* A MN-major (BM = 128), B K-major */                                              \

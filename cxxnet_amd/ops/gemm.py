@@ -152,6 +152,9 @@ GLDS_TILES = {0: (128, 256), 1: (128, 128), 2: (128, 128), 4: (192, 256), 5: (64
               76: (32, 128), 77: (32, 64), 78: (32, 256),
               # 48 computed rows on 64 staged (AlexNet conv2's data-gradient: 48 channels per group)
               79: (48, 128), 80: (48, 256), 81: (48, 64),
+              # 8-wave 3/4-width tiles against wave quantisation: AlexNet conv3's data-gradient has
+              # 169 256x256 tiles for 256 CUs, 226 of 256x192
+              82: (256, 192), 83: (192, 256),
               # 8-phase 256x256 pipeline (gemm_8p.hip): 90 = two barriers per phase, 91 = one
               90: (256, 256), 91: (256, 256),
               # one wave per SIMD, software-pipelined (gemm_4w.hip): 92/93 256x256, 94 128x256, 95 256x128
@@ -176,7 +179,7 @@ _glds_cfg = {"on": os.environ.get("CXXNET_GEMM_GLDS", "1") != "0",
 # 128x256 / 64x256 tiles and the pipelined variants (30-41) win conv2/conv3 forward, fc6 forward
 # and several VGG shapes (profiles/r2_sweep_tiles.jsonl).
 GLDS_CANDS = (1, 7, 10, 15, 2, 0, 13, 17, 21, 25, 30, 31, 34, 37, 38, 39, 40, 41, 50, 51, 72, 76, 77, 78, 79, 80,
-              81)
+              81, 82, 83)
 # conv weight-grad shapes missing from the shipped table are timed on first use too (else the
 # register kernel runs them)
 _CW_TUNE = os.environ.get("CXXNET_CW_TUNE", "0") == "1"
