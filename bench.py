@@ -22,8 +22,9 @@ imgbin/img pipeline hands over after JPEG decode and crop -- normalised (mean
 subtraction) and converted to NHWC bf16 by the fused augment kernel inside the step;
 --input f32 feeds float NCHW batches instead.  A step is the full training step: input
 normalisation/layout conversion, forward, loss gradient, backward, gradient reduction
-(N > 1: bucketed fp32 reduce-scatter overlapped with backward, sliced optimizer, bf16
-weight all-gather; see cxxnet_amd/parallel/dp.py) and the fused SGD-momentum update.
+(N > 1: bucketed fp32 all-reduce overlapped with backward, per-bucket optimizer on a side
+stream; --dp-mode shard: reduce-scatter, sliced optimizer, bf16 weight all-gather; see
+cxxnet_amd/parallel/dp.py) and the fused SGD-momentum update.
 """
 import argparse
 import json
@@ -59,7 +60,8 @@ def _args(argv=None):
                          "(strong scaling); the 1-GPU AlexNet / GoogLeNet steps are GPU-bound, graph replay measured "
                          "-0.4%%/+0.5%% (profiles/r16_graph_ab.jsonl)")
     ap.add_argument("--dp-mode", default="auto", choices=["auto", "shard", "allreduce"],
-                    help="gradient reduction: auto = sharded reduce-scatter/all-gather on the GPU")
+                    help="gradient reduction: auto = fp32 all-reduce (shard: reduce-scatter, sliced update, "
+                         "bf16 all-gather)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
                     help="cpu: gloo ranks on the host (test hook for the launcher and the DP path)")
