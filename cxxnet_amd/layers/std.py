@@ -110,6 +110,28 @@ class FullConnectLayer(Layer):
         lr, wd, mom, clip = upd.hyper(spec, self.ctx.epoch)
         a = upd.arena
         m = a.m1[spec.offset:spec.offset + spec.numel].view(spec.shape)
+        side = getattr(self.ctx, "fc_side", None)
+        if side is not None and xw is None:
+            # side stream: x is copied aside (its buffer receives the data gradient), the data
+            # gradient reads the old shadow weights on the main stream, then the fused step runs
+            # on `side` (joined at the end of the backward pass, NeuralNet.backprop)
+            if getattr(self, "_xs", None) is None or self._xs.shape != x.shape:
+                self._xs = torch.empty_like(x)
+            self._xs.copy_(x)
+            if prop_grad:
+                ops.fc_backward_data(dy, spec.wb, nodes_in[0].gmat(), mask_relu=self.grad_mask_relu)
+            ready = torch.cuda.Event()
+            ready.record()
+            side.wait_event(ready)
+            with torch.cuda.stream(side):
+                ok = ops.fc_backward_weight_sgd(self._xs, dy, spec.w, m, spec.wb, lr, wd, mom, clip)
+            self.ctx.fc_side_used = True
+            if ok:
+                upd.fused_offsets.add(spec.offset)
+            else:
+                torch.cuda.current_stream().wait_stream(side)
+                ops.fc_backward_weight(self._xs, dy, spec.g, overwrite=True)
+            return True
         gx = None
         if prop_grad:
             if self._dx is None or self._dx.shape[0] < x.shape[0] or self._dx.shape[1] != x.shape[1]:

@@ -501,6 +501,10 @@ class NeuralNet:
             conv_weight_flip_multi(flips)
             self.ctx.flipped = seen
         side = self._bias_stream() if defer and hook is None else None
+        # fused fc SGD steps (memory-bound: w / m / shadow streams) on a side stream, overlapping
+        # the compute-bound conv backward below them; joined at the end of the pass
+        self.ctx.fc_side = self._fc_side_stream() if self.ctx.is_gpu and hook is None else None
+        self.ctx.fc_side_used = False
         with _BatchView(self):
             for i in range(len(self.connections) - 1, -1, -1):
                 conn = self.connections[i]
@@ -518,6 +522,9 @@ class NeuralNet:
                     torch.cuda.current_stream().wait_stream(side)
                 else:
                     self._flush_bias(None)
+            if self.ctx.fc_side_used:
+                torch.cuda.current_stream().wait_stream(self.ctx.fc_side)
+            self.ctx.fc_side = None
         self.ctx.deferred_bias = None
         self.ctx.flipped = None
 
@@ -533,6 +540,20 @@ class NeuralNet:
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(device=self.device)
         return self._side
+
+    def _fc_side_stream(self):
+        """Side stream of the fc weight-gradient GEMMs with the fused SGD step
+        (CXXNET_FC_SGD_SIDE=1): they stream each fc layer's fp32 master, momentum and bf16
+        shadow (18 B / parameter, AlexNet fc6: 680 MB) and so are HBM-bound, while the conv
+        backward that follows is MFMA-bound.  None (the default) keeps them on the main stream:
+        interleaved A/B on one MI355X, AlexNet b256 2.320 -> 2.375 ms and VGG-16 b64 9.40 ->
+        9.41 ms with the side stream (profiles/r3_ab_fc_sgd_side.jsonl) -- the concurrent HBM
+        stream slows the GEMMs it overlaps by more than it hides.  Not under HIP-graph capture."""
+        if os.environ.get("CXXNET_FC_SGD_SIDE", "0") != "1" or torch.cuda.is_current_stream_capturing():
+            return None
+        if getattr(self, "_fc_side", None) is None:
+            self._fc_side = torch.cuda.Stream(device=self.device)
+        return self._fc_side
 
     def _pending_bias_bytes(self) -> int:
         q = self.ctx.deferred_bias

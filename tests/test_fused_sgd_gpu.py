@@ -76,3 +76,22 @@ def test_fused_fc_sgd_is_bitwise_the_unfused_step(extra):
 def test_fusion_off_for_other_updaters():
     tr, *_ = _train(True, 1, [("updater", "nag")])
     assert tr._sgd_fuse_target() is None
+
+
+def test_fused_fc_sgd_on_side_stream_is_bitwise(monkeypatch):
+    """CXXNET_FC_SGD_SIDE=1: the fused fc steps run on a side stream overlapping the backward
+    below them (x copied aside, data gradient first on the main stream, joined at the end of the
+    pass) and give bitwise the main-stream result."""
+    extra = [("eta", "0.05"), ("momentum", "0.9"), ("wd", "0.0005")]
+    saved = trainer_mod._FUSE_FC_SGD
+    try:
+        monkeypatch.setenv("CXXNET_FC_SGD_SIDE", "1")
+        tr, w1, m1, b1 = _train(True, 5, extra)
+        assert getattr(tr.net, "_fc_side", None) is not None, "the side stream was not used"
+        monkeypatch.setenv("CXXNET_FC_SGD_SIDE", "0")
+        _, w0, m0, b0 = _train(True, 5, extra)
+    finally:
+        trainer_mod._FUSE_FC_SGD = saved
+    assert torch.equal(w1, w0), (w1 - w0).abs().max().item()
+    assert torch.equal(m1, m0)
+    assert torch.equal(b1, b0)
