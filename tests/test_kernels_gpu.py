@@ -423,6 +423,7 @@ def test_conv1_three_channel_row_runs(N):
 
 
 @pytest.mark.parametrize("N,H,W,C,Cout,K,S,relu", [(2, 227, 228, 3, 96, 11, 4, True), (3, 227, 228, 3, 96, 11, 4, False),
+                                                   (40, 227, 228, 3, 96, 11, 4, True),  # 2-3 work items per block
                                                    (2, 35, 35, 4, 32, 5, 2, True), (2, 43, 44, 3, 128, 7, 4, False),
                                                    (5, 30, 32, 3, 64, 3, 4, True)])
 def test_conv_rowrun_direct_forward(N, H, W, C, Cout, K, S, relu):
@@ -451,6 +452,7 @@ def test_conv_rowrun_direct_forward(N, H, W, C, Cout, K, S, relu):
 
 
 @pytest.mark.parametrize("N,H,W,C,Cout,K,S", [(2, 227, 228, 3, 96, 11, 4), (16, 227, 228, 3, 96, 11, 4),
+                                               (40, 227, 228, 3, 96, 11, 4),  # several work items per block
                                                (3, 35, 36, 4, 64, 7, 2), (2, 43, 44, 3, 128, 7, 4),
                                                (5, 30, 32, 3, 32, 5, 4)])
 def test_conv_rowrun_direct_wgrad(N, H, W, C, Cout, K, S):
