@@ -21,6 +21,7 @@
 //     this one's MFMAs (the tap offset is arithmetic, no LDS table on the dependency chain);
 //   * epilogue: bias + relu in fp32 -> bf16, transposed through LDS (the item's input buffer,
 //     free by then) so each pixel's channels leave as 16-byte chunks.
+#include <cstdlib>
 #include "common.h"
 
 namespace {
@@ -35,11 +36,24 @@ __device__ __forceinline__ void wave_lds_handoff() {
   __builtin_amdgcn_wave_barrier();
 }
 
+template <int N_>
+__device__ __forceinline__ void vm_wait_le() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory"); }
+__device__ __forceinline__ void vm_wait(int n) {  // s_waitcnt vmcnt(n), n uniform, 0..15
+  switch (n) {
+    case 0: vm_wait_le<0>(); break;  case 1: vm_wait_le<1>(); break;  case 2: vm_wait_le<2>(); break;
+    case 3: vm_wait_le<3>(); break;  case 4: vm_wait_le<4>(); break;  case 5: vm_wait_le<5>(); break;
+    case 6: vm_wait_le<6>(); break;  case 7: vm_wait_le<7>(); break;  case 8: vm_wait_le<8>(); break;
+    case 9: vm_wait_le<9>(); break;  case 10: vm_wait_le<10>(); break; case 11: vm_wait_le<11>(); break;
+    case 12: vm_wait_le<12>(); break; case 13: vm_wait_le<13>(); break; case 14: vm_wait_le<14>(); break;
+    default: vm_wait_le<15>(); break;
+  }
+}
+
 template <int CFH>  // 16-channel output fragments per wave (Cout = 32 * CFH)
 __global__ void __launch_bounds__(NT, 1)
 conv_rowrun_fwd(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__restrict__ w, const float *__restrict__ bias,
-                bf16_t *__restrict__ y, int N, int H, int W, int C, int Ho, int Wo, int KH, int LP, FastDiv fd_lp, int S,
-                int ldc, int relu, int KS, int XB, int ndma) {
+                bf16_t *__restrict__ y, long y_bytes, int N, int H, int W, int C, int Ho, int Wo, int KH, int LP, FastDiv fd_lp, int S,
+                int ldc, int relu, int KS, int XB, int ndma, int counted) {
   constexpr int COUT = 32 * CFH;
   constexpr int NWV = NT / 64;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
@@ -66,6 +80,7 @@ conv_rowrun_fwd(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__rest
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_void *)(dst + q * 1024), 16, o, 0, 0, 0);
     }
   };
+  const rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(y, (short)0, static_cast<int>(y_bytes), 0x00020000);
   long it = blockIdx.x;
   if (it < items) issue(it, 0);
 
@@ -95,10 +110,16 @@ conv_rowrun_fwd(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__rest
 #pragma unroll
   for (int pf = 0; pf < 4; ++pf) pxo[pf] = row * S * pitch + min(16 * pf + l16, Wo - 1) * pxs;
   int buf = 0;
+  // this wave's epilogue stores of the previous item: every store instruction is issued (masked
+  // stores go to an out-of-range offset), so the count is fixed and the wait below lets them
+  // drain behind the next item's MFMAs (vector-memory operations retire in issue order)
+  constexpr int NPASS = (16 * CFH * 2 + 63) / 64;
+  const int npf = min(4, (Wo + 15) / 16);
+  int nst = 0;
   for (; it < items; it += gridDim.x) {
     const int n = static_cast<int>(it / groups_per_img), grp = static_cast<int>(it - static_cast<long>(n) * groups_per_img);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // span of `it` landed (every wave's DMAs); weights in; last epilogue done
+    vm_wait(counted ? nst : 0);  // this item's span DMAs landed (only the last item's stores may be in flight)
+    __syncthreads();  // ... for every wave; weights in; every wave done with the other buffer
     if (it + gridDim.x < items) issue(it + gridDim.x, buf ^ 1);
     const char *sx = sx0 + buf * XB;
 
@@ -141,8 +162,9 @@ conv_rowrun_fwd(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__rest
     constexpr int SPB = CFH * 32 + 16;  // staging row pitch (bytes)
     char *st = const_cast<char *>(sx) + wave * 16 * SPB;
     const int ho = grp * RG + row;
+    nst = ho < Ho ? npf * NPASS : 0;
     if (ho < Ho) {  // wave-uniform
-      bf16_t *yrow = y + ((static_cast<long>(n) * Ho + ho) * Wo) * static_cast<long>(ldc) + ch * CFH * 16;
+      const long yrow = (((static_cast<long>(n) * Ho + ho) * Wo) * static_cast<long>(ldc) + ch * CFH * 16) * 2;
 #pragma unroll
       for (int pf = 0; pf < 4; ++pf) {
         const int col0 = 16 * pf;
@@ -161,14 +183,15 @@ conv_rowrun_fwd(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__rest
         wave_lds_handoff();
         constexpr int CH = CFH * 2;  // 16-byte chunks per pixel (of this wave's channels)
 #pragma unroll
-        for (int i = 0; i < (16 * CH + 63) / 64; ++i) {
-          const int c = lane + 64 * i;
-          if (c < 16 * CH) {
-            const int px = c / CH, part = c - px * CH;
-            const int wo = col0 + px;
-            const uint4 v = *reinterpret_cast<const uint4 *>(st + px * SPB + part * 16);
-            if (wo < Wo) *reinterpret_cast<uint4 *>(yrow + static_cast<long>(wo) * ldc + part * 8) = v;
-          }
+        for (int i = 0; i < NPASS; ++i) {
+          const int c = min(lane + 64 * i, 16 * CH - 1);
+          const int px = c / CH, part = c - px * CH;
+          const int wo = col0 + px;
+          const uint4 v = *reinterpret_cast<const uint4 *>(st + px * SPB + part * 16);
+          const bool ok = lane + 64 * i < 16 * CH && wo < Wo;
+          const uint32_t off = ok ? static_cast<uint32_t>(yrow + (static_cast<long>(wo) * ldc + part * 8) * 2) : 0x80000000u;
+          typedef int v4i __attribute__((ext_vector_type(4)));
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), ry, off, 0, 0);
         }
         wave_lds_handoff();
       }
@@ -178,9 +201,17 @@ conv_rowrun_fwd(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__rest
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// CXXNET_ROWRUN_COUNTED=0: drain every store of an item before the next one (s_waitcnt vmcnt(0))
+static const int g_counted = [] {
+  const char *e = getenv("CXXNET_ROWRUN_COUNTED");
+  return e ? atoi(e) : 1;
+}();
+
 template <int CFH>
 int launch(const bf16_t *x, long x_bytes, const bf16_t *w, const float *bias, bf16_t *y, int N, int H, int W, int C,
            int Ho, int Wo, int KH, int LP, int S, int ldc, int relu, hipStream_t s) {
+  const long y_bytes = (static_cast<long>(N) * Ho * Wo * ldc) * 2;
+  if (y_bytes >= (1L << 31)) return -1;
   const int K = KH * LP;
   const int KS = (K + 31) / 32;
   const int cout = 32 * CFH;
@@ -198,8 +229,8 @@ int launch(const bf16_t *x, long x_bytes, const bf16_t *w, const float *bias, bf
   }
   const long items = static_cast<long>(N) * ((Ho + RG - 1) / RG);
   const int grid = static_cast<int>(items < 256 ? items : 256);
-  hipLaunchKernelGGL(conv_rowrun_fwd<CFH>, dim3(grid), dim3(NT), static_cast<size_t>(lds), s, x, x_bytes, w, bias, y, N,
-                     H, W, C, Ho, Wo, KH, LP, make_fastdiv(LP), S, ldc, relu, KS, XB, ndma);
+  hipLaunchKernelGGL(conv_rowrun_fwd<CFH>, dim3(grid), dim3(NT), static_cast<size_t>(lds), s, x, x_bytes, w, bias, y, y_bytes, N,
+                     H, W, C, Ho, Wo, KH, LP, make_fastdiv(LP), S, ldc, relu, KS, XB, ndma, g_counted);
   return 0;
 }
 
@@ -221,19 +252,6 @@ int launch(const bf16_t *x, long x_bytes, const bf16_t *w, const float *bias, bf
 // sweep in its accumulators; one fp32 atomic add per element per block at the end.
 constexpr int WR = 2;    // output rows per weight-grad work item
 constexpr int WS = 64;   // pixel slots per output row (Wo <= 64)
-
-template <int N_>
-__device__ __forceinline__ void vm_wait_le() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory"); }
-__device__ __forceinline__ void vm_wait(int n) {  // s_waitcnt vmcnt(n), n uniform, 0..15
-  switch (n) {
-    case 0: vm_wait_le<0>(); break;  case 1: vm_wait_le<1>(); break;  case 2: vm_wait_le<2>(); break;
-    case 3: vm_wait_le<3>(); break;  case 4: vm_wait_le<4>(); break;  case 5: vm_wait_le<5>(); break;
-    case 6: vm_wait_le<6>(); break;  case 7: vm_wait_le<7>(); break;  case 8: vm_wait_le<8>(); break;
-    case 9: vm_wait_le<9>(); break;  case 10: vm_wait_le<10>(); break; case 11: vm_wait_le<11>(); break;
-    case 12: vm_wait_le<12>(); break; case 13: vm_wait_le<13>(); break; case 14: vm_wait_le<14>(); break;
-    default: vm_wait_le<15>(); break;
-  }
-}
 
 template <int CFH, int KF>
 __global__ void __launch_bounds__(NT, 1)
