@@ -20,7 +20,9 @@
 //     reads (b128) and 8 B reads (b64) for 4 x CFH MFMAs, the next k-step's reads issued before
 //     this one's MFMAs (the tap offset is arithmetic, no LDS table on the dependency chain);
 //   * epilogue: bias + relu in fp32 -> bf16, transposed through LDS (the item's input buffer,
-//     free by then) so each pixel's channels leave as 16-byte chunks.
+//     free by then) so each pixel's channels leave as 16-byte buffer stores; every store
+//     instruction is issued (masked lanes store out of range), so the next item waits with a
+//     counted s_waitcnt for its own DMAs only, not for these stores.
 #include <cstdlib>
 #include "common.h"
 
