@@ -15,6 +15,9 @@ device: src/nnet/nnet_impl-inl.hpp:147-155, example/ImageNet/ImageNet.conf:108):
          global batch is 256*N: the per-GPU work of the conf's 1-GPU run, N times over;
   strong the global batch is --batch (256) and each rank takes ceil(256/N) rows, exactly
          the reference's multi-device semantics for the conf as written.
+With the default weak scaling and N > 1 the same run also times the strong configuration
+(ImageNet.conf's global batch of 256 over the N ranks) and reports it as the nested "strong"
+record of the one JSON line (--strong-record 0 skips it).
 
 Data is synthetic 3x227x227 batches resident on the device with random-init weights (no
 dataset / checkpoint on the box).  By default they are uint8 HWC images -- what the
@@ -50,6 +53,10 @@ def _args(argv=None):
     ap.add_argument("--batch", type=int, default=256,
                     help="weak: per-GPU batch; strong: global batch split over the ranks")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--strong-record", type=int, default=1,
+                    help="with --scaling weak and N > 1, also time the conf's own configuration (global "
+                         "batch --batch split over the ranks, strong scaling) and add it as a nested "
+                         "\"strong\" record to the one JSON line")
     ap.add_argument("--model", default="alexnet")
     ap.add_argument("--input", default="u8", choices=["u8", "f32"],
                     help="u8: decoded-image batches (uint8 HWC) normalised on the GPU by the fused augment kernel, "
@@ -100,37 +107,15 @@ def _baseline(model):
         return None
 
 
-def main():
-    a = _args()
-    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        return _spawn(a)
 
+def _measure(a, world, rank, dev, global_batch, local_batch):
+    """Build the trainer at (global_batch, local_batch), run a.warmup untimed steps, then time
+    a.steps steps bracketed by a barrier + device synchronisation; returns the MAX over ranks."""
     import torch
-    if a.device == "cpu":
-        os.environ.setdefault("CXXNET_DIST_BACKEND", "gloo")
+    import torch.distributed as dist
     from cxxnet_amd.models import load_conf
     from cxxnet_amd.nnet import NetTrainer
     from cxxnet_amd.io.data import DataBatch
-    from cxxnet_amd.parallel import init_distributed
-    import torch.distributed as dist
-
-    rank, world = init_distributed()
-    if world != a.gpus:
-        print(f"bench.py: --gpus {a.gpus} but the process group holds {world} rank(s)", file=sys.stderr)
-        return 2
-    if a.device == "gpu":
-        dev = torch.device("cuda", torch.cuda.current_device())
-        torch.cuda.set_device(dev)
-    else:
-        dev = torch.device("cpu")
-        a.input = "f32"
-
-    if a.scaling == "weak":
-        local_batch = a.batch
-        global_batch = a.batch * world
-    else:
-        global_batch = a.batch
-        local_batch = (a.batch + world - 1) // world
     lo = min(rank * local_batch, global_batch)
     my_rows = min(local_batch, global_batch - lo)  # the reference's ceil split: the last rank may hold fewer
 
@@ -186,11 +171,67 @@ def main():
         dist.all_gather(allt, t)
         per_rank = [float(x.item()) for x in allt]
         el = max(per_rank)
+    return el, per_rank, tr, c, h, w, desc
+
+
+def _dp_info(tr):
+    red = tr.reducer
+    return {"mode": ("shard" if red.shard else "allreduce") if red.active else "none",
+            "buckets": len(red.buckets) if red.active else 0,
+            "comm_bytes_per_step_per_rank": tr.comm_bytes_per_step(),
+            "fullc_gather": any(getattr(c.layer, "_gathering", None) is not None and c.layer._gathering()
+                                for c in tr.net.connections),
+            "overlapped_update": red.handles_update}
+
+
+def main():
+    a = _args()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return _spawn(a)
+
+    import torch
+    if a.device == "cpu":
+        os.environ.setdefault("CXXNET_DIST_BACKEND", "gloo")
+    from cxxnet_amd.parallel import init_distributed
+    import torch.distributed as dist
+
+    rank, world = init_distributed()
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but the process group holds {world} rank(s)", file=sys.stderr)
+        return 2
+    if a.device == "gpu":
+        dev = torch.device("cuda", torch.cuda.current_device())
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
+        a.input = "f32"
+
+    if a.scaling == "weak":
+        local_batch = a.batch
+        global_batch = a.batch * world
+    else:
+        global_batch = a.batch
+        local_batch = (a.batch + world - 1) // world
+
+    el, per_rank, tr, c, h, w, desc = _measure(a, world, rank, dev, global_batch, local_batch)
     ms = el / a.steps * 1000.0
     value = global_batch * a.steps / el
     base = _baseline(a.model)
+    dp = _dp_info(tr)
+    strong = None
+    if a.scaling == "weak" and world > 1 and a.strong_record:
+        # the conf's own configuration: its global batch split over the ranks
+        del tr
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+        sg, sl = a.batch, (a.batch + world - 1) // world
+        sel, sper, str_, *_ = _measure(a, world, rank, dev, sg, sl)
+        strong = {"value": round(sg * a.steps / sel, 1), "unit": "images/sec", "scaling": "strong",
+                  "global_batch": sg, "per_gpu_batch": sl, "ms_per_step": round(sel / a.steps * 1000.0, 3),
+                  "per_rank_ms_per_step": [round(x / a.steps * 1000.0, 3) for x in sper], "dp": _dp_info(str_)}
+    elif a.scaling == "weak" and world == 1:
+        strong = "identical to the weak record at one GPU (global batch = per-GPU batch)"
     if rank == 0:
-        red = tr.reducer
         name = MODEL_NAMES.get(a.model, a.model)
         out = {
             "metric": f"images/sec (whole node) {name} training at 1/2/4/8 MI355X",
@@ -203,11 +244,8 @@ def main():
                        "seq_len": None, "parallelism": f"dp{world}", "input_shape": [c, h, w]},
             "world_size": world,
             "per_rank_ms_per_step": [round(x / a.steps * 1000.0, 3) for x in per_rank],
-            "dp": {"mode": ("shard" if red.shard else "allreduce") if red.active else "none",
-                   "buckets": len(red.buckets) if red.active else 0,
-                   "comm_bytes_per_step_per_rank": tr.comm_bytes_per_step(),
-                   "fullc_gather": any(getattr(c.layer, "fullc_gather", 0) for c in tr.net.connections),
-                   "overlapped_update": red.handles_update},
+            "dp": dp,
+            "strong": strong,
             "baseline": (f"torch eager {a.model} {base:.0f} img/s per GPU x {world} (BASELINE.json measured)"
                          if base else None),
         }

@@ -158,12 +158,11 @@ int launch(const bf16_t *x, const bf16_t *w, const float *bias, bf16_t *y, int N
   const size_t lds = static_cast<size_t>(CF * 16) * (KS * 64 + 16) + KS * 8 * 4 + ((KH * Wp * 8 + 15) & ~15) +
                      4 * 16 * (CF * 32 + 16);
   if (lds > 96 * 1024) return -1;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void *>(conv_fewc_fwd<CF>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                        96 * 1024);
-    attr = true;
-  }
+  // once per instantiation (a thread-safe function-local static); if the attribute cannot be
+  // set, decline (-1) so the caller runs the GEMM instead of failing the launch
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void *>(conv_fewc_fwd<CF>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+  if (attr != hipSuccess) return -1;
   const long rows = static_cast<long>(N) * Ho;
   // persistent: enough blocks for ~4 per CU, each walking output rows
   const int per_cu = lds <= 24 * 1024 ? 6 : lds <= 40 * 1024 ? 4 : lds <= 52 * 1024 ? 3 : 2;

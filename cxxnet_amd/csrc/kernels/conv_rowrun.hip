@@ -223,12 +223,9 @@ int launch(const bf16_t *x, long x_bytes, const bf16_t *w, const float *bias, bf
   const int XB = (ndma * 1024 > epi ? ndma * 1024 : epi + 1023) / 1024 * 1024;
   const long lds = 2L * XB + static_cast<long>(cout) * (KS * 64 + 16);
   if (lds > 160 * 1024) return -1;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(conv_rowrun_fwd<CFH>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
-    attr = true;
-  }
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void *>(conv_rowrun_fwd<CFH>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return -1;  // once per instantiation (thread-safe static); -1: caller falls back
   const long items = static_cast<long>(N) * ((Ho + RG - 1) / RG);
   const int grid = static_cast<int>(items < 256 ? items : 256);
   hipLaunchKernelGGL(conv_rowrun_fwd<CFH>, dim3(grid), dim3(NT), static_cast<size_t>(lds), s, x, x_bytes, w, bias, y, y_bytes, N,
@@ -398,12 +395,9 @@ int launch_wgrad(const bf16_t *x, long x_bytes, const bf16_t *dy, long dy_bytes,
   const long lds = 3L * (XB + DB) + 1024;
   if (lds > 160 * 1024 || Wo > WS) return -1;
   if ((ndma_x + 7) / 8 + (ndma_d + 7) / 8 > 15) return -1;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(conv_rowrun_wgrad<CFH, KF>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void *>(conv_rowrun_wgrad<CFH, KF>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return -1;  // once per instantiation (thread-safe static); -1: caller falls back
   const long items = static_cast<long>(N) * ((Ho + WR - 1) / WR);
   const int grid = static_cast<int>(items < 256 ? items : 256);
   hipLaunchKernelGGL((conv_rowrun_wgrad<CFH, KF>), dim3(grid), dim3(NT), static_cast<size_t>(lds), s, x, x_bytes, dy,

@@ -1,27 +1,38 @@
-// One-wave-per-SIMD bf16 MFMA GEMM tiles for gfx950: 4 waves, each owning a (BM/2) x (BN/2)
-// block of the output (256 x 256 tile: 128 x 128 per wave, 256 accumulator registers), with
-// the fragment reads of the next k-step and the LDS-DMA of the K-tile after next issued in the
-// shadow of the current k-step's MFMAs.
+// One-wave-per-SIMD bf16 MFMA GEMM for gfx950 with address-free DMA issue (tile ids 110-115).
 //
-// Same contract and operand loaders as gemm_glds.hip (C[j][i] (+)= alpha * sum_k A(i,k) B(j,k),
-// K-major A and B); tile ids 92-97.
+// Same contract as gemm_glds.hip: C[j][i] (+)= alpha * sum_k A(i,k) B(j,k), A K-major (weights,
+// fc operands), B K-major or an implicit-im2col gather of an NHWC activation (conv forward /
+// stride-1 data-gradient).
 //
-// Why this shape: PMC on 8192^3 (profiles/r3_pmc_square_gemm.md) shows hipBLASLt's
-// MT256x256x64 kernel at 86 % MFMA utilisation with waves parked 5 % of their cycles, against
-// 57 % / 36 % for our 8-wave (two per SIMD) 256 x 256 tile: two co-resident waves that meet at
-// every barrier leave the SIMD's matrix pipe idle while both wait.  With one wave per SIMD the
-// wave's own instruction stream has to hide every latency, so the loop is software-pipelined:
-//   iteration t (K-tile t in LDS buffer t & 1; fragments F0 = k-step 0 of tile t in registers):
-//     [A]  ds_read F1 = k-step 1 of tile t           | 64 (MR x NR) MFMAs on F0
-//          lgkmcnt(0) (F1 read, so buffer t & 1 is free for this wave), vmcnt(0) (tile t+1's
-//          DMAs, issued one half-iteration ago, have landed), s_barrier
-//     [B]  ds_read F0 = k-step 0 of tile t+1 (buffer (t+1) & 1)
-//          LDS-DMA of tile t+2 into buffer t & 1   | MFMAs on F1
-//   so one barrier per K-tile, no wait on an LDS read in front of an MFMA, and a DMA has
-//   [B] + [A] (two k-steps of MFMAs) to land.  Past the K slice the DMAs are all-OOB dummies.
-// The order is pinned with sched_barrier (hipcc otherwise sinks the reads and DMAs to the end of
-// each k-step, where their latency is exposed).  SCHED = 0: [B]'s DMAs are spread evenly over its
-// MFMAs; SCHED = 1: one in front of each of the first MFMAs (a burst: more time to land).
+// Why this kernel.  The 8-wave tiles park a third of their wave cycles at barriers (two waves
+// per SIMD meet at every one), and round 3's one-wave-per-SIMD tile still issued 62 VALU per 128
+// MFMAs: every LDS-DMA recomputed its global address (add + bounds select) and all 16 row
+// offsets were bumped each K-tile.  A 16x16x32 MFMA holds the SIMD's issue for 8 of its 16
+// cycles, so that address math competes with the MFMAs.  Here the loop issues NO vector
+// arithmetic for its DMAs:
+//   * every lane's DMA offsets are fixed for the whole K loop (row * ld + swizzled chunk, or an
+//     out-of-range sentinel for rows past the operand), computed once;
+//   * the K-tile advance moves the buffer DESCRIPTOR: its base steps by 128 bytes per K-tile
+//     and its record count shrinks by the same amount (scalar arithmetic); K-tiles past the
+//     slice get a zero-record descriptor, so their DMAs are dummies that read zeros and keep
+//     the vmcnt bookkeeping constant;
+//   * gathers (conv): with Cg % 64 == 0 a K-tile lies inside ONE kernel tap (kh, kw) and one
+//     64-channel block, both wave-uniform: the tap's pixel shift goes into the descriptor base,
+//     and the per-row padding test is one bit of a per-row tap mask computed once
+//     (2 VALU per DMA: extract the bit, or it into bit 31 of the offset);
+//   * the loop body is unrolled over the two LDS stages, so every ds_read address is a fixed
+//     base register plus an immediate.
+// Schedule of one K-tile t (stage S = t & 1; F0 / F1 = fragments of k-steps 0 / 1; the DMAs of
+// tile t+1 were issued one K-tile earlier into stage S^1):
+//   [A] k-step-0 MFMAs, the first NF carrying one ds_read of F1 (stage S) each
+//       lgkmcnt(0), barrier                       -> every wave is done reading stage S
+//   [B] the remaining k-step-0 and most k-step-1 MFMAs, with the DMAs of tile t+2 into stage S
+//       spread evenly over them
+//       vmcnt(NA + NB), barrier                   -> tile t+1 landed in stage S^1 for every wave
+//   [C] the last k-step-1 MFMAs, the first NF carrying one ds_read of F0 of tile t+1 (stage S^1)
+// so a DMA has ~one K-tile of MFMAs to land, and each fragment set is read one k-step ahead.
+// MF = 32 selects v_mfma_f32_32x32x16_bf16 (four k-steps of 16 per K-tile, f32x16 accumulators)
+// instead of 16x16x32.
 // Reference: src/layer/convolution_layer-inl.hpp:70-155, src/layer/fullc_layer-inl.hpp:101-130.
 #include "gemm_glds_common.h"
 
@@ -29,41 +40,59 @@ using namespace cxg;
 
 namespace {
 
-// One MFMA row (8 accumulators) as inline asm: with the builtin, hipcc rotated the 256 loop-carried
-// accumulators through other AGPRs / VGPRs (352 v_accvgpr_* per 128 MFMAs); the "+a" operand pins
-// each accumulator in place.  Hazards hipcc no longer pads (cdna guide 5.7 item 2): the chain
-// MFMA D -> next MFMA's C needs none; the A/B operands are written only by ds_read (the loop is
-// audited for VALU writes of them: benchmarks/asm_audit.py); the reads of D after the main loop
-// are padded there.
-__device__ __forceinline__ void mfma_asm(f32x4 &acc, const bf16x8 &a, const bf16x8 &b) {
+template <int N>
+__device__ __forceinline__ void wait_lgkm() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// MFMA with the accumulator pinned in its AGPRs ("+a"): the builtin let hipcc rotate the
+// loop-carried accumulators through other registers.  Hazards hipcc does not pad for inline asm:
+// the A/B operands come only from ds_read (waited with lgkmcnt; benchmarks/asm_audit.py checks
+// that no VALU writes them in the loop); the reads of the accumulators after the loop are padded.
+__device__ __forceinline__ void mfma16(f32x4 &acc, const bf16x8 &a, const bf16x8 &b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
-
-template <int NR>
-__device__ __forceinline__ void mfma_row_asm(f32x4 (&acc)[NR], const bf16x8 &a, const bf16x8 (&fb)[NR]) {
-#pragma unroll
-  for (int n = 0; n < NR; ++n)
-    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[n]) : "v"(a), "v"(fb[n]));
+__device__ __forceinline__ void mfma32(f32x16 &acc, const bf16x8 &a, const bf16x8 &b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
-template <int BM, int BN, int AMODE, int BMODE, int EPI, int SCHED>
+template <int MF>
+struct Acc;
+template <>
+struct Acc<16> {
+  typedef f32x4 T;
+};
+template <>
+struct Acc<32> {
+  typedef f32x16 T;
+};
+
+template <int BM, int BN, int BMODE, int EPI, int MF>
 __global__ void __launch_bounds__(256, 1)
-gemm_4w(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_tiles, int ktiles_total) {
-  constexpr int NW = 4, WM = BM / 2, WN = BN / 2, MR = WM / 16, NR = WN / 16;
-  using OA = Op<AMODE, BM, NW>;
-  using OB = Op<BMODE, BN, NW>;
+gemm_4f(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_tiles, int ktiles_total) {
+  constexpr int NW = 4, WM = BM / 2, WN = BN / 2;
+  constexpr int MR = WM / MF, NR = WN / MF;  // MFMA blocks per wave
+  constexpr int KS = 64 / (MF == 16 ? 32 : 16);  // k-steps per K-tile
+  constexpr int NA = BM / 32, NB = BN / 32;       // 1-KiB DMAs per wave per K-tile
+  constexpr int NQ = NA + NB;
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
-  constexpr int NPT = OA::NI + OB::NI;  // DMA instructions per wave per K-tile
-  static_assert(NPT <= (MR - 1) * NR, "every DMA gets an MFMA slot in rows 1.. of [B]");
-  static_assert(NW * 16 * (WM + 4) * 4 <= 2 * STAGE, "epilogue staging fits");
+  constexpr int PER = MR * NR;      // MFMAs per k-step
+  constexpr int T = KS * PER;       // MFMAs per K-tile
+  constexpr int NF = MR + NR;       // fragment reads per k-step
+  // [A] / [C] lengths: the reads of one k-step one per MFMA plus a tail for them to land
+  constexpr int LA = NF + 10 < PER ? NF + 10 : PER;
+  constexpr int LC = NF + 6 < PER ? NF + 6 : PER;
+  constexpr int LB = T - LA - LC;
+  static_assert(NF <= LA && NF <= LC && LB >= NQ, "schedule");
+  static_assert(NW * MF * (WM + 4) * 4 <= 2 * STAGE, "epilogue staging fits");
+  using AccT = typename Acc<MF>::T;
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
 
   const uint32_t ntile = static_cast<uint32_t>(tiles_i) * tiles_j;
   const GemmBlock wb = gemm_block(ntile);
   const int g = wb.g;
-  const uint32_t tile = wb.tile;
   int ti, tj;
-  tile_ij(tile, tiles_i, tiles_j, E.group_i, ti, tj);
+  tile_ij(wb.tile, tiles_i, tiles_j, E.group_i, ti, tj);
   const int i0 = ti * BM, j0 = tj * BN;
   const int kt_beg = wb.slice * ksplit_tiles;
   const int kt_end = min(kt_beg + ksplit_tiles, ktiles_total);
@@ -73,203 +102,284 @@ gemm_4w(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 1, wc = wave & 1;
-  const rsrc_t rA = make_rsrc(A.ptr, A.nbytes);
-  const rsrc_t rB = make_rsrc(B.ptr, B.nbytes);
+  // DMA s of a wave fills LDS rows 8 (wave + 4 s) + lane / 8 of the operand tile; the 16-byte
+  // chunk lane & 7 of that row holds logical chunk lchunk (XOR swizzle, applied at the source)
+  const int lchunk = (lane & 7) ^ (((wave & 1) << 2) + (lane >> 4));
   const uint32_t goA = static_cast<uint32_t>(g * A.gstride) * 2u;
   const uint32_t goB = static_cast<uint32_t>(g * B.gstride) * 2u;
-  OA oa;
-  OB ob;
-  oa.init(A, i0, goA, wave, lane);
-  ob.init(B, j0, goB, wave, lane);
-  // K_DIRECT operands: DMA s reads rows 32 s further than DMA 0 -- one base register and a
-  // stride instead of one row offset per DMA (rows past the operand read zeros (outside the
-  // buffer) or rows of the next group, which only feed output rows the epilogue never stores)
-  const uint32_t rsA = 32u * static_cast<uint32_t>(A.ld) * 2u, rsB = 32u * static_cast<uint32_t>(B.ld) * 2u;
-  const uint32_t baseA = goA + static_cast<uint32_t>((i0 + 8 * wave + (lane >> 3)) * A.ld) * 2u;
-  const uint32_t baseB = goB + static_cast<uint32_t>((j0 + 8 * wave + (lane >> 3)) * B.ld) * 2u;
-  auto offA = [&](auto sc, const typename OA::Prep &p) __attribute__((always_inline)) -> uint32_t {
-    constexpr int s = decltype(sc)::value;
-    if constexpr (AMODE == K_DIRECT) {
-      uint32_t off = p.kin ? baseA + static_cast<uint32_t>(p.k) * 2u + s * rsA : OOB;
-      asm volatile("" : "+v"(off));
-      return off;
-    } else {
-      return oa.template offset<s>(A, p, wave, lane);
-    }
-  };
-  auto offB = [&](auto sc, const typename OB::Prep &p) __attribute__((always_inline)) -> uint32_t {
-    constexpr int s = decltype(sc)::value;
+
+  uint32_t offA[NA], offB[NB], invB[NB];
+#pragma unroll
+  for (int s = 0; s < NA; ++s) {
+    const int r = i0 + 8 * (wave + 4 * s) + (lane >> 3);
+    offA[s] = r < A.rows ? goA + static_cast<uint32_t>(r * A.ld) * 2u + lchunk * 16u : OOB;
+  }
+#pragma unroll
+  for (int s = 0; s < NB; ++s) {
+    const int r = j0 + 8 * (wave + 4 * s) + (lane >> 3);
     if constexpr (BMODE == K_DIRECT) {
-      uint32_t off = p.kin ? baseB + static_cast<uint32_t>(p.k) * 2u + s * rsB : OOB;
-      asm volatile("" : "+v"(off));
-      return off;
+      offB[s] = r < B.rows ? goB + static_cast<uint32_t>(r * B.ld) * 2u + lchunk * 16u : OOB;
+      invB[s] = 0;
     } else {
-      return ob.template offset<s>(B, p, wave, lane);
+      uint32_t off = OOB, inv = 0xffffffffu;
+      if (r < B.rows) {
+        const uint32_t n = fdiv(static_cast<uint32_t>(r), B.fd_hw);
+        const uint32_t rem = static_cast<uint32_t>(r) - n * static_cast<uint32_t>(B.Ho * B.Wo);
+        const uint32_t ho = fdiv(rem, B.fd_wo);
+        const uint32_t wo = rem - ho * B.Wo;
+        const int hb = static_cast<int>(ho) * B.stride, wbse = static_cast<int>(wo) * B.stride;
+        off = goB + static_cast<uint32_t>(((static_cast<int>(n) * B.H + hb) * B.W + wbse) * B.C) * 2u + lchunk * 16u;
+        // bit (kh * KW + kw) clear <=> input pixel (hb - pad_h + kh, wb - pad_w + kw) inside the image
+        for (int kh = 0, tap = 0; kh < B.KH; ++kh) {
+          const bool hin = static_cast<unsigned>(hb - B.pad_h + kh) < static_cast<unsigned>(B.H);
+          for (int kw = 0; kw < B.KW; ++kw, ++tap) {
+            const bool in = hin && static_cast<unsigned>(wbse - B.pad_w + kw) < static_cast<unsigned>(B.W);
+            if (in) inv &= ~(1u << tap);
+          }
+        }
+      }
+      offB[s] = off;
+      invB[s] = inv;
     }
-  };
+  }
 
-  // DMA instruction q (0 .. NPT-1) of K-tile t into buffer t & 1: A's NI first, then B's
-  auto dma = [&](auto qc, int t, const typename OA::Prep &pa, const typename OB::Prep &pb)
-      __attribute__((always_inline)) -> void {
-    constexpr int q = decltype(qc)::value;
-    char *sa = smem + (t & 1) * STAGE;
-    if constexpr (q < OA::NI) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void *)(sa + (wave + NW * q) * 1024), 16,
-                                               offA(std::integral_constant<int, q>{}, pa), 0, 0, 0);
-    } else {
-      constexpr int s = q - OA::NI;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void *)(sa + A_BYTES + (wave + NW * s) * 1024), 16,
-                                               offB(std::integral_constant<int, s>{}, pb), 0, 0, 0);
-    }
-  };
-  auto issue = [&](int t) __attribute__((always_inline)) {
+  // Descriptors of K-tile t (relative to the slice): scalar base / record arithmetic only
+  auto rsrcA = [&](int t) __attribute__((always_inline)) -> rsrc_t {
     const int kt = kt_beg + t;
-    const typename OA::Prep pa = oa.prep(A, kt, kt_end, goA);
-    const typename OB::Prep pb = ob.prep(B, kt, kt_end, goB);
-    static_for<NPT>([&](auto qc) { dma(qc, t, pa, pb); });
+    const bool in = kt < kt_end;
+    const uint32_t step = in ? static_cast<uint32_t>(kt) * 128u : 0u;
+    return make_rsrc(reinterpret_cast<const char *>(A.ptr) + step, in ? A.nbytes - step : 0u);
+  };
+  // B: K_DIRECT as A; gather: the tap and channel block of the K-tile (Cg % 64 == 0)
+  auto rsrcB = [&](int t, uint32_t &tap) __attribute__((always_inline)) -> rsrc_t {
+    const int kt = kt_beg + t;
+    const bool in = kt < kt_end;
+    if constexpr (BMODE == K_DIRECT) {
+      tap = 0;
+      const uint32_t step = in ? static_cast<uint32_t>(kt) * 128u : 0u;
+      return make_rsrc(reinterpret_cast<const char *>(B.ptr) + step, in ? B.nbytes - step : 0u);
+    } else {
+      const uint32_t k0 = in ? static_cast<uint32_t>(kt) * 64u : 0u;
+      const uint32_t q = fdiv(k0, B.fd_cg);  // tap index kh * KW + kw
+      const int c0 = static_cast<int>(k0 - q * static_cast<uint32_t>(B.Cg));
+      const uint32_t kh = fdiv(q, B.fd_kw);
+      const int kw = static_cast<int>(q - kh * static_cast<uint32_t>(B.KW));
+      const int shift = (((static_cast<int>(kh) - B.pad_h) * B.W + (kw - B.pad_w)) * B.C + c0) * 2;
+      tap = q;
+      return make_rsrc(reinterpret_cast<const char *>(B.ptr) + shift,
+                       in ? static_cast<uint32_t>(static_cast<int>(B.nbytes) - shift) : 0u);
+    }
+  };
+  auto voffB = [&](int s, uint32_t tap) __attribute__((always_inline)) -> uint32_t {
+    if constexpr (BMODE == K_DIRECT) {
+      return offB[s];
+    } else {
+      return offB[s] | (((invB[s] >> tap) & 1u) << 31);
+    }
+  };
+  auto dmaA = [&](const rsrc_t &r, int stage, int s) __attribute__((always_inline)) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void *)(smem + stage * STAGE + (wave + NW * s) * 1024), 16,
+                                             offA[s], 0, 0, 0);
+  };
+  auto dmaB = [&](const rsrc_t &r, uint32_t tap, int stage, int s) __attribute__((always_inline)) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void *)(smem + stage * STAGE + A_BYTES + (wave + NW * s) * 1024),
+                                             16, voffB(s, tap), 0, 0, 0);
   };
 
-  f32x4 acc[MR][NR];
+  // fragment read bases: row (lane & 15) [16x16x32] or (lane & 31) [32x32x16] of a fragment
+  // block, swizzled chunk of k-step kk
+  const char *pa = smem + wr * WM * 128;
+  const char *pb = smem + A_BYTES + wc * WN * 128;
+  auto frag_off = [&](int kk) __attribute__((always_inline)) -> int {
+    if constexpr (MF == 16) {
+      const int row = lane & 15;
+      const int ch = ((kk >> 3) + (lane >> 4)) ^ (row >> 1);
+      return row * 128 + ch * 16;
+    } else {
+      const int row = lane & 31;
+      const int ch = ((kk >> 3) + (lane >> 5)) ^ ((row >> 1) & 7);
+      return row * 128 + ch * 16;
+    }
+  };
+
+  AccT acc[MR][NR];
 #pragma unroll
   for (int m = 0; m < MR; ++m)
 #pragma unroll
-    for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < NR; ++n) acc[m][n] = AccT{};
 
-  // Fragment registers: one A set, refilled row by row right behind its last MFMA, and two B
-  // sets that alternate between k-steps (B fragments are used by every MFMA row, so the next
-  // k-step's B needs registers of its own): 96 fragment VGPRs next to the 256 accumulators.
-  bf16x8 fa[MR], fb0[NR], fb1[NR];
-  auto read_a = [&](auto mc, int t, int kk) __attribute__((always_inline)) -> void {
-    constexpr int m = decltype(mc)::value;
-    fa[m] = frag<K_DIRECT>(smem + (t & 1) * STAGE, wr * WM + m * 16, kk, lane);
+  // one fragment set per k-step (16x16x32: 2 sets of 16 fragments; 32x32x16: 4 sets of 8)
+  bf16x8 fa[KS][MR], fb[KS][NR];
+  auto read_frag = [&](int set, int f, int stage, int kk) __attribute__((always_inline)) {
+    const int o = frag_off(kk);
+    if (f < MR)
+      fa[set][f] = *reinterpret_cast<const bf16x8 *>(pa + stage * STAGE + f * MF * 128 + o);
+    else
+      fb[set][f - MR] = *reinterpret_cast<const bf16x8 *>(pb + stage * STAGE + (f - MR) * MF * 128 + o);
   };
-  auto read_b = [&](int t, int kk, bf16x8 (&fb)[NR]) __attribute__((always_inline)) -> void {
-    const char *sb = smem + (t & 1) * STAGE + A_BYTES;
+  auto mma = [&](int set, int u) __attribute__((always_inline)) {
+    const int m = u / NR, n = u % NR;
+    if constexpr (MF == 16)
+      mfma16(acc[m][n], fa[set][m], fb[set][n]);
+    else
+      mfma32(acc[m][n], fa[set][m], fb[set][n]);
+  };
+
+  // prologue: tiles 0 and 1 in flight, tile 0 landed everywhere, k-step 0 of tile 0 read
+  {
+    uint32_t tap0, tap1;
+    const rsrc_t a0 = rsrcA(0), b0 = rsrcB(0, tap0);
 #pragma unroll
-    for (int n = 0; n < NR; ++n) fb[n] = frag<K_DIRECT>(sb, wc * WN + n * 16, kk, lane);
-  };
-  auto read_b1 = [&](auto nc, int t, int kk, bf16x8 (&fb)[NR]) __attribute__((always_inline)) -> void {
-    constexpr int n = decltype(nc)::value;
-    fb[n] = frag<K_DIRECT>(smem + (t & 1) * STAGE + A_BYTES, wc * WN + n * 16, kk, lane);
-  };
-  auto mfma_row = [&](auto mc, const bf16x8 (&fb)[NR]) __attribute__((always_inline)) -> void {
-    constexpr int m = decltype(mc)::value;
-    mfma_row_asm<NR>(acc[m], fa[m], fb);
-  };
-
-  // prologue: tiles 0 and 1 in flight, tile 0 landed for every wave, k-step 0 of tile 0 read
-  issue(0);
-  issue(1);
-  wait_vmcnt<NPT>();
+    for (int s = 0; s < NA; ++s) dmaA(a0, 0, s);
+#pragma unroll
+    for (int s = 0; s < NB; ++s) dmaB(b0, tap0, 0, s);
+    const rsrc_t a1 = rsrcA(1), b1 = rsrcB(1, tap1);
+#pragma unroll
+    for (int s = 0; s < NA; ++s) dmaA(a1, 1, s);
+#pragma unroll
+    for (int s = 0; s < NB; ++s) dmaB(b1, tap1, 1, s);
+  }
+  wait_vmcnt<NQ>();
   block_barrier();
-  static_for<MR>([&](auto mc) { read_a(mc, 0, 0); });
-  read_b(0, 0, fb0);
-  // retire them here: left pending into the loop, hipcc's wait for them lands in front of the
-  // first MFMA of EVERY iteration (it merges the loop-entry state at the header)
-  __builtin_amdgcn_s_waitcnt(0xc07f);
+#pragma unroll
+  for (int f = 0; f < NF; ++f) read_frag(0, f, 0, 0);
   __builtin_amdgcn_sched_barrier(0);
 
-  for (int t = 0; t < nt; ++t) {
-    // [A] k-step 0 of tile t (fa, fb0); reads of k-step 1: fb1 first, fa row by row
-    // [A] k-step 0 of tile t (fa, fb0); reads of k-step 1: fb1 one per MFMA of row 0, fa row by
-    // row behind each row's last MFMA
-    static_for<MR>([&](auto mc) {
-      constexpr int m = decltype(mc)::value;
-      static_for<NR>([&](auto nc) {
-        constexpr int n = decltype(nc)::value;
-        mfma_asm(acc[m][n], fa[m], fb0[n]);
-        if constexpr (m == 0) read_b1(nc, t, 32, fb1);
-        __builtin_amdgcn_sched_barrier(0);
-      });
-      read_a(mc, t, 32);
+  // One K-tile in stage ST.  MFMA number v of the tile (0 .. T-1) is k-step v / PER, block v % PER.
+  // [A] carries the reads of k-steps 1 .. KS-1 (NRA of them), spread over its first LA - TA MFMAs
+  // (TA MFMAs left for the last ones to land); [C] carries the NF reads of k-step 0 of tile t+1.
+  constexpr int NRA = (KS - 1) * NF;
+  constexpr int TA = MF == 16 ? 8 : 4;
+  auto ktile = [&](auto stc, int t) __attribute__((always_inline)) {
+    constexpr int ST = decltype(stc)::value;
+    wait_lgkm<0>();  // fragments of k-step 0
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<T>([&](auto vc) {
+      constexpr int v = decltype(vc)::value;
+      constexpr int ks = v / PER, u = v % PER;
+      if constexpr (v == LA) {
+        // [A] -> [B]: the reads of k-step 1 are in; every wave is done with stage ST
+        wait_lgkm<0>();
+        block_barrier();
+      }
+      if constexpr (v == T - LC) {
+        // [B] -> [C]: this wave's DMAs of tile t+1 (NQ older than the NQ just issued) have landed
+        wait_vmcnt<NQ>();
+        block_barrier();
+      }
+      if constexpr (v >= LA && v < T - LC) {
+        // [B]: DMA q of tile t+2 in front of MFMA LA + q * LB / NQ
+        static_for<NQ>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          if constexpr (v == LA + q * LB / NQ) {
+            if constexpr (q < NA) {
+              dmaA(rsrcA(t + 2), ST, q);
+            } else {
+              uint32_t tap;
+              const rsrc_t rb = rsrcB(t + 2, tap);
+              dmaB(rb, tap, ST, q - NA);
+            }
+          }
+        });
+      }
+      mma(ks, u);
+      // reads riding on this MFMA
+      if constexpr (v < LA) {
+        static_for<NRA>([&](auto rc) {
+          constexpr int r = decltype(rc)::value;
+          if constexpr (r * (LA - TA) / NRA == v)
+            read_frag(1 + r / NF, r % NF, ST, (1 + r / NF) * (64 / KS));  // [A]: k-steps 1.. of tile t
+        });
+      } else if constexpr (v >= T - LC && v < T - LC + NF) {
+        read_frag(0, v - (T - LC), ST ^ 1, 0);  // [C]: k-step 0 of tile t+1
+      }
       __builtin_amdgcn_sched_barrier(0);
     });
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of buffer t & 1 are done
-    wait_vmcnt<0>();                     // tile t + 1 has landed (this wave's DMAs)
-    block_barrier();
-    // [B] k-step 1 of tile t (fa, fb1); reads of k-step 0 of tile t+1 (fb0 one per MFMA of row 0,
-    // fa row by row) and the DMAs of tile t+2 into buffer t & 1 over the remaining MFMAs
-    {
-      const int kt = kt_beg + t + 2;
-      const typename OA::Prep pa = oa.prep(A, kt, kt_end, goA);
-      const typename OB::Prep pb = ob.prep(B, kt, kt_end, goB);
-      // DMA q goes in front of MFMA number slot(q) of [B] (rows 1..MR-1): spread evenly
-      // (SCHED 0) or one per MFMA from the first (SCHED 1)
-      static_for<MR>([&](auto mc) {
-        constexpr int m = decltype(mc)::value;
-        static_for<NR>([&](auto nc) {
-          constexpr int n = decltype(nc)::value, u = m * NR + n;
-          static_for<NPT>([&](auto qc) {
-            constexpr int q = decltype(qc)::value;
-            constexpr int slot = NR + (SCHED == 1 ? q : q * ((MR - 1) * NR) / NPT);
-            if constexpr (slot == u) {
-              char *sa = smem + (t & 1) * STAGE;
-              if constexpr (q < OA::NI) {
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void *)(sa + (wave + NW * q) * 1024), 16,
-                                                         offA(std::integral_constant<int, q>{}, pa), 0, 0, 0);
-              } else {
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    rB, (lds_void *)(sa + A_BYTES + (wave + NW * (q - OA::NI)) * 1024), 16,
-                    offB(std::integral_constant<int, q - OA::NI>{}, pb), 0, 0, 0);
-              }
-            }
-          });
-          mfma_asm(acc[m][n], fa[m], fb1[n]);
-          if constexpr (m == 0) read_b1(nc, t + 1, 0, fb0);
-          __builtin_amdgcn_sched_barrier(0);
-        });
-        read_a(mc, t + 1, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      });
-    }
-    // retire tile t+1's k-step 0 reads behind [B]'s MFMAs: the next [A] then waits on nothing
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // two K-tiles (both stages) per trip, so every LDS address is a base register + an immediate;
+  // an odd last K-tile runs after the loop (a branch inside the loop made hipcc spill the
+  // accumulators at the join)
+  int t = 0;
+  for (; t + 1 < nt; t += 2) {
+    ktile(std::integral_constant<int, 0>{}, t);
+    ktile(std::integral_constant<int, 1>{}, t + 1);
   }
-  // the last MFMAs' results are read by compiler code below: 8-pass XDL -> 12 wait states
-  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+  if (t < nt) ktile(std::integral_constant<int, 0>{}, t);
+  // results of the last MFMAs are read by compiler code below: XDL passes -> wait states
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
   wait_vmcnt<0>();
+  wait_lgkm<0>();
   __syncthreads();  // the epilogue reuses the stage buffers
 
-  seg_epilogue<EPI, MR, NR, WM>(acc, smem, E, g, wb.slice, A.rows, B.rows, i0 + wr * WM, j0 + wc * WN, wave, lane);
+  if constexpr (MF == 16) {
+    seg_epilogue<EPI, MR, NR, WM>(acc, smem, E, g, wb.slice, A.rows, B.rows, i0 + wr * WM, j0 + wc * WN, wave, lane);
+  } else {
+    // 32x32 block (m, n): the lane holds output column j = lane & 31 and rows i = 8 b + 4 (lane / 32)
+    // + e of register 4 b + e: stage 32 j-rows x WM i-columns per n, then write whole rows
+    float *ep = reinterpret_cast<float *>(smem) + wave * 32 * (WM + 4);
+#pragma unroll
+    for (int n = 0; n < NR; ++n) {
+#pragma unroll
+      for (int m = 0; m < MR; ++m)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const f32x4 v = {acc[m][n][4 * b], acc[m][n][4 * b + 1], acc[m][n][4 * b + 2], acc[m][n][4 * b + 3]};
+          *reinterpret_cast<f32x4 *>(ep + (lane & 31) * (WM + 4) + m * 32 + 8 * b + 4 * (lane >> 5)) = v;
+        }
+      wait_lgkm<0>();
+      wave_lds_handoff<true>();
+      write_staged<EPI, 32, WM>(ep, E, g, wb.slice, A.rows, B.rows, i0 + wr * WM, j0 + wc * WN + n * 32, lane);
+      wait_lgkm<0>();
+      wave_lds_handoff<true>();
+    }
+  }
 }
 
-template <int BM, int BN, int AMODE, int BMODE, int EPI, int SCHED>
-void launch_4w(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int ksplit, hipStream_t s) {
+template <int BM, int BN, int BMODE, int EPI, int MF>
+void launch_4f(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int ksplit, hipStream_t s) {
   const int ti = cdiv(A.rows, BM), tj = cdiv(B.rows, BN);
   const int ktiles = cdiv(A.kdim, BK);
   ksplit = ksplit < 1 ? 1 : (ksplit > ktiles ? ktiles : ksplit);
   const int per = cdiv(ktiles, ksplit);
   ksplit = cdiv(ktiles, per);
   dim3 grid(ti * tj, ksplit, groups);
-  hipLaunchKernelGGL((gemm_4w<BM, BN, AMODE, BMODE, EPI, SCHED>), grid, dim3(256), 0, s, A, B, E, ti, tj, per, ktiles);
+  hipLaunchKernelGGL((gemm_4f<BM, BN, BMODE, EPI, MF>), grid, dim3(256), 0, s, A, B, E, ti, tj, per, ktiles);
 }
 
 }  // namespace
 
 namespace cxg {
-// 92: 256x256, 94: 128x256, 95: 256x128, 98: 96x256 (DMAs spread over [B]); 93 / 96 / 97 / 100: the same
-// with the DMAs in a burst
+// Operands the address-free loop supports: whole K-tiles (kdim % 64 == 0: no partial tile to
+// mask), gathers with whole 64-channel blocks per tap (Cg % 64 == 0), at most 32 taps, unit
+// dilation; descriptor ranges that stay below 2^31 after the tap shifts.
+static bool fast_ok(int bmode, const GOperand &A, const GOperand &B) {
+  if (A.kdim % 64 != 0) return false;
+  if (bmode == K_GATHER) {
+    if (B.Cg % 64 != 0 || B.KH * B.KW > 32 || B.KH * B.KW * B.Cg != B.kdim) return false;
+    const long span = (static_cast<long>(B.KH + B.pad_h) * B.W + B.KW + B.pad_w) * B.C * 2;
+    if (static_cast<long>(B.nbytes) + span >= (1L << 31)) return false;
+  }
+  return true;
+}
+
+// 110: 256x256, 111: 256x128, 112: 128x256 (16x16x32); 113: 256x256 (32x32x16)
 int dispatch_4w(int amode, int bmode, int epi, int tile, const GOperand &A, const GOperand &B, const GEpi &E,
                 int groups, int ksplit, hipStream_t s) {
-#define CX4(AMV, BMV, EPV)                                                                                 \
-  if (amode == AMV && bmode == BMV && epi == EPV) {                                                        \
-    switch (tile) {                                                                                        \
-      case 92: launch_4w<256, 256, AMV, BMV, EPV, 0>(A, B, E, groups, ksplit, s); return 0;                \
-      case 93: launch_4w<256, 256, AMV, BMV, EPV, 1>(A, B, E, groups, ksplit, s); return 0;                \
-      case 94: launch_4w<128, 256, AMV, BMV, EPV, 0>(A, B, E, groups, ksplit, s); return 0;                \
-      case 95: launch_4w<256, 128, AMV, BMV, EPV, 0>(A, B, E, groups, ksplit, s); return 0;                \
-      case 96: launch_4w<128, 256, AMV, BMV, EPV, 1>(A, B, E, groups, ksplit, s); return 0;                \
-      case 97: launch_4w<256, 128, AMV, BMV, EPV, 1>(A, B, E, groups, ksplit, s); return 0;                \
-      case 98: launch_4w<96, 256, AMV, BMV, EPV, 0>(A, B, E, groups, ksplit, s); return 0;                 \
-      case 100: launch_4w<96, 256, AMV, BMV, EPV, 1>(A, B, E, groups, ksplit, s); return 0;                \
-      default: return -1;                                                                                  \
-    }                                                                                                      \
+  if (amode != K_DIRECT || !fast_ok(bmode, A, B)) return -1;
+#define CX4(BMV, EPV)                                                                \
+  if (bmode == BMV && epi == EPV) {                                                  \
+    switch (tile) {                                                                  \
+      case 110: launch_4f<256, 256, BMV, EPV, 16>(A, B, E, groups, ksplit, s); return 0; \
+      case 111: launch_4f<256, 128, BMV, EPV, 16>(A, B, E, groups, ksplit, s); return 0; \
+      case 112: launch_4f<128, 256, BMV, EPV, 16>(A, B, E, groups, ksplit, s); return 0; \
+      case 113: launch_4f<256, 256, BMV, EPV, 32>(A, B, E, groups, ksplit, s); return 0; \
+      default: return -1;                                                            \
+    }                                                                                \
   }
-  CX4(K_DIRECT, K_GATHER, EPI_BF16)     // conv fwd / dgrad
-  CX4(K_DIRECT, K_ROWGATHER, EPI_BF16)  // conv fwd, few input channels (AlexNet conv1)
-  CX4(K_DIRECT, K_DIRECT, EPI_BF16)  // fc fwd, square GEMMs
-  CX4(K_DIRECT, K_DIRECT, EPI_F32)   // fc fwd split-K
+  CX4(K_GATHER, EPI_BF16)  // conv fwd / dgrad
+  CX4(K_DIRECT, EPI_BF16)  // fc fwd, square GEMMs
+  CX4(K_DIRECT, EPI_F32)   // fc fwd split-K
 #undef CX4
   return -1;
 }

@@ -699,8 +699,7 @@ int dispatch(int amode, int bmode, int epi, int tile, const GOperand &A, const G
     if (tile == 51) { launch_seg<128, 256, AMV, BMV, EPV>(A, B, E, groups, ksplit, s); return 0; }  \
   }
   // (99 is the Python-side pseudo-tile of the register kernel, never passed here)
-  if ((tile >= 92 && tile <= 98) || (tile >= 100 && tile <= 109)) return cxg::dispatch_4w(amode, bmode, epi, tile, A, B, E, groups, ksplit, s);
-  if (tile >= 90 && tile <= 99) return cxg::dispatch_8p(amode, bmode, epi, tile, A, B, E, groups, ksplit, s);
+  if (tile >= 110 && tile <= 119) return cxg::dispatch_4w(amode, bmode, epi, tile, A, B, E, groups, ksplit, s);
   if (tile >= 50 && tile <= 51) {
     CXG_SEG(K_DIRECT, K_GATHER, EPI_BF16)
     CXG_SEG(K_DIRECT, K_DIRECT, EPI_BF16)
@@ -795,7 +794,7 @@ void fill(GOperand &r, const CxnOperandG *o, int mode) {
   r.nbytes = static_cast<uint32_t>(o->nbytes);
   r.ld = o->ld; r.rows = o->rows; r.kdim = o->kdim;
   if (mode == K_GATHER || mode == MN_GATHER) {
-    r.H = o->H; r.W = o->W; r.C = o->C; r.Ho = o->Ho; r.Wo = o->Wo; r.KW = o->KW;
+    r.H = o->H; r.W = o->W; r.C = o->C; r.Ho = o->Ho; r.Wo = o->Wo; r.KW = o->KW; r.KH = o->KH;
     r.stride = o->stride; r.pad_h = o->pad_h; r.pad_w = o->pad_w; r.Cg = o->Cg;
     r.fd_cg = make_fastdiv(o->Cg);
     r.fd_kw = make_fastdiv(o->KW > 0 ? o->KW : 1);

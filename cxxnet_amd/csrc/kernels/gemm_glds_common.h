@@ -1,4 +1,4 @@
-// Shared pieces of the LDS-DMA GEMM kernels (gemm_glds.hip, gemm_8p.hip): operand records,
+// Shared pieces of the LDS-DMA GEMM kernels (gemm_glds.hip, gemm_4w.hip): operand records,
 // epilogue record, LDS-DMA loaders, fragment readers and the 8-wave epilogue.
 #pragma once
 #include <utility>
@@ -378,6 +378,72 @@ __device__ __forceinline__ bf16x8 seg_frag(const char *tile, int base, int lane)
 // Epilogue of the 8-wave kernels: each wave stages 16 output rows (j) x WM columns (i) of its
 // fp32 tile in LDS, then writes contiguous row segments: bf16 (+bias, relu, relu'-mask of the old
 // value) or an fp32 split-K slab.
+// Write JR staged output rows (j = jrow0 .. jrow0 + JR - 1, WM columns i from ibase; staging row
+// pitch WM + 4 floats) of one wave: bf16 (+bias, relu, relu'-mask of the old value) or an fp32
+// split-K slab.
+template <int EPI, int JR, int WM>
+__device__ __forceinline__ void write_staged(const float *ep, const GEpi &E, int g, int slice, int Mi, int Nj,
+                                             int ibase, int jrow0, int lane) {
+  const float *bias = E.bias ? E.bias + g * E.bias_gstride : nullptr;
+  if constexpr (EPI == EPI_BF16) {
+    bf16_t *out = reinterpret_cast<bf16_t *>(E.out) + g * E.gstride;
+    constexpr int LPR = WM / 8;
+    constexpr int RPI = 64 / LPR;
+    const int il = (lane % LPR) * 8;
+    const int i = ibase + il;
+    const bool vec_store = ((E.ldc & 7) == 0) && (i + 8 <= Mi);
+#pragma unroll
+    for (int jl = lane / LPR; jl < JR; jl += RPI) {
+      const int j = jrow0 + jl;
+      if (j < Nj && i < Mi) {
+        const f32x4 x0 = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il);
+        const f32x4 x1 = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il + 4);
+        float f[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          f[e] = f[e] * E.alpha + ((bias && i + e < Mi) ? bias[i + e] : 0.f);
+          if (E.relu) f[e] = fmaxf(f[e], 0.f);
+        }
+        bf16_t *dst = out + static_cast<long>(j) * E.ldc + i;
+        if (vec_store) {
+          if (E.mask_relu) {
+            float old[8];
+            unpack8(*reinterpret_cast<const uint4 *>(dst), old);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = old[e] > 0.f ? f[e] : 0.f;
+          }
+          *reinterpret_cast<uint4 *>(dst) = pack8(f);
+        } else {
+          for (int e = 0; e < 8 && i + e < Mi; ++e) {
+            if (E.mask_relu && !(bf2f(dst[e]) > 0.f)) f[e] = 0.f;
+            dst[e] = f2bf(f[e]);
+          }
+        }
+      }
+    }
+  } else {  // EPI_F32: split-K slab (fc forward)
+    float *out = reinterpret_cast<float *>(E.out) + g * E.gstride + slice * E.kstride;
+    constexpr int LPR = WM / 4;
+    constexpr int RPI = 64 / LPR;
+    const int il = (lane % LPR) * 4;
+    const int i = ibase + il;
+    const bool vec = ((E.ldc & 3) == 0) && (i + 4 <= Mi);
+#pragma unroll
+    for (int jl = lane / LPR; jl < JR; jl += RPI) {
+      const int j = jrow0 + jl;
+      if (j < Nj && i < Mi) {
+        f32x4 v = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il) * E.alpha;
+        float *dst = out + static_cast<long>(j) * E.ldc + i;
+        if (vec) {
+          *reinterpret_cast<f32x4 *>(dst) = v;
+        } else {
+          for (int e = 0; e < 4 && i + e < Mi; ++e) dst[e] = v[e];
+        }
+      }
+    }
+  }
+}
+
 template <int EPI, int MR, int NR, int WM>
 __device__ __forceinline__ void seg_epilogue(f32x4 (&acc)[MR][NR], char *smem, const GEpi &E, int g, int slice, int Mi,
                                              int Nj, int ibase, int jbase, int wave, int lane) {
@@ -450,11 +516,8 @@ __device__ __forceinline__ void seg_epilogue(f32x4 (&acc)[MR][NR], char *smem, c
   }
 }
 
-// the 8-phase 256 x 256 kernels (gemm_8p.hip): tiles 90-99; -1 when unsupported
-// the one-wave-per-SIMD tiles (gemm_4w.hip): tiles 92-97; -1 when unsupported
+// the one-wave-per-SIMD address-free tiles (gemm_4w.hip): tiles 110-113; -1 when unsupported
 int dispatch_4w(int amode, int bmode, int epi, int tile, const GOperand &A, const GOperand &B, const GEpi &E,
-                int groups, int ksplit, hipStream_t s);
-int dispatch_8p(int amode, int bmode, int epi, int tile, const GOperand &A, const GOperand &B, const GEpi &E,
                 int groups, int ksplit, hipStream_t s);
 
 }  // namespace cxg

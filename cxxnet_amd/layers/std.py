@@ -39,14 +39,17 @@ class FullConnectLayer(Layer):
 
     def __init__(self, ctx):
         super().__init__(ctx)
-        self.fullc_gather = 0
+        self.fullc_gather = -1  # 1 on, 0 off, -1 auto (_gathering)
         self.fuse_relu = False
         self._dx = None
+        self._rows = 0
+        self._gbuf = {}      # persistent gather sources / outputs (graph-capturable)
+        self._xwork = None   # the forward's all-gather of x, waited in backprop
 
     def set_param(self, name, val):
         super().set_param(name, val)
         if name == "fullc_gather":
-            self.fullc_gather = int(val)
+            self.fullc_gather = -1 if str(val).strip().lower() == "auto" else int(val)
 
     def init_connection(self, nodes_in, nodes_out):
         _check(len(nodes_in) == 1 and len(nodes_out) == 1, "FullcLayer: only support 1-1 connection")
@@ -59,6 +62,7 @@ class FullConnectLayer(Layer):
         else:
             _check(self.lp.num_input_node == nin, "FullcLayer: input hidden nodes is not consistent")
         nodes_out[0].set_shape(x.batch, 1, 1, self.lp.num_hidden)
+        self._rows = x.batch
         nh, ni = self.lp.num_hidden, self.lp.num_input_node
 
         def init_w(t):
@@ -80,17 +84,69 @@ class FullConnectLayer(Layer):
         """fullc_gather (reference fullc_layer-inl.hpp:120-122 + async_updater-inl.hpp:
         67-93): instead of all-reducing the nout x nin weight gradient, all-gather the
         B x (nin + nout) activations/gradients of every rank and form the global
-        gradient locally.  Active only under plain (non-sharded) data parallelism."""
+        gradient locally.  Under data parallelism only (dp_force: a one-rank process group
+        runs the gather too -- the RCCL path on one GPU).
+
+        fullc_gather = -1 (auto, the default) gathers when the gathered rows are fewer bytes
+        than the fp32 gradient they replace: world * B_local * (nin + nout) * 2 (bf16) <
+        nin * nout * 4.  AlexNet fc6 at 8 x 32 rows: 6.8 MB against 151 MB; the layer then
+        also takes its SGD step inside the weight-gradient GEMM (_fused_sgd).  The result is
+        the same global gradient either way; only the traffic differs."""
         from ..parallel.dp import world_info
-        # (dp_force: a one-rank process group runs the gather too -- the RCCL path on one GPU)
-        return bool(self.fullc_gather) and (world_info()[1] > 1 or bool(getattr(self.ctx, "dp_force", False)))
+        world = world_info()[1]
+        if not (world > 1 or bool(getattr(self.ctx, "dp_force", False))):
+            return False
+        if self.fullc_gather >= 0:
+            return bool(self.fullc_gather)
+        if self.ctx.is_gpu:
+            import torch.distributed as dist
+            if dist.get_backend() != "nccl":  # gloo rehearsal ranks on a GPU: device tensors stay on all-reduce
+                return False
+        nin, nout = self.lp.num_input_node, self.lp.num_hidden
+        return world * max(self._rows, 1) * (nin + nout) * 2 < nin * nout * 4
+
+    def _collective(self, fn):
+        """Run the collective call fn now -- or, while the step is being captured as HIP
+        graphs (NetTrainer._capture_plans sets ctx.graph_cut), end the current graph segment
+        and record fn as an eager call between segments: RCCL cannot join a capturing stream,
+        and every replay re-issues the gather on the same persistent buffers."""
+        cut = getattr(self.ctx, "graph_cut", None)
+        if cut is not None and torch.cuda.is_current_stream_capturing():
+            cut(fn)
+        else:
+            fn()
+
+    def _gather_io(self, key, t, rows):
+        """(source, output) of the all-gather of matrix t: persistent buffers, the source
+        zero-padded to `rows` (the node's capacity = the trainer's ceil(B/world) split, equal
+        on every rank), so an uneven split still gathers equal pieces and zero rows add
+        nothing to dW = dy^T x."""
+        import torch.distributed as dist
+        world = dist.get_world_size()
+        cols = t.shape[1]
+        buf = self._gbuf.get(key)
+        if buf is None or buf[1].shape != (world * rows, cols) or buf[1].dtype != t.dtype:
+            src = torch.zeros((rows, cols), dtype=t.dtype, device=t.device)
+            buf = (src, torch.empty((world * rows, cols), dtype=t.dtype, device=t.device))
+            self._gbuf[key] = buf
+        src, out = buf
+        if t.shape[0] == rows and t.is_contiguous():
+            return t, out
+        src[: t.shape[0]].copy_(t)
+        return src, out
 
     def forward(self, is_train, nodes_in, nodes_out):
         bias = self.b.w if self.b is not None else None
         x = nodes_in[0].mat()
         if is_train and self._gathering():
-            # backprop overwrites the input node with its gradient: gather it now
-            self._x_all = _all_gather_rows(x, nodes_in[0].shape[0])
+            # backprop overwrites the input node with its gradient: gather it now (async:
+            # the gather overlaps the rest of the forward and the backward above this layer)
+            import torch.distributed as dist
+            src, out = self._gather_io("x", x, nodes_in[0].shape[0])
+
+            def gather_x():
+                self._xwork = dist.all_gather_into_tensor(out, src, async_op=True)
+            self._collective(gather_x)
         ops.fc_forward(x, self.w.wb, bias, nodes_out[0].mat(), relu=self.fuse_relu)
 
     def _fused_sgd(self, x, dy, prop_grad, nodes_in, xw=None, dyw=None) -> bool:
@@ -104,8 +160,10 @@ class FullConnectLayer(Layer):
         upd = getattr(self.ctx, "sgd_fuse", None)
         if upd is None or not (getattr(self.ctx, "grad_overwrite", False) and self.w.overwrite) or not self.ctx.is_gpu:
             return False
-        if getattr(self.ctx, "dp_active", False) and xw is None:
-            return False  # a reduced gradient: the step must follow the reduction
+        if getattr(self.ctx, "sgd_fuse_gather_only", False) and xw is None:
+            return False  # a gradient still to be reduced: the step must follow the reduction
+        # under data parallelism the trainer hands out the updater for gathered layers only
+        assert not getattr(self.ctx, "dp_active", False) or getattr(self.ctx, "sgd_fuse_gather_only", False)
         spec = self.w
         lr, wd, mom, clip = upd.hyper(spec, self.ctx.epoch)
         a = upd.arena
@@ -123,6 +181,11 @@ class FullConnectLayer(Layer):
             ready = torch.cuda.Event()
             ready.record()
             side.wait_event(ready)
+            # the side stream reads tensors the main stream allocated: keep the allocator from
+            # recycling them until its work is done (dy is a persistent node today; this keeps it
+            # safe if it ever becomes a temporary)
+            dy.record_stream(side)
+            self._xs.record_stream(side)
             with torch.cuda.stream(side):
                 ok = ops.fc_backward_weight_sgd(self._xs, dy, spec.w, m, spec.wb, lr, wd, mom, clip)
             self.ctx.fc_side_used = True
@@ -156,10 +219,17 @@ class FullConnectLayer(Layer):
                 self.ctx.bias_grad(dy, self.b.g)
             return
         if self._gathering():
-            dy_all = _all_gather_rows(dy, nodes_out[0].shape[0])
-            x_all = self._x_all.wait()
-            self._x_all = None
-            dyw = dy_all.wait()
+            import torch.distributed as dist
+            dsrc, dyw = self._gather_io("dy", dy, nodes_out[0].shape[0])
+            x_all = self._gbuf["x"][1]
+
+            def gather_dy():
+                # the compute stream waits for both gathers (no host block)
+                dist.all_gather_into_tensor(dyw, dsrc)
+                if self._xwork is not None:
+                    self._xwork.wait()
+                    self._xwork = None
+            self._collective(gather_dy)
             if self._fused_sgd(x, dy, prop_grad, nodes_in, xw=x_all, dyw=dyw):
                 if self.b is not None:
                     self.ctx.bias_grad(dy, self.b.g)
@@ -187,32 +257,6 @@ class FullConnectLayer(Layer):
         if self.lp.no_bias == 0:
             out.append(b)
         return out
-
-
-class _Gathered:
-    def __init__(self, out, work):
-        self.out, self.work = out, work
-
-    def wait(self):
-        self.work.wait()
-        return self.out
-
-
-def _all_gather_rows(t: torch.Tensor, rows: int) -> _Gathered:
-    """Async all-gather of a (rows, cols) matrix over the data-parallel ranks.  Every
-    rank's slice is zero-padded to `rows` (the node's capacity = the trainer's
-    ceil(B/world) split, equal on all ranks), so an uneven split -- the last rank holding
-    fewer rows, as the reference allows -- still gathers equal-sized pieces; zero rows of
-    both x and dy add nothing to dW = dy^T x."""
-    import torch.distributed as dist
-    world = dist.get_world_size()
-    src = t.contiguous()
-    if src.shape[0] < rows:
-        pad = torch.zeros((rows,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
-        pad[: src.shape[0]] = src
-        src = pad
-    out = torch.empty((world * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
-    return _Gathered(out, dist.all_gather_into_tensor(out, src, async_op=True))
 
 
 # ============================================================================ conv

@@ -357,6 +357,9 @@ class NetTrainer:
     # ------------------------------------------------------------------ training
     def start_round(self, r: int):
         self.net.start_round(r)
+        # every rank calls start_round at the same point: adopt one tile choice for whatever any
+        # rank timed since the last sync (a short last batch, eval forwards)
+        self._sync_tiles(force=True)
         if self.test_on_server and self.reducer is not None:
             self.reducer.check_consistency()
 
@@ -403,13 +406,14 @@ class NetTrainer:
         ev = self._events()
         if self._graph_step(ev):
             self._after_step(ev)
+            self._sync_tiles()
             return
         net.forward(True, pre_hook=self.reducer.before_forward)
         self._mark(ev, 1)
         evals = self._train_eval(batch)
         if need_update:
             self.reducer.start_step()
-            net.ctx.sgd_fuse = self._sgd_fuse_target()
+            net.ctx.sgd_fuse, net.ctx.sgd_fuse_gather_only = self._sgd_fuse_target()
             net.ctx.dp_active = self.reducer.active
             net.ctx.epoch = self.epoch_counter
             red = self.reducer
@@ -417,7 +421,7 @@ class NetTrainer:
             try:
                 net.backprop(False, hook=hook, first=first, hook_due=red.due if hook is not None else None)
             finally:
-                net.ctx.sgd_fuse = None
+                net.ctx.sgd_fuse, net.ctx.sgd_fuse_gather_only = None, False
             self.reducer.finish()
             self._check_grads()
             self._mark(ev, 2)
@@ -440,15 +444,16 @@ class NetTrainer:
             self.sample_counter = 0
             self.epoch_counter += 1
 
-    def _sync_tiles(self):
+    def _sync_tiles(self, force: bool = False):
         """Data parallelism: after each of the first two updates (the eager step that times
-        the GEMM tile-table misses, and the step after it), every rank adopts the same tile
-        choice for every signature any rank timed (ops.gemm.sync_tune_table) -- a fixed point
-        in the schedule, so every rank enters the collective."""
-        if self.world <= 1 or not self.net.ctx.is_gpu:
+        the GEMM tile-table misses, and the step after it -- eager or graph-replayed) and at
+        every round start (force), every rank adopts the same tile choice for every signature
+        any rank timed (ops.gemm.sync_tune_table) -- fixed points in the schedule, so every
+        rank enters the collective."""
+        if self.world <= 1 or self.net is None or not self.net.ctx.is_gpu:
             return
         self._tile_syncs = getattr(self, "_tile_syncs", 0)
-        if self._tile_syncs < 2:
+        if self._tile_syncs < 2 or force:
             self._tile_syncs += 1
             from ..ops import gemm
             gemm.sync_tune_table()
@@ -539,47 +544,71 @@ class NetTrainer:
         if sync:
             self.prepare_save(opt_state=True)
         a = self.net.arena
-        state = {"m1": a.m1.detach().cpu(), "epoch_counter": torch.tensor([self.epoch_counter]),
+        # per parameter, keyed "layer:tag": the arena layout depends on the world size
+        # (fullc_gather segments sit on world * ALIGN boundaries), so a raw arena dump would map
+        # momentum onto the wrong parameters when resumed at another world size
+        state = {"m1_params": self._per_param(a.m1), "epoch_counter": torch.tensor([self.epoch_counter]),
                  "step_counter": self.net.ctx.step_counter.detach().cpu()}
         if a.m2 is not None:
-            state["m2"] = a.m2.detach().cpu()
+            state["m2_params"] = self._per_param(a.m2)
         torch.save(state, path)
+
+    def _per_param(self, buf):
+        return {f"{li}:{s.tag}": buf[s.offset:s.offset + s.numel].detach().cpu().clone()
+                for li, s in self.net.arena.specs}
+
+    def _load_per_param(self, buf, params, path):
+        for li, s in self.net.arena.specs:
+            key = f"{li}:{s.tag}"
+            t = params.get(key)
+            if t is None or t.numel() != s.numel:
+                raise ValueError(f"optimizer state {path}: parameter {key} missing or of another size")
+            buf[s.offset:s.offset + s.numel].copy_(t.reshape(-1))
 
     def load_optimizer_state(self, path: str):
         state = torch.load(path, map_location="cpu", weights_only=True)
         a = self.net.arena
-        if state["m1"].numel() != a.m1.numel():
-            raise ValueError(f"optimizer state {path}: {state['m1'].numel()} values, net has {a.m1.numel()}")
-        a.m1.copy_(state["m1"])
-        if "m2" in state:
-            a.ensure_second_moment()
-            a.m2.copy_(state["m2"])
+        if "m1_params" in state:
+            self._load_per_param(a.m1, state["m1_params"], path)
+            if "m2_params" in state:
+                a.ensure_second_moment()
+                self._load_per_param(a.m2, state["m2_params"], path)
+        else:  # round-3 sidecars: the raw arena of a run at the same world size
+            if state["m1"].numel() != a.m1.numel():
+                raise ValueError(f"optimizer state {path}: {state['m1'].numel()} values, net has {a.m1.numel()}")
+            a.m1.copy_(state["m1"])
+            if "m2" in state:
+                a.ensure_second_moment()
+                a.m2.copy_(state["m2"])
         self.net.ctx.step_counter.copy_(state["step_counter"])
 
     def _sgd_fuse_target(self):
-        """The arena updater when the fc weight steps may run inside the weight-gradient
-        GEMM (FullConnectLayer._fused_sgd): SGD, one micro-batch per update, no non-finite
-        check (the gradient never reaches memory).  One GPU: every fc layer; under data
-        parallelism only fullc_gather layers (ctx.dp_active), whose all-gathered gradient is
-        already global -- a reduced gradient must be reduced before its step."""
+        """(updater, gather_only): the arena updater when the fc weight steps may run inside
+        the weight-gradient GEMM (FullConnectLayer._fused_sgd) -- SGD, one micro-batch per
+        update, no non-finite check (the gradient never reaches memory) -- else None.
+        gather_only is True under data parallelism: then only fullc_gather layers may fuse,
+        whose all-gathered gradient is already global; any other gradient must be reduced
+        before its step (_fused_sgd asserts the pairing)."""
         net, red = self.net, self.reducer
         if not _FUSE_FC_SGD or net.device.type != "cuda" or self.update_period != 1 or self.check_nonfinite:
-            return None
+            return None, False
         upd = net.updater
         if upd is None or upd.algo != "sgd" or red is None:
-            return None
-        if not red.active and red.handles_update:
-            return None
-        return upd
+            return None, False
+        if red.active:
+            return upd, True
+        if red.handles_update:
+            # one process with the per-bucket side-stream update (overlap_update = 1): the
+            # buckets step the weights, so nothing fuses
+            return None, False
+        return upd, False
 
     def _graph_eligible(self) -> bool:
         net, red = self.net, self.reducer
         if not (self.cuda_graph != 0 and net.ctx.is_gpu and self.update_period == 1 and red is not None):
             return False
-        # fullc_gather layers run their all-gathers inside forward / backward: a collective
-        # cannot be captured (RCCL refuses to join a capturing stream), so those steps stay eager
-        if any(getattr(c.layer, "_gathering", None) is not None and c.layer._gathering() for c in net.connections):
-            return False
+        # (fullc_gather layers issue their all-gathers through ctx.graph_cut: eager calls between
+        # graph segments, like the bucket collectives)
         if self.cuda_graph < 0:
             return red.handles_update and self._local_batch() <= 64
         if red.handles_update:  # data parallel: segmented graphs around the collectives
@@ -593,7 +622,8 @@ class NetTrainer:
         that must wait for a bucket (the wait is an eager stream-event wait) and the
         backward is cut after each layer that completes a bucket (the eager call launches
         its RCCL collective and side-stream update), so collectives and waits stay
-        outside the graphs and replays keep the eager schedule."""
+        outside the graphs and replays keep the eager schedule.  fullc_gather layers cut the
+        graphs themselves around their row all-gathers (ctx.graph_cut)."""
         net, red = self.net, self.reducer
         dp = red.handles_update
         red.sync()
@@ -634,13 +664,17 @@ class NetTrainer:
                 cut(functools.partial(red.ready_buckets, bs))
 
         fwd, bwd = [], []
-        with torch.cuda.stream(torch.cuda.Stream()):
-            begin(fwd)
-            net.forward(True, pre_hook=fwd_hook if dp else None)
-            end()
-            begin(bwd)
-            net.backprop(False, hook=bwd_hook if dp else None, first=True, hook_due=bwd_due if dp else None)
-            end()
+        net.ctx.graph_cut = cut
+        try:
+            with torch.cuda.stream(torch.cuda.Stream()):
+                begin(fwd)
+                net.forward(True, pre_hook=fwd_hook if dp else None)
+                end()
+                begin(bwd)
+                net.backprop(False, hook=bwd_hook if dp else None, first=True, hook_due=bwd_due if dp else None)
+                end()
+        finally:
+            net.ctx.graph_cut = None
         torch.cuda.synchronize()
         return fwd, bwd
 

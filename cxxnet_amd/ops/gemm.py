@@ -155,11 +155,8 @@ GLDS_TILES = {0: (128, 256), 1: (128, 128), 2: (128, 128), 4: (192, 256), 5: (64
               # 8-wave 3/4-width tiles against wave quantisation: AlexNet conv3's data-gradient has
               # 169 256x256 tiles for 256 CUs, 226 of 256x192
               82: (256, 192), 83: (192, 256),
-              # 8-phase 256x256 pipeline (gemm_8p.hip): 90 = two barriers per phase, 91 = one
-              90: (256, 256), 91: (256, 256),
-              # one wave per SIMD, software-pipelined (gemm_4w.hip): 92/93 256x256, 94 128x256, 95 256x128
-              92: (256, 256), 93: (256, 256), 94: (128, 256), 95: (256, 128), 96: (128, 256), 97: (256, 128),
-              98: (96, 256), 100: (96, 256)}
+              # one wave per SIMD, address-free DMA issue (gemm_4w.hip): 113 = 32x32x16 MFMA
+              110: (256, 256), 111: (256, 128), 112: (128, 256), 113: (256, 256)}
 # operand loaders of gemm_glds.hip
 GL_K, GL_KG, GL_MN, GL_MNG, GL_KR = 0, 1, 2, 3, 4  # K_DIRECT, K_GATHER, MN_DIRECT, MN_GATHER, K_ROWGATHER
 EPI_F32_ACC_G, EPI_F32_ATOMIC_G, EPI_BF16_DB_G = 2, 3, 5
@@ -401,7 +398,11 @@ def _glds(a, b, amode, bmode, out, out_gstride, ldc, *, alpha=1.0, bias=None, bi
     if rc == -1:
         return False
     native.check(rc, "gemm_glds")
+    LAST_GLDS[0] = tile
     return True
+
+
+LAST_GLDS = [None]  # tile of the last LDS-DMA launch (tests check that a forced tile really ran)
 
 
 def _pick_tile(rows_i, rows_j, groups):

@@ -63,15 +63,19 @@ def test_bench_8_ranks_weak():
     out = _json(r.stdout)
     assert out["n_gpus"] == 8 and out["world_size"] == 8 and len(out["per_rank_ms_per_step"]) == 8
     assert out["config"]["global_batch"] == 64 and out["dp"]["mode"] == "allreduce"
+    # the same run times the conf's own (strong-scaling) configuration: 8 images over 8 ranks
+    st = out["strong"]
+    assert st["scaling"] == "strong" and st["global_batch"] == 8 and st["per_gpu_batch"] == 1
+    assert st["value"] > 0 and len(st["per_rank_ms_per_step"]) == 8
 
 
 def test_bench_8_ranks_strong_alexnet_fullc_gather():
-    """AlexNet at the strong-scaling split (256 over 8 ranks = 32 rows each) with fullc_gather:
-    the fc layers all-gather [in | out-grad] rows instead of reducing their 58.6 M gradient
-    values, so a rank hands <= 40 MB per step to collectives (fp32 here; the GPU gathers bf16)
-    against 244 MB of fp32 gradients without it."""
+    """AlexNet at the strong-scaling split (256 over 8 ranks = 32 rows each): fullc_gather's
+    default (auto) all-gathers the fc layers' [in | out-grad] rows instead of reducing their
+    58.6 M gradient values, so a rank hands <= 40 MB per step to collectives (fp32 here; the GPU
+    gathers bf16) against 244 MB of fp32 gradients without it."""
     r = _run(["bench.py", "--gpus", "8", "--device", "cpu", "--model", "alexnet", "--batch", "256",
-              "--scaling", "strong", "--set", "fullc_gather=1", "--steps", "1", "--warmup", "0"], timeout=900)
+              "--scaling", "strong", "--steps", "1", "--warmup", "0"], timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]
     out = _json(r.stdout)
     assert out["config"]["per_gpu_batch"] == 32 and out["dp"]["fullc_gather"]

@@ -69,11 +69,10 @@ def _worker(rank, world, port, steps, out, update_period, shard=0, B=8):
     extra = [("update_period", str(update_period))]
     if shard == 2:  # fullc_gather on both fc layers instead of sharding
         extra += [("fullc_gather", "1")]
-    else:
-        extra += [("update_on_server", str(shard))]
+    else:  # every gradient through the bucket collectives (fullc_gather off, not auto)
+        extra += [("update_on_server", str(shard)), ("fullc_gather", "0")]
     tr = _make(B, extra)
-    if shard == 2:
-        assert sum(getattr(s, "no_reduce", False) for _, s in tr.net.arena.specs) == 2
+    assert sum(getattr(s, "no_reduce", False) for _, s in tr.net.arena.specs) == (2 if shard == 2 else 0)
     if rank == 1:
         # different local init: the rank-0 broadcast must overwrite it
         pass
@@ -138,7 +137,7 @@ def test_shard_bucket_plan():
     from cxxnet_amd.parallel import dp
     with mock.patch.object(dp, "world_info", return_value=(1, 4)), \
             mock.patch.object(dp.GradReducer, "broadcast_params", lambda self, src=0: None):
-        tr = _make(4)
+        tr = _make(4, [("fullc_gather", "0")])  # (auto would all-gather the fc layers at world 4)
         red = dp.GradReducer(tr.net.arena, bucket_mb=0.001, shard=True)
     assert red.shard and red.buckets[0].start == 0 and red.buckets[-1].end == tr.net.arena.total
     for a, b in zip(red.buckets, red.buckets[1:]):

@@ -37,12 +37,22 @@ def _worker(rank, world, port, steps, out, mode, update_period, B, save_dir):
         extra += [("fullc_gather", "1")]
     elif mode == "shard_gather":  # sharded conv buckets + all-gathered fc layers
         extra += [("fullc_gather", "1"), ("dp_mode", "shard")]
+    elif mode == "auto":  # fullc_gather left at its default (auto: gather when fewer bytes move)
+        extra += [("dp_mode", "allreduce")]
     else:
         extra += [("dp_mode", "allreduce")]
+    if mode in ("allreduce", "shard", "shard_inplace"):
+        extra += [("fullc_gather", "0")]  # every gradient through the bucket collectives
     tr = _make(B, extra)
     assert tr.reducer.shard == (mode in ("shard", "shard_inplace", "shard_gather"))
     if "gather" in mode:
         assert len(tr.reducer.extra_ranges) == 2  # both fc weight matrices
+    elif mode == "auto":
+        # f1 (128 -> 16) gathers: 4 ranks x 3 rows x 144 values x 2 B < 128 x 16 x 4 B of gradient;
+        # f2 (16 -> 5) does not: 504 B of rows against 320 B of gradient
+        assert len(tr.reducer.extra_ranges) == 1
+    else:
+        assert not tr.reducer.extra_ranges
     if mode == "shard_inplace":
         assert tr.reducer.inplace
     x, y = _data(B)
@@ -106,6 +116,7 @@ def _single(B, update_period, steps=3):
     (8, "gather", 1, 16),
     (4, "shard_gather", 1, 10),   # fullc_gather composed with the sharded update
     (8, "shard_gather", 2, 16),
+    (4, "auto", 1, 10),           # the default: fullc_gather = auto picks the gather for both fc layers
 ])
 def test_dp_multi_rank_equals_single_process(tmp_path, world, mode, update_period, B):
     rs = _run(tmp_path, world, mode, update_period, B)
@@ -117,9 +128,9 @@ def test_dp_multi_rank_equals_single_process(tmp_path, world, mode, update_perio
     assert rs[0]["blob"] is not None
     # optimizer state: sharded mode gathers every rank's momentum slice before the save; the
     # saved state is in the multi-rank arena layout, compared per parameter
-    m1 = torch.load(str(tmp_path / "opt.state"), weights_only=True)["m1"]
-    trw = _make_world_layout(tmp_path, world)
-    assert _close([m1[o:o + n] for o, n in trw], _opt_params(tr, tr.net.arena.m1))
+    m1 = torch.load(str(tmp_path / "opt.state"), weights_only=True)["m1_params"]
+    keys = [f"{li}:{s.tag}" for li, s in tr.net.arena.specs]
+    assert _close([m1[k] for k in keys], _opt_params(tr, tr.net.arena.m1))
 
 
 def test_device_pruning_rule():

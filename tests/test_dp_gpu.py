@@ -55,11 +55,12 @@ def _worker(rank, world, port, steps, out, extra, backend="gloo"):
         tr.update(DataBatch(x.cuda(), y.cuda()))
     torch.cuda.synchronize()
     assert tr.reducer.check_consistency() == 0.0
-    if any(k == "cuda_graph" and v == "1" for k, v in extra) and not any(k == "fullc_gather" for k, _ in extra):
+    graph = any(k == "cuda_graph" and v == "1" for k, v in extra)
+    if graph:
         assert tr._graphs, "the data-parallel step did not run as graph segments"
         fwd, bwd = next(iter(tr._graphs.values()))
         assert sum(callable(i) and not isinstance(i, torch.cuda.CUDAGraph) for i in fwd + bwd) > 0
-    if any(k == "fullc_gather" for k, _ in extra):
+    if any(k == "fullc_gather" and v == "1" for k, v in extra) and not graph:
         # the gathered fc layer the kernel covers (f1: 16 x 128; f2's 5 outputs are not a multiple
         # of 8) ran its SGD step inside the weight-gradient GEMM
         assert tr.net.ctx.dp_active and len(tr.net.updater.fused_offsets) == 1, tr.net.updater.fused_offsets
@@ -135,12 +136,15 @@ def test_rccl_forced_fullc_gather_fused_sgd(tmp_path, mode):
     assert torch.equal(r0[: tr.net.arena.total], tr.net.arena.w.cpu())
 
 
-def test_rccl_forced_fullc_gather_graph_stays_eager(tmp_path):
-    """cuda_graph = 1 with fullc_gather under RCCL: the gathers cannot be captured, so the step
-    runs eagerly (it used to abort with hipErrorStreamCaptureImplicit) and stays exact."""
-    steps = 3
+@pytest.mark.parametrize("mode", ["shard", "allreduce"])
+def test_rccl_forced_fullc_gather_graph_segments(tmp_path, mode):
+    """cuda_graph = 1 with fullc_gather under RCCL: RCCL cannot join a capturing stream, so
+    the fc layers cut the graphs around their row all-gathers (ctx.graph_cut) and every replay
+    re-issues them on persistent buffers; step 1 eager (fused SGD), step 2 captures, steps 3-5
+    replay.  Bit-exact against the single-GPU run."""
+    steps = 5
     out = str(tmp_path / "w")
-    extra = [("dp_mode", "allreduce"), ("fullc_gather", "1"), ("cuda_graph", "1")]
+    extra = [("dp_mode", mode), ("dp_bucket_mb", "0.002"), ("fullc_gather", "1"), ("cuda_graph", "1")]
     mp.spawn(_worker, args=(1, _free_port(), steps, out, extra, "nccl"), nprocs=1, join=True)
     r0 = torch.load(out + ".r0", weights_only=True)
     from cxxnet_amd.io.data import DataBatch
