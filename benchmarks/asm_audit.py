@@ -123,7 +123,7 @@ def audit(body):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--src", default=os.path.join(KDIR, "gemm_4w.hip"))
-    ap.add_argument("--match", default="gemm_4w")
+    ap.add_argument("--match", default="gemm_4f")
     a = ap.parse_args()
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "k.s")

@@ -22,7 +22,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-GPU_IMG_S = 94800.0  # AlexNet b256 on one MI355X (bench.py, this round)
+GPU_IMG_S = 109200.0  # AlexNet b256 on one MI355X (bench.py, round 4 baseline: profiles/r4_baseline_models_1gpu.jsonl)
 
 
 def make_dataset(root, n, size, seed=0):

@@ -91,8 +91,22 @@ def build_kernels(verbose=False, force=False, jobs=8) -> str:
             list(ex.map(lambda c: _run(c, verbose), jobs_list))
     if force or _newer(target, objs) or jobs_list:
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", target + ".tmp"], verbose)
+        _check_stubs(target + ".tmp")
         os.replace(target + ".tmp", target)
     return target
+
+
+def _check_stubs(lib):
+    """Fail the build when a kernel's host launch stub is undefined: hipcc's host pass can drop
+    one silently (gemm_4w.hip lds_dma16), and the library would then fail only at dlopen on a
+    GPU box."""
+    nm = os.path.join(ROCM, "lib", "llvm", "bin", "llvm-nm")
+    if not os.path.exists(nm):
+        return
+    out = subprocess.run([nm, "-D", "--undefined-only", lib], stdout=subprocess.PIPE, text=True).stdout
+    bad = [l.split()[-1] for l in out.splitlines() if "__device_stub__" in l]
+    if bad:
+        raise RuntimeError(f"build failed: {len(bad)} undefined kernel launch stub(s) in {lib}, e.g. {bad[0]}")
 
 
 def build_wrapper(verbose=False, force=False) -> str:

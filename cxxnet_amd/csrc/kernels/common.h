@@ -3,6 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <functional>
+#include <vector>
+
 #define CXN_API extern "C" __attribute__((visibility("default")))
 
 typedef unsigned short bf16_t;  // storage type for bf16 tensors
@@ -103,3 +106,52 @@ static inline int cdiv(long a, long b) { return static_cast<int>((a + b - 1) / b
 // atomics in a run-dependent order (cross-block channel sums, bias-grad partials) use one
 // ordered pass instead, so two identical runs produce bitwise-identical results.
 extern int cxn_deterministic;
+
+// ----------------------------------------------------------------------------------------------
+// Launch-list recorder (launch_list.hip, cxn_rec_*): the native replay executor.  While a list is
+// open on the calling thread, every library launch also stores a closure over its launch shape
+// and argument VALUES; cxn_rec_replay re-issues the list on a stream from C++ in one call -- no
+// Python per kernel, no graph capture.  Every launch site goes through CXN_LAUNCH.
+namespace cxr {
+struct LaunchList {
+  std::vector<std::function<void(hipStream_t)>> ops;
+};
+LaunchList *&rec_slot();  // this thread's open list (nullptr: not recording)
+}  // namespace cxr
+
+#define CXN_LAUNCH(KER, GRID, BLOCK, SHMEM, STREAM, ...)                                          \
+  do {                                                                                           \
+    const dim3 cxn_grid_ = dim3(GRID), cxn_block_ = dim3(BLOCK);                                             \
+    const size_t cxn_shm_ = static_cast<size_t>(SHMEM);                                          \
+    hipLaunchKernelGGL(KER, cxn_grid_, cxn_block_, cxn_shm_, (STREAM), __VA_ARGS__);              \
+    if (::cxr::LaunchList *cxn_rec_ = ::cxr::rec_slot())                                         \
+      cxn_rec_->ops.emplace_back([=](hipStream_t cxn_s_) {                                       \
+        hipLaunchKernelGGL(KER, cxn_grid_, cxn_block_, cxn_shm_, cxn_s_, __VA_ARGS__);            \
+      });                                                                                        \
+  } while (0)
+
+// stream-ordered memset, recorded like a launch
+#define CXN_MEMSET(PTR, VAL, BYTES, STREAM)                                                      \
+  ([&]() -> hipError_t {                                                                         \
+    void *cxn_p_ = (PTR);                                                                        \
+    const int cxn_v_ = (VAL);                                                                    \
+    const size_t cxn_n_ = (BYTES);                                                               \
+    const hipError_t cxn_e_ = hipMemsetAsync(cxn_p_, cxn_v_, cxn_n_, (STREAM));                  \
+    if (::cxr::LaunchList *cxn_rec_ = ::cxr::rec_slot())                                         \
+      cxn_rec_->ops.emplace_back([=](hipStream_t cxn_s_) { (void)hipMemsetAsync(cxn_p_, cxn_v_, cxn_n_, cxn_s_); }); \
+    return cxn_e_;                                                                               \
+  }())
+
+// stream-ordered device-to-device copy, recorded like a launch
+#define CXN_MEMCPY_D2D(DST, SRC, BYTES, STREAM)                                                  \
+  ([&]() -> hipError_t {                                                                         \
+    void *cxn_d_ = (DST);                                                                        \
+    const void *cxn_s0_ = (SRC);                                                                 \
+    const size_t cxn_n_ = (BYTES);                                                               \
+    const hipError_t cxn_e_ = hipMemcpyAsync(cxn_d_, cxn_s0_, cxn_n_, hipMemcpyDeviceToDevice, (STREAM)); \
+    if (::cxr::LaunchList *cxn_rec_ = ::cxr::rec_slot())                                         \
+      cxn_rec_->ops.emplace_back([=](hipStream_t cxn_s_) {                                       \
+        (void)hipMemcpyAsync(cxn_d_, cxn_s0_, cxn_n_, hipMemcpyDeviceToDevice, cxn_s_);           \
+      });                                                                                        \
+    return cxn_e_;                                                                               \
+  }())

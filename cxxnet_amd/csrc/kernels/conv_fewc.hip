@@ -168,7 +168,7 @@ int launch(const bf16_t *x, const bf16_t *w, const float *bias, bf16_t *y, int N
   const int per_cu = lds <= 24 * 1024 ? 6 : lds <= 40 * 1024 ? 4 : lds <= 52 * 1024 ? 3 : 2;
   const long want = 256L * per_cu;
   const int grid = static_cast<int>(rows < want ? rows : want);
-  hipLaunchKernelGGL(conv_fewc_fwd<CF>, dim3(grid), dim3(NT), lds, s, x, w, bias, y, N, H, W, Ho, Wo, KH, KW, S, P,
+  CXN_LAUNCH(conv_fewc_fwd<CF>, dim3(grid), dim3(NT), lds, s, x, w, bias, y, N, H, W, Ho, Wo, KH, KW, S, P,
                      ldc, relu, KS);
   return 0;
 }

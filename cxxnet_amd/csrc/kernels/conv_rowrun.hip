@@ -228,7 +228,7 @@ int launch(const bf16_t *x, long x_bytes, const bf16_t *w, const float *bias, bf
   if (attr != hipSuccess) return -1;  // once per instantiation (thread-safe static); -1: caller falls back
   const long items = static_cast<long>(N) * ((Ho + RG - 1) / RG);
   const int grid = static_cast<int>(items < 256 ? items : 256);
-  hipLaunchKernelGGL(conv_rowrun_fwd<CFH>, dim3(grid), dim3(NT), static_cast<size_t>(lds), s, x, x_bytes, w, bias, y, y_bytes, N,
+  CXN_LAUNCH(conv_rowrun_fwd<CFH>, dim3(grid), dim3(NT), static_cast<size_t>(lds), s, x, x_bytes, w, bias, y, y_bytes, N,
                      H, W, C, Ho, Wo, KH, LP, make_fastdiv(LP), S, ldc, relu, KS, XB, ndma, g_counted);
   return 0;
 }
@@ -400,7 +400,7 @@ int launch_wgrad(const bf16_t *x, long x_bytes, const bf16_t *dy, long dy_bytes,
   if (attr != hipSuccess) return -1;  // once per instantiation (thread-safe static); -1: caller falls back
   const long items = static_cast<long>(N) * ((Ho + WR - 1) / WR);
   const int grid = static_cast<int>(items < 256 ? items : 256);
-  hipLaunchKernelGGL((conv_rowrun_wgrad<CFH, KF>), dim3(grid), dim3(NT), static_cast<size_t>(lds), s, x, x_bytes, dy,
+  CXN_LAUNCH((conv_rowrun_wgrad<CFH, KF>), dim3(grid), dim3(NT), static_cast<size_t>(lds), s, x, x_bytes, dy,
                      dy_bytes, dw, N, H, W, C, Ho, Wo, KH, LP, S, KR, XB, ndma_x, DB, ndma_d);
   return 0;
 }

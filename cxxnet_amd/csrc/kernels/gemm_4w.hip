@@ -40,6 +40,13 @@ using namespace cxg;
 
 namespace {
 
+// One 1-KiB LDS-DMA (16 bytes per lane) through a descriptor built from (base, records).  A free
+// function on purpose: with the builtin called directly inside the kernel's lambdas, hipcc's host
+// pass silently dropped the kernel's launch stub (undefined __device_stub__ at load time).
+__device__ __forceinline__ void lds_dma16(const char *p, uint32_t n, char *dst, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(p, n), (lds_void *)dst, 16, voff, 0, 0, 0);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_lgkm() {
   asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
@@ -143,21 +150,25 @@ gemm_4f(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
     }
   }
 
-  // Descriptors of K-tile t (relative to the slice): scalar base / record arithmetic only
-  auto rsrcA = [&](int t) __attribute__((always_inline)) -> rsrc_t {
+  // Descriptor of K-tile t (relative to the slice): base and record count, scalar arithmetic only
+  struct Desc {
+    const char *p;
+    uint32_t n;
+    uint32_t tap;  // gather: the K-tile's tap index kh * KW + kw
+  };
+  auto descA = [&](int t) __attribute__((always_inline)) -> Desc {
     const int kt = kt_beg + t;
     const bool in = kt < kt_end;
     const uint32_t step = in ? static_cast<uint32_t>(kt) * 128u : 0u;
-    return make_rsrc(reinterpret_cast<const char *>(A.ptr) + step, in ? A.nbytes - step : 0u);
+    return {reinterpret_cast<const char *>(A.ptr) + step, in ? A.nbytes - step : 0u, 0u};
   };
   // B: K_DIRECT as A; gather: the tap and channel block of the K-tile (Cg % 64 == 0)
-  auto rsrcB = [&](int t, uint32_t &tap) __attribute__((always_inline)) -> rsrc_t {
+  auto descB = [&](int t) __attribute__((always_inline)) -> Desc {
     const int kt = kt_beg + t;
     const bool in = kt < kt_end;
     if constexpr (BMODE == K_DIRECT) {
-      tap = 0;
       const uint32_t step = in ? static_cast<uint32_t>(kt) * 128u : 0u;
-      return make_rsrc(reinterpret_cast<const char *>(B.ptr) + step, in ? B.nbytes - step : 0u);
+      return {reinterpret_cast<const char *>(B.ptr) + step, in ? B.nbytes - step : 0u, 0u};
     } else {
       const uint32_t k0 = in ? static_cast<uint32_t>(kt) * 64u : 0u;
       const uint32_t q = fdiv(k0, B.fd_cg);  // tap index kh * KW + kw
@@ -165,9 +176,8 @@ gemm_4f(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
       const uint32_t kh = fdiv(q, B.fd_kw);
       const int kw = static_cast<int>(q - kh * static_cast<uint32_t>(B.KW));
       const int shift = (((static_cast<int>(kh) - B.pad_h) * B.W + (kw - B.pad_w)) * B.C + c0) * 2;
-      tap = q;
-      return make_rsrc(reinterpret_cast<const char *>(B.ptr) + shift,
-                       in ? static_cast<uint32_t>(static_cast<int>(B.nbytes) - shift) : 0u);
+      return {reinterpret_cast<const char *>(B.ptr) + shift,
+              in ? static_cast<uint32_t>(static_cast<int>(B.nbytes) - shift) : 0u, q};
     }
   };
   auto voffB = [&](int s, uint32_t tap) __attribute__((always_inline)) -> uint32_t {
@@ -177,13 +187,11 @@ gemm_4f(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
       return offB[s] | (((invB[s] >> tap) & 1u) << 31);
     }
   };
-  auto dmaA = [&](const rsrc_t &r, int stage, int s) __attribute__((always_inline)) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void *)(smem + stage * STAGE + (wave + NW * s) * 1024), 16,
-                                             offA[s], 0, 0, 0);
+  auto dmaA = [&](const char *p, uint32_t n, int stage, int s) __attribute__((always_inline)) {
+    lds_dma16(p, n, smem + stage * STAGE + (wave + NW * s) * 1024, offA[s]);
   };
-  auto dmaB = [&](const rsrc_t &r, uint32_t tap, int stage, int s) __attribute__((always_inline)) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void *)(smem + stage * STAGE + A_BYTES + (wave + NW * s) * 1024),
-                                             16, voffB(s, tap), 0, 0, 0);
+  auto dmaB = [&](const char *p, uint32_t n, uint32_t tap, int stage, int s) __attribute__((always_inline)) {
+    lds_dma16(p, n, smem + stage * STAGE + A_BYTES + (wave + NW * s) * 1024, voffB(s, tap));
   };
 
   // fragment read bases: row (lane & 15) [16x16x32] or (lane & 31) [32x32x16] of a fragment
@@ -227,17 +235,15 @@ gemm_4f(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
 
   // prologue: tiles 0 and 1 in flight, tile 0 landed everywhere, k-step 0 of tile 0 read
   {
-    uint32_t tap0, tap1;
-    const rsrc_t a0 = rsrcA(0), b0 = rsrcB(0, tap0);
+    const Desc a0 = descA(0), b0 = descB(0), a1 = descA(1), b1 = descB(1);
 #pragma unroll
-    for (int s = 0; s < NA; ++s) dmaA(a0, 0, s);
+    for (int s = 0; s < NA; ++s) dmaA(a0.p, a0.n, 0, s);
 #pragma unroll
-    for (int s = 0; s < NB; ++s) dmaB(b0, tap0, 0, s);
-    const rsrc_t a1 = rsrcA(1), b1 = rsrcB(1, tap1);
+    for (int s = 0; s < NB; ++s) dmaB(b0.p, b0.n, b0.tap, 0, s);
 #pragma unroll
-    for (int s = 0; s < NA; ++s) dmaA(a1, 1, s);
+    for (int s = 0; s < NA; ++s) dmaA(a1.p, a1.n, 1, s);
 #pragma unroll
-    for (int s = 0; s < NB; ++s) dmaB(b1, tap1, 1, s);
+    for (int s = 0; s < NB; ++s) dmaB(b1.p, b1.n, b1.tap, 1, s);
   }
   wait_vmcnt<NQ>();
   block_barrier();
@@ -273,11 +279,11 @@ gemm_4f(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
           constexpr int q = decltype(qc)::value;
           if constexpr (v == LA + q * LB / NQ) {
             if constexpr (q < NA) {
-              dmaA(rsrcA(t + 2), ST, q);
+              const Desc d = descA(t + 2);
+              dmaA(d.p, d.n, ST, q);
             } else {
-              uint32_t tap;
-              const rsrc_t rb = rsrcB(t + 2, tap);
-              dmaB(rb, tap, ST, q - NA);
+              const Desc d = descB(t + 2);
+              dmaB(d.p, d.n, d.tap, ST, q - NA);
             }
           }
         });
@@ -344,7 +350,7 @@ void launch_4f(const GOperand &A, const GOperand &B, const GEpi &E, int groups, 
   const int per = cdiv(ktiles, ksplit);
   ksplit = cdiv(ktiles, per);
   dim3 grid(ti * tj, ksplit, groups);
-  hipLaunchKernelGGL((gemm_4f<BM, BN, BMODE, EPI, MF>), grid, dim3(256), 0, s, A, B, E, ti, tj, per, ktiles);
+  CXN_LAUNCH((gemm_4f<BM, BN, BMODE, EPI, MF>), grid, dim3(256), 0, s, A, B, E, ti, tj, per, ktiles);
 }
 
 }  // namespace

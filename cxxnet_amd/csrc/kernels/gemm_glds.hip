@@ -373,12 +373,12 @@ int launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int 
     const long rows = static_cast<long>(tj) * WGN;
     if (rows * E.part_ld > E.part_elems) return -1;  // workspace too small: the caller sums dx itself
   }
-  hipLaunchKernelGGL((gemm_glds<BM, BN, WGM, WGN, STAGES, AMODE, BMODE, EPI, PIPE, BMC>), grid, dim3(64 * WGM * WGN), 0, s,
+  CXN_LAUNCH((gemm_glds<BM, BN, WGM, WGN, STAGES, AMODE, BMODE, EPI, PIPE, BMC>), grid, dim3(64 * WGM * WGN), 0, s,
                      A, B, E, ti, tj, per, ktiles);
   if constexpr (EPI == EPI_BF16_DB) {
     const int rows = tj * WGN;
     const int chunks = (rows + 255) / 256;  // 256 rows per block: <= ~10^3 adders per address
-    hipLaunchKernelGGL(db_partials_reduce, dim3((E.part_ld + 31) / 32, chunks), dim3(256), 0, s, E.dbias, rows,
+    CXN_LAUNCH(db_partials_reduce, dim3((E.part_ld + 31) / 32, chunks), dim3(256), 0, s, E.dbias, rows,
                        E.part_ld, E.dbias_final);
   }
   return 0;
@@ -487,7 +487,7 @@ void launch_seg(const GOperand &A, const GOperand &B, const GEpi &E, int groups,
   const int per = cdiv(ktiles, ksplit);
   ksplit = cdiv(ktiles, per);
   dim3 grid(ti * tj, ksplit, groups);
-  hipLaunchKernelGGL((gemm_seg<BM, BN, AMODE, BMODE, EPI>), grid, dim3(512), 0, s, A, B, E, ti, tj, per, ktiles);
+  CXN_LAUNCH((gemm_seg<BM, BN, AMODE, BMODE, EPI>), grid, dim3(512), 0, s, A, B, E, ti, tj, per, ktiles);
 }
 
 // ======================================================================================
@@ -636,7 +636,7 @@ void launch_pp(const GOperand &A, const GOperand &B, const GEpi &E, int groups, 
   const int per = cdiv(ktiles, ksplit);
   ksplit = cdiv(ktiles, per);
   dim3 grid(ti * tj, ksplit, groups);
-  hipLaunchKernelGGL((gemm_pp<AMODE, BMODE, EPI, NS>), grid, dim3(512), 0, s, A, B, E, ti, tj, per, ktiles);
+  CXN_LAUNCH((gemm_pp<AMODE, BMODE, EPI, NS>), grid, dim3(512), 0, s, A, B, E, ti, tj, per, ktiles);
 }
 
 // Tile ids (BM x BN, wave grid, stages); MN-major operands need a 128-wide tile side:

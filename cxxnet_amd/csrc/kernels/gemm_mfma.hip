@@ -546,10 +546,10 @@ void launch_t(const Operand &A, const Operand &B, const Epilogue &E, int groups,
   ksplit = cdiv(ktiles, per);
   dim3 grid(ti * tj, ksplit, groups);
   if (gemm_prefetch_depth() == 1)
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, WMs, AM, BMo, VA, VB, EPI, 1>), grid, dim3(NT), 0, s, A, B, E, ti, tj,
+    CXN_LAUNCH((gemm_kernel<BM, BN, WMs, AM, BMo, VA, VB, EPI, 1>), grid, dim3(NT), 0, s, A, B, E, ti, tj,
                        per, ktiles);
   else
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, WMs, AM, BMo, VA, VB, EPI, 2>), grid, dim3(NT), 0, s, A, B, E, ti, tj,
+    CXN_LAUNCH((gemm_kernel<BM, BN, WMs, AM, BMo, VA, VB, EPI, 2>), grid, dim3(NT), 0, s, A, B, E, ti, tj,
                        per, ktiles);
 }
 

@@ -272,12 +272,12 @@ __global__ void ins_pool_bwd(const bf16_t *__restrict__ x, const bf16_t *__restr
 CXN_API int cxn_rand_fill(float *out, long n, unsigned seed, int dist, float a, float b, void *stream) {
   if (n < 0 || n > 0x7fffffffL) return -1;
   if (n == 0) return 0;
-  rand_fill<<<nblocks(n, 256 * 64), NT, 0, S_>>>(out, static_cast<uint32_t>(n), seed, dist, a, b);
+  CXN_LAUNCH((rand_fill), nblocks(n, 256 * 64), NT, 0, S_, out, static_cast<uint32_t>(n), seed, dist, a, b);
   RET;
 }
 CXN_API int cxn_chan_reduce(const void *x, const void *g, const float *mean, float *out, long rows, int C, int mode,
                             void *stream) {
-  if (hipMemsetAsync(out, 0, sizeof(float) * 3 * C, S_) != hipSuccess) return -3;
+  if (CXN_MEMSET(out, 0, sizeof(float) * 3 * C, S_) != hipSuccess) return -3;
   const int cg = (C + 63) / 64;
   int rb = static_cast<int>((rows + 255) / 256);
   if (rb > 1024 / cg + 1) rb = 1024 / cg + 1;
@@ -285,7 +285,7 @@ CXN_API int cxn_chan_reduce(const void *x, const void *g, const float *mean, flo
   const int rpb = static_cast<int>((rows + rb - 1) / rb);
   rb = static_cast<int>((rows + rpb - 1) / rpb);
   if (rb < 1) rb = 1;
-  chan_reduce<<<dim3(rb, cg), NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)g, mean, out, rows, C, mode, rpb);
+  CXN_LAUNCH((chan_reduce), dim3(rb, cg), NT, 0, S_, (const bf16_t *)x, (const bf16_t *)g, mean, out, rows, C, mode, rpb);
   RET;
 }
 // stats: 3*C fp32 workspace; mean, inv: C fp32 outputs.  Two-pass (mean, then centred squares).
@@ -294,15 +294,15 @@ CXN_API int cxn_bn_stats(const void *x, float *stats, float *mean, float *inv, l
   const float scale = 1.f / static_cast<float>(rows);
   int rc = cxn_chan_reduce(x, nullptr, nullptr, stats, rows, C, 0, stream);
   if (rc) return rc;
-  bn_mean<<<(C + NT - 1) / NT, NT, 0, S_>>>(stats, mean, C, scale);
+  CXN_LAUNCH((bn_mean), (C + NT - 1) / NT, NT, 0, S_, stats, mean, C, scale);
   rc = cxn_chan_reduce(x, nullptr, mean, stats, rows, C, 1, stream);
   if (rc) return rc;
-  bn_inv<<<(C + NT - 1) / NT, NT, 0, S_>>>(stats, inv, C, scale, eps);
+  CXN_LAUNCH((bn_inv), (C + NT - 1) / NT, NT, 0, S_, stats, inv, C, scale, eps);
   RET;
 }
 CXN_API int cxn_bn_fwd(const void *x, void *y, void *xhat, void *xsave, const float *mean, const float *inv,
                        const float *slope, const float *bias, long rows, int C, void *stream) {
-  bn_fwd<<<nblocks(rows * C), NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, (bf16_t *)xhat, (bf16_t *)xsave, mean, inv,
+  CXN_LAUNCH((bn_fwd), nblocks(rows * C), NT, 0, S_, (const bf16_t *)x, (bf16_t *)y, (bf16_t *)xhat, (bf16_t *)xsave, mean, inv,
                                             slope, bias, rows, C);
   RET;
 }
@@ -312,33 +312,33 @@ CXN_API int cxn_bn_bwd(const void *g, const void *xsave, void *dx, const float *
                        void *stream) {
   int rc = cxn_chan_reduce(xsave, g, mean, sums, rows, C, 2, stream);
   if (rc) return rc;
-  bn_bwd_coeffs<<<(C + NT - 1) / NT, NT, 0, S_>>>(sums, inv, slope, gslope, gbias, coef, C,
+  CXN_LAUNCH((bn_bwd_coeffs), (C + NT - 1) / NT, NT, 0, S_, sums, inv, slope, gslope, gbias, coef, C,
                                                    1.f / static_cast<float>(rows));
-  bn_bwd<<<nblocks(rows * C), NT, 0, S_>>>((const bf16_t *)g, (const bf16_t *)xsave, (bf16_t *)dx, mean, coef, rows, C);
+  CXN_LAUNCH((bn_bwd), nblocks(rows * C), NT, 0, S_, (const bf16_t *)g, (const bf16_t *)xsave, (bf16_t *)dx, mean, coef, rows, C);
   RET;
 }
 CXN_API int cxn_prelu(const void *x, const void *g, void *y, const float *slope, long rows, int C, unsigned seed,
                       const int *counter, float rnd, int mode, void *stream) {
-  prelu_apply<<<nblocks(rows * C), NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)g, (bf16_t *)y, slope, rows, C,
+  CXN_LAUNCH((prelu_apply), nblocks(rows * C), NT, 0, S_, (const bf16_t *)x, (const bf16_t *)g, (bf16_t *)y, slope, rows, C,
                                                  seed, counter, rnd, mode);
   RET;
 }
 CXN_API int cxn_insanity(const void *x, const void *g, void *y, void *y2, long n, float lb, float ub, int train,
                          unsigned seed, const int *counter, int mode, void *stream) {
-  insanity_apply<<<nblocks(n), NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)g, (bf16_t *)y, (bf16_t *)y2, n, lb,
+  CXN_LAUNCH((insanity_apply), nblocks(n), NT, 0, S_, (const bf16_t *)x, (const bf16_t *)g, (bf16_t *)y, (bf16_t *)y2, n, lb,
                                              ub, train, seed, counter, mode);
   RET;
 }
 CXN_API int cxn_ins_pool_fwd(const void *x, void *y, void *ysave, int N, int H, int W, int C, int Ho, int Wo, int K,
                              int S, float keep, unsigned seed, const int *counter, void *stream) {
-  ins_pool_fwd<<<nblocks(static_cast<long>(N) * Ho * Wo * C), NT, 0, S_>>>(
+  CXN_LAUNCH((ins_pool_fwd), nblocks(static_cast<long>(N) * Ho * Wo * C), NT, 0, S_, 
       (const bf16_t *)x, (bf16_t *)y, (bf16_t *)ysave, N, H, W, C, Ho, Wo, K, S, keep, seed, counter);
   RET;
 }
 CXN_API int cxn_ins_pool_bwd(const void *x, const void *ypool, const void *gy, void *dx, int N, int H, int W, int C,
                              int Ho, int Wo, int K, int S, float keep, unsigned seed, const int *counter,
                              void *stream) {
-  ins_pool_bwd<<<nblocks(static_cast<long>(N) * H * W * C), NT, 0, S_>>>(
+  CXN_LAUNCH((ins_pool_bwd), nblocks(static_cast<long>(N) * H * W * C), NT, 0, S_, 
       (const bf16_t *)x, (const bf16_t *)ypool, (const bf16_t *)gy, (bf16_t *)dx, N, H, W, C, Ho, Wo, K, S, keep,
       seed, counter);
   RET;

@@ -1716,7 +1716,7 @@ __global__ void metric_accum(const float *__restrict__ part, int nb, int nm, dou
 CXN_API int cxn_nchw_f32_to_nhwc_bf16(const float *x, void *y, int N, int C, int H, int W, int Cp, int Wp,
                                       float scale, void *stream) {
   if (Wp < W) return -2;
-  nchw_f32_to_nhwc_bf16<<<nblocks(static_cast<long>(N) * H * W), NT, 0, S_>>>(x, (bf16_t *)y, N, C, H, W, Cp, Wp,
+  CXN_LAUNCH((nchw_f32_to_nhwc_bf16), nblocks(static_cast<long>(N) * H * W), NT, 0, S_, x, (bf16_t *)y, N, C, H, W, Cp, Wp,
                                                                               scale);
   RET;
 }
@@ -1731,7 +1731,7 @@ CXN_API int cxn_image_u8_to_nhwc_bf16(const void *pix, const int *prm, const flo
   const long nq = static_cast<long>(B) * h * (Wp / 4);
   if (C == 3 && Cp == 3 && mode <= 1 && Wp % 4 == 0 && reinterpret_cast<uintptr_t>(y) % 8 == 0 &&
       reinterpret_cast<uintptr_t>(pix) % 4 == 0 && npix * 3 >= 16 && nq < (1L << 31)) {
-    image_u8c3_nhwc3p<<<cdiv(nq, NT), NT, 0, S_>>>((const uint32_t *)pix, (npix * 3 + 3) / 4, cm, mean,
+    CXN_LAUNCH((image_u8c3_nhwc3p), cdiv(nq, NT), NT, 0, S_, (const uint32_t *)pix, (npix * 3 + 3) / 4, cm, mean,
                                                     make_fastdiv(static_cast<uint32_t>(Wp / 4)),
                                                     make_fastdiv(static_cast<uint32_t>(h)), w, Wp, mode, scale,
                                                     static_cast<uint32_t>(nq), (uint2 *)y);
@@ -1739,29 +1739,29 @@ CXN_API int cxn_image_u8_to_nhwc_bf16(const void *pix, const int *prm, const flo
   }
   if (C == 3 && Cp == 4 && Wp == w && mode <= 1 && npix % 4 == 0 && npix < (1L << 32) &&
       reinterpret_cast<uintptr_t>(pix) % 4 == 0) {
-    image_u8c3_nhwc4<<<nblocks(npix / 4), NT, 0, S_>>>((const uint32_t *)pix, cm, mean, npix / 4,
+    CXN_LAUNCH((image_u8c3_nhwc4), nblocks(npix / 4), NT, 0, S_, (const uint32_t *)pix, cm, mean, npix / 4,
                                                         make_fastdiv(static_cast<uint32_t>(h * w)), mode, scale,
                                                         (uint4 *)y);
     RET;
   }
   dim3 grid(cdiv(w, NT), B * h);
-  image_u8_to_nhwc_bf16<<<grid, NT, 0, S_>>>((const uint8_t *)pix, prm, cm, mean, B, h, w, C, Cp, Wp, Hm, Wm, mode,
+  CXN_LAUNCH((image_u8_to_nhwc_bf16), grid, NT, 0, S_, (const uint8_t *)pix, prm, cm, mean, B, h, w, C, Cp, Wp, Hm, Wm, mode,
                                              scale, (bf16_t *)y);
   RET;
 }
 CXN_API int cxn_nhwc_bf16_to_nchw_f32(const void *x, float *y, int N, int C, int H, int W, int Cp, int Wp,
                                       void *stream) {
-  nhwc_bf16_to_nchw_f32<<<nblocks(static_cast<long>(N) * C * H * W), NT, 0, S_>>>((const bf16_t *)x, y, N, C, H, W, Cp,
+  CXN_LAUNCH((nhwc_bf16_to_nchw_f32), nblocks(static_cast<long>(N) * C * H * W), NT, 0, S_, (const bf16_t *)x, y, N, C, H, W, Cp,
                                                                                   Wp);
   RET;
 }
 CXN_API int cxn_transpose(const void *x, void *y, int B, int R, int Cc, void *stream) {
   dim3 grid(cdiv(R, 32), cdiv(Cc, 32), B);
-  batched_transpose<<<grid, NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, R, Cc);
+  CXN_LAUNCH((batched_transpose), grid, NT, 0, S_, (const bf16_t *)x, (bf16_t *)y, R, Cc);
   RET;
 }
 CXN_API int cxn_conv_weight_flip(const void *w, void *wt, int G, int Co, int KH, int KW, int Ci, void *stream) {
-  conv_weight_flip<<<nblocks(static_cast<long>(G) * Co * KH * KW * Ci), NT, 0, S_>>>((const bf16_t *)w, (bf16_t *)wt,
+  CXN_LAUNCH((conv_weight_flip), nblocks(static_cast<long>(G) * Co * KH * KW * Ci), NT, 0, S_, (const bf16_t *)w, (bf16_t *)wt,
                                                                                      G, Co, KH, KW, Ci);
   RET;
 }
@@ -1782,7 +1782,7 @@ CXN_API int cxn_conv_weight_flip_multi(const void *const *ws, void *const *wts, 
       tab.b0[i] = nblk;
       nblk += d[0] * d[2] * d[3] * cdiv(d[1], 64) * cdiv(d[4], 64);  // 64 x 64 (co, ci) tiles per (g, tap)
     }
-    if (nblk) conv_weight_flip_multi<<<nblk, NT, 0, S_>>>(tab);
+    if (nblk) CXN_LAUNCH((conv_weight_flip_multi), nblk, NT, 0, S_, tab);
   }
   RET;
 }
@@ -1809,7 +1809,7 @@ CXN_API int cxn_pool_fwd(const void *x, void *y, void *arg, int N, int H, int W,
     const long total = static_cast<long>(N) * Ho * Wo * (C / 8);
     if (total >= (1L << 31)) return -2;  // fdiv (mulhi + n) stays exact below 2^31
 #define CXN_POOL_FWD(SSV, KSV)                                                                              \
-  pool_fwd_rows<SSV, KSV><<<cdiv(total, NT), NT, 0, S_>>>(                                                  \
+  CXN_LAUNCH((pool_fwd_rows<SSV, KSV>), cdiv(total, NT), NT, 0, S_,                                                   \
       (const bf16_t *)x, (bf16_t *)y, (uint8_t *)arg, H, W, C, Ho, Wo, KH, KW, S, P, mode, relu,             \
       make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(Wo * (C / 8))),        \
       make_fastdiv(static_cast<uint32_t>(Ho)), static_cast<uint32_t>(total))
@@ -1818,7 +1818,7 @@ CXN_API int cxn_pool_fwd(const void *x, void *y, void *arg, int N, int H, int W,
       constexpr int R = 4;
       const int HS = (Ho + R - 1) / R;
       const long tot = static_cast<long>(N) * HS * Wo * (C / 8);
-      pool_fwd_s1k3<R><<<cdiv(tot, NT), NT, 0, S_>>>(
+      CXN_LAUNCH((pool_fwd_s1k3<R>), cdiv(tot, NT), NT, 0, S_, 
           (const bf16_t *)x, (bf16_t *)y, (uint8_t *)arg, H, W, C, Ho, Wo, P, relu,
           make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(Wo * (C / 8))),
           make_fastdiv(static_cast<uint32_t>(HS)), static_cast<uint32_t>(tot));
@@ -1828,7 +1828,7 @@ CXN_API int cxn_pool_fwd(const void *x, void *y, void *arg, int N, int H, int W,
     else CXN_POOL_FWD(0, 0);
 #undef CXN_POOL_FWD
   } else {
-    pool_fwd<1><<<nblocks(static_cast<long>(N) * Ho * Wo * C), NT, 0, S_>>>(
+    CXN_LAUNCH((pool_fwd<1>), nblocks(static_cast<long>(N) * Ho * Wo * C), NT, 0, S_, 
         (const bf16_t *)x, (bf16_t *)y, (uint8_t *)arg, N, H, W, C, Ho, Wo, KH, KW, S, P, mode, relu);
   }
   RET;
@@ -1836,7 +1836,7 @@ CXN_API int cxn_pool_fwd(const void *x, void *y, void *arg, int N, int H, int W,
 
 CXN_API int cxn_pool_bwd_tie_all(const void *x, const void *y, const void *dy, void *dx, int N, int H, int W, int C,
                                  int Ho, int Wo, int KH, int KW, int S, int P, int relu, void *stream) {
-  pool_bwd_tie_all<<<nblocks(static_cast<long>(N) * H * W * C), NT, 0, S_>>>(
+  CXN_LAUNCH((pool_bwd_tie_all), nblocks(static_cast<long>(N) * H * W * C), NT, 0, S_, 
       (const bf16_t *)x, (const bf16_t *)y, (const bf16_t *)dy, (bf16_t *)dx, N, H, W, C, Ho, Wo, KH, KW, S, P, relu);
   RET;
 }
@@ -1847,7 +1847,7 @@ CXN_API int cxn_pool_bwd(const void *x, const void *arg, const void *dy, void *d
     const long total = static_cast<long>(N) * H * W * (C / 8);
     if (total >= (1L << 31)) return -2;  // fdiv (mulhi + n) stays exact below 2^31
 #define CXN_POOL_BWD(SSV, KSV)                                                                                  \
-  pool_bwd_rows<SSV, KSV><<<cdiv(total, NT), NT, 0, S_>>>(                                                      \
+  CXN_LAUNCH((pool_bwd_rows<SSV, KSV>), cdiv(total, NT), NT, 0, S_,                                                       \
       (const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, H, W, C, Ho, Wo, KH, KW, S, P, mode, \
       relu, make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(W * (C / 8))),          \
       make_fastdiv(static_cast<uint32_t>(H)), static_cast<uint32_t>(total))
@@ -1856,7 +1856,7 @@ CXN_API int cxn_pool_bwd(const void *x, const void *arg, const void *dy, void *d
       constexpr int R = 4;
       const int HS = (H + R - 1) / R;
       const long tot = static_cast<long>(N) * HS * W * (C / 8);
-      pool_bwd_s1k3<R><<<cdiv(tot, NT), NT, 0, S_>>>(
+      CXN_LAUNCH((pool_bwd_s1k3<R>), cdiv(tot, NT), NT, 0, S_, 
           (const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, H, W, C, Ho, Wo, P, relu,
           make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(W * (C / 8))),
           make_fastdiv(static_cast<uint32_t>(HS)), static_cast<uint32_t>(tot));
@@ -1864,7 +1864,7 @@ CXN_API int cxn_pool_bwd(const void *x, const void *arg, const void *dy, void *d
       const int i0 = P / 2, j0 = P / 2;
       const int HC = (P + H - 1) / 2 - i0 + 1, WC = (P + W - 1) / 2 - j0 + 1;
       const long tot = static_cast<long>(N) * HC * WC * (C / 8);
-      pool_bwd_s2k3<<<cdiv(tot, NT), NT, 0, S_>>>(
+      CXN_LAUNCH((pool_bwd_s2k3), cdiv(tot, NT), NT, 0, S_, 
           (const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, H, W, C, Ho, Wo, P, relu, i0,
           j0, WC, make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(WC * (C / 8))),
           make_fastdiv(static_cast<uint32_t>(HC)), static_cast<uint32_t>(tot));
@@ -1889,12 +1889,12 @@ CXN_API int cxn_pool_bwd(const void *x, const void *arg, const void *dy, void *d
       shm = static_cast<size_t>(C) * sizeof(float);
     }
     if (db && (ws == nullptr || ws_elems < static_cast<long>(nb) * C)) return -2;
-    pool_bwd<8><<<nb, NT, shm, S_>>>((const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, N, H,
+    CXN_LAUNCH((pool_bwd<8>), nb, NT, shm, S_, (const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, N, H,
                                      W, C, Ho, Wo, KH, KW, S, P, mode, relu, db ? ws : nullptr);
-    if (db) partials_reduce<<<partials_grid(nb, C), NT, 0, S_>>>(ws, nb, C, db);
+    if (db) CXN_LAUNCH((partials_reduce), partials_grid(nb, C), NT, 0, S_, ws, nb, C, db);
   } else {
     if (db) return -2;
-    pool_bwd<1><<<nblocks(static_cast<long>(N) * H * W * C), NT, 0, S_>>>(
+    CXN_LAUNCH((pool_bwd<1>), nblocks(static_cast<long>(N) * H * W * C), NT, 0, S_, 
         (const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, N, H, W, C, Ho, Wo, KH, KW, S, P,
         mode, relu, nullptr);
   }
@@ -1909,15 +1909,15 @@ CXN_API int cxn_lrn_fwd(const void *x, void *y, long npix, int C, int nsize, flo
     const int blocks = static_cast<int>((waves + NT / 64 - 1) / (NT / 64));
     const float sa = alpha / nsize;
     switch (nsize / 2) {
-      case 0: lrn_fwd_shfl<0><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, npix, C, sa, beta, knorm); break;
-      case 1: lrn_fwd_shfl<1><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, npix, C, sa, beta, knorm); break;
-      case 2: lrn_fwd_shfl<2><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, npix, C, sa, beta, knorm); break;
-      case 3: lrn_fwd_shfl<3><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, npix, C, sa, beta, knorm); break;
-      default: lrn_fwd_shfl<4><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, npix, C, sa, beta, knorm); break;
+      case 0: CXN_LAUNCH((lrn_fwd_shfl<0>), blocks, NT, 0, S_, (const bf16_t *)x, (bf16_t *)y, npix, C, sa, beta, knorm); break;
+      case 1: CXN_LAUNCH((lrn_fwd_shfl<1>), blocks, NT, 0, S_, (const bf16_t *)x, (bf16_t *)y, npix, C, sa, beta, knorm); break;
+      case 2: CXN_LAUNCH((lrn_fwd_shfl<2>), blocks, NT, 0, S_, (const bf16_t *)x, (bf16_t *)y, npix, C, sa, beta, knorm); break;
+      case 3: CXN_LAUNCH((lrn_fwd_shfl<3>), blocks, NT, 0, S_, (const bf16_t *)x, (bf16_t *)y, npix, C, sa, beta, knorm); break;
+      default: CXN_LAUNCH((lrn_fwd_shfl<4>), blocks, NT, 0, S_, (const bf16_t *)x, (bf16_t *)y, npix, C, sa, beta, knorm); break;
     }
     RET;
   }
-  lrn_fwd<<<nblocks(npix * C / 8), NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, npix, C, nsize / 2, alpha / nsize,
+  CXN_LAUNCH((lrn_fwd), nblocks(npix * C / 8), NT, 0, S_, (const bf16_t *)x, (bf16_t *)y, npix, C, nsize / 2, alpha / nsize,
                                                  beta, knorm);
   RET;
 }
@@ -1931,11 +1931,11 @@ CXN_API int cxn_lrn_bwd(const void *x, const void *dy, void *dx, long npix, int 
     const int blocks = static_cast<int>((waves + NT / 64 - 1) / (NT / 64));
     const float sa = alpha / nsize;
     switch (half) {
-      case 0: lrn_bwd_shfl<0><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm, mask_relu); break;
-      case 1: lrn_bwd_shfl<1><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm, mask_relu); break;
-      case 2: lrn_bwd_shfl<2><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm, mask_relu); break;
-      case 3: lrn_bwd_shfl<3><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm, mask_relu); break;
-      default: lrn_bwd_shfl<4><<<blocks, NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm, mask_relu); break;
+      case 0: CXN_LAUNCH((lrn_bwd_shfl<0>), blocks, NT, 0, S_, (const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm, mask_relu); break;
+      case 1: CXN_LAUNCH((lrn_bwd_shfl<1>), blocks, NT, 0, S_, (const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm, mask_relu); break;
+      case 2: CXN_LAUNCH((lrn_bwd_shfl<2>), blocks, NT, 0, S_, (const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm, mask_relu); break;
+      case 3: CXN_LAUNCH((lrn_bwd_shfl<3>), blocks, NT, 0, S_, (const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm, mask_relu); break;
+      default: CXN_LAUNCH((lrn_bwd_shfl<4>), blocks, NT, 0, S_, (const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, sa, beta, knorm, mask_relu); break;
     }
     RET;
   }
@@ -1945,28 +1945,28 @@ CXN_API int cxn_lrn_bwd(const void *x, const void *dy, void *dx, long npix, int 
     const int ppb = NT / tpp;
     const int blocks = static_cast<int>((npix + ppb - 1) / ppb);
     const size_t smem = static_cast<size_t>(ppb) * (C + 2 * half) * 3 * sizeof(float);
-    lrn_bwd_lds<<<blocks, NT, smem, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, half,
+    CXN_LAUNCH((lrn_bwd_lds), blocks, NT, smem, S_, (const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C, half,
                                           alpha / nsize, beta, knorm, mask_relu);
     RET;
   }
   if (half > 4 || x == dx) return -1;
-  lrn_bwd<<<nblocks(npix * C / 8), NT, 0, S_>>>((const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C,
+  CXN_LAUNCH((lrn_bwd), nblocks(npix * C / 8), NT, 0, S_, (const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, npix, C,
                                                  half, alpha / nsize, beta, knorm, mask_relu);
   RET;
 }
 CXN_API int cxn_act_fwd(const void *x, void *y, void *y2, long n, int kind, float b, void *stream) {
-  act_fwd<<<nblocks(n / 8 + 1), NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, (bf16_t *)y2, n, kind, b);
+  CXN_LAUNCH((act_fwd), nblocks(n / 8 + 1), NT, 0, S_, (const bf16_t *)x, (bf16_t *)y, (bf16_t *)y2, n, kind, b);
   RET;
 }
 CXN_API int cxn_act_bwd(const void *y, const void *dy, void *dx, long n, int kind, float b, void *stream) {
-  act_bwd<<<nblocks(n / 8 + 1), NT, 0, S_>>>((const bf16_t *)y, (const bf16_t *)dy, (bf16_t *)dx, n, kind, b);
+  CXN_LAUNCH((act_bwd), nblocks(n / 8 + 1), NT, 0, S_, (const bf16_t *)y, (const bf16_t *)dy, (bf16_t *)dx, n, kind, b);
   RET;
 }
 CXN_API int cxn_dropout(const void *x, void *y, long n, unsigned seed, const int *counter, float pkeep,
                         void *stream) {
   const double t = static_cast<double>(pkeep) * 4294967296.0;
   const uint32_t thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : static_cast<uint32_t>(t);
-  dropout_apply<<<nblocks(n / 8 + 1), NT, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, n, seed, counter, thresh, 1.0f / pkeep);
+  CXN_LAUNCH((dropout_apply), nblocks(n / 8 + 1), NT, 0, S_, (const bf16_t *)x, (bf16_t *)y, n, seed, counter, thresh, 1.0f / pkeep);
   RET;
 }
 
@@ -1982,23 +1982,23 @@ CXN_API int cxn_metric_eval(const float *p, int ldp, const float *lab, int ldl, 
   }
   int nb = (B + 3) / 4;
   if (nb > 256) nb = 256;
-  metric_rows<<<nb, 256, 0, S_>>>(p, ldp, lab, ldl, lw, B, K, ms, part);
-  metric_accum<<<1, 64, 0, S_>>>(part, nb, nm, acc);
+  CXN_LAUNCH((metric_rows), nb, 256, 0, S_, p, ldp, lab, ldl, lw, B, K, ms, part);
+  CXN_LAUNCH((metric_accum), 1, 64, 0, S_, part, nb, nm, acc);
   RET;
 }
 
 CXN_API int cxn_softmax(const void *x, void *y, float *pf, int rows, int K, void *stream) {
-  softmax_rows<<<cdiv(rows, 4), 256, 0, S_>>>((const bf16_t *)x, (bf16_t *)y, pf, rows, K);
+  CXN_LAUNCH((softmax_rows), cdiv(rows, 4), 256, 0, S_, (const bf16_t *)x, (bf16_t *)y, pf, rows, K);
   RET;
 }
 CXN_API int cxn_loss_grad(const float *p32, void *node, const float *label, int rows, int K, int lw, float scale,
                           int kind, void *stream) {
-  loss_grad<<<nblocks(static_cast<long>(rows) * K), NT, 0, S_>>>(p32, (bf16_t *)node, label, rows, K, lw, scale, kind);
+  CXN_LAUNCH((loss_grad), nblocks(static_cast<long>(rows) * K), NT, 0, S_, p32, (bf16_t *)node, label, rows, K, lw, scale, kind);
   RET;
 }
 CXN_API int cxn_colsum(const void *dy, float *db, long rows, int C, float *ws, long ws_elems, void *stream) {
   if (C % 8) {
-    colsum_scalar<<<cdiv(C, NT), NT, 0, S_>>>((const bf16_t *)dy, db, rows, C);
+    CXN_LAUNCH((colsum_scalar), cdiv(C, NT), NT, 0, S_, (const bf16_t *)dy, db, rows, C);
     RET;
   }
   const int CV = C / 8;
@@ -2012,11 +2012,11 @@ CXN_API int cxn_colsum(const void *dy, float *db, long rows, int C, float *ws, l
   if (static_cast<long>(cdiv(rows, rpb)) * C > ws_elems) return -2;
   dim3 grid(cdiv(rows, rpb), cdiv(CV, 64));
   if (!cxn_deterministic) {  // per-block atomics straight into db
-    colsum_bf16<<<grid, NT, 0, S_>>>((const bf16_t *)dy, ws, rows, C, rpb, db);
+    CXN_LAUNCH((colsum_bf16), grid, NT, 0, S_, (const bf16_t *)dy, ws, rows, C, rpb, db);
     RET;
   }
-  colsum_bf16<<<grid, NT, 0, S_>>>((const bf16_t *)dy, ws, rows, C, rpb, nullptr);
-  partials_reduce<<<partials_grid(static_cast<int>(grid.x), C), NT, 0, S_>>>(ws, static_cast<int>(grid.x), C, db);
+  CXN_LAUNCH((colsum_bf16), grid, NT, 0, S_, (const bf16_t *)dy, ws, rows, C, rpb, nullptr);
+  CXN_LAUNCH((partials_reduce), partials_grid(static_cast<int>(grid.x), C), NT, 0, S_, ws, static_cast<int>(grid.x), C, db);
   RET;
 }
 // dys / dbs / rows / Cs: n deferred bias gradients (C % 8 == 0 each); masks: nullable array of
@@ -2059,7 +2059,7 @@ CXN_API int cxn_colsum_multi(const void *const *dys, float *const *dbs, const lo
       tab.b0[i] = nblk;
       nblk += tab.s[i].nblk;
     }
-    if (nblk > 0) colsum_multi<<<nblk, NT, 0, S_>>>(tab);
+    if (nblk > 0) CXN_LAUNCH((colsum_multi), nblk, NT, 0, S_, tab);
   }
   RET;
 }
@@ -2074,7 +2074,7 @@ CXN_API int cxn_splitk_accumulate(const float *ws, int nsplit, long slab, float 
   long b = (slab / 4 + NT - 1) / NT;
   if (b > 4096) b = 4096;
   if (b < 1) b = 1;
-  splitk_accumulate<<<static_cast<int>(b), NT, 0, S_>>>(ws, nsplit, slab, out);
+  CXN_LAUNCH((splitk_accumulate), static_cast<int>(b), NT, 0, S_, ws, nsplit, slab, out);
   RET;
 }
 
@@ -2082,21 +2082,21 @@ CXN_API int cxn_splitk_finalize(const float *ws, int nsplit, long slab, void *ou
                                 const float *bias, int relu, int mask_relu, void *stream) {
   if (cols % 8) return -2;
   dim3 grid(cdiv(cols / 8, NT), static_cast<unsigned>(rows));
-  splitk_finalize<<<grid, NT, 0, S_>>>(ws, nsplit, slab, (bf16_t *)out, rows, cols, bias, relu, mask_relu);
+  CXN_LAUNCH((splitk_finalize), grid, NT, 0, S_, ws, nsplit, slab, (bf16_t *)out, rows, cols, bias, relu, mask_relu);
   RET;
 }
 CXN_API int cxn_cast_f32_bf16(const float *x, void *y, long n, void *stream) {
-  cast_f32_bf16<<<nblocks(n), NT, 0, S_>>>(x, (bf16_t *)y, n);
+  CXN_LAUNCH((cast_f32_bf16), nblocks(n), NT, 0, S_, x, (bf16_t *)y, n);
   RET;
 }
 CXN_API int cxn_add_bf16(const void *a, const void *b, void *y, long n, void *stream) {
-  add_bf16<<<nblocks(n / 8 + 1), NT, 0, S_>>>((const bf16_t *)a, (const bf16_t *)b, (bf16_t *)y, n);
+  CXN_LAUNCH((add_bf16), nblocks(n / 8 + 1), NT, 0, S_, (const bf16_t *)a, (const bf16_t *)b, (bf16_t *)y, n);
   RET;
 }
 CXN_API int cxn_fanout_bf16(const void *src, void *d0, void *d1, void *d2, void *d3, int nd, long n, void *stream) {
   if (nd < 1 || nd > 4 || (n & 7) != 0) return -2;
   const long n8 = n / 8;
-  fanout_bf16<<<nblocks(n8), NT, 0, S_>>>((const uint4 *)src, (uint4 *)d0, (uint4 *)d1, (uint4 *)d2, (uint4 *)d3, nd,
+  CXN_LAUNCH((fanout_bf16), nblocks(n8), NT, 0, S_, (const uint4 *)src, (uint4 *)d0, (uint4 *)d1, (uint4 *)d2, (uint4 *)d3, nd,
                                           n8);
   RET;
 }
@@ -2104,7 +2104,7 @@ CXN_API int cxn_sum_bf16(const void *s0, const void *s1, const void *s2, const v
                          void *stream, int mask) {
   if (ns < 2 || ns > 4 || (n & 7) != 0) return -2;
   const long n8 = n / 8;
-  sum_bf16<<<nblocks(n8), NT, 0, S_>>>((const uint4 *)s0, (const uint4 *)s1, (const uint4 *)s2, (const uint4 *)s3, ns,
+  CXN_LAUNCH((sum_bf16), nblocks(n8), NT, 0, S_, (const uint4 *)s0, (const uint4 *)s1, (const uint4 *)s2, (const uint4 *)s3, ns,
                                        (uint4 *)y, n8, mask);
   RET;
 }
@@ -2124,7 +2124,7 @@ CXN_API int cxn_concat(void *const *ins, const int *cs, int n, void *out, int Ct
   if (off != Ct) return -1;
   const long total8 = npix * (Ct / 8);
   if (total8 >= (1L << 32)) return -1;
-  concat8<<<nblocks(total8), NT, 0, S_>>>(a, n, static_cast<uint4 *>(out), Ct / 8, static_cast<uint32_t>(total8), bwd,
+  CXN_LAUNCH((concat8), nblocks(total8), NT, 0, S_, a, n, static_cast<uint4 *>(out), Ct / 8, static_cast<uint32_t>(total8), bwd,
                                           mask);
   RET;
 }
@@ -2133,16 +2133,16 @@ CXN_API int cxn_channel_copy(const void *src, int Cs, int soff, void *dst, int C
   const long total8 = npix * (Cc / 8);
   if (((Cs | soff | Cd | doff | Cc) & 7) == 0 && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0 &&
       total8 > 0 && total8 < (1L << 31)) {
-    channel_copy8<<<nblocks(total8), NT, 0, S_>>>((const uint4 *)src, Cs / 8, soff / 8, (uint4 *)dst, Cd / 8, doff / 8,
+    CXN_LAUNCH((channel_copy8), nblocks(total8), NT, 0, S_, (const uint4 *)src, Cs / 8, soff / 8, (uint4 *)dst, Cd / 8, doff / 8,
                                                   Cc / 8, static_cast<uint32_t>(total8), accumulate);
     RET;
   }
-  channel_copy<<<nblocks(npix * Cc), NT, 0, S_>>>((const bf16_t *)src, Cs, soff, (bf16_t *)dst, Cd, doff, Cc, npix,
+  CXN_LAUNCH((channel_copy), nblocks(npix * Cc), NT, 0, S_, (const bf16_t *)src, Cs, soff, (bf16_t *)dst, Cd, doff, Cc, npix,
                                                   accumulate);
   RET;
 }
 
 CXN_API int cxn_pad_rows(const void *src, void *dst, long rows, int L, int Lp, void *stream) {
-  pad_rows<<<nblocks(rows * Lp), NT, 0, S_>>>((const bf16_t *)src, (bf16_t *)dst, rows, L, Lp);
+  CXN_LAUNCH((pad_rows), nblocks(rows * Lp), NT, 0, S_, (const bf16_t *)src, (bf16_t *)dst, rows, L, Lp);
   RET;
 }

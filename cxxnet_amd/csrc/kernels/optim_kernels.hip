@@ -128,7 +128,7 @@ CXN_API int cxn_fused_update(const long *offs, const long *ns, const float *hype
     long bx = (maxn + NT * 4 - 1) / (NT * 4);
     if (bx > 2048) bx = 2048;
     dim3 grid(static_cast<unsigned>(bx), cnt);
-    fused_update<<<grid, NT, 0, s>>>(tab, w, g, st1, st2, static_cast<bf16_t *>(wb), algo, d1, d2);
+    CXN_LAUNCH((fused_update), grid, NT, 0, s, tab, w, g, st1, st2, static_cast<bf16_t *>(wb), algo, d1, d2);
   }
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
@@ -137,7 +137,7 @@ CXN_API int cxn_nonfinite_check(const float *g, long n, int *flag, void *stream)
   long b = (n + NT * 8 - 1) / (NT * 8);
   if (b > 1024) b = 1024;
   if (b < 1) b = 1;
-  nonfinite_check<<<b, NT, 0, static_cast<hipStream_t>(stream)>>>(g, n, flag);
+  CXN_LAUNCH((nonfinite_check), b, NT, 0, static_cast<hipStream_t>(stream), g, n, flag);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -145,6 +145,16 @@ CXN_API int cxn_scale_f32(float *x, long n, float sc, void *stream) {
   long b = (n + NT * 8 - 1) / (NT * 8);
   if (b > 2048) b = 2048;
   if (b < 1) b = 1;
-  scale_f32<<<b, NT, 0, static_cast<hipStream_t>(stream)>>>(x, n, sc);
+  CXN_LAUNCH((scale_f32), b, NT, 0, static_cast<hipStream_t>(stream), x, n, sc);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// *p += v on the device (the step counter that dropout seeds and the updaters read): a library
+// launch, so recorded launch lists and HIP graphs both advance it on every replay
+__global__ void add_i32(int *p, int v) {
+  if (threadIdx.x == 0) *p += v;
+}
+CXN_API int cxn_add_i32(int *p, int v, void *stream) {
+  CXN_LAUNCH((add_i32), 1, 64, 0, static_cast<hipStream_t>(stream), p, v);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -133,6 +133,14 @@ class Layer:
     type_name = "layer"
     allow_sharing = True
 
+
+    def replay_safe(self) -> bool:
+        """Whether this layer's GPU forward / backward launch only library kernels whose
+        arguments are step-invariant (per-step values read from device memory), so that the
+        C++ launch-list executor can record the step once and replay it (NetTrainer._list_step).
+        Layers that issue torch ops or pass per-step host values override this."""
+        return True
+
     def __init__(self, ctx: LayerContext):
         self.ctx = ctx
         self.lp = native.rt().LayerParam()

@@ -240,6 +240,10 @@ class PReluLayer(Layer):
     visited with tag "bias")."""
     type_name = "prelu"
 
+
+    def replay_safe(self) -> bool:
+        return False  # host-side per-step values / torch ops: the eager executor runs it
+
     def __init__(self, ctx):
         super().__init__(ctx)
         self.init_slope = 0.25
@@ -298,6 +302,10 @@ class InsanityLayer(Layer):
     x / U[lb,ub] for x<=0 in training, x / ((lb+ub)/2) at test; calm_start/calm_end anneal."""
     type_name = "insanity"
 
+
+    def replay_safe(self) -> bool:
+        return False  # host-side per-step values / torch ops: the eager executor runs it
+
     def __init__(self, ctx):
         super().__init__(ctx)
         self.lb, self.ub = 5.0, 10.0
@@ -348,6 +356,10 @@ class InsanityPoolingLayer(PoolingLayer):
     """`insanity_max_pooling` -- reference src/layer/insanity_pooling_layer-inl.hpp:222-286:
     in training each source pixel is shifted by +-1 in y or x with probability (1-keep)/4."""
 
+
+    def replay_safe(self) -> bool:
+        return False  # host-side per-step values / torch ops: the eager executor runs it
+
     def __init__(self, ctx):
         super().__init__(ctx, "max")
         self.type_name = "insanity_max_pooling"
@@ -387,6 +399,10 @@ class FixConnectLayer(Layer):
     """`fixconn` -- reference src/layer/fixconn_layer-inl.hpp:14-92: fixed sparse weight
     from a text file (`nrow ncol nnz` then `row col value` triples); no weight gradient."""
     type_name = "fixconn"
+
+
+    def replay_safe(self) -> bool:
+        return False  # host-side per-step values / torch ops: the eager executor runs it
 
     def __init__(self, ctx):
         super().__init__(ctx)
@@ -434,6 +450,10 @@ class PairTestLayer(Layer):
     each side.  The master's results are propagated."""
     type_name = "pairtest"
     allow_sharing = False
+
+
+    def replay_safe(self) -> bool:
+        return False  # host-side per-step values / torch ops: the eager executor runs it
 
     def __init__(self, ctx, master, slave):
         super().__init__(ctx)

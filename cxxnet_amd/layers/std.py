@@ -107,11 +107,12 @@ class FullConnectLayer(Layer):
 
     def _collective(self, fn):
         """Run the collective call fn now -- or, while the step is being captured as HIP
-        graphs (NetTrainer._capture_plans sets ctx.graph_cut), end the current graph segment
-        and record fn as an eager call between segments: RCCL cannot join a capturing stream,
-        and every replay re-issues the gather on the same persistent buffers."""
+        graphs or recorded as C++ launch lists (NetTrainer._capture_plans / _record_plans set
+        ctx.graph_cut), end the current segment and keep fn as an eager call between segments:
+        RCCL cannot join a capturing stream, a launch list holds library kernels only, and
+        every replay re-issues the gather on the same persistent buffers."""
         cut = getattr(self.ctx, "graph_cut", None)
-        if cut is not None and torch.cuda.is_current_stream_capturing():
+        if cut is not None:
             cut(fn)
         else:
             fn()
@@ -132,7 +133,7 @@ class FullConnectLayer(Layer):
         src, out = buf
         if t.shape[0] == rows and t.is_contiguous():
             return t, out
-        src[: t.shape[0]].copy_(t)
+        ops.copy_(src[: t.shape[0]], t.contiguous())
         return src, out
 
     def forward(self, is_train, nodes_in, nodes_out):
@@ -356,6 +357,10 @@ class ConvolutionLayer(Layer):
     def b(self):
         return self.params[1] if len(self.params) > 1 else None
 
+    def replay_safe(self) -> bool:
+        # the pre-pad path copies x into its zero-bordered buffer with a torch copy
+        return not (self._prepad_on and self.ctx.is_gpu)
+
     def _padded(self, x, refresh):
         """(input, geometry) for forward / weight-grad: x itself, or (pre-pad path) the
         zero-bordered copy of x with a pad-0 geometry.  refresh=False reuses the forward's copy
@@ -524,6 +529,9 @@ class PoolingLayer(Layer):
     def _tie_all(self) -> bool:
         return self.tie_all and self.mode == "max"
 
+    def replay_safe(self) -> bool:
+        return not self._tie_all()  # keeps its output with a torch copy
+
     def forward(self, is_train, nodes_in, nodes_out):
         lp = self.lp
         st = self._state(nodes_out[0]) if is_train else None
@@ -654,7 +662,7 @@ class FlattenLayer(Layer):
         x, y = nodes_in[0].data, nodes_out[0].data
         c, hw = self.dims
         if hw == 1 or c == 1:
-            y.view(-1).copy_(x.view(-1))
+            ops.copy_(y.view(-1), x.view(-1))
         else:
             ops.transpose(x, y, x.shape[0], hw, c)
 
@@ -664,7 +672,7 @@ class FlattenLayer(Layer):
         x, y = nodes_in[0].data, nodes_out[0].data
         c, hw = self.dims
         if hw == 1 or c == 1:
-            x.view(-1).copy_(y.view(-1))
+            ops.copy_(x.view(-1), y.view(-1))
         else:
             ops.transpose(y, x, x.shape[0], c, hw)
 
@@ -732,6 +740,9 @@ class L2LossLayer(LossLayerBase):
     type_name = "l2_loss"
     kind = "l2"
 
+    def replay_safe(self) -> bool:
+        return False  # fp32 copy of the scores through torch
+
     def forward(self, is_train, nodes_in, nodes_out):
         m = nodes_in[0].mat()
         self._p32(nodes_in[0]).copy_(m)
@@ -741,6 +752,9 @@ class MultiLogisticLayer(LossLayerBase):
     """`multi_logistic` -- reference src/layer/loss/multi_logistic_layer-inl.hpp (fwd sigmoid, grad s - y)."""
     type_name = "multi_logistic"
     kind = "multi_logistic"
+
+    def replay_safe(self) -> bool:
+        return False  # fp32 copy of the scores through torch
 
     def forward(self, is_train, nodes_in, nodes_out):
         m = nodes_in[0].mat()

@@ -117,7 +117,17 @@ _SIGS = {
     "cxn_fused_update": [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _F, _F, _P],
     "cxn_nonfinite_check": [_P, _L, _P, _P],
     "cxn_scale_f32": [_P, _L, _F, _P],
+    "cxn_add_i32": [_P, _I, _P],
+    # launch-list recorder (csrc/kernels/launch_list.hip)
+    "cxn_rec_begin": [],
+    "cxn_rec_end": [],
+    "cxn_rec_size": [_P],
+    "cxn_rec_replay": [_P, _P],
+    "cxn_rec_replay_many": [_P, _I, _P],
+    "cxn_rec_free": [_P],
+    "cxn_copy_d2d": [_P, _P, _L, _P],
 }
+_RESTYPE = {"cxn_rec_end": ctypes.c_void_p, "cxn_rec_free": None}
 
 
 def kernel_lib_path() -> str:
@@ -138,7 +148,7 @@ def kernels():
                 for name, args in _SIGS.items():
                     fn = getattr(lib, name)
                     fn.argtypes = args
-                    fn.restype = ctypes.c_int
+                    fn.restype = _RESTYPE.get(name, ctypes.c_int)
                 _k = lib
     return _k
 

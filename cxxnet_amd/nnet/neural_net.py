@@ -27,6 +27,7 @@ from ..layers import K_SHARED, LayerContext, Node, create_layer
 from ..layers.base import BinReader, BinWriter
 from ..updater import ArenaUpdater
 from .arena import ParamArena
+from ..ops.mode import frozen
 from ..io.data import U8Images
 
 K_CONV, K_FULLC, K_RELU, K_MAXPOOL, K_DROPOUT = 10, 1, 3, 11, 8
@@ -462,7 +463,11 @@ class NeuralNet:
         """pre_hook(layer_index) runs before each layer: the data-parallel reducer uses it
         to make the compute stream wait for the bucket holding that layer's weights (the
         reference's per-layer UpdateWait, neural_net-inl.hpp:125-131) and nothing more."""
-        self.ctx.step_counter.add_(1)
+        if self.ctx.is_gpu:  # a library launch: HIP graphs and recorded launch lists replay it
+            native.check(native.kernels().cxn_add_i32(self.ctx.step_counter.data_ptr(), 1, ops.gemm._stream()),
+                         "add_i32")
+        else:
+            self.ctx.step_counter.add_(1)
         with _BatchView(self):
             for i, conn in enumerate(self.connections):
                 if pre_hook is not None:
@@ -535,7 +540,7 @@ class NeuralNet:
         the default: interleaved A/B on one MI355X measured AlexNet b256 -0.6 %, GoogLeNet b128
         +2.0 %, VGG-16 b64 +0.5 % ms/step with the side stream (profiles/r2_ab_bias_side.jsonl)
         -- the column sums steal HBM and CU slots from the GEMMs they overlap."""
-        if os.environ.get("CXXNET_BIAS_SIDE", "0") != "1":
+        if os.environ.get("CXXNET_BIAS_SIDE", "0") != "1" or frozen():
             return None
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(device=self.device)
@@ -549,7 +554,7 @@ class NeuralNet:
         interleaved A/B on one MI355X, AlexNet b256 2.320 -> 2.375 ms and VGG-16 b64 9.40 ->
         9.41 ms with the side stream (profiles/r3_ab_fc_sgd_side.jsonl) -- the concurrent HBM
         stream slows the GEMMs it overlaps by more than it hides.  Not under HIP-graph capture."""
-        if os.environ.get("CXXNET_FC_SGD_SIDE", "0") != "1" or torch.cuda.is_current_stream_capturing():
+        if os.environ.get("CXXNET_FC_SGD_SIDE", "0") != "1" or frozen():
             return None
         if getattr(self, "_fc_side", None) is None:
             self._fc_side = torch.cuda.Stream(device=self.device)

@@ -27,6 +27,28 @@ from ..utils.metric import DeviceMetricSet, MetricSet
 from .neural_net import NeuralNet
 
 
+class LaunchList:
+    """One recorded run of library launches (csrc/kernels/launch_list.hip), replayed from C++."""
+    __slots__ = ("h", "n")
+
+    def __init__(self, h):
+        self.h = h
+        self.n = native.kernels().cxn_rec_size(h) if h else 0
+
+    def replay(self):
+        if self.n:
+            from ..ops.gemm import _stream
+            native.check(native.kernels().cxn_rec_replay(self.h, _stream()), "rec_replay")
+
+    def __del__(self):
+        if self.h:
+            try:
+                native.kernels().cxn_rec_free(self.h)
+            except Exception:
+                pass
+            self.h = None
+
+
 def _dist_ready() -> bool:
     import torch.distributed as dist
     return dist.is_available() and dist.is_initialized()
@@ -90,6 +112,12 @@ class NetTrainer:
         self.cuda_graph = int(os.environ.get("CXXNET_CUDA_GRAPH", "-1"))
         self._graphs = {}
         self._graph_warm = {}
+        # native launch-list executor (csrc/kernels/launch_list.hip): when graphs are not used,
+        # the step's library launches are recorded once into C++ lists and replayed from C++
+        # (one call per segment instead of ~10 us of Python per kernel); -1 auto, 0 off, 1 on
+        self.launch_replay = int(os.environ.get("CXXNET_LAUNCH_REPLAY", "-1"))
+        self._lists = {}
+        self._list_warm = {}
         # failure detection: every N updates, fail fast if any gradient was non-finite
         # (the reference only zeroes NaN inside clip, sgd_updater-inl.hpp:17)
         self.check_nonfinite = 0
@@ -149,6 +177,8 @@ class NetTrainer:
             self.overlap_update = int(val)
         elif name == "cuda_graph":
             self.cuda_graph = int(val)
+        elif name == "launch_replay":
+            self.launch_replay = int(val)
         elif name == "precision":
             if val not in ("bf16", "fp32"):
                 raise ValueError(f"precision must be bf16 or fp32, not {val}")
@@ -404,7 +434,7 @@ class NetTrainer:
         net = self.net
         self._cur_batch = batch
         ev = self._events()
-        if self._graph_step(ev):
+        if self._graph_step(ev) or self._list_step(ev):
             self._after_step(ev)
             self._sync_tiles()
             return
@@ -681,10 +711,142 @@ class NetTrainer:
     @staticmethod
     def _replay(plan):
         for item in plan:
-            if isinstance(item, torch.cuda.CUDAGraph):
+            if isinstance(item, (torch.cuda.CUDAGraph, LaunchList)):
                 item.replay()
             else:
                 item()
+
+    # ------------------------------------------------------------------ native launch lists
+    def _list_eligible(self) -> bool:
+        """The C++ launch-list executor runs a step when HIP graphs do not.  Auto (-1): in the
+        host-bound regime only -- per-GPU batch <= 32, where Python enqueues a step about as
+        slowly as the GPU runs it; larger steps are GPU-bound and keep the eager path, whose fc
+        weight steps run inside the weight-gradient GEMMs (a planned step takes them through
+        the arena updater: its learning rate is a host value per step)."""
+        net, red = self.net, self.reducer
+        if self.launch_replay == 0 or not net.ctx.is_gpu or self.update_period != 1 or red is None:
+            return False
+        if self._graph_eligible():
+            return False
+        if not all(c.layer.replay_safe() for c in net.connections):
+            return False
+        if self.launch_replay < 0:
+            return self._local_batch() <= 32
+        return True
+
+    def _list_step(self, ev=None) -> bool:
+        """One training step replayed from recorded C++ launch lists: the forward and backward
+        passes as runs of library launches, with the same eager calls between them as the
+        graph plan (bucket collectives and waits, fullc_gather all-gathers).  The first step
+        of each batch size runs eagerly (GEMM tile tuning, lazy buffers); the second runs AND
+        records (_record_step); later steps replay.  Returns False to take the eager path."""
+        if not self._list_eligible():
+            return False
+        net, red = self.net, self.reducer
+        key = net.cur_batch
+        plans = self._lists.get(key)
+        if plans is None:
+            if self._list_warm.get(key, 0) < 1:
+                self._list_warm[key] = 1
+                return False
+            self._lists[key] = self._record_step(ev)
+            return True
+        fwd, bwd = plans[0], plans[1]
+        self._replay(fwd)
+        self._mark(ev, 1)
+        self._finish_planned_step(ev, lambda: self._replay(bwd))
+        return True
+
+    def _finish_planned_step(self, ev, run_bwd):
+        """The part of a planned (graph / launch-list) step after the forward: training
+        metrics, the backward (run_bwd) framed by the reducer, the optimizer."""
+        net, red = self.net, self.reducer
+        evals = self._train_eval(self._cur_batch)
+        if red.handles_update:
+            red.start_step()
+            run_bwd()
+            red.finish()
+            self._check_grads()
+            self._mark(ev, 2)
+        else:
+            run_bwd()
+            self._check_grads()
+            self._mark(ev, 2)
+            net.update(self.epoch_counter)
+        if evals is not None:
+            self.train_metric.add_eval(evals, self._label_fields(self._cur_batch))
+        self.epoch_counter += 1
+
+    def _record_step(self, ev):
+        """Run one step while recording its library launches into C++ lists, cut at the same
+        points as _capture_plans (here the eager calls also run, since the recording run is
+        a real step).  Allocations of the recording run come from a private memory pool kept
+        with the plan, so every address a list holds stays valid for its replays."""
+        from ..ops.mode import set_recording
+        net, red = self.net, self.reducer
+        dp = red.handles_update
+        k = native.kernels()
+        pool = torch.cuda.MemPool()
+        cur = {}
+
+        def begin(plan):
+            native.check(k.cxn_rec_begin(), "rec_begin")
+            cur["plan"] = plan
+
+        def end():
+            cur["plan"].append(LaunchList(k.cxn_rec_end()))
+
+        def cut(fn):
+            plan = cur["plan"]
+            end()
+            fn()
+            plan.append(fn)
+            begin(plan)
+
+        waited, ready = set(), set()
+
+        def fwd_hook(li):
+            new = [bi for bi in red.layer_buckets.get(li, ()) if bi not in waited]
+            if new:
+                waited.update(new)
+                cut(functools.partial(red.before_forward, li))
+
+        def bwd_due(li):
+            return any(bi not in ready and li <= b.li_min for bi, b in enumerate(red.buckets))
+
+        def bwd_hook(li):
+            bs = [bi for bi, b in enumerate(red.buckets) if bi not in ready and li <= b.li_min]
+            if bs:
+                ready.update(bs)
+                cut(functools.partial(red.ready_buckets, bs))
+
+        fwd, bwd = [], []
+
+        def record_bwd():
+            begin(bwd)
+            try:
+                net.backprop(False, hook=bwd_hook if dp else None, first=True, hook_due=bwd_due if dp else None)
+            finally:
+                end()
+
+        net.ctx.graph_cut = cut
+        set_recording(True)
+        try:
+            with torch.cuda.use_mem_pool(pool):
+                begin(fwd)
+                try:
+                    net.forward(True, pre_hook=fwd_hook if dp else None)
+                finally:
+                    end()
+                self._mark(ev, 1)
+                self._finish_planned_step(ev, record_bwd)
+        finally:
+            set_recording(False)
+            net.ctx.graph_cut = None
+            h = k.cxn_rec_end()  # an exception left a list open: drop it
+            if h:
+                k.cxn_rec_free(h)
+        return fwd, bwd, pool
 
     def _graph_step(self, ev=None) -> bool:
         """One training step as HIP-graph replays of the forward and backward passes plus
@@ -715,21 +877,7 @@ class NetTrainer:
         fwd, bwd = gr
         self._replay(fwd)
         self._mark(ev, 1)
-        evals = self._train_eval(self._cur_batch)
-        if red.handles_update:
-            red.start_step()
-            self._replay(bwd)
-            red.finish()
-            self._check_grads()
-            self._mark(ev, 2)
-        else:
-            self._replay(bwd)
-            self._check_grads()
-            self._mark(ev, 2)
-            net.update(self.epoch_counter)
-        if evals is not None:
-            self.train_metric.add_eval(evals, self._label_fields(self._cur_batch))
-        self.epoch_counter += 1
+        self._finish_planned_step(ev, lambda: self._replay(bwd))
         return True
 
     # ------------------------------------------------------------------ inference

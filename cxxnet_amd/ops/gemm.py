@@ -21,7 +21,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import native
-from .mode import native as _native_t
+from .mode import frozen, native as _native_t
 
 DIRECT_K, DIRECT_MN, GATHER_K, GATHER_MN = 0, 1, 2, 3
 EPI_BF16, EPI_F32, EPI_F32_ACC, EPI_F32_ATOMIC = 0, 1, 2, 3
@@ -281,7 +281,7 @@ def _tuned_tile(key, run, out, default, extra=(), tune=True, cands=None):
     t = _TUNE.get(key)
     if t is not None:
         return t
-    if not (tune and _glds_cfg["tune"]) or torch.cuda.is_current_stream_capturing():
+    if not (tune and _glds_cfg["tune"]) or frozen():
         return default()
     if _TUNE_LOG:
         import sys

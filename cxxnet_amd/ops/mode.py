@@ -22,3 +22,17 @@ def reference_precision() -> bool:
 def native(t: torch.Tensor) -> bool:
     """Whether an op on tensor t runs its HIP kernel (GPU tensor, bf16 mode)."""
     return t.is_cuda and not _REF["on"]
+
+
+_REC = {"on": False}
+
+
+def set_recording(on: bool):
+    """A C++ launch list is being recorded (NetTrainer._list_step)."""
+    _REC["on"] = bool(on)
+
+
+def frozen() -> bool:
+    """The step's launches are being frozen for replay -- recorded into a C++ launch list or
+    captured into a HIP graph: no autotuning launches, no side streams, no host reads."""
+    return _REC["on"] or torch.cuda.is_current_stream_capturing()

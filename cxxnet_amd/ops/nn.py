@@ -83,6 +83,17 @@ def nhwc_to_nchw(x: torch.Tensor, C: int, W: int = 0) -> torch.Tensor:
     return out
 
 
+def copy_(dst: torch.Tensor, src: torch.Tensor):
+    """dst <- src for contiguous tensors of equal size: a library copy on the GPU (recorded into
+    launch lists, so a replayed step repeats it), torch on the CPU."""
+    if not (_native_t(src) and dst.is_contiguous() and src.is_contiguous()):
+        dst.copy_(src)
+        return
+    assert dst.numel() == src.numel() and dst.dtype == src.dtype
+    native.check(_k().cxn_copy_d2d(dst.data_ptr(), src.data_ptr(), src.numel() * src.element_size(), _stream()),
+                 "copy_d2d")
+
+
 def transpose(x: torch.Tensor, y: torch.Tensor, B: int, R: int, Cc: int):
     """y[b][Cc][R] = x[b][R][Cc]."""
     if not _native_t(x):

@@ -37,7 +37,7 @@ CONV = [
     (4, 12, 12, 256, 256, 3, 1, 1, 2),   # 2 groups of 128 channels
     (4, 15, 15, 64, 128, 3, 2, 1, 1),    # stride 2
     (8, 7, 7, 192, 64, 1, 1, 0, 1),      # 1x1
-    (2, 9, 9, 128, 96, 5, 1, 2, 1),      # 5x5 pad 2: 25 taps
+    (2, 9, 9, 128, 128, 5, 1, 2, 1),     # 5x5 pad 2: 25 taps
 ]
 
 
