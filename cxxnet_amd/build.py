@@ -128,10 +128,24 @@ def build_wrapper(verbose=False, force=False) -> str:
     return target
 
 
+def build_im2bin(verbose=False, force=False) -> str:
+    """The native im2bin executable (csrc/tools/im2bin.cpp)."""
+    src = os.path.join(CSRC, "tools", "im2bin.cpp")
+    deps = [src] + glob.glob(os.path.join(CSRC, "runtime", "*.h"))
+    target = os.path.join(OUT, "im2bin")
+    if force or _newer(target, deps):
+        os.makedirs(OUT, exist_ok=True)
+        _run(["g++", "-O2", "-std=c++17", "-Wall", "-Wno-unused-result"] + (SAN_FLAGS if _san["on"] else []) +
+             [src, "-o", target + ".tmp", "-lz", "-lpthread", "-ldl"], verbose)
+        os.replace(target + ".tmp", target)
+    return target
+
+
 def build_all(verbose=False, force=False):
     rt = build_runtime(verbose, force)
     k = build_kernels(verbose, force)
     w = build_wrapper(verbose, force)
+    build_im2bin(verbose, force)
     return rt, k, w
 
 

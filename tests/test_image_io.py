@@ -345,3 +345,19 @@ def test_native_decode_iterator_matches_its_crop_params(jpegset, kind):
             if m:
                 ref = ref[:, ::-1]
             assert np.array_equal(pix[r].numpy(), ref)
+
+
+def test_native_im2bin_executable_matches_python_tool(imgset, tmp_path):
+    """The C++ im2bin executable (csrc/tools/im2bin.cpp, the reference tool's command line)
+    writes the same pages, byte for byte, as the Python tool."""
+    import subprocess
+    from cxxnet_amd import build
+    exe = build.build_im2bin()
+    d, _ = imgset
+    out = tmp_path / "native.bin"
+    r = subprocess.run([exe, str(d / "all.lst"), str(d) + "/", str(out)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert "images processed to 1 pages" in r.stdout
+    assert out.read_bytes() == (d / "all.bin").read_bytes()
+    bad = subprocess.run([exe, "only-one-arg"], capture_output=True, text=True)
+    assert bad.returncode == 255 and "Usage: im2bin" in bad.stderr
