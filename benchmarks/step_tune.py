@@ -20,7 +20,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 KK = (0, 1, 2, 7, 10, 15, 20, 21, 25, 30, 31, 33, 34, 35, 36, 37, 38, 39, 50, 51, 70, 71, 72, 73, 74, 75, 76, 77,
-      78, 79, 80, 81, 82, 83)
+      78, 79, 80, 81, 82, 83, 110, 111, 112, 113, 114, 115)
 MM = (1, 2, 13, 17, 23, 36, 40, 41)
 SHORT = (0, 1, 2, 7, 10, 15, 34, 37, 38, 75, 76, 77, 78, 79, 80, 81)
 

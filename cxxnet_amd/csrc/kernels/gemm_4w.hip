@@ -90,7 +90,17 @@ gemm_4f(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
   constexpr int LA = NF + 10 < PER ? NF + 10 : PER;
   constexpr int LC = NF + 6 < PER ? NF + 6 : PER;
   constexpr int LB = T - LA - LC;
-  static_assert(NF <= LA && NF <= LC && LB >= NQ, "schedule");
+  static_assert(NF <= LA && NF <= LC && LA + LC <= T, "schedule");
+  // DMA q of tile t+2 rides in front of MFMA dslot(q): spread over [B] when it has an MFMA per
+  // DMA (the large tiles), else over [B] and [C] (small tiles: stage S is free from the first
+  // barrier on); the second barrier then waits for tile t+1 with vmcnt(NQB), the DMAs of tile
+  // t+2 issued before it
+  constexpr int DSPAN = LB >= NQ ? LB : T - LA;
+  constexpr int NQB = [&]() constexpr {
+    int n = 0;
+    for (int q = 0; q < NQ; ++q) n += (LA + q * DSPAN / NQ) < T - LC;
+    return n;
+  }();
   static_assert(NW * MF * (WM + 4) * 4 <= 2 * STAGE, "epilogue staging fits");
   using AccT = typename Acc<MF>::T;
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
@@ -269,15 +279,15 @@ gemm_4f(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
         block_barrier();
       }
       if constexpr (v == T - LC) {
-        // [B] -> [C]: this wave's DMAs of tile t+1 (NQ older than the NQ just issued) have landed
-        wait_vmcnt<NQ>();
+        // [B] -> [C]: this wave's DMAs of tile t+1 (older than the NQB of tile t+2) have landed
+        wait_vmcnt<NQB>();
         block_barrier();
       }
-      if constexpr (v >= LA && v < T - LC) {
-        // [B]: DMA q of tile t+2 in front of MFMA LA + q * LB / NQ
+      if constexpr (v >= LA) {
+        // DMA q of tile t+2 in front of MFMA dslot(q)
         static_for<NQ>([&](auto qc) {
           constexpr int q = decltype(qc)::value;
-          if constexpr (v == LA + q * LB / NQ) {
+          if constexpr (v == LA + q * DSPAN / NQ) {
             if constexpr (q < NA) {
               const Desc d = descA(t + 2);
               dmaA(d.p, d.n, ST, q);
@@ -369,7 +379,7 @@ static bool fast_ok(int bmode, const GOperand &A, const GOperand &B) {
   return true;
 }
 
-// 110: 256x256, 111: 256x128, 112: 128x256 (16x16x32); 113: 256x256 (32x32x16)
+// 110: 256x256, 111: 256x128, 112: 128x256, 114: 128x128, 115: 64x256 (16x16x32); 113: 256x256 (32x32x16)
 int dispatch_4w(int amode, int bmode, int epi, int tile, const GOperand &A, const GOperand &B, const GEpi &E,
                 int groups, int ksplit, hipStream_t s) {
   if (amode != K_DIRECT || !fast_ok(bmode, A, B)) return -1;
@@ -380,6 +390,8 @@ int dispatch_4w(int amode, int bmode, int epi, int tile, const GOperand &A, cons
       case 111: launch_4f<256, 128, BMV, EPV, 16>(A, B, E, groups, ksplit, s); return 0; \
       case 112: launch_4f<128, 256, BMV, EPV, 16>(A, B, E, groups, ksplit, s); return 0; \
       case 113: launch_4f<256, 256, BMV, EPV, 32>(A, B, E, groups, ksplit, s); return 0; \
+      case 114: launch_4f<128, 128, BMV, EPV, 16>(A, B, E, groups, ksplit, s); return 0; \
+      case 115: launch_4f<64, 256, BMV, EPV, 16>(A, B, E, groups, ksplit, s); return 0;  \
       default: return -1;                                                            \
     }                                                                                \
   }

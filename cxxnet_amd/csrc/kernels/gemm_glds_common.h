@@ -516,7 +516,7 @@ __device__ __forceinline__ void seg_epilogue(f32x4 (&acc)[MR][NR], char *smem, c
   }
 }
 
-// the one-wave-per-SIMD address-free tiles (gemm_4w.hip): tiles 110-113; -1 when unsupported
+// the one-wave-per-SIMD address-free tiles (gemm_4w.hip): tiles 110-115; -1 when unsupported
 int dispatch_4w(int amode, int bmode, int epi, int tile, const GOperand &A, const GOperand &B, const GEpi &E,
                 int groups, int ksplit, hipStream_t s);
 

@@ -13,7 +13,7 @@ from cxxnet_amd.ops.gemm import ConvGeom, conv_out_size
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-TILES = (110, 111, 112, 113)
+TILES = (110, 111, 112, 113, 114, 115)
 
 
 def _rnd(shape, scale, seed):
