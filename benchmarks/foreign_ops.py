@@ -53,8 +53,7 @@ def main():
     for ev in prof.events():
         if ev.device_type == torch.autograd.DeviceType.CUDA or not ev.name.startswith("aten::"):
             continue
-        if not any(k.device_type == torch.autograd.DeviceType.CUDA for k in (ev.kernels or [])) and \
-                getattr(ev, "device_time_total", 0) == 0:
+        if not (ev.kernels or []) and getattr(ev, "device_time_total", 0) == 0:
             continue
         site = next((f for f in (ev.stack or []) if "cxxnet_amd" in f), "?")
         foreign[(ev.name, site)] += 1

@@ -33,7 +33,7 @@ def _time(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ops", default="sq8192_fwd")
-    ap.add_argument("--tiles", default="21,90,91")
+    ap.add_argument("--tiles", default="21,90,91", help="tile ids; -1 = the shipped table's choice")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--groups", default="0", help="tile-order groups to A/B (ops.gemm.set_tile_group), e.g. 0,8")
@@ -55,7 +55,7 @@ def main():
                 out.zero_()
                 run()
                 torch.cuda.synchronize()
-                tag = f"t{t}" + (f"g{gi}" if len(groups) > 1 else "")
+                tag = (f"t{t}" if t >= 0 else "tdef") + (f"g{gi}" if len(groups) > 1 else "")
                 errs[tag] = ((out.float() - ref).norm() / ref.norm().clamp_min(1e-6)).item()
                 arms[tag] = (lambda t=t, gi=gi: (G.set_glds(True, t), G.set_tile_group(gi), run()))
         if name.startswith("sq"):

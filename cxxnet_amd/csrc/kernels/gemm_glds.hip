@@ -280,6 +280,7 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
         if (j < Nj && i < Mi) {
           f32x4 v = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il) * E.alpha;
           if constexpr (EPI == EPI_F32_SGD) {
+            const SgdHyp hy = sgd_hyper(E);
             const long idx = static_cast<long>(j) * E.ldc + i;
             if (vec) {
               f32x4 wv = *reinterpret_cast<const f32x4 *>(E.sgd_w + idx);
@@ -287,7 +288,7 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 float mm = mv[e];
-                wv[e] = sgd_step(E, v[e], mm, wv[e]);
+                wv[e] = sgd_step(hy, v[e], mm, wv[e]);
                 mv[e] = mm;
               }
               *reinterpret_cast<f32x4 *>(E.sgd_w + idx) = wv;
@@ -296,7 +297,7 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
             } else {
               for (int e = 0; e < 4 && i + e < Mi; ++e) {
                 float mm = E.sgd_m[idx + e];
-                const float wn = sgd_step(E, v[e], mm, E.sgd_w[idx + e]);
+                const float wn = sgd_step(hy, v[e], mm, E.sgd_w[idx + e]);
                 E.sgd_m[idx + e] = mm;
                 E.sgd_w[idx + e] = wn;
                 E.sgd_wb[idx + e] = f2bf(wn);
@@ -700,6 +701,7 @@ int dispatch(int amode, int bmode, int epi, int tile, const GOperand &A, const G
   }
   // (99 is the Python-side pseudo-tile of the register kernel, never passed here)
   if (tile >= 110 && tile <= 119) return cxg::dispatch_4w(amode, bmode, epi, tile, A, B, E, groups, ksplit, s);
+  if (tile >= 130 && tile <= 131) return cxg::dispatch_halo(amode, bmode, epi, tile, A, B, E, groups, ksplit, s);
   if (tile >= 50 && tile <= 51) {
     CXG_SEG(K_DIRECT, K_GATHER, EPI_BF16)
     CXG_SEG(K_DIRECT, K_DIRECT, EPI_BF16)
@@ -841,7 +843,8 @@ CXN_API int cxn_gemm_glds(const CxnOperandG *a, const CxnOperandG *b, int amode,
 //   g = clip(dw); m = mom*m - lr*(g + wd*w); w += m; wb = bf16(w)
 // to the layer's master / momentum / shadow slices instead of storing dw.
 CXN_API int cxn_gemm_glds_sgd(const CxnOperandG *a, const CxnOperandG *b, int ldc, float alpha, float *w, float *m,
-                              void *wb, float lr, float wd, float mom, float clip, int tile, void *stream) {
+                              void *wb, float lr, float wd, float mom, float clip, const float *hyp, int tile,
+                              void *stream) {
   if (a->kdim != b->kdim) return -1;
   if (!supported(a, MN_DIRECT) || !supported(b, MN_DIRECT)) return -1;
   if (a->rows % 4 != 0 || ldc % 4 != 0 || (reinterpret_cast<uintptr_t>(w) & 15) || (reinterpret_cast<uintptr_t>(m) & 15) ||
@@ -852,7 +855,7 @@ CXN_API int cxn_gemm_glds_sgd(const CxnOperandG *a, const CxnOperandG *b, int ld
   fill(A, a, MN_DIRECT);
   fill(B, b, MN_DIRECT);
   GEpi E{nullptr, 0, ldc, alpha, nullptr, 0, 0, 0, 0, w, m, static_cast<bf16_t *>(wb), lr, wd, mom, clip, nullptr, 0, 0, nullptr,
-         g_gemm_group_i};
+         g_gemm_group_i, hyp};
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int rc = dispatch(MN_DIRECT, MN_DIRECT, EPI_F32_SGD, tile, A, B, E, 1, 1, s);
   if (rc != 0) return rc;

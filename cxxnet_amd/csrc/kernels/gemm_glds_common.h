@@ -50,6 +50,9 @@ struct GEpi {
   long part_elems;     // workspace capacity
   float *dbias_final;  // += the workspace's column sums (db_partials_reduce)
   int group_i;         // tile order (common.h tile_ij); set at launch from cxn_gemm_set_group
+  // EPI_F32_SGD: when set, (lr, wd, mom, clip) are read from this device array instead of the
+  // fields above -- a recorded / captured step then takes each replay's schedule values
+  const float *sgd_hyp;
 };
 
 }  // namespace cxg
@@ -57,9 +60,16 @@ namespace cxg {
 // host-side tile-order setting copied into every GEpi at launch (cxn_gemm_set_group)
 extern int g_gemm_group_i;
 
-__device__ __forceinline__ float sgd_step(const GEpi &E, float g, float &m, float w) {
-  if (E.clip != 0.f) g = (g != g) ? 0.f : fminf(fmaxf(g, -E.clip), E.clip);
-  m = fmaf(E.mom, m, -E.lr * fmaf(E.wd, w, g));  // as optim_kernels.hip step1 (SGD)
+struct SgdHyp {
+  float lr, wd, mom, clip;
+};
+__device__ __forceinline__ SgdHyp sgd_hyper(const GEpi &E) {
+  if (E.sgd_hyp) return {E.sgd_hyp[0], E.sgd_hyp[1], E.sgd_hyp[2], E.sgd_hyp[3]};
+  return {E.lr, E.wd, E.mom, E.clip};
+}
+__device__ __forceinline__ float sgd_step(const SgdHyp &h, float g, float &m, float w) {
+  if (h.clip != 0.f) g = (g != g) ? 0.f : fminf(fmaxf(g, -h.clip), h.clip);
+  m = fmaf(h.mom, m, -h.lr * fmaf(h.wd, w, g));  // as optim_kernels.hip step1 (SGD)
   return w + m;
 }
 
@@ -519,5 +529,8 @@ __device__ __forceinline__ void seg_epilogue(f32x4 (&acc)[MR][NR], char *smem, c
 // the one-wave-per-SIMD address-free tiles (gemm_4w.hip): tiles 110-115; -1 when unsupported
 int dispatch_4w(int amode, int bmode, int epi, int tile, const GOperand &A, const GOperand &B, const GEpi &E,
                 int groups, int ksplit, hipStream_t s);
+// direct 3x3 convolution on a resident input halo (conv_halo.hip): tiles 130-131; -1 when unsupported
+int dispatch_halo(int amode, int bmode, int epi, int tile, GOperand A, GOperand B, const GEpi &E, int groups,
+                  int ksplit, hipStream_t s);
 
 }  // namespace cxg

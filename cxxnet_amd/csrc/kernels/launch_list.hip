@@ -64,3 +64,10 @@ CXN_API int cxn_copy_d2d(void *dst, const void *src, long bytes, void *stream) {
   if (bytes <= 0) return 0;
   return CXN_MEMCPY_D2D(dst, src, static_cast<size_t>(bytes), static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : -3;
 }
+
+// Zero `bytes` bytes at dst on `stream` (recorded when a list is open): gradient zeroing at the
+// start of a backward pass must be part of the replayed step.
+CXN_API int cxn_zero(void *dst, long bytes, void *stream) {
+  if (bytes <= 0) return 0;
+  return CXN_MEMSET(dst, 0, static_cast<size_t>(bytes), static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : -3;
+}

@@ -1577,6 +1577,33 @@ __global__ void pad_rows(const bf16_t *__restrict__ src, bf16_t *__restrict__ ds
 }
 
 
+// Interior of a zero-bordered NHWC copy: dst[n][h + py][w + px][:] = src[n][h][w][:] in units of
+// U bytes per pixel-chunk (the pre-pad conv path's input copy; the border stays as written once)
+template <typename U>
+__global__ void pad_interior(const U *__restrict__ src, U *__restrict__ dst, long npix, int H, int W, int H2, int W2,
+                             int py, int px, int cu) {
+  const long total = npix * cu;
+  for (long i = grid_stride_start(); i < total; i += grid_stride()) {
+    const long p = i / cu;
+    const int c = static_cast<int>(i - p * cu);
+    const long n = p / (static_cast<long>(H) * W);
+    const int r = static_cast<int>(p - n * H * W);
+    const int h = r / W, w = r - h * W;
+    dst[((n * H2 + h + py) * W2 + w + px) * cu + c] = src[i];
+  }
+}
+
+
+// dst[r][0:L] += src[r][0:L] (fp32; src rows of Ls >= L elements): the row-padded weight-grad
+// buffer of the conv1 row-run path added into the layer's gradient
+__global__ void add_rows_f32(const float *__restrict__ src, float *__restrict__ dst, long rows, int L, int Ls) {
+  const long total = rows * L;
+  for (long i = grid_stride_start(); i < total; i += grid_stride()) {
+    const long r = i / L;
+    dst[i] += src[r * Ls + (i - r * L)];
+  }
+}
+
 // Max-unpool with the reference's tie semantics (src/layer/pooling_layer-inl.hpp:55-86,
 // `unpool<red::maximum>`): EVERY input of a window that equals the window's max receives
 // that window's gradient (pool_tie = all).  Gather form: one thread per input element sums
@@ -2139,6 +2166,26 @@ CXN_API int cxn_channel_copy(const void *src, int Cs, int soff, void *dst, int C
   }
   CXN_LAUNCH((channel_copy), nblocks(npix * Cc), NT, 0, S_, (const bf16_t *)src, Cs, soff, (bf16_t *)dst, Cd, doff, Cc, npix,
                                                   accumulate);
+  RET;
+}
+
+CXN_API int cxn_pad_interior(const void *src, void *dst, int N, int H, int W, int C, int H2, int W2, int py, int px,
+                             void *stream) {
+  const long npix = static_cast<long>(N) * H * W;
+  const int bytes = C * 2;
+  if (bytes % 8 == 0 && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 7) == 0) {
+    CXN_LAUNCH((pad_interior<uint2>), nblocks(npix * (bytes / 8)), NT, 0, S_, (const uint2 *)src, (uint2 *)dst, npix, H, W,
+               H2, W2, py, px, bytes / 8);
+  } else {
+    CXN_LAUNCH((pad_interior<bf16_t>), nblocks(npix * C), NT, 0, S_, (const bf16_t *)src, (bf16_t *)dst, npix, H, W, H2,
+               W2, py, px, C);
+  }
+  RET;
+}
+
+CXN_API int cxn_add_rows_f32(const float *src, float *dst, long rows, int L, int Ls, void *stream) {
+  if (rows <= 0 || L <= 0) return 0;
+  CXN_LAUNCH((add_rows_f32), nblocks(rows * L), NT, 0, S_, src, dst, rows, L, Ls);
   RET;
 }
 

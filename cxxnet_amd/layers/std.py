@@ -167,6 +167,9 @@ class FullConnectLayer(Layer):
         assert not getattr(self.ctx, "dp_active", False) or getattr(self.ctx, "sgd_fuse_gather_only", False)
         spec = self.w
         lr, wd, mom, clip = upd.hyper(spec, self.ctx.epoch)
+        # a planned step (launch list / HIP graph) reads the schedule values from the updater's
+        # device table, refreshed before every replay (NetTrainer._stage_fused_sgd)
+        hyp = upd.hyper_dev(spec) if getattr(self.ctx, "sgd_hyp_dev", False) else None
         a = upd.arena
         m = a.m1[spec.offset:spec.offset + spec.numel].view(spec.shape)
         side = getattr(self.ctx, "fc_side", None)
@@ -176,7 +179,7 @@ class FullConnectLayer(Layer):
             # on `side` (joined at the end of the backward pass, NeuralNet.backprop)
             if getattr(self, "_xs", None) is None or self._xs.shape != x.shape:
                 self._xs = torch.empty_like(x)
-            self._xs.copy_(x)
+            ops.copy_(self._xs, x)  # a library copy: recorded launch lists repeat it
             if prop_grad:
                 ops.fc_backward_data(dy, spec.wb, nodes_in[0].gmat(), mask_relu=self.grad_mask_relu)
             ready = torch.cuda.Event()
@@ -188,7 +191,7 @@ class FullConnectLayer(Layer):
             dy.record_stream(side)
             self._xs.record_stream(side)
             with torch.cuda.stream(side):
-                ok = ops.fc_backward_weight_sgd(self._xs, dy, spec.w, m, spec.wb, lr, wd, mom, clip)
+                ok = ops.fc_backward_weight_sgd(self._xs, dy, spec.w, m, spec.wb, lr, wd, mom, clip, hyp)
             self.ctx.fc_side_used = True
             if ok:
                 upd.fused_offsets.add(spec.offset)
@@ -203,7 +206,7 @@ class FullConnectLayer(Layer):
             gx = self._dx[:x.shape[0]]
             ops.fc_backward_data(dy, spec.wb, gx)
         xg, dyg = (x, dy) if xw is None else (xw, dyw)
-        if ops.fc_backward_weight_sgd(xg, dyg, spec.w, m, spec.wb, lr, wd, mom, clip):
+        if ops.fc_backward_weight_sgd(xg, dyg, spec.w, m, spec.wb, lr, wd, mom, clip, hyp):
             upd.fused_offsets.add(spec.offset)
         else:  # the kernel does not cover this shape: plain gradient, updated by the updater
             ops.fc_backward_weight(xg, dyg, spec.g, overwrite=True)
@@ -357,10 +360,6 @@ class ConvolutionLayer(Layer):
     def b(self):
         return self.params[1] if len(self.params) > 1 else None
 
-    def replay_safe(self) -> bool:
-        # the pre-pad path copies x into its zero-bordered buffer with a torch copy
-        return not (self._prepad_on and self.ctx.is_gpu)
-
     def _padded(self, x, refresh):
         """(input, geometry) for forward / weight-grad: x itself, or (pre-pad path) the
         zero-bordered copy of x with a pad-0 geometry.  refresh=False reuses the forward's copy
@@ -375,7 +374,7 @@ class ConvolutionLayer(Layer):
             refresh = True
         xp = self._xpad[:N]
         if refresh:
-            xp[:, g.pad_y:g.pad_y + g.H, g.pad_x:g.pad_x + g.W].copy_(x)
+            ops.pad_interior(x, xp, g.pad_y, g.pad_x)
         return xp, ConvGeom(N, H2, W2, g.C, g.Ho, g.Wo, g.Cout, g.KH, g.KW, g.stride, 0, 0, g.groups)
 
     def forward(self, is_train, nodes_in, nodes_out):

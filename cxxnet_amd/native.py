@@ -68,12 +68,15 @@ _SIGS = {
     "cxn_gemm": [ctypes.POINTER(CxnOperand), ctypes.POINTER(CxnOperand), _I, _I, _I, _I,
                  _P, _L, _I, _F, _P, _L, _I, _I, _I, _I, _I, _I, _L, _P],
     "cxn_gemm_glds_sgd": [ctypes.POINTER(CxnOperand), ctypes.POINTER(CxnOperand), _I, _F, _P, _P, _P, _F, _F, _F, _F,
-                          _I, _P],
+                          _P, _I, _P],
     "cxn_gemm_set_group": [_I],
     "cxn_set_kernel_variant": [_I, _I],
     "cxn_gemm_glds": [ctypes.POINTER(CxnOperand), ctypes.POINTER(CxnOperand), _I, _I, _P, _L, _I, _F, _P, _L, _I,
                       _I, _I, _I, _I, _I, _L, _P, _P, _L, _I, _P],
     "cxn_pad_rows": [_P, _P, _L, _I, _I, _P],
+    "cxn_pad_interior": [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "cxn_zero": [_P, _L, _P],
+    "cxn_add_rows_f32": [_P, _P, _L, _I, _I, _P],
     "cxn_conv_rowrun_fwd": [_P, _L, _P, _P, _P] + [_I] * 12 + [_P],
     "cxn_conv_rowrun_wgrad": [_P, _L, _P, _L, _P] + [_I] * 10 + [_P],
     "cxn_conv_fewc_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],

@@ -77,8 +77,9 @@ class ParamArena:
         return self._acc_ranges
 
     def zero_accumulated_grads(self):
+        from .. import ops  # a library memset: launch lists record it (a torch zero_ they would not)
         for a, b in self.accumulate_ranges():
-            self.g[a:b].zero_()
+            ops.zero_(self.g[a:b])
 
     def ensure_second_moment(self):
         if self.m2 is None:

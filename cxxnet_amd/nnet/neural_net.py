@@ -413,6 +413,9 @@ class NeuralNet:
         if b == self.cur_batch:
             return
         self.cur_batch = b
+        # layers may now reallocate shape-dependent buffers: recorded launch lists and captured
+        # graphs of every batch size are stale (NetTrainer._drop_stale_plans)
+        self.batch_gen = getattr(self, "batch_gen", 0) + 1
         for conn in self.connections:
             conn.layer.on_batch_size_changed(conn.nodes_in, conn.nodes_out)
 

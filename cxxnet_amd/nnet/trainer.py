@@ -118,6 +118,7 @@ class NetTrainer:
         self.launch_replay = int(os.environ.get("CXXNET_LAUNCH_REPLAY", "-1"))
         self._lists = {}
         self._list_warm = {}
+        self._plan_gen = None  # NeuralNet.batch_gen the recorded / captured plans were made at
         # failure detection: every N updates, fail fast if any gradient was non-finite
         # (the reference only zeroes NaN inside clip, sgd_updater-inl.hpp:17)
         self.check_nonfinite = 0
@@ -434,6 +435,8 @@ class NetTrainer:
         net = self.net
         self._cur_batch = batch
         ev = self._events()
+        if self.net.ctx.is_gpu:
+            self._drop_stale_plans()
         if self._graph_step(ev) or self._list_step(ev):
             self._after_step(ev)
             self._sync_tiles()
@@ -700,13 +703,18 @@ class NetTrainer:
                 begin(fwd)
                 net.forward(True, pre_hook=fwd_hook if dp else None)
                 end()
+                self._plan_fuse(True)  # (stages the device schedule row before capturing)
                 begin(bwd)
                 net.backprop(False, hook=bwd_hook if dp else None, first=True, hook_due=bwd_due if dp else None)
                 end()
         finally:
             net.ctx.graph_cut = None
+            self._plan_fuse(False)
         torch.cuda.synchronize()
-        return fwd, bwd
+        fused = frozenset(net.updater.fused_offsets) if net.updater is not None else frozenset()
+        if net.updater is not None:
+            net.updater.fused_offsets.clear()  # the capture ran nothing; the replays add them back
+        return fwd, bwd, fused
 
     @staticmethod
     def _replay(plan):
@@ -734,6 +742,22 @@ class NetTrainer:
             return self._local_batch() <= 32
         return True
 
+    def _drop_stale_plans(self):
+        """Launch lists and HIP graphs hold raw addresses of layer buffers; a batch-size change
+        lets layers reallocate shape-dependent ones (pool state, softmax scores, pad copies), so
+        plans made before it may point at freed memory.  Drop them all; the next steps warm up
+        and record again (plans are per batch size, and batch sizes rarely alternate)."""
+        gen = getattr(self.net, "batch_gen", 0)
+        if self._plan_gen == gen:
+            return
+        if self._lists or self._graphs:
+            torch.cuda.synchronize()  # no replay of the old plans is still running
+        self._lists.clear()
+        self._list_warm.clear()
+        self._graphs.clear()
+        self._graph_warm.clear()
+        self._plan_gen = gen
+
     def _list_step(self, ev=None) -> bool:
         """One training step replayed from recorded C++ launch lists: the forward and backward
         passes as runs of library launches, with the same eager calls between them as the
@@ -751,16 +775,40 @@ class NetTrainer:
                 return False
             self._lists[key] = self._record_step(ev)
             return True
-        fwd, bwd = plans[0], plans[1]
+        fwd, bwd, fused = plans[0], plans[1], plans[3]
         self._replay(fwd)
         self._mark(ev, 1)
-        self._finish_planned_step(ev, lambda: self._replay(bwd))
+        self._finish_planned_step(ev, lambda: self._replay(bwd), fused)
         return True
 
-    def _finish_planned_step(self, ev, run_bwd):
+    def _plan_fuse(self, on: bool):
+        """Fused fc SGD steps inside a planned step being recorded / captured: the same
+        eligibility as the eager step (_sgd_fuse_target), with the schedule values read from
+        the updater's device table (ArenaUpdater.stage_hyper) so every replay follows the lr /
+        momentum schedule.  Returns whether the plan fuses."""
+        net = self.net
+        if not on:
+            net.ctx.sgd_fuse, net.ctx.sgd_fuse_gather_only, net.ctx.sgd_hyp_dev = None, False, False
+            return False
+        upd, gather_only = self._sgd_fuse_target()
+        net.ctx.sgd_fuse, net.ctx.sgd_fuse_gather_only = upd, gather_only
+        net.ctx.sgd_hyp_dev = upd is not None
+        net.ctx.dp_active = self.reducer.active
+        net.ctx.epoch = self.epoch_counter
+        if upd is not None:
+            upd.stage_hyper(self.epoch_counter)
+        return upd is not None
+
+    def _finish_planned_step(self, ev, run_bwd, fused=None):
         """The part of a planned (graph / launch-list) step after the forward: training
-        metrics, the backward (run_bwd) framed by the reducer, the optimizer."""
+        metrics, the backward (run_bwd) framed by the reducer, the optimizer.  fused: the arena
+        offsets whose SGD step the plan's backward runs inside fc weight-gradient GEMMs (the
+        optimizer and the per-bucket updates skip them); their device schedule row is
+        refreshed first."""
         net, red = self.net, self.reducer
+        if fused:
+            net.updater.stage_hyper(self.epoch_counter)
+            net.updater.fused_offsets.update(fused)
         evals = self._train_eval(self._cur_batch)
         if red.handles_update:
             red.start_step()
@@ -823,11 +871,13 @@ class NetTrainer:
         fwd, bwd = [], []
 
         def record_bwd():
+            self._plan_fuse(True)
             begin(bwd)
             try:
                 net.backprop(False, hook=bwd_hook if dp else None, first=True, hook_due=bwd_due if dp else None)
             finally:
                 end()
+                self._plan_fuse(False)
 
         net.ctx.graph_cut = cut
         set_recording(True)
@@ -846,7 +896,8 @@ class NetTrainer:
             h = k.cxn_rec_end()  # an exception left a list open: drop it
             if h:
                 k.cxn_rec_free(h)
-        return fwd, bwd, pool
+        fused = frozenset(net.updater.fused_offsets) if net.updater is not None else frozenset()
+        return fwd, bwd, pool, fused
 
     def _graph_step(self, ev=None) -> bool:
         """One training step as HIP-graph replays of the forward and backward passes plus
@@ -874,10 +925,10 @@ class NetTrainer:
                 torch.cuda.synchronize()
                 return False
             self._graphs[key] = gr
-        fwd, bwd = gr
+        fwd, bwd, fused = gr
         self._replay(fwd)
         self._mark(ev, 1)
-        self._finish_planned_step(ev, lambda: self._replay(bwd))
+        self._finish_planned_step(ev, lambda: self._replay(bwd), fused)
         return True
 
     # ------------------------------------------------------------------ inference

@@ -552,8 +552,17 @@ _detws = {}
 def _det_ws(n, device):
     buf = _detws.get(str(device))
     if buf is None or buf.numel() < n:
+        from .mode import retire
+        retire(buf)  # a recorded / captured step may still point at it
         buf = _detws[str(device)] = torch.empty(n, dtype=torch.float32, device=device)
     return buf[:n]
+
+
+def _add_rows(src, dst, rows, L, Ls):
+    """dst[r][0:L] += src[r][0:L] for fp32 [rows][Ls] -> [rows][L] (the row-padded weight-grad
+    buffer into the layer's gradient), as a library kernel."""
+    native.check(native.kernels().cxn_add_rows_f32(src.data_ptr(), dst.data_ptr(), rows, L, Ls, _stream()),
+                 "add_rows_f32")
 
 
 def _wgrad_pad_buf(cout, kr, device):
@@ -799,7 +808,8 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
                 split = 1
             return _glds(Ar, B, GL_MNG, GL_MN, o, 0, kr, epi=EPI_F32_ATOMIC_G, ksplit=split, tile=t)
         key = ("cwr", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride)
-        ws.zero_()
+        from .nn import zero_
+        zero_(ws)  # library memset / add below: a replayed launch list repeats them (torch ops it would not)
         if _ROWRUN_WGRAD and not _DET["on"] and x.is_contiguous() and dy.is_contiguous():
             # conv_rowrun.hip: input rows and dy rows staged once per 2 output rows (off by default:
             # 169-189 us against the split-K GEMM's 159 on AlexNet conv1, profiles/r3_conv1_direct.md)
@@ -807,14 +817,12 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
                 x.data_ptr(), x.numel() * x.element_size(), dy.data_ptr(), dy.numel() * dy.element_size(), ws.data_ptr(),
                 g.N, g.H, g.W, g.C, g.Ho, g.Wo, g.Cout, g.KH, lp, g.stride, _stream())
             if rc == 0:
-                L = g.KW * g.C
-                dw.view(g.Cout, g.KH, L).add_(ws.view(g.Cout, g.KH, lp)[:, :, :L])
+                _add_rows(ws, dw, g.Cout * g.KH, g.KW * g.C, lp)
                 return
             if rc != -1:
                 native.check(rc, "conv_rowrun_wgrad")
         if run(_tuned_tile(key, run, ws, lambda: 1), ws):
-            L = g.KW * g.C
-            dw.view(g.Cout, g.KH, L).add_(ws.view(g.Cout, g.KH, lp)[:, :, :L])
+            _add_rows(ws, dw, g.Cout * g.KH, g.KW * g.C, lp)
             return
     if cg % va:
         raise RuntimeError(f"conv weight-grad: no GPU kernel for {cg} channels per group ({g})")
@@ -857,13 +865,15 @@ def fc_backward_data(dy, w, dx, mask_relu=False):
     _gemm_bf16_out(A, Bo, DIRECT_MN, DIRECT_K, dx, nin, mask_relu=mask_relu)
 
 
-def fc_backward_weight_sgd(x, dy, w, m, wb, lr, wd, mom, clip) -> bool:
+def fc_backward_weight_sgd(x, dy, w, m, wb, lr, wd, mom, clip, hyp=None) -> bool:
     """The fc weight-gradient dy^T . x fused with the SGD step of those weights: the
     epilogue applies m = mom*m - lr*(clip(g) + wd*w); w += m; wb = bf16(w) to the fp32
     master w, momentum m and bf16 shadow wb ([nout][nin] slices of the arena) and the
     gradient never goes to memory.  Same arithmetic as the fused optimizer, so the
     result is bitwise the unfused one.  False when the LDS-DMA kernel does not cover the
-    shape (the caller then takes the unfused path)."""
+    shape (the caller then takes the unfused path).  hyp (fp32 device [4], optional): the
+    kernel reads (lr, wd, mom, clip) from it instead -- a recorded / captured step then follows
+    the schedule through a per-step host-to-device refresh of hyp."""
     if not (_native_t(x) and _glds_cfg["on"] and _use("fw")):
         return False
     Bn, nin = x.shape
@@ -877,7 +887,8 @@ def fc_backward_weight_sgd(x, dy, w, m, wb, lr, wd, mom, clip) -> bool:
         if tile is None:
             tile = _TUNE.get(f"fw|{nin}|{nout}|{Bn}", 1)
     rc = native.kernels().cxn_gemm_glds_sgd(A, Bo, nin, 1.0, w.data_ptr(), m.data_ptr(), wb.data_ptr(), float(lr),
-                                            float(wd), float(mom), float(clip), tile, _stream())
+                                            float(wd), float(mom), float(clip),
+                                            hyp.data_ptr() if hyp is not None else None, tile, _stream())
     if rc == -1:
         return False
     native.check(rc, "gemm_glds_sgd")

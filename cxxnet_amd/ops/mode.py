@@ -36,3 +36,18 @@ def frozen() -> bool:
     """The step's launches are being frozen for replay -- recorded into a C++ launch list or
     captured into a HIP graph: no autotuning launches, no side streams, no host reads."""
     return _REC["on"] or torch.cuda.is_current_stream_capturing()
+
+
+# Buffers a recorded launch list or captured HIP graph may still point at.  A module-level
+# workspace that grows is replaced, and a replay of a step recorded before the growth would write
+# into the freed block -- which the caching allocator may have handed to a live tensor by then
+# (round 4: a step recorded while the unfused fc weight-grad grew the split-K workspace replayed
+# its earlier partial sums into the next batch's input).  Replaced workspaces are retired here
+# instead of freed; they only grow, so this holds less than the final size again.
+_GRAVE = []
+
+
+def retire(t):
+    """Keep a replaced workspace alive for the plans that may still reference it."""
+    if t is not None:
+        _GRAVE.append(t)

@@ -94,6 +94,28 @@ def copy_(dst: torch.Tensor, src: torch.Tensor):
                  "copy_d2d")
 
 
+def zero_(t: torch.Tensor):
+    """t <- 0 for a contiguous tensor: a library memset on the GPU (recorded into launch lists,
+    so a replayed step repeats it -- a torch zero_() would run only in the recording step),
+    torch on the CPU."""
+    if not (t.is_cuda and t.is_contiguous()):
+        t.zero_()
+        return
+    native.check(_k().cxn_zero(t.data_ptr(), t.numel() * t.element_size(), _stream()), "zero")
+
+
+def pad_interior(x: torch.Tensor, xp: torch.Tensor, py: int, px: int):
+    """xp[:, py:py+H, px:px+W] <- x (NHWC; xp's border is left as is): a library kernel on the
+    GPU, so launch lists record it; torch on the CPU."""
+    N, H, W, C = x.shape
+    if not (_native_t(x) and x.is_contiguous() and xp.is_contiguous()):
+        xp[:, py:py + H, px:px + W].copy_(x)
+        return
+    assert xp.shape[0] == N and xp.shape[3] == C and xp.dtype == x.dtype
+    native.check(_k().cxn_pad_interior(x.data_ptr(), xp.data_ptr(), N, H, W, C, xp.shape[1], xp.shape[2], py, px,
+                                       _stream()), "pad_interior")
+
+
 def transpose(x: torch.Tensor, y: torch.Tensor, B: int, R: int, Cc: int):
     """y[b][Cc][R] = x[b][R][Cc]."""
     if not _native_t(x):
@@ -402,6 +424,8 @@ def _workspace(n: int, device) -> torch.Tensor:
     key = str(device)
     t = _WS.get(key)
     if t is None or t.numel() < n:
+        from .mode import retire
+        retire(t)  # a recorded / captured step may still point at it
         t = torch.empty(max(n, 1 << 16), dtype=torch.float32, device=device)
         _WS[key] = t
     return t
@@ -423,12 +447,25 @@ def bias_grad(dy2d, db, mask=None):
         bias_grad_multi([(dy2d, db, mask)])
         return
     if not dy2d.is_contiguous():  # a channel slice of a zero-copy ch_concat output
-        dy2d = dy2d.contiguous()
+        dy2d = _rows_contiguous(dy2d)
     rows, C = dy2d.shape
     n = max(4096, -(-rows // 512)) * C
     ws = _workspace(n, dy2d.device)
     native.check(_k().cxn_colsum(dy2d.data_ptr(), db.data_ptr(), rows, C, ws.data_ptr(), ws.numel(), _stream()),
                  "colsum")
+
+
+def _rows_contiguous(d):
+    """Contiguous copy of a [rows][C] GPU view with unit column stride (a channel slice of a
+    wider NHWC buffer) through the library's channel copy: a torch .contiguous() would not be
+    part of a recorded launch list, and its replay would read a stale temporary."""
+    rows, C = d.shape
+    if d.stride(1) != 1:
+        raise ValueError("bias gradient: unit column stride expected")
+    out = torch.empty((rows, C), dtype=d.dtype, device=d.device)
+    native.check(_k().cxn_channel_copy(d.data_ptr(), d.stride(0), 0, out.data_ptr(), C, 0, C, rows, 0, _stream()),
+                 "channel_copy")
+    return out
 
 
 def _det() -> bool:
@@ -457,7 +494,12 @@ def bias_grad_multi(items):
     for d, b, m in items:
         if not bias_fast_ok(d, m):
             if m is not None and _native_t(d):
-                bias_grad(d * (m < 128).to(d.dtype), b)
+                # (no torch math here: a launch list would not record it) a contiguous copy of
+                # d makes the one-launch masked kernel applicable
+                dc = _rows_contiguous(d) if not d.is_contiguous() else d
+                if not (bias_fast_ok(dc, m) and m.is_contiguous()):
+                    raise RuntimeError(f"masked bias gradient: no GPU kernel for {tuple(d.shape)}")
+                fast.append((dc, b, m))
             else:
                 bias_grad(d, b, m)
     if not fast:

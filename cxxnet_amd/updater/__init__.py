@@ -162,6 +162,43 @@ class ArenaUpdater:
                 return lr, wd, mom, clip
         raise KeyError(f"no updater segment at arena offset {spec.offset}")
 
+    def stage_hyper(self, epoch: int):
+        """Refresh the device table of every entry's (lr, wd, momentum, clip) for this epoch's
+        update: the fused fc steps of a recorded launch list / captured graph read their
+        schedule values from it (ops.fc_backward_weight_sgd hyp), one host-to-device copy per
+        step."""
+        import torch
+        if getattr(self, "_hyp_dev", None) is None:
+            dev = self.arena.w.device
+            pin = dev.type == "cuda"
+            # a ring of pinned sources: slot k is rewritten only after the copy that read it
+            # (event), so staging never waits on the GPU in steady state
+            self._hyp_host = [torch.zeros((len(self.entries), 4), dtype=torch.float32, pin_memory=pin)
+                              for _ in range(4)]
+            self._hyp_ev = [None] * 4
+            self._hyp_slot = 0
+            self._hyp_dev = torch.zeros((len(self.entries), 4), dtype=torch.float32, device=dev)
+            self._hyp_row = {spec.offset: i for i, (spec, _) in enumerate(self.entries)}
+        if getattr(self, "_seg_epoch", None) != epoch:
+            self._segs = self.segments(epoch)
+            self._seg_epoch = epoch
+        if getattr(self, "_hyp_epoch", None) == epoch:
+            return
+        k = self._hyp_slot = (self._hyp_slot + 1) % len(self._hyp_host)
+        if self._hyp_ev[k] is not None:
+            self._hyp_ev[k].synchronize()
+        host = self._hyp_host[k]
+        host.copy_(torch.tensor([seg[2:6] for seg in self._segs], dtype=torch.float32))
+        self._hyp_dev.copy_(host, non_blocking=True)
+        if self._hyp_dev.is_cuda:
+            self._hyp_ev[k] = torch.cuda.Event()
+            self._hyp_ev[k].record()
+        self._hyp_epoch = epoch
+
+    def hyper_dev(self, spec):
+        """Device row (lr, wd, momentum, clip) of `spec` (stage_hyper fills it)."""
+        return self._hyp_dev[self._hyp_row[spec.offset]]
+
     def update(self, epoch: int, ranges=None):
         """ranges: optional [start, end) arena ranges to update (sharded data
         parallelism updates only this rank's slice; the overlapped update calls this once

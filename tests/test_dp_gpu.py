@@ -58,19 +58,25 @@ def _worker(rank, world, port, steps, out, extra, backend="gloo"):
     graph = any(k == "cuda_graph" and v == "1" for k, v in extra)
     if graph:
         assert tr._graphs, "the data-parallel step did not run as graph segments"
-        fwd, bwd = next(iter(tr._graphs.values()))
+        fwd, bwd = next(iter(tr._graphs.values()))[:2]
         assert sum(callable(i) and not isinstance(i, torch.cuda.CUDAGraph) for i in fwd + bwd) > 0
     if any(k == "fullc_gather" and v == "1" for k, v in extra) and not graph:
         # the gathered fc layer the kernel covers (f1: 16 x 128; f2's 5 outputs are not a multiple
         # of 8) ran its SGD step inside the weight-gradient GEMM
-        assert tr.net.ctx.dp_active and len(tr.net.updater.fused_offsets) == 1, tr.net.updater.fused_offsets
+        fcs = [c.layer for c in tr.net.connections if c.layer.type_name == "fullc"]
+        assert tr.net.ctx.dp_active and len(tr.net.updater.fused_offsets) == 1, \
+            (tr.net.updater.fused_offsets, [f._gathering() for f in fcs], list(tr._lists), list(tr._graphs))
     tr.reducer.sync_master()  # sharded: each rank updated only its slice of the fp32 masters
     torch.save(tr.net.arena.w.cpu(), out + f".r{rank}")
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("extra", [(), (("dp_comm_dtype", "bf16"),), (("update_period", "2"),),
-                                   (("dp_mode", "allreduce"),), (("cuda_graph", "1"),)])
+                                   (("dp_mode", "allreduce"),), (("cuda_graph", "1"),),
+                                   # the gloo CPU tests' 1e-4 bound: deterministic GEMMs (no fp32
+                                   # atomics), so only the 2-rank sum order differs (measured 1e-9)
+                                   (("deterministic", "1"),),
+                                   (("deterministic", "1"), ("dp_mode", "allreduce"))])
 def test_dp_two_ranks_gpu_equals_single(tmp_path, extra):
     steps = 4
     out = str(tmp_path / "w")
@@ -88,7 +94,11 @@ def test_dp_two_ranks_gpu_equals_single(tmp_path, extra):
     w0 = _make(8, list(extra)).net.arena.w.cpu()  # same seed: the initial weights
     n = w.numel()
     err = ((r0[:n] - w).norm() / (w - w0).norm()).item()  # relative to the distance trained
-    assert err < 5e-2, err
+    print(f"dp 2-rank vs single, {extra}: err {err:.3g}")
+    # default mode: fp32 atomics in the weight gradients make the summation order run-dependent,
+    # and a 1-ulp flip of a bf16 weight shadow moves later activations by bf16 ulps
+    tol = 1e-4 if ("deterministic", "1") in extra else 5e-2
+    assert err < tol, err
 
 
 @pytest.mark.parametrize("graph", [0, 1])
@@ -123,11 +133,12 @@ def test_rccl_forced_fullc_gather_fused_sgd(tmp_path, mode):
     are reduced (sharded or all-reduced).  Bit-exact against the single-GPU run."""
     steps = 4
     out = str(tmp_path / "w")
-    extra = [("dp_mode", mode), ("dp_bucket_mb", "0.002"), ("fullc_gather", "1")]
+    # eager steps on both sides (a planned step -- launch list or graph -- runs the arena update)
+    extra = [("dp_mode", mode), ("dp_bucket_mb", "0.002"), ("fullc_gather", "1"), ("launch_replay", "0")]
     mp.spawn(_worker, args=(1, _free_port(), steps, out, extra, "nccl"), nprocs=1, join=True)
     r0 = torch.load(out + ".r0", weights_only=True)
     from cxxnet_amd.io.data import DataBatch
-    tr = _make(8, [])
+    tr = _make(8, [("launch_replay", "0")])
     x, y = _data(8)
     for _ in range(steps):
         tr.update(DataBatch(x.cuda(), y.cuda()))

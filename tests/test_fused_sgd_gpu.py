@@ -63,7 +63,7 @@ def test_fused_fc_sgd_is_bitwise_the_unfused_step(extra):
     saved = trainer_mod._FUSE_FC_SGD
     try:
         tr, w1, m1, b1 = _train(True, 5, extra)
-        assert tr._sgd_fuse_target() is not None
+        assert tr._sgd_fuse_target()[0] is not None
         _, w0, m0, b0 = _train(False, 5, extra)
     finally:
         trainer_mod._FUSE_FC_SGD = saved
@@ -75,7 +75,7 @@ def test_fused_fc_sgd_is_bitwise_the_unfused_step(extra):
 
 def test_fusion_off_for_other_updaters():
     tr, *_ = _train(True, 1, [("updater", "nag")])
-    assert tr._sgd_fuse_target() is None
+    assert tr._sgd_fuse_target()[0] is None
 
 
 def test_fused_fc_sgd_on_side_stream_is_bitwise(monkeypatch):

@@ -425,7 +425,8 @@ def test_conv1_three_channel_row_runs(N):
 @pytest.mark.parametrize("N,H,W,C,Cout,K,S,relu", [(2, 227, 228, 3, 96, 11, 4, True), (3, 227, 228, 3, 96, 11, 4, False),
                                                    (40, 227, 228, 3, 96, 11, 4, True),  # 2-3 work items per block
                                                    (2, 35, 35, 4, 32, 5, 2, True), (2, 43, 44, 3, 128, 7, 4, False),
-                                                   (5, 30, 32, 3, 64, 3, 4, True)])
+                                                   (5, 30, 32, 3, 64, 3, 4, True),
+                                                   (2, 34, 36, 4, 64, 4, 2, True)])  # even KH: no unpaired row
 def test_conv_rowrun_direct_forward(N, H, W, C, Cout, K, S, relu):
     """conv_rowrun.hip (input rows staged once per 4 output rows, LDS-DMA double buffer) called
     directly -- it must serve the shape (rc 0, no GEMM fallback) -- against fp32 torch."""

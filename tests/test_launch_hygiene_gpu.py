@@ -1,0 +1,44 @@
+"""Every GPU kernel of a training step's forward and backward passes must come from the library
+(libcxxnet_kernels.so): the C++ launch-list executor replays only library launches, so a torch
+op on that path (a .zero_(), .contiguous(), .add_() ...) runs in the recording step and silently
+not in the replays.  Round 4 found three such ops by their effect (gradients never zeroed, a
+stale concat-slice copy read as NaN, conv1's weight gradient never added); this test finds the
+next one by its kernel name, on the real graphs, in both GEMM modes."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _make(model, batch, det):
+    from cxxnet_amd.models import load_conf
+    from cxxnet_amd.nnet import NetTrainer
+    tr = NetTrainer()
+    base = [(k, v) for k, v in load_conf(model, []) if not k.startswith("metric")]
+    for k, v in base + [("batch_size", str(batch)), ("dev", "gpu"), ("eval_train", "0"), ("silent", "1"),
+                        ("cuda_graph", "0"), ("launch_replay", "0"), ("deterministic", str(det))]:
+        tr.set_param(k, v)
+    tr.init_model()
+    return tr
+
+
+@pytest.mark.parametrize("det", [0, 1])
+@pytest.mark.parametrize("model,batch", [("alexnet", 16), ("inception_v1", 8), ("vgg16", 4)])
+def test_forward_backward_launch_only_library_kernels(model, batch, det):
+    from torch.profiler import ProfilerActivity, profile
+    from cxxnet_amd.io.data import DataBatch
+    tr = _make(model, batch, det)
+    c, h, w = tr.net_cfg.input_shape
+    b = DataBatch(torch.randn(batch, c, h, w, device="cuda"), torch.zeros(batch, 1, device="cuda"))
+    for _ in range(2):  # tile tuning and lazy buffers happen in the first steps
+        tr.update(b)
+    tr._set_batch(b)
+    torch.cuda.synchronize()
+    net = tr.net
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        net.forward(True)
+        net.backprop(False, first=True)
+        torch.cuda.synchronize()
+    foreign = sorted({e.name for e in prof.events()
+                      if e.device_type == torch.autograd.DeviceType.CUDA and "at::native" in e.name})
+    assert not foreign, foreign

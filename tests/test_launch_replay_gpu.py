@@ -14,6 +14,18 @@ from test_dp_gloo import CONF
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _unfused_fc_sgd():
+    """Both arms take the same fc path: the eager step would otherwise fuse the fc SGD step
+    into a one-slice weight-grad GEMM while a planned step runs the arena update after the
+    (possibly split-K) GEMM -- equal math, different fp32 summation order."""
+    from cxxnet_amd.nnet import trainer as trainer_mod
+    saved = trainer_mod._FUSE_FC_SGD
+    trainer_mod._FUSE_FC_SGD = False
+    yield
+    trainer_mod._FUSE_FC_SGD = saved
+
+
 def _make(batch, extra=(), conf=None, model=None):
     from cxxnet_amd import native
     from cxxnet_amd.models import load_conf
@@ -21,8 +33,9 @@ def _make(batch, extra=(), conf=None, model=None):
     tr = NetTrainer()
     base = list(native.rt().parse_config(conf or CONF)) if model is None else \
         [(k, v) for k, v in load_conf(model, []) if not k.startswith("metric")]
+    # deterministic: no fp32 atomics in the weight gradients, so the arms can agree bit for bit
     for k, v in base + [("batch_size", str(batch)), ("dev", "gpu"), ("eval_train", "0"), ("silent", "1"),
-                        ("seed", "5"), ("cuda_graph", "0")] + list(extra):
+                        ("seed", "5"), ("cuda_graph", "0"), ("deterministic", "1")] + list(extra):
         tr.set_param(k, v)
     tr.init_model()
     return tr
@@ -77,7 +90,9 @@ def _worker(rank, port, steps, out, extra):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
                       LOCAL_RANK="0", CXXNET_DIST_BACKEND="nccl", CXXNET_DIST_FORCE="1")
     import torch.distributed as dist
+    from cxxnet_amd.nnet import trainer as trainer_mod
     from cxxnet_amd.parallel import init_distributed
+    trainer_mod._FUSE_FC_SGD = False  # as the parent's arm (spawned: the fixture does not reach here)
     init_distributed()
     tr = _make(8, extra)
     x, y = _data(8)
