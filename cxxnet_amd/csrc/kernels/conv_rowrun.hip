@@ -62,6 +62,8 @@ __device__ __forceinline__ void vm_wait(int n) {  // s_waitcnt vmcnt(n), n unifo
   }
 }
 
+constexpr int KSM = 16;  // k-steps the forward kernel unrolls (KS <= KSM served)
+
 template <int CFH>  // 16-channel output fragments per wave (Cout = 32 * CFH)
 __global__ void __launch_bounds__(NT, 1)
 conv_rowrun_fwd(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__restrict__ w, const float *__restrict__ bias,
@@ -142,6 +144,10 @@ conv_rowrun_fwd(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__rest
     return kh * pitch + (c - kh * NJ) * 16;
   };
 
+  int toffs[KSM];  // the lane's chunk offset of every k-step (the pad steps past KS: unused)
+#pragma unroll
+  for (int s = 0; s < KSM; ++s) toffs[s] = s < KS ? tap(s) : 0;
+
   const int pxs = S * C * 2;  // bytes per output-pixel step in a staged row
   int pxo[4];  // byte offset of this lane's pixel in each fragment: pixel 32 (pf / 2) + 2 l16 + (pf & 1)
 #pragma unroll
@@ -173,7 +179,7 @@ conv_rowrun_fwd(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__rest
     auto load = [&](int s, bf16x8 (&a)[CFH], bf16x8 (&b)[4]) {
 #pragma unroll
       for (int cf = 0; cf < CFH; ++cf) a[cf] = *reinterpret_cast<const bf16x8 *>(wrow + cf * 16 * WPB + s * 64);
-      const char *p0 = sx + tap(s);
+      const char *p0 = sx + toffs[s];
 #pragma unroll
       for (int pf = 0; pf < 4; ++pf) {
         const uint2 lo = *reinterpret_cast<const uint2 *>(p0 + pxo[pf]);
@@ -189,12 +195,16 @@ conv_rowrun_fwd(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__rest
           acc[cf][pf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[cf], b[pf], acc[cf][pf], 0, 0, 0);
     };
     bf16x8 a0[CFH], b0[4], a1[CFH], b1[4];
+    // fully unrolled over KSM k-steps (runtime KS <= KSM): every tap offset is a register
+    // computed once per block (toffs), every weight read a base + immediate
     load(0, a0, b0);
-    for (int s = 0; s < KS; s += 2) {
-      load(min(s + 1, KS - 1), a1, b1);
+#pragma unroll
+    for (int s = 0; s < KSM; s += 2) {
+      if (s >= KS) break;
+      if (s + 1 < KS) load(s + 1, a1, b1);
       mma(a0, b0);
       if (s + 1 >= KS) break;
-      load(min(s + 2, KS - 1), a0, b0);
+      if (s + 2 < KS) load(s + 2 < KSM ? s + 2 : KSM - 1, a0, b0);
       mma(a1, b1);
     }
     __syncthreads();  // every wave is done reading the span: its buffer becomes epilogue staging
@@ -263,6 +273,7 @@ int launch(const bf16_t *x, long x_bytes, const bf16_t *w, const float *bias, bf
   if (y_bytes >= (1L << 31)) return -1;
   const int K = KH * LP;
   const int KS = (K + 31) / 32;
+  if (KS > KSM) return -1;
   const int cout = 32 * CFH;
   const long span = static_cast<long>(S * (RG - 1) + KH) * W * C * 2 + 16;  // + the last run's pad reads
   const int ndma = static_cast<int>((span + 1023) / 1024);

@@ -494,7 +494,9 @@ class NeuralNet:
         # bucket (hook_due(i): the hook would launch one after layer i), since a bucket needs every
         # gradient of its layers.  The dy buffers they read are not rewritten later in the pass.
         from ..ops.gemm import deterministic
-        defer = self.ctx.is_gpu and not deterministic()
+        from ..ops.mode import reference_precision
+        # (the fp32 reference mode sums each bias gradient at once, as the CPU path does)
+        defer = self.ctx.is_gpu and not deterministic() and not reference_precision()
         self.ctx.deferred_bias = [] if defer else None
         if self.ctx.is_gpu:
             # every conv data-gradient's flipped weights in one launch (weights do not change

@@ -157,7 +157,9 @@ GLDS_TILES = {0: (128, 256), 1: (128, 128), 2: (128, 128), 4: (192, 256), 5: (64
               82: (256, 192), 83: (192, 256),
               # one wave per SIMD, address-free DMA issue (gemm_4w.hip): 113 = 32x32x16 MFMA
               110: (256, 256), 111: (256, 128), 112: (128, 256), 113: (256, 256), 114: (128, 128),
-              115: (64, 256)}
+              115: (64, 256),
+              # direct 3x3 halo convolution (conv_halo.hip): output channels x 256-pixel patch
+              130: (64, 256), 131: (128, 256)}
 # operand loaders of gemm_glds.hip
 GL_K, GL_KG, GL_MN, GL_MNG, GL_KR = 0, 1, 2, 3, 4  # K_DIRECT, K_GATHER, MN_DIRECT, MN_GATHER, K_ROWGATHER
 EPI_F32_ACC_G, EPI_F32_ATOMIC_G, EPI_BF16_DB_G = 2, 3, 5
@@ -177,7 +179,7 @@ _glds_cfg = {"on": os.environ.get("CXXNET_GEMM_GLDS", "1") != "0",
 # 128x256 / 64x256 tiles and the pipelined variants (30-41) win conv2/conv3 forward, fc6 forward
 # and several VGG shapes (profiles/r2_sweep_tiles.jsonl).
 GLDS_CANDS = (1, 7, 10, 15, 2, 0, 13, 17, 21, 25, 30, 31, 34, 37, 38, 39, 40, 41, 50, 51, 72, 76, 77, 78, 79, 80,
-              81, 82, 83, 110, 111, 112, 113, 114, 115)
+              81, 82, 83, 110, 111, 112, 113, 114, 115, 130, 131)
 # conv weight-grad shapes missing from the shipped table are timed on first use too (else the
 # register kernel runs them)
 _CW_TUNE = os.environ.get("CXXNET_CW_TUNE", "0") == "1"

@@ -27,7 +27,7 @@ def test_every_entry_names_a_known_tile():
 
 def test_tuning_candidates_are_known_tiles():
     assert set(G.GLDS_CANDS) <= set(G.GLDS_TILES)
-    for t in (82, 83):  # wave-quantisation tiles (round 3)
+    for t in (82, 83, 110, 114, 115, 130, 131):  # wave-quantisation (r3), one-wave-per-SIMD, halo (r4)
         assert t in G.GLDS_CANDS
 
 

@@ -24,3 +24,5 @@ for m in "alexnet 256" "vgg16 64" "inception_v1 128"; do
   CXXNET_GEMM_TUNE_DB=$OUT/t4.json timeout -k 10 300 python -u bench.py --model $1 --batch $2 --steps 20 --warmup 5 >> $OUT/bench.jsonl 2> $OUT/bench_$1.err || { echo "$1 bench failed"; tail -5 $OUT/bench_$1.err; exit 1; }
 done
 cut -c1-200 $OUT/bench.jsonl
+export CXXNET_GEMM_TUNE_DB=$OUT/t4.json
+bash tools/gpu_prof_model.sh r4alex alexnet 256 || exit 1
