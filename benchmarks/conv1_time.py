@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=9)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--arms", default="new", help="comma list of arms (new: conv_rowrun.hip)")
     a = ap.parse_args()
     from cxxnet_amd import native
     from cxxnet_amd.ops import gemm as G
@@ -29,24 +30,36 @@ def main():
     y = torch.empty(N, Ho, Wo, Cout, device="cuda", dtype=torch.bfloat16)
     k = native.kernels()
 
-    def run():
-        rc = k.cxn_conv_rowrun_fwd(x.data_ptr(), x.numel() * 2, wp.data_ptr(), b.data_ptr(), y.data_ptr(), N, H, W, C,
+    def run(fn):
+        rc = fn(x.data_ptr(), x.numel() * 2, wp.data_ptr(), b.data_ptr(), y.data_ptr(), N, H, W, C,
                                    Ho, Wo, Cout, K, lp, S, Cout, 1, torch.cuda.current_stream().cuda_stream)
         assert rc == 0, rc
-    run()
-    torch.cuda.synchronize()
+    fns = {"new": k.cxn_conv_rowrun_fwd}
+    arms = a.arms.split(",")
+    outs = {}
+    for arm in arms:
+        run(fns[arm])
+        torch.cuda.synchronize()
+        outs[arm] = y.float().clone()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ts = []
+    ts = {arm: [] for arm in arms}
     for _ in range(a.rounds):
-        s.record()
-        for _ in range(a.iters):
-            run()
-        e.record()
-        e.synchronize()
-        ts.append(s.elapsed_time(e) / a.iters * 1000)
+        for arm in arms:
+            s.record()
+            for _ in range(a.iters):
+                run(fns[arm])
+            e.record()
+            e.synchronize()
+            ts[arm].append(s.elapsed_time(e) / a.iters * 1000)
     flops = 2.0 * N * Ho * Wo * Cout * K * K * C
-    us = statistics.median(ts)
-    print(json.dumps({"op": "conv1_rowrun_fwd", "batch": N, "us": round(us, 1), "tflops": round(flops / us / 1e6, 1)}))
+    rec = {"op": "conv1_rowrun_fwd", "batch": N}
+    for arm in arms:
+        us = statistics.median(ts[arm])
+        rec[f"{arm}_us"] = round(us, 1)
+        rec[f"{arm}_tflops"] = round(flops / us / 1e6, 1)
+    if len(arms) > 1:
+        rec["max_abs_diff"] = (outs[arms[0]] - outs[arms[1]]).abs().max().item()
+    print(json.dumps(rec))
 
 
 if __name__ == "__main__":

@@ -130,17 +130,12 @@ LaunchList *&rec_slot();  // this thread's open list (nullptr: not recording)
       });                                                                                        \
   } while (0)
 
-// stream-ordered memset, recorded like a launch
-#define CXN_MEMSET(PTR, VAL, BYTES, STREAM)                                                      \
-  ([&]() -> hipError_t {                                                                         \
-    void *cxn_p_ = (PTR);                                                                        \
-    const int cxn_v_ = (VAL);                                                                    \
-    const size_t cxn_n_ = (BYTES);                                                               \
-    const hipError_t cxn_e_ = hipMemsetAsync(cxn_p_, cxn_v_, cxn_n_, (STREAM));                  \
-    if (::cxr::LaunchList *cxn_rec_ = ::cxr::rec_slot())                                         \
-      cxn_rec_->ops.emplace_back([=](hipStream_t cxn_s_) { (void)hipMemsetAsync(cxn_p_, cxn_v_, cxn_n_, cxn_s_); }); \
-    return cxn_e_;                                                                               \
-  }())
+// Stream-ordered byte fill as a library KERNEL (launch_list.hip cxn_fill_bytes), recorded like a
+// launch.  Not hipMemsetAsync: inside a captured HIP graph its memset node zeroed the range on
+// the first replay only (later replays left 0x00000106 words; tools/diag_memset_graph.py), which
+// let every captured step accumulate gradients on top of the previous one.
+hipError_t cxn_fill_bytes(void *p, int v, size_t n, hipStream_t s);
+#define CXN_MEMSET(PTR, VAL, BYTES, STREAM) ::cxn_fill_bytes((PTR), (VAL), (BYTES), (STREAM))
 
 // stream-ordered device-to-device copy, recorded like a launch
 #define CXN_MEMCPY_D2D(DST, SRC, BYTES, STREAM)                                                  \

@@ -19,21 +19,10 @@
 //     row of 64 pixels: CFH x 4 accumulator tiles of v_mfma_f32_16x16x32_bf16; per k-step CFH A
 //     reads (b128) and 8 B reads (b64) for 4 x CFH MFMAs, the next k-step's reads issued before
 //     this one's MFMAs (the tap offset is arithmetic, no LDS table on the dependency chain);
-//   * bank-conflict-free operand reads (round 3 measured 25 % conflict cycles):
-//       - B: a fragment takes every other pixel (lanes 2 l16 + parity), so a 16-lane half's
-//         reads step 2 S C elements (AlexNet: 12 dwords: 16 distinct 4-dword slots mod 64), and
-//         the two halves of a 32-lane read group take k chunks (kh, jj) / (kh + 1, jj) of
-//         adjacent kernel rows, whose offsets differ by the row pitch (342 dwords = 2 mod 4): the
-//         halves fill the other two dwords of every slot.  The K order is permuted accordingly
-//         (weights are staged in the same slot order); fragment pixels past Wo clamp to the last
-//         pixel OF THE SAME PARITY;
-//       - A: weight rows at a pitch of (4 m + 2) x 16 bytes, so the 16 lanes of every b128 group
-//         (rows l16, chunks g4 / g4 + 1) land on 16 distinct 16-byte slots;
 //   * epilogue: bias + relu in fp32 -> bf16, transposed through LDS (the item's input buffer,
-//     free by then; 32 pixels x 128-byte rows per wave, 8-byte pieces XOR-swizzled by the pixel
-//     pair so the fragment writes are conflict-free) so each pixel's channels leave as 16-byte
-//     buffer stores; every store instruction is issued (masked lanes store out of range), so the
-//     next item waits with a counted s_waitcnt for its own DMAs only, not for these stores.
+//     free by then) so each pixel's channels leave as 16-byte buffer stores; every store
+//     instruction is issued (masked lanes store out of range), so the next item waits with a
+//     counted s_waitcnt for its own DMAs only, not for these stores.
 #include <cstdlib>
 #include "common.h"
 
@@ -62,21 +51,18 @@ __device__ __forceinline__ void vm_wait(int n) {  // s_waitcnt vmcnt(n), n unifo
   }
 }
 
-constexpr int KSM = 16;  // k-steps the forward kernel unrolls (KS <= KSM served)
-
 template <int CFH>  // 16-channel output fragments per wave (Cout = 32 * CFH)
 __global__ void __launch_bounds__(NT, 1)
 conv_rowrun_fwd(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__restrict__ w, const float *__restrict__ bias,
-                bf16_t *__restrict__ y, long y_bytes, int N, int H, int W, int C, int Ho, int Wo, int KH, int LP, FastDiv fd_nj, int S,
-                int ldc, int relu, int KS, int XB, int ndma, int counted, int WPB) {
+                bf16_t *__restrict__ y, long y_bytes, int N, int H, int W, int C, int Ho, int Wo, int KH, int LP, FastDiv fd_lp, int S,
+                int ldc, int relu, int KS, int XB, int ndma, int counted) {
   constexpr int COUT = 32 * CFH;
   constexpr int NWV = NT / 64;
-  static_assert(CFH <= 4, "epilogue staging rows of 128 bytes");
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int KP = KS * 32;                  // k padded to whole k-steps
+  const int WPB = KP * 2 + 16;             // weight row pitch (bytes)
   const int pitch = W * C * 2;             // input row (bytes)
-  const int NJ = LP / 8;                   // 16-byte k chunks per kernel row
-  const int R2 = KH / 2;                   // kernel-row pairs
+  const int K = KH * LP;
   char *sx0 = smem;                        // [2][XB] staged input spans
   char *sw = smem + 2 * XB;                // [COUT][WPB]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -100,32 +86,11 @@ conv_rowrun_fwd(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__rest
   long it = blockIdx.x;
   if (it < items) issue(it, 0);
 
-  // K slot order: k-step s holds chunk pairs q = 2 s (lanes 0-31) and 2 s + 1 (lanes 32-63), the
-  // lane quarter g4 & 1 picks the member.  Pair q < R2 NJ: chunk jj = q % NJ of kernel rows
-  // 2 (q / NJ) and + 1; then (KH odd) chunks 2 r, 2 r + 1 of the last row; the rest is padding
-  // (-1: zero weights)
-  auto slot_chunk = [&](int s, int g) -> int {  // kh * NJ + jj, or -1
-    const int q = 2 * s + (g >> 1), m = g & 1;
-    int kh, jj;
-    if (q < R2 * NJ) {
-      const int a = static_cast<int>(fdiv(static_cast<uint32_t>(q), fd_nj));
-      kh = 2 * a + m;
-      jj = q - a * NJ;
-    } else {
-      kh = KH - 1;
-      jj = 2 * (q - R2 * NJ) + m;
-    }
-    return (KH % 2 == 1 || q < R2 * NJ) && jj < NJ && kh < KH ? kh * NJ + jj : -1;
-  };
-  // weights, staged in slot order, zero in the pad slots (they arrive row-padded to LP per kernel row)
+  // weights, zero-padded to KP along k (they arrive row-padded to LP per kernel row)
   for (int e = tid; e < COUT * (KP / 8); e += NT) {
     const int co = e / (KP / 8), kc = e - co * (KP / 8);
-    const int c = slot_chunk(kc >> 2, kc & 3);
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (c >= 0) {
-      const int kh = c / NJ, jj = c - kh * NJ;
-      v = *reinterpret_cast<const uint4 *>(w + static_cast<long>(co) * KH * LP + kh * LP + jj * 8);
-    }
+    if (kc * 8 < K) v = *reinterpret_cast<const uint4 *>(w + static_cast<long>(co) * K + kc * 8);
     *reinterpret_cast<uint4 *>(sw + co * WPB + kc * 16) = v;
   }
   float bv[CFH][4];
@@ -135,33 +100,23 @@ conv_rowrun_fwd(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__rest
 #pragma unroll
     for (int j = 0; j < 4; ++j) bv[cf][j] = bias ? bias[(ch * CFH + cf) * 16 + 4 * g4 + j] : 0.f;
   const char *wrow = sw + (ch * CFH * 16 + l16) * WPB + 16 * g4;
-  // the lane's k chunk of k-step s: byte offset in a span (pad slots: the odd row's offset, whose
-  // bank parity is the partner's complement; zero weights)
+  // the lane's k chunk of k-step s: byte offset in a span (pad chunks: offset 0, zero weights)
   auto tap = [&](int s) -> int {
-    const int c = slot_chunk(s, g4);
-    if (c < 0) return KH > 1 ? pitch : 0;
-    const int kh = static_cast<int>(fdiv(static_cast<uint32_t>(c), fd_nj));
-    return kh * pitch + (c - kh * NJ) * 16;
+    const int k = s * 32 + 8 * g4;
+    const int kh = static_cast<int>(fdiv(static_cast<uint32_t>(k), fd_lp));
+    return k < K ? kh * pitch + (k - kh * LP) * 2 : 0;
   };
 
-  int toffs[KSM];  // the lane's chunk offset of every k-step (the pad steps past KS: unused)
-#pragma unroll
-  for (int s = 0; s < KSM; ++s) toffs[s] = s < KS ? tap(s) : 0;
-
   const int pxs = S * C * 2;  // bytes per output-pixel step in a staged row
-  int pxo[4];  // byte offset of this lane's pixel in each fragment: pixel 32 (pf / 2) + 2 l16 + (pf & 1)
+  int pxo[4];                 // byte offset of this lane's pixel (column) in each of the wave's 4 fragments
 #pragma unroll
-  for (int pf = 0; pf < 4; ++pf) {
-    int px = 32 * (pf >> 1) + 2 * l16 + (pf & 1);
-    if (px >= Wo) px = ((Wo - 1 - px) & 1) ? Wo - 2 : Wo - 1;  // same parity: same bank half
-    pxo[pf] = row * S * pitch + max(px, 0) * pxs;
-  }
+  for (int pf = 0; pf < 4; ++pf) pxo[pf] = row * S * pitch + min(16 * pf + l16, Wo - 1) * pxs;
   int buf = 0;
   // this wave's epilogue stores of the previous item: every store instruction is issued (masked
   // stores go to an out-of-range offset), so the count is fixed and the wait below lets them
   // drain behind the next item's MFMAs (vector-memory operations retire in issue order)
-  constexpr int NPASS = (32 * CFH * 2 + 63) / 64;
-  const int npp = min(2, (Wo + 31) / 32);
+  constexpr int NPASS = (16 * CFH * 2 + 63) / 64;
+  const int npf = min(4, (Wo + 15) / 16);
   int nst = 0;
   for (; it < items; it += gridDim.x) {
     const int n = static_cast<int>(it / groups_per_img), grp = static_cast<int>(it - static_cast<long>(n) * groups_per_img);
@@ -179,7 +134,7 @@ conv_rowrun_fwd(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__rest
     auto load = [&](int s, bf16x8 (&a)[CFH], bf16x8 (&b)[4]) {
 #pragma unroll
       for (int cf = 0; cf < CFH; ++cf) a[cf] = *reinterpret_cast<const bf16x8 *>(wrow + cf * 16 * WPB + s * 64);
-      const char *p0 = sx + toffs[s];
+      const char *p0 = sx + tap(s);
 #pragma unroll
       for (int pf = 0; pf < 4; ++pf) {
         const uint2 lo = *reinterpret_cast<const uint2 *>(p0 + pxo[pf]);
@@ -195,59 +150,47 @@ conv_rowrun_fwd(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__rest
           acc[cf][pf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[cf], b[pf], acc[cf][pf], 0, 0, 0);
     };
     bf16x8 a0[CFH], b0[4], a1[CFH], b1[4];
-    // fully unrolled over KSM k-steps (runtime KS <= KSM): every tap offset is a register
-    // computed once per block (toffs), every weight read a base + immediate
     load(0, a0, b0);
-#pragma unroll
-    for (int s = 0; s < KSM; s += 2) {
-      if (s >= KS) break;
-      if (s + 1 < KS) load(s + 1, a1, b1);
+    for (int s = 0; s < KS; s += 2) {
+      load(min(s + 1, KS - 1), a1, b1);
       mma(a0, b0);
       if (s + 1 >= KS) break;
-      if (s + 2 < KS) load(s + 2 < KSM ? s + 2 : KSM - 1, a0, b0);
+      load(min(s + 2, KS - 1), a0, b0);
       mma(a1, b1);
     }
     __syncthreads();  // every wave is done reading the span: its buffer becomes epilogue staging
 
-    // epilogue: per fragment pair (pf = 2 pp, 2 pp + 1: pixels 32 pp .. + 31), 32 pixels x
-    // (CFH*16) channels through this wave's staging rows (128 bytes; 8-byte piece L of pixel px at
-    // L ^ ((px >> 1) & 15))
-    char *st = const_cast<char *>(sx) + wave * 32 * 128;
+    // epilogue: per fragment, 16 pixels x (CFH*16) channels through this wave's staging rows
+    constexpr int SPB = CFH * 32 + 16;  // staging row pitch (bytes)
+    char *st = const_cast<char *>(sx) + wave * 16 * SPB;
     const int ho = grp * RG + row;
-    nst = ho < Ho ? npp * NPASS : 0;
+    nst = ho < Ho ? npf * NPASS : 0;
     if (ho < Ho) {  // wave-uniform
       const long yrow = (((static_cast<long>(n) * Ho + ho) * Wo) * static_cast<long>(ldc) + ch * CFH * 16) * 2;
 #pragma unroll
-      for (int pp = 0; pp < 2; ++pp) {
-        const int col0 = 32 * pp;
+      for (int pf = 0; pf < 4; ++pf) {
+        const int col0 = 16 * pf;
         if (col0 >= Wo) break;  // wave-uniform
 #pragma unroll
-        for (int par = 0; par < 2; ++par) {
-          const int pf = 2 * pp + par;
-          const int px = 2 * l16 + par;
+        for (int cf = 0; cf < CFH; ++cf) {
+          float v[4];
 #pragma unroll
-          for (int cf = 0; cf < CFH; ++cf) {
-            float v[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              v[j] = acc[cf][pf][j] + bv[cf][j];
-              if (relu) v[j] = fmaxf(v[j], 0.f);
-            }
-            *reinterpret_cast<uint2 *>(st + px * 128 + 8 * ((cf * 4 + g4) ^ l16)) =
-                make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+          for (int j = 0; j < 4; ++j) {
+            v[j] = acc[cf][pf][j] + bv[cf][j];
+            if (relu) v[j] = fmaxf(v[j], 0.f);
           }
+          *reinterpret_cast<uint2 *>(st + l16 * SPB + (cf * 16 + 4 * g4) * 2) =
+              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
         }
         wave_lds_handoff();
         constexpr int CH = CFH * 2;  // 16-byte chunks per pixel (of this wave's channels)
 #pragma unroll
         for (int i = 0; i < NPASS; ++i) {
-          const int c = min(lane + 64 * i, 32 * CH - 1);
+          const int c = min(lane + 64 * i, 16 * CH - 1);
           const int px = c / CH, part = c - px * CH;
-          const int h = (px >> 1) & 15;
           const int wo = col0 + px;
-          uint4 v = *reinterpret_cast<const uint4 *>(st + px * 128 + 16 * (part ^ (h >> 1)));
-          if (h & 1) v = make_uint4(v.z, v.w, v.x, v.y);
-          const bool ok = lane + 64 * i < 32 * CH && wo < Wo;
+          const uint4 v = *reinterpret_cast<const uint4 *>(st + px * SPB + part * 16);
+          const bool ok = lane + 64 * i < 16 * CH && wo < Wo;
           const uint32_t off = ok ? static_cast<uint32_t>(yrow + (static_cast<long>(wo) * ldc + part * 8) * 2) : 0x80000000u;
           typedef int v4i __attribute__((ext_vector_type(4)));
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), ry, off, 0, 0);
@@ -273,15 +216,12 @@ int launch(const bf16_t *x, long x_bytes, const bf16_t *w, const float *bias, bf
   if (y_bytes >= (1L << 31)) return -1;
   const int K = KH * LP;
   const int KS = (K + 31) / 32;
-  if (KS > KSM) return -1;
   const int cout = 32 * CFH;
   const long span = static_cast<long>(S * (RG - 1) + KH) * W * C * 2 + 16;  // + the last run's pad reads
   const int ndma = static_cast<int>((span + 1023) / 1024);
-  const int epi = (NT / 64) * 32 * 128;  // epilogue staging reuses the item's buffer
+  const int epi = (NT / 64) * 16 * (CFH * 32 + 16);  // epilogue staging reuses the item's buffer
   const int XB = (ndma * 1024 > epi ? ndma * 1024 : epi + 1023) / 1024 * 1024;
-  int WPB = KS * 64;  // weight row pitch: (4 m + 2) 16-byte chunks
-  while ((WPB / 16) % 4 != 2) WPB += 16;
-  const long lds = 2L * XB + static_cast<long>(cout) * WPB;
+  const long lds = 2L * XB + static_cast<long>(cout) * (KS * 64 + 16);
   if (lds > 160 * 1024) return -1;
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void *>(conv_rowrun_fwd<CFH>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -289,7 +229,7 @@ int launch(const bf16_t *x, long x_bytes, const bf16_t *w, const float *bias, bf
   const long items = static_cast<long>(N) * ((Ho + RG - 1) / RG);
   const int grid = static_cast<int>(items < 256 ? items : 256);
   CXN_LAUNCH(conv_rowrun_fwd<CFH>, dim3(grid), dim3(NT), static_cast<size_t>(lds), s, x, x_bytes, w, bias, y, y_bytes, N,
-                     H, W, C, Ho, Wo, KH, LP, make_fastdiv(LP / 8), S, ldc, relu, KS, XB, ndma, g_counted, WPB);
+                     H, W, C, Ho, Wo, KH, LP, make_fastdiv(LP), S, ldc, relu, KS, XB, ndma, g_counted);
   return 0;
 }
 

@@ -65,6 +65,33 @@ CXN_API int cxn_copy_d2d(void *dst, const void *src, long bytes, void *stream) {
   return CXN_MEMCPY_D2D(dst, src, static_cast<size_t>(bytes), static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : -3;
 }
 
+namespace {
+// 16 bytes per thread where the range is 16-byte aligned, the unaligned head / tail byte-wise
+__global__ void fill_bytes_k(unsigned char *p, unsigned v, size_t n) {
+  const size_t tid = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const size_t head = ((16 - (a & 15)) & 15) < n ? ((16 - (a & 15)) & 15) : n;
+  const size_t nv = (n - head) / 16;
+  const unsigned w = v * 0x01010101u;
+  uint4 *pv = reinterpret_cast<uint4 *>(p + head);
+  for (size_t i = tid; i < nv; i += stride) pv[i] = make_uint4(w, w, w, w);
+  const size_t tail0 = head + nv * 16;
+  for (size_t i = tid; i < head + (n - tail0); i += stride) {
+    const size_t b = i < head ? i : tail0 + (i - head);
+    p[b] = static_cast<unsigned char>(v);
+  }
+}
+}  // namespace
+
+hipError_t cxn_fill_bytes(void *p, int v, size_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const size_t nv = n / 16 + 1;
+  const unsigned blocks = static_cast<unsigned>(nv / 256 + 1 < 2048 ? nv / 256 + 1 : 2048);
+  CXN_LAUNCH(fill_bytes_k, dim3(blocks), dim3(256), 0, s, static_cast<unsigned char *>(p), static_cast<unsigned>(v) & 0xffu, n);
+  return hipGetLastError();
+}
+
 // Zero `bytes` bytes at dst on `stream` (recorded when a list is open): gradient zeroing at the
 // start of a backward pass must be part of the replayed step.
 CXN_API int cxn_zero(void *dst, long bytes, void *stream) {

@@ -15,6 +15,8 @@ from __future__ import annotations
 
 from typing import List, Sequence
 
+import os
+
 import torch
 
 ALIGN = 64  # elements; keeps every view 256-B aligned in fp32 and 128-B in bf16
@@ -78,8 +80,12 @@ class ParamArena:
 
     def zero_accumulated_grads(self):
         from .. import ops  # a library memset: launch lists record it (a torch zero_ they would not)
+        torch_zero = os.environ.get("CXXNET_ZERO_TORCH", "0") == "1"  # diagnostics
         for a, b in self.accumulate_ranges():
-            ops.zero_(self.g[a:b])
+            if torch_zero:
+                self.g[a:b].zero_()
+            else:
+                ops.zero_(self.g[a:b])
 
     def ensure_second_moment(self):
         if self.m2 is None:

@@ -14,7 +14,10 @@ def main():
     from cxxnet_amd.io.data import DataBatch
     model, batch = "alexnet", 16
     over = {"eval_train": "1", "metric": "error", "lr:schedule": "expdecay", "lr:gamma": "0.5", "lr:step": "2"}
-    eager = T._trainer(T._pairs(model, batch, **over), "gpu")
+    eager_over = dict(over)
+    if os.environ.get("DIAG_EAGER") == "1":
+        eager_over["launch_replay"] = "0"
+    eager = T._trainer(T._pairs(model, batch, **eager_over), "gpu")
     graph = T._trainer(T._pairs(model, batch, cuda_graph="1", **over), "gpu")
     graph.net.arena.w.copy_(eager.net.arena.w)
     graph.net.arena.sync_shadow()
@@ -29,6 +32,12 @@ def main():
         print(f"step {step}: rel m1 {T._rel(graph.net.arena.m1, eager.net.arena.m1):.3g} "
               f"eager plans {list(eager._lists)} {list(eager._graphs)} graph plans {list(graph._graphs)} "
               f"fused e {sorted(eager.net.updater.fused_offsets)} g {sorted(graph.net.updater.fused_offsets)}", flush=True)
+        specs = dict(((li, s.tag), s) for li, s in eager.net.arena.specs)
+        sb = specs.get((22, "bias"))
+        if sb is not None:
+            sl = slice(sb.offset, sb.offset + sb.numel)
+            print(f"   fc8 bias |g| eager {eager.net.arena.g[sl].norm().item():.4g} graph {graph.net.arena.g[sl].norm().item():.4g}"
+                  f" |w| eager {eager.net.arena.w[sl].norm().item():.4g} graph {graph.net.arena.w[sl].norm().item():.4g}", flush=True)
         for li, s in eager.net.arena.specs:
             a = graph.net.arena.m1[s.offset:s.offset + s.numel]
             b = eager.net.arena.m1[s.offset:s.offset + s.numel]

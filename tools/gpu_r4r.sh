@@ -9,3 +9,4 @@ timeout -k 10 300 python -u tools/diag_e2e.py > $OUT/e2e.log 2>&1; echo "diag rc
 timeout -k 10 300 python -u -m pytest tests/test_e2e_gpu.py tests/test_launch_hygiene_gpu.py -q -rfE --timeout 150 --timeout-method thread -p no:cacheprovider > $OUT/t.log 2>&1; echo "tests rc=$?"; grep -E "passed|failed|^FAILED" $OUT/t.log
 timeout -k 10 600 bash tools/gpu_dp4.sh || exit $?
 timeout -k 10 500 bash tools/gpu_io4.sh
+bash tools/pmc_tiles.sh r4sq sq8192_fwd 21 110 113 && cat gpurun_out/pmct_r4sq/summary.txt
