@@ -643,7 +643,13 @@ class NetTrainer:
         # (fullc_gather layers issue their all-gathers through ctx.graph_cut: eager calls between
         # graph segments, like the bucket collectives)
         if self.cuda_graph < 0:
-            return red.handles_update and self._local_batch() <= 64
+            # auto: data parallel at per-GPU batch <= 64, and only when the C++ launch lists
+            # cannot take the step -- they replay the same plan faster (AlexNet b32, RCCL forced
+            # at world 1: 1.233 vs 1.307 ms with fullc_gather, 1.139 vs 1.198 ms without,
+            # profiles/r4_dp_graph_vs_lists_b32.jsonl: fewer, cheaper segment launches)
+            if not (red.handles_update and self._local_batch() <= 64):
+                return False
+            return self.launch_replay == 0 or not all(c.layer.replay_safe() for c in net.connections)
         if red.handles_update:  # data parallel: segmented graphs around the collectives
             return True
         return self.world == 1 and not red.shard
@@ -726,11 +732,12 @@ class NetTrainer:
 
     # ------------------------------------------------------------------ native launch lists
     def _list_eligible(self) -> bool:
-        """The C++ launch-list executor runs a step when HIP graphs do not.  Auto (-1): in the
-        host-bound regime only -- per-GPU batch <= 32, where Python enqueues a step about as
-        slowly as the GPU runs it; larger steps are GPU-bound and keep the eager path, whose fc
-        weight steps run inside the weight-gradient GEMMs (a planned step takes them through
-        the arena updater: its learning rate is a host value per step)."""
+        """The C++ launch-list executor runs a step when HIP graphs do not (under data
+        parallelism it is the auto choice, _graph_eligible).  Auto (-1): in the host-bound regime
+        only -- per-GPU batch <= 32 on one GPU (<= 64 data parallel), where Python enqueues a
+        step about as slowly as the GPU runs it; larger steps are GPU-bound and stay eager.  A
+        planned step keeps the fused fc SGD steps (schedule values from the updater's device
+        table, _plan_fuse)."""
         net, red = self.net, self.reducer
         if self.launch_replay == 0 or not net.ctx.is_gpu or self.update_period != 1 or red is None:
             return False
@@ -739,7 +746,9 @@ class NetTrainer:
         if not all(c.layer.replay_safe() for c in net.connections):
             return False
         if self.launch_replay < 0:
-            return self._local_batch() <= 32
+            # host-bound regime: per-GPU batch <= 32 on one GPU, <= 64 under data parallelism
+            # (where the collectives add host work between the segments)
+            return self._local_batch() <= (64 if red.handles_update else 32)
         return True
 
     def _drop_stale_plans(self):

@@ -158,6 +158,8 @@ GLDS_TILES = {0: (128, 256), 1: (128, 128), 2: (128, 128), 4: (192, 256), 5: (64
               # one wave per SIMD, address-free DMA issue (gemm_4w.hip): 113 = 32x32x16 MFMA
               110: (256, 256), 111: (256, 128), 112: (128, 256), 113: (256, 256), 114: (128, 128),
               115: (64, 256),
+              # one wave per SIMD, MN-major operands (gemm_4w_mn.hip): conv weight-gradients
+              120: (128, 128),
               # direct 3x3 halo convolution (conv_halo.hip): output channels x 256-pixel patch
               130: (64, 256), 131: (128, 256)}
 # operand loaders of gemm_glds.hip
