@@ -266,6 +266,64 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
             atomicAdd(out + static_cast<long>(j) * E.ldc + i, ep[jl * (WM + 4) + il] * E.alpha);
         }
       }
+    } else if constexpr (EPI == EPI_F32_SGD) {
+      // The fused SGD step is a memory stream (18 bytes per parameter: w and m read and written,
+      // the bf16 shadow written).  All of this lane's w / m loads of the fragment are issued
+      // before any store: loop iterations that store to w and m cannot be reordered by the
+      // compiler (it cannot prove the rows distinct), so a load-compute-store loop kept one
+      // HBM round trip in flight per lane (AlexNet fc6 at b32: 172 us for 680 MB).
+      const SgdHyp hy = sgd_hyper(E);
+      constexpr int LPR = WM / 4;
+      constexpr int RPI = 64 / LPR;
+      constexpr int NJL = (16 + RPI - 1) / RPI;
+      const int il = (lane % LPR) * 4;
+      const int i = ibase + il;
+      const int jl0 = lane < LPR * RPI ? lane / LPR : 16;
+      if (((E.ldc & 3) == 0) && (i + 4 <= Mi)) {
+        f32x4 wv[NJL], mv[NJL];
+#pragma unroll
+        for (int r = 0; r < NJL; ++r) {
+          const int jl = jl0 + r * RPI, j = jbase + n * 16 + jl;
+          if (jl < 16 && j < Nj) {
+            const long idx = static_cast<long>(j) * E.ldc + i;
+            wv[r] = *reinterpret_cast<const f32x4 *>(E.sgd_w + idx);
+            mv[r] = *reinterpret_cast<const f32x4 *>(E.sgd_m + idx);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < NJL; ++r) {
+          const int jl = jl0 + r * RPI, j = jbase + n * 16 + jl;
+          if (jl < 16 && j < Nj) {
+            const long idx = static_cast<long>(j) * E.ldc + i;
+            const f32x4 v = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il) * E.alpha;
+            f32x4 w4 = wv[r], m4 = mv[r];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float mm = m4[e];
+              w4[e] = sgd_step(hy, v[e], mm, w4[e]);
+              m4[e] = mm;
+            }
+            *reinterpret_cast<f32x4 *>(E.sgd_w + idx) = w4;
+            *reinterpret_cast<f32x4 *>(E.sgd_m + idx) = m4;
+            *reinterpret_cast<uint2 *>(E.sgd_wb + idx) = make_uint2(pack2(w4[0], w4[1]), pack2(w4[2], w4[3]));
+          }
+        }
+      } else {
+        for (int jl = jl0; jl < 16; jl += RPI) {
+          const int j = jbase + n * 16 + jl;
+          if (j < Nj && i < Mi) {
+            const f32x4 v = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il) * E.alpha;
+            const long idx = static_cast<long>(j) * E.ldc + i;
+            for (int e = 0; e < 4 && i + e < Mi; ++e) {
+              float mm = E.sgd_m[idx + e];
+              const float wn = sgd_step(hy, v[e], mm, E.sgd_w[idx + e]);
+              E.sgd_m[idx + e] = mm;
+              E.sgd_w[idx + e] = wn;
+              E.sgd_wb[idx + e] = f2bf(wn);
+            }
+          }
+        }
+      }
     } else {
       float *out = reinterpret_cast<float *>(E.out) + g * E.gstride;
       if constexpr (EPI == EPI_F32) out += wb.slice * E.kstride;
@@ -279,31 +337,7 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
         const int j = jbase + n * 16 + jl;
         if (j < Nj && i < Mi) {
           f32x4 v = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il) * E.alpha;
-          if constexpr (EPI == EPI_F32_SGD) {
-            const SgdHyp hy = sgd_hyper(E);
-            const long idx = static_cast<long>(j) * E.ldc + i;
-            if (vec) {
-              f32x4 wv = *reinterpret_cast<const f32x4 *>(E.sgd_w + idx);
-              f32x4 mv = *reinterpret_cast<const f32x4 *>(E.sgd_m + idx);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                float mm = mv[e];
-                wv[e] = sgd_step(hy, v[e], mm, wv[e]);
-                mv[e] = mm;
-              }
-              *reinterpret_cast<f32x4 *>(E.sgd_w + idx) = wv;
-              *reinterpret_cast<f32x4 *>(E.sgd_m + idx) = mv;
-              *reinterpret_cast<uint2 *>(E.sgd_wb + idx) = make_uint2(pack2(wv[0], wv[1]), pack2(wv[2], wv[3]));
-            } else {
-              for (int e = 0; e < 4 && i + e < Mi; ++e) {
-                float mm = E.sgd_m[idx + e];
-                const float wn = sgd_step(hy, v[e], mm, E.sgd_w[idx + e]);
-                E.sgd_m[idx + e] = mm;
-                E.sgd_w[idx + e] = wn;
-                E.sgd_wb[idx + e] = f2bf(wn);
-              }
-            }
-          } else {
+          {
             float *dst = out + static_cast<long>(j) * E.ldc + i;
             if (vec) {
               if constexpr (EPI == EPI_F32_ACC) v += *reinterpret_cast<const f32x4 *>(dst);
