@@ -91,8 +91,9 @@ def main():
             cands = list(SHORT if a.short else KK) + ([G.REG] if op in ("cf", "cd") else [])
         elif op in ("fw", "fws", "cwr"):
             cands = list(MM)
-        elif op == "cw":  # conv weight-grad: the register split-K kernel, LDS-DMA MN tiles, tile 120
-            cands = [G.REG] + list(MM) + [120]
+        elif op == "cw":  # conv weight-grad: the register split-K kernel, LDS-DMA MN tiles, tile 120,
+            # the direct 3x3 kernel (140; it declines other shapes and the entry then runs REG)
+            cands = [G.REG] + list(MM) + [120, 140]
         elif op == "cws":
             N, H, W, C, Co, KH, KW, st, py, px, g = (int(v) for v in key.split("|")[1:])
             Ho, Wo = conv_out_size(H, W, KH, KW, st, py, px)

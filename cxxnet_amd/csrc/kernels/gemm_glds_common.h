@@ -535,5 +535,8 @@ int dispatch_4m(int amode, int bmode, int epi, int tile, const GOperand &A, cons
 // direct 3x3 convolution on a resident input halo (conv_halo.hip): tiles 130-131; -1 when unsupported
 int dispatch_halo(int amode, int bmode, int epi, int tile, GOperand A, GOperand B, const GEpi &E, int groups,
                   int ksplit, hipStream_t s);
+// direct 3x3 weight-gradient on resident halo / dy tiles (conv_wgrad_halo.hip): tiles 140-142
+int dispatch_wgrad_halo(int amode, int bmode, int epi, int tile, const GOperand &A, const GOperand &B, const GEpi &E,
+                        int groups, hipStream_t s);
 
 }  // namespace cxg

@@ -161,7 +161,10 @@ GLDS_TILES = {0: (128, 256), 1: (128, 128), 2: (128, 128), 4: (192, 256), 5: (64
               # one wave per SIMD, MN-major operands (gemm_4w_mn.hip): conv weight-gradients
               120: (128, 128),
               # direct 3x3 halo convolution (conv_halo.hip): output channels x 256-pixel patch
-              130: (64, 256), 131: (128, 256)}
+              130: (64, 256), 131: (128, 256),
+              # direct 3x3 weight-gradient on resident halo / dy tiles (conv_wgrad_halo.hip): 64 x 64
+              # channel pairs, persistent over 128-pixel patches (140 auto width, 141 16, 142 32)
+              140: (64, 64), 141: (64, 64), 142: (64, 64)}
 # operand loaders of gemm_glds.hip
 GL_K, GL_KG, GL_MN, GL_MNG, GL_KR = 0, 1, 2, 3, 4  # K_DIRECT, K_GATHER, MN_DIRECT, MN_GATHER, K_ROWGATHER
 EPI_F32_ACC_G, EPI_F32_ATOMIC_G, EPI_BF16_DB_G = 2, 3, 5
