@@ -282,10 +282,254 @@ int launch_halo(const GOperand &A, const GOperand &B, const GEpi &E, hipStream_t
   return 0;
 }
 
+// Persistent form for ONE output-channel block (tiles 132-133: VGG conv1_2 forward / data-
+// gradient, conv2_1 forward, conv2_2).  With one or two channel blocks the kernel above stages
+// its first halo, runs its K-tiles and writes out with nothing overlapping the first halo's HBM
+// fetch or the epilogue inside the block; conv1_2 ran at ~590 TFLOP/s against ~1,000 for the
+// conv3-4 layers with 4-8 blocks.  Here one block per CU walks work items (patch, channel
+// block) over an XCD-contiguous patch range (the patches an XCD runs together are neighbours and
+// share halo rows in its L2).  The NEXT item's halo -- the next channel block of this patch, or
+// block 0 of the next patch -- rides on the current item's K-tiles exactly as in the kernel
+// above, and so do the next item's first two weight K-tiles (taps 7-8: the ring's t + 2 records;
+// one output-channel block, so every patch uses the same weights).  After a patch's last channel
+// block the epilogue stages through that item's halo buffer (no wave reads it after the tap-8
+// barrier) and a barrier closes it before the item after next streams into that buffer.
+template <int BM, int WT>
+__global__ void __launch_bounds__(256, 1)
+conv_halo_ps(GOperand A, GOperand B, GEpi E, int tiles_w, int tiles_h, uint32_t ntile, int ncb) {
+  using Cf = HaloCfg<BM, WT, true>;
+  constexpr int P = Cf::P, HALO = Cf::HALO, NHD = Cf::NHD, NG = Cf::NG;
+  constexpr int WM = Cf::WM, WN = Cf::WN, MR = Cf::MR, NR = Cf::NR, NA = Cf::NA, NHK = Cf::NHK;
+  constexpr int PER = MR * NR, NF = MR + NR;
+  __shared__ __attribute__((aligned(1024))) char smem[Cf::LDS];
+
+  // block b runs on XCD b % 8; XCD x owns patches [x ntile / 8, (x + 1) ntile / 8)
+  const uint32_t g8 = gridDim.x / 8, xcd = blockIdx.x % 8;
+  const uint32_t lo = static_cast<uint32_t>(static_cast<uint64_t>(ntile) * xcd / 8);
+  const uint32_t hi = static_cast<uint32_t>(static_cast<uint64_t>(ntile) * (xcd + 1) / 8);
+  uint32_t t = lo + blockIdx.x / 8;
+  if (t >= hi) return;  // whole block, before any barrier
+  const int H = B.H, W = B.W;
+  auto coords = [&](uint32_t tt, int &h0, int &w0, int &img) {
+    const int tw = static_cast<int>(tt % static_cast<uint32_t>(tiles_w));
+    tt /= static_cast<uint32_t>(tiles_w);
+    const int th = static_cast<int>(tt % static_cast<uint32_t>(tiles_h));
+    img = static_cast<int>(tt / static_cast<uint32_t>(tiles_h));
+    h0 = th * Cf::R;
+    w0 = tw * WT;
+  };
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave / Cf::WGN, wc = wave % Cf::WGN;
+  const int l16 = lane & 15, g4 = lane >> 4;
+
+  const int lchunk = (lane & 7) ^ (((wave & 1) << 2) + (lane >> 4));
+  uint32_t offA[NA];
+#pragma unroll
+  for (int s = 0; s < NA; ++s) {
+    const int row = 8 * (wave + 4 * s) + (lane >> 3);
+    offA[s] = row < A.rows ? static_cast<uint32_t>(row * A.ld) * 2u + lchunk * 16u : OOB;
+  }
+  // halo DMA offsets of the current patch (offH) and of the next item's halo (offN)
+  uint32_t offH[NHD], offN[NHD];
+  auto set_halo = [&](uint32_t (&off)[NHD], bool valid, int h0, int w0, int img) {
+#pragma unroll
+    for (int s = 0; s < NHD; ++s) {
+      const int q = wave + 4 * s;
+      const int slot = 8 * q + (lane >> 3);
+      const int hr = slot / P, hc = slot - hr * P;
+      const int gh = h0 - 1 + hr, gw = w0 - 1 + hc;
+      const bool ok = valid && q < NG && hc < WT + 2 && static_cast<unsigned>(gh) < static_cast<unsigned>(H) &&
+                      static_cast<unsigned>(gw) < static_cast<unsigned>(W);
+      off[s] = ok ? static_cast<uint32_t>(((img * H + gh) * W + gw) * B.C) * 2u + (((lane & 7) ^ (lane >> 3)) * 16u) : OOB;
+    }
+  };
+  auto halo_dst = [&](int buf, int s) -> char * {
+    const int q = wave + 4 * s;
+    return q < NG ? smem + buf * HALO + q * 1024 : smem + Cf::SINK;
+  };
+  const char *const wptr = reinterpret_cast<const char *>(A.ptr);
+  // weight K-tile (cb, tap): columns tap * Cg + 64 cb; in = false: no records
+  auto issue_A = [&](bool in, int cb, int tap, int stage) __attribute__((always_inline)) {
+    const uint32_t step = in ? static_cast<uint32_t>(tap * B.Cg + 64 * cb) * 2u : 0u;
+    const uint32_t n = in ? A.nbytes - step : 0u;
+#pragma unroll
+    for (int s = 0; s < NA; ++s)
+      lds_dma16h(wptr + step, n, smem + Cf::A_OFF + stage * Cf::ASTAGE + (wave + 4 * s) * 1024, offA[s]);
+  };
+
+  const char *pa = smem + Cf::A_OFF + wr * WM * 128;
+  const int fa_off0 = l16 * 128 + ((0 + g4) ^ (l16 >> 1)) * 16;
+  const int fa_off1 = l16 * 128 + ((4 + g4) ^ (l16 >> 1)) * 16;
+  int fb_off[3][2];
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+      fb_off[kw][kk] = (l16 + kw) * 128 + (((4 * kk + g4) ^ ((l16 + kw) & 7)) * 16) + wc * (WN / WT) * P * 128;
+
+  f32x4 acc[MR][NR];
+  bf16x8 fa[2][MR], fb[2][NR];
+  auto read_frag = [&](int set, int f, int st, int hb, int tap, int kk) __attribute__((always_inline)) {
+    if (f < MR) {
+      fa[set][f] = *reinterpret_cast<const bf16x8 *>(pa + st * Cf::ASTAGE + f * 16 * 128 + (kk ? fa_off1 : fa_off0));
+    } else {
+      const int n = f - MR;
+      const int kh = tap / 3, kw = tap % 3;
+      const int rr = (16 * n) / WT, c0 = (16 * n) % WT;
+      fb[set][n] = *reinterpret_cast<const bf16x8 *>(smem + hb * HALO + ((rr + kh) * P + c0) * 128 + fb_off[kw][kk]);
+    }
+  };
+
+  int h0, w0, img;
+  coords(t, h0, w0, img);
+  set_halo(offH, true, h0, w0, img);
+  const char *const hp = reinterpret_cast<const char *>(B.ptr);
+#pragma unroll
+  for (int s = 0; s < NHD; ++s) lds_dma16h(hp, B.nbytes, halo_dst(0, s), offH[s]);
+  issue_A(true, 0, 0, 0);
+  issue_A(true, 0, 1, 1);
+  wait_vmcnt<NA>();
+  block_barrier();
+#pragma unroll
+  for (int f = 0; f < NF; ++f) read_frag(0, f, 0, 0, 0, 0);
+  __builtin_amdgcn_sched_barrier(0);
+
+  int hb = 0, cb = 0;
+  uint32_t tn = t;
+  int h0n = h0, w0n = w0, imgn = img;
+  for (;;) {
+    const bool last_cb = cb == ncb - 1;
+    bool more = true;
+    int cbn = cb + 1;
+    if (last_cb) {  // the next item is block 0 of the next patch (if any)
+      tn = t + g8;
+      more = tn < hi;
+      cbn = 0;
+      if (more) coords(tn, h0n, w0n, imgn);
+      set_halo(offN, more, h0n, w0n, imgn);
+    } else {
+#pragma unroll
+      for (int s = 0; s < NHD; ++s) offN[s] = offH[s];
+    }
+    const uint32_t hstep = more ? 128u * cbn : 0u;
+    const char *const hpn = hp + hstep;
+    const uint32_t hn = more ? B.nbytes - hstep : 0u;
+    if (cb == 0) {
+#pragma unroll
+      for (int m = 0; m < MR; ++m)
+#pragma unroll
+        for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    asm volatile("s_nop 7" ::: "memory");  // accumulator writes before the first inline-asm MFMA
+    static_for<9>([&](auto tc) {
+      constexpr int tap = decltype(tc)::value;
+      constexpr int st = tap % 3;
+      constexpr int NQ = NA + (tap < 7 ? NHK : 0);
+      wait_lgkm_h<0>();
+      __builtin_amdgcn_sched_barrier(0);
+      static_for<PER>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        if constexpr (u == 0) {  // weights of K-tile t + 2: this item's, or taps 0-1 of the next
+          if constexpr (tap + 2 < 9) issue_A(true, cb, tap + 2, (tap + 2) % 3);
+          else issue_A(more, cbn, tap + 2 - 9, (tap + 2) % 3);
+        }
+        static_for<NHK>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          if constexpr (tap < 7 && u == (j + 1) * PER / (NHK + 1)) {
+            constexpr int hs = tap * NHK + j;
+            if constexpr (hs < NHD) {
+              lds_dma16h(hpn, hn, halo_dst(hb ^ 1, hs), offN[hs]);
+            } else {
+              lds_dma16h(hp, 0u, smem + Cf::SINK, OOB);
+            }
+          }
+        });
+        mfma_h(acc[u / NR][u % NR], fa[0][u / NR], fb[0][u % NR]);
+        if constexpr (u < NF) read_frag(1, u, st, hb, tap, 1);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      wait_lgkm_h<0>();
+      wait_vmcnt<NQ>();
+      block_barrier();
+      static_for<PER>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        mfma_h(acc[u / NR][u % NR], fa[1][u / NR], fb[1][u % NR]);
+        if constexpr (u < NF) {
+          if constexpr (tap < 8) {
+            read_frag(0, u, (tap + 1) % 3, hb, tap + 1, 0);
+          } else {
+            read_frag(0, u, 0, hb ^ 1, 0, 0);  // next item, tap 0 (garbage past the last: unused)
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+    if (last_cb) {
+      asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+      wait_lgkm_h<0>();
+      // epilogue through this item's (dead) halo buffer
+      float *ep = reinterpret_cast<float *>(smem + hb * HALO) + wave * 16 * (WM + 4);
+#pragma unroll
+      for (int n = 0; n < NR; ++n) {
+#pragma unroll
+        for (int m = 0; m < MR; ++m)
+          *reinterpret_cast<f32x4 *>(ep + l16 * (WM + 4) + m * 16 + g4 * 4) = acc[m][n];
+        wait_lgkm_h<0>();
+        const int p0 = wc * WN + 16 * n;
+        const int h = h0 + p0 / WT, w = w0 + p0 % WT;
+        const int valid = h < H ? min(16, W - w) : 0;
+        const int jrow0 = (img * H + h) * W + w;
+        write_staged<EPI_BF16, 16, WM>(ep, E, 0, 0, A.rows, jrow0 + max(valid, 0), wr * WM, jrow0, lane);
+        wait_lgkm_h<0>();
+      }
+      block_barrier();  // staging reads done before the item after next streams into this buffer
+      if (!more) break;
+      t = tn;
+      h0 = h0n;
+      w0 = w0n;
+      img = imgn;
+#pragma unroll
+      for (int s = 0; s < NHD; ++s) offH[s] = offN[s];
+    }
+    cb = cbn;
+    hb ^= 1;
+  }
+  wait_vmcnt<0>();
+}
+
+int num_cu_h() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+template <int BM, int WT>
+int launch_halo_ps(const GOperand &A, const GOperand &B, const GEpi &E, hipStream_t s) {
+  const int N = B.Ho;
+  const int tiles_w = cdiv(B.W, WT), tiles_h = cdiv(B.H, HaloCfg<BM, WT, true>::R);
+  const long nt = static_cast<long>(tiles_w) * tiles_h * N;
+  if (nt >= (1L << 31)) return -1;
+  // one block per CU, a multiple of 8 (one share per XCD), no more than 8 x the patches per XCD
+  long g = num_cu_h() / 8 * 8;
+  const long per_xcd = (nt + 7) / 8;
+  if (g / 8 > per_xcd) g = per_xcd * 8;
+  if (g < 8) g = 8;
+  CXN_LAUNCH((conv_halo_ps<BM, WT>), dim3(static_cast<unsigned>(g)), dim3(256), 0, s, A, B, E, tiles_w, tiles_h,
+             static_cast<uint32_t>(nt), B.Cg / 64);
+  return 0;
+}
+
 }  // namespace
 
 namespace cxg {
-// 130: 64 output channels per block, 131: 128.  The operands are the implicit-GEMM ones of a
+// 130: 64 output channels per block, 131: 128; 132 / 133: the persistent forms of 130 / 131
+// (one output-channel block only).  The operands are the implicit-GEMM ones of a
 // conv forward or stride-1 data-gradient (A: weights [rows][9 Cg], B: K_GATHER of an NHWC map);
 // served: one group, 3 x 3, stride 1, pad 1, same-size output, Cg % 64 == 0, whole pixels of the
 // B map addressable in 31 bits.  -1 otherwise (the caller falls back).
@@ -308,6 +552,15 @@ int dispatch_halo(int amode, int bmode, int epi, int tile, GOperand A, GOperand 
   if (tile == 131) {
     if (wide) return dbl ? launch_halo<128, 32, true>(A, B, E, s) : launch_halo<128, 32, false>(A, B, E, s);
     return dbl ? launch_halo<128, 16, true>(A, B, E, s) : launch_halo<128, 16, false>(A, B, E, s);
+  }
+  // persistent item walk: one output-channel block
+  if (tile == 132 || tile == 133) {
+    if (tile == 132) {
+      if (A.rows > 64) return -1;
+      return wide ? launch_halo_ps<64, 32>(A, B, E, s) : launch_halo_ps<64, 16>(A, B, E, s);
+    }
+    if (A.rows > 128) return -1;
+    return wide ? launch_halo_ps<128, 32>(A, B, E, s) : launch_halo_ps<128, 16>(A, B, E, s);
   }
   return -1;
 }

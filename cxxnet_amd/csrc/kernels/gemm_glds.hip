@@ -735,7 +735,7 @@ int dispatch(int amode, int bmode, int epi, int tile, const GOperand &A, const G
   }
   // (99 is the Python-side pseudo-tile of the register kernel, never passed here)
   if (tile >= 110 && tile <= 119) return cxg::dispatch_4w(amode, bmode, epi, tile, A, B, E, groups, ksplit, s);
-  if (tile >= 130 && tile <= 131) return cxg::dispatch_halo(amode, bmode, epi, tile, A, B, E, groups, ksplit, s);
+  if (tile >= 130 && tile <= 133) return cxg::dispatch_halo(amode, bmode, epi, tile, A, B, E, groups, ksplit, s);
   if (tile == 120) return cxg::dispatch_4m(amode, bmode, epi, tile, A, B, E, groups, ksplit, s);
   if (tile >= 140 && tile <= 142) return cxg::dispatch_wgrad_halo(amode, bmode, epi, tile, A, B, E, groups, s);
   if (tile >= 50 && tile <= 51) {

@@ -162,6 +162,8 @@ GLDS_TILES = {0: (128, 256), 1: (128, 128), 2: (128, 128), 4: (192, 256), 5: (64
               120: (128, 128),
               # direct 3x3 halo convolution (conv_halo.hip): output channels x 256-pixel patch
               130: (64, 256), 131: (128, 256),
+              # ... its persistent patch walk for one input / one output channel block (132 / 133)
+              132: (64, 256), 133: (128, 256),
               # direct 3x3 weight-gradient on resident halo / dy tiles (conv_wgrad_halo.hip): 64 x 64
               # channel pairs, persistent over 128-pixel patches (140 auto width, 141 16, 142 32)
               140: (64, 64), 141: (64, 64), 142: (64, 64)}
@@ -184,7 +186,7 @@ _glds_cfg = {"on": os.environ.get("CXXNET_GEMM_GLDS", "1") != "0",
 # 128x256 / 64x256 tiles and the pipelined variants (30-41) win conv2/conv3 forward, fc6 forward
 # and several VGG shapes (profiles/r2_sweep_tiles.jsonl).
 GLDS_CANDS = (1, 7, 10, 15, 2, 0, 13, 17, 21, 25, 30, 31, 34, 37, 38, 39, 40, 41, 50, 51, 72, 76, 77, 78, 79, 80,
-              81, 82, 83, 110, 111, 112, 113, 114, 115, 130, 131)
+              81, 82, 83, 110, 111, 112, 113, 114, 115, 130, 131, 132, 133)
 # conv weight-grad shapes missing from the shipped table are timed on first use too (else the
 # register kernel runs them)
 _CW_TUNE = os.environ.get("CXXNET_CW_TUNE", "0") == "1"

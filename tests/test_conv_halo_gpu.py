@@ -101,3 +101,80 @@ def test_halo_declines_other_convs():
         assert gemm.LAST_GLDS[0] != 130
         ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, stride=geo.stride, padding=1)
         assert _rel(y, ref.permute(0, 2, 3, 1)) < 1e-2
+
+
+# persistent forms (one output-channel block; any number of 64-channel input blocks):
+# (N, H, W, C, Cout)
+PS_TILES = {132: 64, 133: 128}
+PS_CASES = [
+    (2, 16, 64, 64, 64),     # two 32-wide x 8-row patches per row band, whole patches
+    (3, 20, 48, 64, 64),     # 16-wide patches, bottom edge cut
+    (1, 9, 36, 64, 40),      # right edge cut, 40 of 64 output channels
+    (24, 16, 32, 64, 64),    # 48 patches: several per block on every XCD share
+    (2, 24, 112, 64, 128),   # VGG conv2_1's width (16-wide patches)
+    (5, 16, 64, 128, 128),   # two channel blocks per patch (conv2_2)
+    (3, 12, 40, 192, 64),    # three channel blocks, cut edges
+]
+
+
+@pytest.mark.parametrize("tile", sorted(PS_TILES))
+@pytest.mark.parametrize("case", PS_CASES, ids=lambda c: "x".join(map(str, c)))
+def test_halo_persistent_forward(tile, case):
+    N, H, W, C, Cout = case
+    if Cout > PS_TILES[tile]:
+        pytest.skip("more output channels than the persistent block")
+    g = _geom(N, H, W, C, Cout)
+    x = _rnd((N, H, W, C), 1.0, 11)
+    w = _rnd((Cout, 3, 3, C), 0.05, 12)
+    b = torch.randn(Cout, device=DEV) * 0.1
+    y = torch.full((N, H, W, Cout), 9.0, dtype=torch.bfloat16, device=DEV)
+    gemm.set_glds(tile=tile)
+    gemm.LAST_GLDS[0] = None
+    try:
+        ops.conv_forward(x, w, b, y, g, relu=True)
+    finally:
+        gemm.set_glds(tile=-1)
+    assert gemm.LAST_GLDS[0] == tile
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, padding=1)
+    assert _rel(y, ref.clamp_min(0).permute(0, 2, 3, 1)) < 1e-2
+
+
+@pytest.mark.parametrize("tile", sorted(PS_TILES))
+@pytest.mark.parametrize("mask", [False, True])
+@pytest.mark.parametrize("cin", [64, 128])
+def test_halo_persistent_data_grad(tile, mask, cin):
+    N, H, W = 6, 24, 64  # dy cin channels (the blocked operand) -> dx 64 channels
+    g = _geom(N, H, W, 64, cin)
+    dy = _rnd((N, H, W, cin), 1.0, 13)
+    w = _rnd((cin, 3, 3, 64), 0.05, 14)
+    z = _rnd((N, H, W, 64), 1.0, 15)
+    dx = z.clamp_min(0) if mask else torch.empty_like(z)
+    gemm.set_glds(tile=tile)
+    gemm.LAST_GLDS[0] = None
+    try:
+        ops.conv_backward_data(dy, w, dx, g, mask_relu=mask)
+    finally:
+        gemm.set_glds(tile=-1)
+    assert gemm.LAST_GLDS[0] == tile
+    ref = torch.nn.grad.conv2d_input((N, 64, H, W), w.float().permute(0, 3, 1, 2),
+                                     dy.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    if mask:
+        ref = ref * (z.float() > 0)
+    assert _rel(dx, ref) < 1e-2
+
+
+def test_halo_persistent_declines_two_output_blocks():
+    """128 output channels on the 64-channel persistent block: 132 declines."""
+    geo = _geom(2, 16, 32, 64, 128)
+    x = _rnd((2, 16, 32, 64), 1.0, 16)
+    w = _rnd((128, 3, 3, 64), 0.05, 17)
+    y = torch.empty(2, 16, 32, 128, dtype=torch.bfloat16, device=DEV)
+    gemm.set_glds(tile=132)
+    gemm.LAST_GLDS[0] = None
+    try:
+        ops.conv_forward(x, w, None, y, geo)
+    finally:
+        gemm.set_glds(tile=-1)
+    assert gemm.LAST_GLDS[0] != 132
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, padding=1)
+    assert _rel(y, ref.permute(0, 2, 3, 1)) < 1e-2
