@@ -331,6 +331,15 @@ conv_halo_ps(GOperand A, GOperand B, GEpi E, int tiles_w, int tiles_h, uint32_t 
     const int row = 8 * (wave + 4 * s) + (lane >> 3);
     offA[s] = row < A.rows ? static_cast<uint32_t>(row * A.ld) * 2u + lchunk * 16u : OOB;
   }
+  // bias of the lane's accumulator rows (channel wr 64 + 16 m + 4 g4 + j), loaded once
+  float bv[MR][4];
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ch = wr * WM + 16 * m + 4 * g4 + j;
+      bv[m][j] = (E.bias != nullptr && ch < A.rows) ? E.bias[ch] : 0.f;
+    }
   // halo DMA offsets of the current patch (offH) and of the next item's halo (offN)
   uint32_t offH[NHD], offN[NHD];
   auto set_halo = [&](uint32_t (&off)[NHD], bool valid, int h0, int w0, int img) {
@@ -469,21 +478,70 @@ conv_halo_ps(GOperand A, GOperand B, GEpi E, int tiles_w, int tiles_h, uint32_t 
     if (last_cb) {
       asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
       wait_lgkm_h<0>();
-      // epilogue through this item's (dead) halo buffer
-      float *ep = reinterpret_cast<float *>(smem + hb * HALO) + wave * 16 * (WM + 4);
+      // Epilogue.  alpha, bias and relu are applied in registers; the wave's bf16 [pixel][channel]
+      // image of 64 pixels (16-byte chunk c of pixel p at c ^ (p & 7)) is staged in this item's
+      // dead halo buffer and leaves as 16-byte row segments.  The 8-wave kernels' staged writer
+      // loads the bias (and the relu'-mask's old value) next to every store, and in-order vmcnt
+      // then makes each of those loads wait for the stores before it; here the bias sits in
+      // registers and a half's mask loads are all issued before its first store.
+      char *eb = smem + hb * HALO + wave * 8192;
+      bf16_t *const out = reinterpret_cast<bf16_t *>(E.out);
+      const int ic = wr * WM + (lane & 7) * 8;
+      static_for<NR / 4>([&](auto hc) {
+        constexpr int half = decltype(hc)::value;
 #pragma unroll
-      for (int n = 0; n < NR; ++n) {
+        for (int n4 = 0; n4 < 4; ++n4) {
+          const int pix = n4 * 16 + l16;
 #pragma unroll
-        for (int m = 0; m < MR; ++m)
-          *reinterpret_cast<f32x4 *>(ep + l16 * (WM + 4) + m * 16 + g4 * 4) = acc[m][n];
-        wait_lgkm_h<0>();
-        const int p0 = wc * WN + 16 * n;
-        const int h = h0 + p0 / WT, w = w0 + p0 % WT;
-        const int valid = h < H ? min(16, W - w) : 0;
-        const int jrow0 = (img * H + h) * W + w;
-        write_staged<EPI_BF16, 16, WM>(ep, E, 0, 0, A.rows, jrow0 + max(valid, 0), wr * WM, jrow0, lane);
-        wait_lgkm_h<0>();
-      }
+          for (int m = 0; m < MR; ++m) {
+            const f32x4 v = acc[m][half * 4 + n4];
+            float f[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              f[j] = v[j] * E.alpha + bv[m][j];
+              if (E.relu) f[j] = fmaxf(f[j], 0.f);
+            }
+            const int c16 = 2 * m + (g4 >> 1);
+            *reinterpret_cast<uint2 *>(eb + pix * 128 + ((c16 ^ (pix & 7)) * 16) + (g4 & 1) * 8) =
+                make_uint2(pack2(f[0], f[1]), pack2(f[2], f[3]));
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        uint4 q[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int pix = (lane >> 3) + 8 * k;
+          q[k] = *reinterpret_cast<const uint4 *>(eb + pix * 128 + (((lane & 7) ^ (pix & 7)) * 16));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the next half rewrites the image)
+        long row[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int pp = wc * WN + half * 64 + (lane >> 3) + 8 * k;
+          const int h = h0 + pp / WT, w = w0 + pp % WT;
+          row[k] = (h < H && w < W && ic < A.rows) ? (static_cast<long>(img * H + h) * W + w) * E.ldc + ic : -1;
+        }
+        if (E.mask_relu) {
+          uint4 old[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (row[k] >= 0) old[k] = *reinterpret_cast<const uint4 *>(out + row[k]);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            if (row[k] >= 0) {
+              float o[8], f[8];
+              unpack8(old[k], o);
+              unpack8(q[k], f);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) f[e] = o[e] > 0.f ? f[e] : 0.f;
+              q[k] = pack8(f);
+            }
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (row[k] >= 0) *reinterpret_cast<uint4 *>(out + row[k]) = q[k];
+      });
       block_barrier();  // staging reads done before the item after next streams into this buffer
       if (!more) break;
       t = tn;
@@ -555,6 +613,7 @@ int dispatch_halo(int amode, int bmode, int epi, int tile, GOperand A, GOperand 
   }
   // persistent item walk: one output-channel block
   if (tile == 132 || tile == 133) {
+    if (A.rows % 8 != 0) return -1;  // whole 16-byte output segments
     if (tile == 132) {
       if (A.rows > 64) return -1;
       return wide ? launch_halo_ps<64, 32>(A, B, E, s) : launch_halo_ps<64, 16>(A, B, E, s);

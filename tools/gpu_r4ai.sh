@@ -7,7 +7,7 @@ OUT=gpurun_out/r4ai
 mkdir -p $OUT
 timeout -k 10 300 python -u -m pytest tests/test_conv_halo_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/halo_tests.log 2>&1 || { tail -30 $OUT/halo_tests.log; exit 1; }
 tail -1 $OUT/halo_tests.log
-timeout -k 10 300 python -u benchmarks/gemm_tile_probe.py --ops vgg.c1_2_fwd,vgg.c1_2_dgrad,vgg.c2_1_fwd --tiles -1,130,131,132,133 --rounds 5 > $OUT/probe.jsonl 2> $OUT/probe.err || { tail -20 $OUT/probe.err; exit 1; }
+timeout -k 10 300 python -u benchmarks/gemm_tile_probe.py --ops vgg.c1_2_fwd,vgg.c1_2_dgrad,vgg.c2_1_fwd --tiles=-1,130,131,132,133 --rounds 5 > $OUT/probe.jsonl 2> $OUT/probe.err || { tail -20 $OUT/probe.err; exit 1; }
 cut -c1-400 $OUT/probe.jsonl
 timeout -k 10 900 python -u -m pytest tests/ -q -rfE -m gpu --timeout 150 --timeout-method thread -p no:cacheprovider > $OUT/tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -40 $OUT/tests.log | grep -E "passed|failed|FAILED|error" | head -20
