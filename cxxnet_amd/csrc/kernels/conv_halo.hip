@@ -48,6 +48,16 @@ __device__ __forceinline__ void mfma_h(f32x4 &acc, const bf16x8 &a, const bf16x8
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
+// an empty volatile asm that "rewrites" every accumulator: register code reading or writing
+// them cannot move across it, and it keeps its order with the other volatile asm
+template <int MR, int NR>
+__device__ __forceinline__ void pin_acc(f32x4 (&acc)[MR][NR]) {
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int n = 0; n < NR; ++n) asm volatile("" : "+a"(acc[m][n]));
+}
+
 constexpr int halo_pitch(int wt) { return (wt + 2 + 7) / 8 * 8; }
 
 template <int BM, int WT, bool DBL>
@@ -431,7 +441,11 @@ conv_halo_ps(GOperand A, GOperand B, GEpi E, int tiles_w, int tiles_h, uint32_t 
 #pragma unroll
         for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    asm volatile("s_nop 7" ::: "memory");  // accumulator writes before the first inline-asm MFMA
+    // accumulator writes, then wait states, then the first inline-asm MFMA.  The empty asm
+    // statements pin the register writes above the s_nop (volatile asm keeps its order; plain
+    // register code does not)
+    pin_acc(acc);
+    asm volatile("s_nop 7" ::: "memory");
     static_for<9>([&](auto tc) {
       constexpr int tap = decltype(tc)::value;
       constexpr int st = tap % 3;
@@ -476,7 +490,11 @@ conv_halo_ps(GOperand A, GOperand B, GEpi E, int tiles_w, int tiles_h, uint32_t 
       });
     });
     if (last_cb) {
+      // MFMA results land after the wait states; pin_acc keeps every accumulator read below them
+      // (without it hipcc hoisted the epilogue's AGPR reads and arithmetic above the s_nop and read
+      // accumulators the last MFMAs had not written yet)
       asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+      pin_acc(acc);
       wait_lgkm_h<0>();
       // Epilogue.  alpha, bias and relu are applied in registers; the wave's bf16 [pixel][channel]
       // image of 64 pixels (16-byte chunk c of pixel p at c ^ (p & 7)) is staged in this item's

@@ -215,10 +215,24 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
       const int il = il_b;
       const int i = ibase + il;
       const bool vec_store = ((E.ldc & 7) == 0) && (i + 8 <= Mi);
+      // relu'-mask: the fragment's old values are all loaded before its first store (a load
+      // issued after a store waits for it: vmcnt counts both in issue order)
+      constexpr int NIT = (16 + RPI - 1) / RPI;
+      const int jl0 = lane < LPR * RPI ? lane / LPR : 16;
+      uint4 oldv[NIT];
+      if (E.mask_relu && vec_store) {
 #pragma unroll
-      for (int jl = lane < LPR * RPI ? lane / LPR : 16; jl < 16; jl += RPI) {  // WM = 96: 4 lanes idle
+        for (int k = 0; k < NIT; ++k) {
+          const int jl = jl0 + k * RPI;
+          if (jl < 16 && jbase + n * 16 + jl < Nj && i < Mi)
+            oldv[k] = *reinterpret_cast<const uint4 *>(out + static_cast<long>(jbase + n * 16 + jl) * E.ldc + i);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NIT; ++k) {  // WM = 96: 4 lanes idle
+        const int jl = jl0 + k * RPI;
         const int j = jbase + n * 16 + jl;
-        if (j < Nj && i < Mi) {
+        if (jl < 16 && j < Nj && i < Mi) {
           const f32x4 x0 = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il);
           const f32x4 x1 = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il + 4);
           float f[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
@@ -231,7 +245,7 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
           if (vec_store) {
             if (E.mask_relu) {
               float old[8];
-              unpack8(*reinterpret_cast<const uint4 *>(dst), old);
+              unpack8(oldv[k], old);
 #pragma unroll
               for (int e = 0; e < 8; ++e) f[e] = old[e] > 0.f ? f[e] : 0.f;
             }

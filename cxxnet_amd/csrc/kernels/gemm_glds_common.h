@@ -402,10 +402,24 @@ __device__ __forceinline__ void write_staged(const float *ep, const GEpi &E, int
     const int il = (lane % LPR) * 8;
     const int i = ibase + il;
     const bool vec_store = ((E.ldc & 7) == 0) && (i + 8 <= Mi);
+    // relu'-mask: every old value of the lane's rows is loaded before the first store.  A load
+    // issued after a store waits for it (vmcnt counts loads and stores in issue order), so
+    // load / store pairs would serialise the epilogue on store latency.
+    constexpr int NIT = (JR + RPI - 1) / RPI;
+    uint4 oldv[NIT];
+    if (E.mask_relu && vec_store) {
 #pragma unroll
-    for (int jl = lane / LPR; jl < JR; jl += RPI) {
+      for (int k = 0; k < NIT; ++k) {
+        const int jl = lane / LPR + k * RPI;
+        if (jl < JR && jrow0 + jl < Nj && i < Mi)
+          oldv[k] = *reinterpret_cast<const uint4 *>(out + static_cast<long>(jrow0 + jl) * E.ldc + i);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int jl = lane / LPR + k * RPI;
       const int j = jrow0 + jl;
-      if (j < Nj && i < Mi) {
+      if (jl < JR && j < Nj && i < Mi) {
         const f32x4 x0 = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il);
         const f32x4 x1 = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il + 4);
         float f[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
@@ -418,7 +432,7 @@ __device__ __forceinline__ void write_staged(const float *ep, const GEpi &E, int
         if (vec_store) {
           if (E.mask_relu) {
             float old[8];
-            unpack8(*reinterpret_cast<const uint4 *>(dst), old);
+            unpack8(oldv[k], old);
 #pragma unroll
             for (int e = 0; e < 8; ++e) f[e] = old[e] > 0.f ? f[e] : 0.f;
           }
@@ -472,10 +486,22 @@ __device__ __forceinline__ void seg_epilogue(f32x4 (&acc)[MR][NR], char *smem, c
       const int il = (lane % LPR) * 8;
       const int i = ibase + il;
       const bool vec_store = ((E.ldc & 7) == 0) && (i + 8 <= Mi);
+      // relu'-mask old values all loaded before the fragment's first store (as write_staged)
+      constexpr int NIT = (16 + RPI - 1) / RPI;
+      uint4 oldv[NIT];
+      if (E.mask_relu && vec_store) {
 #pragma unroll
-      for (int jl = lane / LPR; jl < 16; jl += RPI) {
+        for (int k = 0; k < NIT; ++k) {
+          const int jl = lane / LPR + k * RPI;
+          if (jl < 16 && jbase + n * 16 + jl < Nj && i < Mi)
+            oldv[k] = *reinterpret_cast<const uint4 *>(out + static_cast<long>(jbase + n * 16 + jl) * E.ldc + i);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NIT; ++k) {
+        const int jl = lane / LPR + k * RPI;
         const int j = jbase + n * 16 + jl;
-        if (j < Nj && i < Mi) {
+        if (jl < 16 && j < Nj && i < Mi) {
           const f32x4 x0 = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il);
           const f32x4 x1 = *reinterpret_cast<const f32x4 *>(ep + jl * (WM + 4) + il + 4);
           float f[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
@@ -488,7 +514,7 @@ __device__ __forceinline__ void seg_epilogue(f32x4 (&acc)[MR][NR], char *smem, c
           if (vec_store) {
             if (E.mask_relu) {
               float old[8];
-              unpack8(*reinterpret_cast<const uint4 *>(dst), old);
+              unpack8(oldv[k], old);
 #pragma unroll
               for (int e = 0; e < 8; ++e) f[e] = old[e] > 0.f ? f[e] : 0.f;
             }
