@@ -265,6 +265,8 @@ conv_halo(GOperand A, GOperand B, GEpi E, int tiles_o, int tiles_w, int tiles_h,
 
   // epilogue: one 16-pixel fragment (one patch-row segment) at a time
   float *ep = reinterpret_cast<float *>(smem) + wave * 16 * (WM + 4);
+  float bv8[8];
+  staged_bias<WM>(E, 0, A.rows, i0 + wr * WM, lane, bv8);
 #pragma unroll
   for (int n = 0; n < NR; ++n) {
 #pragma unroll
@@ -275,7 +277,7 @@ conv_halo(GOperand A, GOperand B, GEpi E, int tiles_o, int tiles_w, int tiles_h,
     const int h = h0 + p0 / WT, w = w0 + p0 % WT;
     const int valid = h < H ? min(16, W - w) : 0;
     const int jrow0 = (img * H + h) * W + w;
-    write_staged<EPI_BF16, 16, WM>(ep, E, 0, 0, A.rows, jrow0 + max(valid, 0), i0 + wr * WM, jrow0, lane);
+    write_staged<EPI_BF16, 16, WM>(ep, E, 0, 0, A.rows, jrow0 + max(valid, 0), i0 + wr * WM, jrow0, lane, bv8);
     wait_lgkm_h<0>();
   }
 }

@@ -334,6 +334,8 @@ gemm_4f(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
     // 32x32 block (m, n): the lane holds output column j = lane & 31 and rows i = 8 b + 4 (lane / 32)
     // + e of register 4 b + e: stage 32 j-rows x WM i-columns per n, then write whole rows
     float *ep = reinterpret_cast<float *>(smem) + wave * 32 * (WM + 4);
+    float bv8[8];
+    staged_bias<WM>(E, g, A.rows, i0 + wr * WM, lane, bv8);
 #pragma unroll
     for (int n = 0; n < NR; ++n) {
 #pragma unroll
@@ -345,7 +347,7 @@ gemm_4f(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_til
         }
       wait_lgkm<0>();
       wave_lds_handoff<true>();
-      write_staged<EPI, 32, WM>(ep, E, g, wb.slice, A.rows, B.rows, i0 + wr * WM, j0 + wc * WN + n * 32, lane);
+      write_staged<EPI, 32, WM>(ep, E, g, wb.slice, A.rows, B.rows, i0 + wr * WM, j0 + wc * WN + n * 32, lane, bv8);
       wait_lgkm<0>();
       wave_lds_handoff<true>();
     }

@@ -391,9 +391,20 @@ __device__ __forceinline__ bf16x8 seg_frag(const char *tile, int base, int lane)
 // Write JR staged output rows (j = jrow0 .. jrow0 + JR - 1, WM columns i from ibase; staging row
 // pitch WM + 4 floats) of one wave: bf16 (+bias, relu, relu'-mask of the old value) or an fp32
 // split-K slab.
+// The bias of a lane's 8 output columns (i = ibase + (lane % (WM / 8)) * 8 + e): loaded once per
+// epilogue, before its first store -- a load issued after a store waits for it (vmcnt counts
+// loads and stores in issue order), so per-row bias loads serialised the epilogue on store latency.
+template <int WM>
+__device__ __forceinline__ void staged_bias(const GEpi &E, int g, int Mi, int ibase, int lane, float (&bv)[8]) {
+  const float *bias = E.bias ? E.bias + g * E.bias_gstride : nullptr;
+  const int i = ibase + (lane % (WM / 8)) * 8;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bv[e] = (bias && i + e < Mi) ? bias[i + e] : 0.f;
+}
+
 template <int EPI, int JR, int WM>
 __device__ __forceinline__ void write_staged(const float *ep, const GEpi &E, int g, int slice, int Mi, int Nj,
-                                             int ibase, int jrow0, int lane) {
+                                             int ibase, int jrow0, int lane, const float *bv8 = nullptr) {
   const float *bias = E.bias ? E.bias + g * E.bias_gstride : nullptr;
   if constexpr (EPI == EPI_BF16) {
     bf16_t *out = reinterpret_cast<bf16_t *>(E.out) + g * E.gstride;
@@ -401,6 +412,9 @@ __device__ __forceinline__ void write_staged(const float *ep, const GEpi &E, int
     constexpr int RPI = 64 / LPR;
     const int il = (lane % LPR) * 8;
     const int i = ibase + il;
+    float bv[8];  // bv8: preloaded by the caller (staged_bias)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bv[e] = bv8 ? bv8[e] : ((bias && i + e < Mi) ? bias[i + e] : 0.f);
     const bool vec_store = ((E.ldc & 7) == 0) && (i + 8 <= Mi);
     // relu'-mask: every old value of the lane's rows is loaded before the first store.  A load
     // issued after a store waits for it (vmcnt counts loads and stores in issue order), so
@@ -425,7 +439,7 @@ __device__ __forceinline__ void write_staged(const float *ep, const GEpi &E, int
         float f[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          f[e] = f[e] * E.alpha + ((bias && i + e < Mi) ? bias[i + e] : 0.f);
+          f[e] = f[e] * E.alpha + bv[e];
           if (E.relu) f[e] = fmaxf(f[e], 0.f);
         }
         bf16_t *dst = out + static_cast<long>(j) * E.ldc + i;
@@ -472,7 +486,8 @@ template <int EPI, int MR, int NR, int WM>
 __device__ __forceinline__ void seg_epilogue(f32x4 (&acc)[MR][NR], char *smem, const GEpi &E, int g, int slice, int Mi,
                                              int Nj, int ibase, int jbase, int wave, int lane) {
   float *ep = reinterpret_cast<float *>(smem) + wave * 16 * (WM + 4);
-  const float *bias = E.bias ? E.bias + g * E.bias_gstride : nullptr;
+  float bv[8];  // the lane's 8 bias columns, loaded before the first store (staged_bias)
+  if constexpr (EPI == EPI_BF16) staged_bias<WM>(E, g, Mi, ibase, lane, bv);
 #pragma unroll
   for (int n = 0; n < NR; ++n) {
 #pragma unroll
@@ -507,7 +522,7 @@ __device__ __forceinline__ void seg_epilogue(f32x4 (&acc)[MR][NR], char *smem, c
           float f[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            f[e] = f[e] * E.alpha + ((bias && i + e < Mi) ? bias[i + e] : 0.f);
+            f[e] = f[e] * E.alpha + bv[e];
             if (E.relu) f[e] = fmaxf(f[e], 0.f);
           }
           bf16_t *dst = out + static_cast<long>(j) * E.ldc + i;
