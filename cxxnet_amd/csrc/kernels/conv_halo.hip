@@ -417,6 +417,20 @@ conv_halo_ps(GOperand A, GOperand B, GEpi E, int tiles_w, int tiles_h, uint32_t 
   for (int f = 0; f < NF; ++f) read_frag(0, f, 0, 0, 0, 0);
   __builtin_amdgcn_sched_barrier(0);
 
+  // BM = 64 (one half): the epilogue's 8 row-segment stores per lane are deferred into taps 0-3 of
+  // the next item, two per tap after that tap's DMAs, as fixed-count buffer stores (OOB = dropped)
+  // counted in the waits -- a store ahead of a DMA would make every later wait for that DMA wait
+  // for the store as well (vmcnt retires in issue order); past the last item they are flushed
+  constexpr bool DEFER = NR == 4;
+  const rsrc_t ro = make_rsrc(E.out, 0x80000000u);
+  uint4 pq[8];
+  uint32_t poff[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    pq[k] = make_uint4(0, 0, 0, 0);
+    poff[k] = OOB;
+  }
+  typedef int v4i __attribute__((ext_vector_type(4)));
   int hb = 0, cb = 0;
   uint32_t tn = t;
   int h0n = h0, w0n = w0, imgn = img;
@@ -452,6 +466,7 @@ conv_halo_ps(GOperand A, GOperand B, GEpi E, int tiles_w, int tiles_h, uint32_t 
       constexpr int tap = decltype(tc)::value;
       constexpr int st = tap % 3;
       constexpr int NQ = NA + (tap < 7 ? NHK : 0);
+      constexpr int ST = (DEFER && tap < 4) ? 2 : 0, STP = (DEFER && tap >= 1 && tap < 5) ? 2 : 0;
       wait_lgkm_h<0>();
       __builtin_amdgcn_sched_barrier(0);
       static_for<PER>([&](auto uc) {
@@ -459,6 +474,11 @@ conv_halo_ps(GOperand A, GOperand B, GEpi E, int tiles_w, int tiles_h, uint32_t 
         if constexpr (u == 0) {  // weights of K-tile t + 2: this item's, or taps 0-1 of the next
           if constexpr (tap + 2 < 9) issue_A(true, cb, tap + 2, (tap + 2) % 3);
           else issue_A(more, cbn, tap + 2 - 9, (tap + 2) % 3);
+        }
+        if constexpr (ST > 0 && u == PER - 1) {  // the previous patch's stores, after this tap's DMAs
+#pragma unroll
+          for (int k = 2 * tap; k < 2 * tap + 2; ++k)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, pq[k]), ro, poff[k], 0, 0);
         }
         static_for<NHK>([&](auto jc) {
           constexpr int j = decltype(jc)::value;
@@ -476,7 +496,7 @@ conv_halo_ps(GOperand A, GOperand B, GEpi E, int tiles_w, int tiles_h, uint32_t 
         __builtin_amdgcn_sched_barrier(0);
       });
       wait_lgkm_h<0>();
-      wait_vmcnt<NQ>();
+      wait_vmcnt<NQ + ST + STP>();  // all but this tap's DMAs and the stores after the last waited DMA
       block_barrier();
       static_for<PER>([&](auto uc) {
         constexpr int u = decltype(uc)::value;
@@ -558,9 +578,17 @@ conv_halo_ps(GOperand A, GOperand B, GEpi E, int tiles_w, int tiles_h, uint32_t 
             }
           }
         }
+        if constexpr (DEFER) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (row[k] >= 0) *reinterpret_cast<uint4 *>(out + row[k]) = q[k];
+          for (int k = 0; k < 8; ++k) {
+            pq[k] = q[k];
+            poff[k] = row[k] >= 0 ? static_cast<uint32_t>(row[k] * 2) : OOB;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (row[k] >= 0) *reinterpret_cast<uint4 *>(out + row[k]) = q[k];
+        }
       });
       block_barrier();  // staging reads done before the item after next streams into this buffer
       if (!more) break;
@@ -573,6 +601,10 @@ conv_halo_ps(GOperand A, GOperand B, GEpi E, int tiles_w, int tiles_h, uint32_t 
     }
     cb = cbn;
     hb ^= 1;
+  }
+  if constexpr (DEFER) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, pq[k]), ro, poff[k], 0, 0);
   }
   wait_vmcnt<0>();
 }
@@ -593,6 +625,8 @@ int launch_halo_ps(const GOperand &A, const GOperand &B, const GEpi &E, hipStrea
   const int tiles_w = cdiv(B.W, WT), tiles_h = cdiv(B.H, HaloCfg<BM, WT, true>::R);
   const long nt = static_cast<long>(tiles_w) * tiles_h * N;
   if (nt >= (1L << 31)) return -1;
+  // BM = 64 defers its stores as buffer stores with 32-bit byte offsets (OOB = 2^31)
+  if (HaloCfg<BM, WT, true>::NR == 4 && static_cast<long>(N) * B.H * B.W * E.ldc * 2 >= (1L << 31)) return -1;
   // one block per CU, a multiple of 8 (one share per XCD), no more than 8 x the patches per XCD
   long g = num_cu_h() / 8 * 8;
   const long per_xcd = (nt + 7) / 8;
