@@ -1,4 +1,4 @@
-// Direct 3x3 / stride-1 / pad-1 convolution on a resident input halo (tile ids 130-131) for
+// Direct 3x3 / stride-1 / pad-1 convolution on a resident input halo (tile ids 130-133) for
 // gfx950: VGG-16's high-resolution layers (conv1_2, conv2_x: 224^2 / 112^2 maps, 64-128
 // channels), forward and stride-1 data-gradient (the same product with the flipped weights).
 // Reference: src/layer/convolution_layer-inl.hpp:70-155 (im2col + GEMM).
