@@ -33,6 +33,10 @@
 
 using namespace cxg;
 
+namespace cxg {
+void launch_db_reduce(const GEpi &E, int rows, hipStream_t s);  // gemm_glds.hip
+}
+
 namespace {
 
 __device__ __forceinline__ void lds_dma16h(const char *p, uint32_t n, char *dst, uint32_t voff) {
@@ -83,7 +87,7 @@ struct HaloCfg {
   static_assert(WN % WT == 0, "a wave owns whole patch rows");
 };
 
-template <int BM, int WT, bool DBL>
+template <int BM, int WT, bool DBL, int EPI = EPI_BF16>
 __global__ void __launch_bounds__(256, 1)
 conv_halo(GOperand A, GOperand B, GEpi E, int tiles_o, int tiles_w, int tiles_h, int ncb) {
   using Cf = HaloCfg<BM, WT, DBL>;
@@ -267,6 +271,7 @@ conv_halo(GOperand A, GOperand B, GEpi E, int tiles_o, int tiles_w, int tiles_h,
   float *ep = reinterpret_cast<float *>(smem) + wave * 16 * (WM + 4);
   float bv8[8];
   staged_bias<WM>(E, 0, A.rows, i0 + wr * WM, lane, bv8);
+  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int n = 0; n < NR; ++n) {
 #pragma unroll
@@ -277,20 +282,45 @@ conv_halo(GOperand A, GOperand B, GEpi E, int tiles_o, int tiles_w, int tiles_h,
     const int h = h0 + p0 / WT, w = w0 + p0 % WT;
     const int valid = h < H ? min(16, W - w) : 0;
     const int jrow0 = (img * H + h) * W + w;
-    write_staged<EPI_BF16, 16, WM>(ep, E, 0, 0, A.rows, jrow0 + max(valid, 0), i0 + wr * WM, jrow0, lane, bv8);
+    write_staged<EPI_BF16, 16, WM>(ep, E, 0, 0, A.rows, jrow0 + max(valid, 0), i0 + wr * WM, jrow0, lane, bv8,
+                                   EPI == EPI_BF16_DB ? bsum : nullptr);
     wait_lgkm_h<0>();
+  }
+  if constexpr (EPI == EPI_BF16_DB) {
+    // the lower conv's bias gradient: lanes l, l + 8, ... summed the same 8 channels; their sums
+    // meet in the wave's staging area and one row of the partials workspace per (patch, wave
+    // column) takes them (rows: patch x WGN; db_partials_reduce adds the rows)
+    constexpr int LPR = WM / 8, RPI = 64 / LPR;
+    static_assert(16 * (WM + 4) >= 64 * 9, "staging area holds the lane sums");
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ep[lane * 9 + e] = bsum[e];
+    wait_lgkm_h<0>();
+    if (lane < LPR) {
+      float *row = E.dbias + static_cast<long>(gb.tile / static_cast<uint32_t>(tiles_o) * Cf::WGN + wc) * E.part_ld;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < RPI; ++q) t += ep[(lane + q * LPR) * 9 + e];
+        const int i = i0 + wr * WM + lane * 8 + e;
+        if (i < A.rows) row[i] = t;
+      }
+    }
   }
 }
 
-template <int BM, int WT, bool DBL>
+template <int BM, int WT, bool DBL, int EPI = EPI_BF16>
 int launch_halo(const GOperand &A, const GOperand &B, const GEpi &E, hipStream_t s) {
   const int N = B.Ho;
   const int tiles_o = cdiv(A.rows, BM), tiles_w = cdiv(B.W, WT), tiles_h = cdiv(B.H, HaloCfg<BM, WT, DBL>::R);
   const int ncb = B.Cg / 64;
   const long nt = static_cast<long>(tiles_o) * tiles_w * tiles_h * N;
   if (nt >= (1L << 31)) return -1;
-  CXN_LAUNCH((conv_halo<BM, WT, DBL>), dim3(static_cast<unsigned>(nt)), dim3(256), 0, s, A, B, E, tiles_o, tiles_w,
-             tiles_h, ncb);
+  const long rows = nt / tiles_o * HaloCfg<BM, WT, DBL>::WGN;  // EPI_BF16_DB partial rows
+  if (EPI == EPI_BF16_DB && rows * E.part_ld > E.part_elems) return -1;  // the caller sums dx itself
+  CXN_LAUNCH((conv_halo<BM, WT, DBL, EPI>), dim3(static_cast<unsigned>(nt)), dim3(256), 0, s, A, B, E, tiles_o,
+             tiles_w, tiles_h, ncb);
+  if (EPI == EPI_BF16_DB) launch_db_reduce(E, static_cast<int>(rows), s);
   return 0;
 }
 
@@ -647,7 +677,9 @@ namespace cxg {
 // B map addressable in 31 bits.  -1 otherwise (the caller falls back).
 int dispatch_halo(int amode, int bmode, int epi, int tile, GOperand A, GOperand B, const GEpi &E, int groups, int ksplit,
                   hipStream_t s) {
-  if (amode != K_DIRECT || bmode != K_GATHER || epi != EPI_BF16 || groups != 1 || ksplit > 1) return -1;
+  if (amode != K_DIRECT || bmode != K_GATHER || (epi != EPI_BF16 && epi != EPI_BF16_DB) || groups != 1 || ksplit > 1)
+    return -1;
+  const bool db = epi == EPI_BF16_DB;  // 130 / 131 only: + the lower conv's bias gradient
   if (B.KH != 3 || B.KW != 3 || B.stride != 1 || B.pad_h != 1 || B.pad_w != 1) return -1;
   if (B.Cg % 64 != 0 || B.kdim != 9 * B.Cg || A.kdim != B.kdim || A.ld < A.kdim) return -1;
   if (B.Ho != B.H || B.Wo != B.W) return -1;  // pad 1, stride 1: the output has the input's size
@@ -657,6 +689,19 @@ int dispatch_halo(int amode, int bmode, int epi, int tile, GOperand A, GOperand 
   if (B.C % 8 != 0 || B.C < B.Cg || (E.ldc & 7) != 0) return -1;
   const bool wide = B.W % 32 == 0 || B.W % 16 != 0;
   const bool dbl = B.Cg > 64;
+  if (db && (E.dbias == nullptr || E.dbias_final == nullptr || E.bias != nullptr)) return -1;
+  if (db && tile == 130) {
+    if (wide)
+      return dbl ? launch_halo<64, 32, true, EPI_BF16_DB>(A, B, E, s) : launch_halo<64, 32, false, EPI_BF16_DB>(A, B, E, s);
+    return dbl ? launch_halo<64, 16, true, EPI_BF16_DB>(A, B, E, s) : launch_halo<64, 16, false, EPI_BF16_DB>(A, B, E, s);
+  }
+  if (db && tile == 131) {
+    if (wide)
+      return dbl ? launch_halo<128, 32, true, EPI_BF16_DB>(A, B, E, s)
+                 : launch_halo<128, 32, false, EPI_BF16_DB>(A, B, E, s);
+    return dbl ? launch_halo<128, 16, true, EPI_BF16_DB>(A, B, E, s) : launch_halo<128, 16, false, EPI_BF16_DB>(A, B, E, s);
+  }
+  if (db) return -1;
   if (tile == 130) {
     if (wide) return dbl ? launch_halo<64, 32, true>(A, B, E, s) : launch_halo<64, 32, false>(A, B, E, s);
     return dbl ? launch_halo<64, 16, true>(A, B, E, s) : launch_halo<64, 16, false>(A, B, E, s);

@@ -410,6 +410,17 @@ __global__ void db_partials_reduce(const float *__restrict__ part, int nrows, in
   }
 }
 
+}  // namespace
+namespace cxg {
+// db[c] += column sums of the partial rows an EPI_BF16_DB epilogue wrote (conv_halo.hip uses it)
+void launch_db_reduce(const GEpi &E, int rows, hipStream_t s) {
+  const int chunks = (rows + 255) / 256;
+  CXN_LAUNCH(db_partials_reduce, dim3((E.part_ld + 31) / 32, chunks), dim3(256), 0, s, E.dbias, rows, E.part_ld,
+             E.dbias_final);
+}
+}  // namespace cxg
+namespace {
+
 template <int BM, int BN, int WGM, int WGN, int STAGES, int AMODE, int BMODE, int EPI, int PIPE = 0, int BMC = BM>
 int launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int ksplit, hipStream_t s) {
   const int ti = cdiv(A.rows, BMC), tj = cdiv(B.rows, BN);

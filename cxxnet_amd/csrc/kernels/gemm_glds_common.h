@@ -404,7 +404,10 @@ __device__ __forceinline__ void staged_bias(const GEpi &E, int g, int Mi, int ib
 
 template <int EPI, int JR, int WM>
 __device__ __forceinline__ void write_staged(const float *ep, const GEpi &E, int g, int slice, int Mi, int Nj,
-                                             int ibase, int jrow0, int lane, const float *bv8 = nullptr) {
+                                             int ibase, int jrow0, int lane, const float *bv8 = nullptr,
+                                             float *bsum = nullptr) {
+  // bsum (EPI_BF16, optional): += the stored bf16 values of the lane's 8 columns (a conv
+  // data-gradient handing over the lower conv's bias gradient, as EPI_BF16_DB)
   const float *bias = E.bias ? E.bias + g * E.bias_gstride : nullptr;
   if constexpr (EPI == EPI_BF16) {
     bf16_t *out = reinterpret_cast<bf16_t *>(E.out) + g * E.gstride;
@@ -450,11 +453,19 @@ __device__ __forceinline__ void write_staged(const float *ep, const GEpi &E, int
 #pragma unroll
             for (int e = 0; e < 8; ++e) f[e] = old[e] > 0.f ? f[e] : 0.f;
           }
-          *reinterpret_cast<uint4 *>(dst) = pack8(f);
+          const uint4 packed = pack8(f);
+          *reinterpret_cast<uint4 *>(dst) = packed;
+          if (bsum) {
+            float r[8];
+            unpack8(packed, r);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bsum[e] += r[e];
+          }
         } else {
           for (int e = 0; e < 8 && i + e < Mi; ++e) {
             if (E.mask_relu && !(bf2f(dst[e]) > 0.f)) f[e] = 0.f;
             dst[e] = f2bf(f[e]);
+            if (bsum) bsum[e] += bf2f(f2bf(f[e]));
           }
         }
       }

@@ -187,6 +187,9 @@ _glds_cfg = {"on": os.environ.get("CXXNET_GEMM_GLDS", "1") != "0",
 # and several VGG shapes (profiles/r2_sweep_tiles.jsonl).
 GLDS_CANDS = (1, 7, 10, 15, 2, 0, 13, 17, 21, 25, 30, 31, 34, 37, 38, 39, 40, 41, 50, 51, 72, 76, 77, 78, 79, 80,
               81, 82, 83, 110, 111, 112, 113, 114, 115, 130, 131, 132, 133)
+# the halo data-gradient tiles (130 / 131) hand over the lower conv's bias gradient from their
+# epilogue (EPI_BF16_DB) instead of a separate column-sum pass; CXXNET_HALO_DB=0 turns that off
+_HALO_DB = os.environ.get("CXXNET_HALO_DB", "1") != "0"
 # conv weight-grad shapes missing from the shipped table are timed on first use too (else the
 # register kernel runs them)
 _CW_TUNE = os.environ.get("CXXNET_CW_TUNE", "0") == "1"
@@ -728,7 +731,7 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False, wt_
             return _glds(A, B, GL_K, GL_KG, o, cg_in, g.C, groups=g.groups, mask_relu=mask_relu, tile=t)
         key = ("cd", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
         t = _tuned_tile(key, run, dx, lambda: _pick_glds(A.rows, B.rows, g.groups), extra=(REG,))
-        if dbias is not None and t != REG:
+        if dbias is not None and t != REG and (t not in (130, 131) or _HALO_DB):
             from .nn import _workspace
             ws = _workspace((-(-B.rows // 16) + 8) * g.C, dx.device)  # >= tiles_j * waves_j rows
             if _glds(A, B, GL_K, GL_KG, dx, cg_in, g.C, groups=g.groups, mask_relu=mask_relu, tile=t,

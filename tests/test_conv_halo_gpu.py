@@ -178,3 +178,31 @@ def test_halo_persistent_declines_two_output_blocks():
     assert gemm.LAST_GLDS[0] != 132
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, padding=1)
     assert _rel(y, ref.permute(0, 2, 3, 1)) < 1e-2
+
+
+@pytest.mark.parametrize("tile", TILES)
+@pytest.mark.parametrize("mask", [False, True])
+@pytest.mark.parametrize("case", [(2, 16, 64, 64, 64), (3, 20, 48, 128, 128), (2, 9, 40, 64, 192), (1, 13, 13, 128, 256)],
+                         ids=lambda c: "x".join(map(str, c)))
+def test_halo_data_grad_bias_sum(tile, mask, case):
+    """EPI_BF16_DB on the halo tiles: dx exactly as the plain epilogue writes it, and dbias += the
+    column sums of the stored (relu'-masked) dx, from per-(patch, wave) partial rows."""
+    g = _geom(*case)
+    dy = _rnd((g.N, g.H, g.W, g.Cout), 1.0, 21)
+    w = _rnd((g.Cout, 3, 3, g.C), 0.05, 22)
+    z = _rnd((g.N, g.H, g.W, g.C), 1.0, 23)
+    gemm.set_glds(tile=tile)
+    try:
+        dx_ref = z.clamp_min(0) if mask else torch.empty_like(z)
+        ops.conv_backward_data(dy, w, dx_ref, g, mask_relu=mask)
+        dx = z.clamp_min(0) if mask else torch.empty_like(z)
+        db = torch.full((g.C,), 0.25, device=DEV)
+        gemm.LAST_GLDS[0] = None
+        fused = ops.conv_backward_data(dy, w, dx, g, mask_relu=mask, dbias=db)
+    finally:
+        gemm.set_glds(tile=-1)
+    torch.cuda.synchronize()
+    assert fused and gemm.LAST_GLDS[0] == tile
+    assert torch.equal(dx, dx_ref)
+    ref = 0.25 + dx_ref.float().reshape(-1, g.C).sum(0)
+    assert _rel(db, ref) < 1e-3
