@@ -1,0 +1,398 @@
+// Direct stride-1 "same" convolution WEIGHT gradient for small maps (AlexNet conv3-5: 13 x 13,
+// 3 x 3, grouped), gfx950:  dW[co][kh][kw][ci] += sum_p dy[p][co] * x[p + (kh, kw) - pad][ci].
+// Reference: src/layer/convolution_layer-inl.hpp:121-138 (im2col + gemm into gwmat per group).
+//
+// Why.  The split-K implicit GEMM (gemm_mfma.hip GATHER_MN) rebuilds every pixel's im2col address
+// per 16-byte load (3.66 VALU per MFMA) and meets its K slices in fp32 atomics; on AlexNet's
+// 13 x 13 layers it ran 455-635 TFLOP/s (profiles/r4_alexnet_b256_kernels_final.md).  The VGG
+// halo kernel (conv_wgrad_halo.hip) tiles 2-D patches of 16-32 columns, which waste a third of
+// the MFMAs on a 13-wide map.  Here:
+//   * Pixel "slots": every image row is followed by a P-wide zero gap (pitch PW = W + P), and
+//     images of a stage are stacked with P zero separator rows.  In that linear slot space the
+//     input pixel under tap (kh, kw) of output slot s is slot s + kh * PW + kw of the staged x
+//     image, for EVERY slot: a tap is a constant shift, zero padding falls on gap / separator
+//     slots (zeros), and the K walk over output slots has no per-pixel index arithmetic.  The dy
+//     gap slots are zero, so they add nothing (13 x 13: 169 of 192 walked slots are pixels).
+//   * A stage = IPS whole images; one block streams its images' x (32 channels) and dy (64
+//     channels) through a double-buffered LDS pair by LDS-DMA.  Every lane's DMA source offsets
+//     within a stage are fixed for the whole kernel (computed once); per stage only the buffer
+//     descriptors move, and slots outside the map read as zeros through out-of-range offsets.
+//   * LDS images are channel-unit-major ([16-channel unit][slot][16 ch], 32 B per slot-unit).
+//     An MFMA k-index -> slot permutation makes each 32-lane half of a ds_read_b64_tr_b16 read 8
+//     consecutive slots (256 contiguous bytes): conflict-free for dy and for every tap shift.
+//   * Block tile 64 co x 32 ci x all taps.  The four waves (one per SIMD) each accumulate the
+//     WHOLE tile (4 x 2 x 9 f32x4 = 288 AGPRs) over every fourth K-step, so per K-step a wave
+//     reads 4 dy + 18 x fragments for 72 MFMAs (0.31 reads per MFMA) with constant addresses.
+//     The four partial tiles meet through LDS after the loop.
+//   * Split over images: (pairs x splits) ~ one block per CU, XCD-contiguous so the blocks that
+//     read the same images share an L2.  No atomics: each block stores its partial tile with
+//     plain coalesced 16-byte stores into a workspace, and conv_wgrad_direct_reduce sums the
+//     splits in a fixed order into dW (+=), so the result is bitwise reproducible.
+#include "gemm_glds_common.h"
+
+using namespace cxg;
+
+namespace {
+
+// One 1-KiB LDS-DMA (16 bytes per lane) as inline asm: hipcc cannot tell the LDS bytes it writes
+// from the ones the ds_reads of the current stage touch, and for the builtin it inserts a
+// vmcnt(0) before the first ds_read after the DMAs -- the next stage's loads would then be waited
+// for at the start of the current stage instead of landing under its MFMAs.  Completion is
+// counted by hand (wait_vmcnt + barrier at the end of the stage).  M0 is saved and restored in
+// the statement (compiler-reserved).
+__device__ __forceinline__ void dma16d(rsrc_t r, uint32_t lds_addr, uint32_t voff) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(r), "s"(lds_addr) : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_lgkm_d() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// accumulators beyond the 256-register AGPR file live in VGPRs (gfx950 MFMAs take either)
+template <bool AGPR>
+__device__ __forceinline__ void mfma_d(f32x4 &acc, const bf16x8 &a, const bf16x8 &b) {
+  if constexpr (AGPR) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  else asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+}
+template <bool AGPR>
+__device__ __forceinline__ void pin_d(f32x4 &acc) {
+  if constexpr (AGPR) asm volatile("" : "+a"(acc));
+  else asm volatile("" : "+v"(acc));
+}
+constexpr int NAGPR_ACC = 56;  // f32x4 accumulators kept in AGPRs (224 of the 256)
+
+// two transposed 8-byte reads (k-rows 8 g4 + q and 8 g4 + 4 + q) -> one 16x16x32 operand fragment
+__device__ __forceinline__ bf16x8 frag_d(const char *p0, const char *p1) {
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p1));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+constexpr int fdiv_floor(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+
+template <int H, int W, int KS, int IPS>
+struct Wd {
+  static constexpr int P = (KS - 1) / 2;
+  static constexpr int T = KS * KS;
+  static constexpr int PW = W + P;                       // slot pitch
+  static constexpr int VR = H + P;                       // virtual rows per image
+  static constexpr int WALK = (IPS * VR - P) * PW;       // output slots that can hold pixels
+  static constexpr int NK = (WALK + 127) / 128 * 4;      // K-steps per stage, a multiple of 4
+  static constexpr int KW4 = NK / 4;                     // K-steps per wave per stage
+  static constexpr int NKS = NK * 32;                    // dy slots per stage
+  static constexpr int NX = (NKS + (KS - 1) * (PW + 1) + 31) / 32;  // x slot groups of 32
+  static constexpr int NXS = NX * 32;
+  static constexpr int XLEAD = P * PW + P;               // x slot of linear position 0
+  static constexpr int CO_U = 4, CI_U = 2;               // 64 co x 32 ci per block
+  static constexpr int DYB = CO_U * NKS * 32;            // dy bytes per buffer
+  static constexpr int XB = CI_U * NXS * 32;
+  static constexpr int BUF = DYB + XB;
+  static constexpr int NQD = CO_U * NK / 4;              // dy DMA instructions per wave
+  static constexpr int NQX = (CI_U * NX + 3) / 4;        // x DMA instructions per wave (last maybe idle)
+  static constexpr int NACC = CO_U * CI_U * T;           // f32x4 accumulators per wave
+  static_assert(2 * BUF <= 160 * 1024, "LDS");
+  static_assert(4 * NACC * 64 * 16 / 2 <= 2 * BUF, "epilogue staging fits the stage buffers");
+};
+
+// (image, row, col) of a linear position in a stage's virtual slot space; -1 when it is padding
+template <int H, int W, int KS, int IPS>
+__device__ __forceinline__ int slot_pixel(int lin) {
+  using G = Wd<H, W, KS, IPS>;
+  const int vrow = fdiv_floor(lin, G::PW);
+  const int col = lin - vrow * G::PW;
+  const int img = fdiv_floor(vrow, G::VR);
+  const int row = vrow - img * G::VR;
+  if (img < 0 || img >= IPS || row >= H || col >= W) return -1;
+  return (img * H + row) * W + col;
+}
+
+template <int H, int W, int KS, int IPS>
+__global__ void __launch_bounds__(256, 1)
+conv_wgrad_direct(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, float *__restrict__ ws, int N, int C,
+                  int ldy, int Cg, int Cog, int npairs, int nci_b, int nco_b, int per, int nstages) {
+  using G = Wd<H, W, KS, IPS>;
+  constexpr int T = G::T, NK = G::NK, KW4 = G::KW4, NKS = G::NKS, NX = G::NX, NXS = G::NXS, PW = G::PW;
+  constexpr int CO_U = G::CO_U, CI_U = G::CI_U, BUF = G::BUF, DYB = G::DYB, NQD = G::NQD, NQX = G::NQX;
+  constexpr int HW = H * W;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+
+  const uint32_t L = xcd_remap(blockIdx.x, gridDim.x);
+  const int pair = static_cast<int>(L % static_cast<uint32_t>(npairs));
+  const int split = static_cast<int>(L / static_cast<uint32_t>(npairs));
+  const int per_g = nco_b * nci_b;
+  const int g = pair / per_g, rem = pair - g * per_g;
+  const int cob = rem / nci_b, cib = rem - cob * nci_b;
+  const int ci0 = g * Cg + cib * 16 * CI_U, co0 = g * Cog + cob * 16 * CO_U;
+  const int sb = split * per, se = min(nstages, sb + per);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void *)smem)));
+  // ---- per-lane DMA source offsets within a stage (fixed for the whole kernel)
+  uint32_t vd[NQD], vx[NQX];
+#pragma unroll
+  for (int i = 0; i < NQD; ++i) {
+    const int q = wave + 4 * i;
+    const int u = q / NK, sg = q - u * NK;
+    const int pix = slot_pixel<H, W, KS, IPS>(32 * sg + (lane >> 1));
+    vd[i] = pix >= 0 ? static_cast<uint32_t>((pix * ldy + 16 * u + 8 * (lane & 1)) * 2) : OOB;
+  }
+#pragma unroll
+  for (int i = 0; i < NQX; ++i) {
+    const int q = wave + 4 * i;
+    const int u = q / NX, sg = q - u * NX;
+    const int pix = slot_pixel<H, W, KS, IPS>(32 * sg + (lane >> 1) - G::XLEAD);
+    vx[i] = (q < CI_U * NX && pix >= 0) ? static_cast<uint32_t>((pix * C + 16 * u + 8 * (lane & 1)) * 2) : OOB;
+  }
+  // stage st -> buffer b: every DMA of this wave (descriptors cover the stage's whole images; a
+  // missing last image is out of range, so its slots read as zeros)
+  auto issue = [&](int st, int b) __attribute__((always_inline)) {
+    const int n0 = st * IPS;
+    const int nimg = min(IPS, N - n0);
+    const long pd = static_cast<long>(n0) * HW;
+    const rsrc_t rd = make_rsrc(dy + pd * ldy + co0, static_cast<uint32_t>((nimg * HW * static_cast<long>(ldy) - co0) * 2));
+    const rsrc_t rx = make_rsrc(x + pd * C + ci0, static_cast<uint32_t>((nimg * HW * static_cast<long>(C) - ci0) * 2));
+    const uint32_t base = lds0 + b * BUF + wave * 1024;  // wave-uniform LDS byte address
+#pragma unroll
+    for (int i = 0; i < NQD; ++i) dma16d(rd, base + i * 4096, vd[i]);
+#pragma unroll
+    for (int i = 0; i < NQX; ++i)
+      if (wave + 4 * i < CI_U * NX) dma16d(rx, base + DYB + i * 4096, vx[i]);
+  };
+
+  // ---- fragment read bases: lane (l16, g4) = (4 q + p, g4) reads slot sl(hl) bytes 8p..8p+7
+  const int l16 = lane & 15, g4 = lane >> 4;
+  int bd[2][2], bx[2][2];  // [buffer][hl]
+#pragma unroll
+  for (int hl = 0; hl < 2; ++hl) {
+    const int sl = ((g4 >> 1) << 4) | (hl << 3) | ((g4 & 1) << 2) | (l16 >> 2);
+    const int o = (sl + 32 * wave) * 32 + 8 * (l16 & 3);  // this wave's first K-step
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      bd[b][hl] = b * BUF + o;
+      bx[b][hl] = b * BUF + DYB + o;
+    }
+  }
+
+  // accumulator i = (m CI_U + u) T + t
+  f32x4 acc[G::NACC];
+#pragma unroll
+  for (int i = 0; i < G::NACC; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa[2][CO_U], fb[3][CI_U];
+
+  // K-step j (0..KW4-1) of this wave in buffer b: slots 32 (wave + 4 j) ..
+  auto read_a = [&](int set, int b, int j) __attribute__((always_inline)) {
+#pragma unroll
+    for (int m = 0; m < CO_U; ++m) {
+      const int off = (m * NKS + 128 * j) * 32;
+      fa[set][m] = frag_d(smem + bd[b][0] + off, smem + bd[b][1] + off);
+    }
+  };
+  auto read_b = [&](int set, int b, int j, int t) __attribute__((always_inline)) {
+    const int kh = t / KS, kw = t - kh * KS;
+#pragma unroll
+    for (int u = 0; u < CI_U; ++u) {
+      const int off = (u * NXS + 128 * j + kh * PW + kw) * 32;
+      fb[set][u] = frag_d(smem + bx[b][0] + off, smem + bx[b][1] + off);
+    }
+  };
+
+  // prologue: stage sb
+  issue(sb, 0);
+  wait_vmcnt<0>();
+  block_barrier();
+  read_a(0, 0, 0);
+  read_b(0, 0, 0, 0);
+  read_b(1, 0, 0, 1);
+  __builtin_amdgcn_sched_barrier(0);
+
+  // One stage from buffer B (landed; K-step 0's dy and taps 0-1 are being read).  KW4 K-steps of
+  // T taps; during tap t the reads of tap t + 2 (or of the next K-step's dy / taps 0-1) are
+  // issued between the MFMAs.  Set indices are compile-time over a pair of stages: KW4 * T taps
+  // per stage is a multiple of 3 (T = 9), and fa alternates per K-step.
+  auto stage = [&](auto bc, int st) __attribute__((always_inline)) {
+    constexpr int B = decltype(bc)::value;
+    const bool next = st + 1 < se;
+    if (next) issue(st + 1, B ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<KW4>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      constexpr int ja = (B * KW4 + j) & 1;  // fa set of this K-step
+      constexpr bool more = j + 1 < KW4;
+      static_for<T>([&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        constexpr int gt = B * KW4 * T + j * T + t;  // running tap index over the stage pair
+        constexpr int sb3 = gt % 3;
+        // wait for tap t (and at t = 0 the K-step's dy): what may stay in flight is the reads
+        // issued after them
+        if constexpr (t == T - 1) {
+          if constexpr (more) wait_lgkm_d<2 * CI_U + 2 * CO_U>();
+          else wait_lgkm_d<0>();
+        } else if constexpr (t == T - 2 && !more) {
+          wait_lgkm_d<2 * CI_U>();
+        } else {
+          wait_lgkm_d<2 * CI_U>();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        static_for<CO_U * CI_U>([&](auto uc) {
+          constexpr int q = decltype(uc)::value;
+          constexpr int m = q / CI_U, u = q % CI_U;
+          constexpr int ai = (m * CI_U + u) * T + t;
+          mfma_d<(ai < NAGPR_ACC)>(acc[ai], fa[ja][m], fb[sb3][u]);
+          if constexpr (q == 1) {
+            if constexpr (t + 2 < T) read_b((gt + 2) % 3, B, j, t + 2);
+            else if (more) read_b((gt + 2) % 3, B, j + 1, t + 2 - T);
+          }
+          if constexpr (q == 3 && t == T - 2) {
+            if (more) read_a(ja ^ 1, B, j + 1);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        });
+      });
+    });
+    wait_vmcnt<0>();
+    block_barrier();
+    if (next) {
+      constexpr int gt0 = ((B ^ 1) * KW4 * T) % 3;
+      read_a(((B ^ 1) * KW4) & 1, B ^ 1, 0);
+      read_b(gt0, B ^ 1, 0, 0);
+      read_b((gt0 + 1) % 3, B ^ 1, 0, 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  static_assert((2 * G::KW4 * G::T) % 3 == 0 && (2 * G::KW4) % 2 == 0, "set indices repeat over a stage pair");
+  int st = sb;
+  for (; st + 1 < se; st += 2) {
+    stage(std::integral_constant<int, 0>{}, st);
+    stage(std::integral_constant<int, 1>{}, st + 1);
+  }
+  if (st < se) stage(std::integral_constant<int, 0>{}, st);
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");  // inline-asm MFMA results
+  static_for<G::NACC>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    pin_d<(i < NAGPR_ACC)>(acc[i]);
+  });
+
+  // ---- the four waves' partial tiles meet through LDS (both stage buffers are free: the last
+  // stage ended with a barrier), CH accumulators at a time so that no more than a few sums are
+  // live in VGPRs: every wave writes its CH accumulators (lane l's f32x4 of accumulator i at
+  // byte (i - c0) * 1024 + 16 l of the wave's region), then wave w sums accumulators
+  // c0 + CH/4 w .. over the four regions and stores them (coalesced 1-KiB rows).
+  constexpr int NACC = G::NACC, CH = 24, NCH = NACC / CH, Q = CH / 4, RB = CH * 1024;
+  static_assert(NACC % CH == 0 && 4 * RB <= 2 * BUF, "epilogue chunks");
+  float *out = ws + (static_cast<long>(split) * npairs + pair) * (NACC * 256) + 4 * lane;
+  static_for<NCH>([&](auto cc) {
+    constexpr int c0 = decltype(cc)::value * CH;
+    static_for<CH>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      *reinterpret_cast<f32x4 *>(smem + wave * RB + i * 1024 + 16 * lane) = acc[c0 + i];
+    });
+    block_barrier();
+#pragma unroll
+    for (int k = 0; k < Q; ++k) {
+      const int i = Q * wave + k;
+      f32x4 v = *reinterpret_cast<const f32x4 *>(smem + i * 1024 + 16 * lane);
+#pragma unroll
+      for (int w = 1; w < 4; ++w) v += *reinterpret_cast<const f32x4 *>(smem + w * RB + i * 1024 + 16 * lane);
+      *reinterpret_cast<f32x4 *>(out + (c0 + i) * 256) = v;
+    }
+    block_barrier();
+  });
+}
+
+// dW[co][t][ci] += sum over splits of the partial tiles (fixed order).  Thread = (pair, acc i,
+// lane): its f32x4 holds output channels co0 + 16 m + 4 (lane >> 4) + j, input channel ci0 + 16 u +
+// (lane & 15), tap t, with i = (m CI_U + u) T + t.
+template <int T>
+__global__ void __launch_bounds__(256)
+conv_wgrad_direct_reduce(const float *__restrict__ ws, float *__restrict__ dw, int nsplit, int npairs, int nci_b,
+                         int nco_b, int Cg, int Cog, float alpha) {
+  constexpr int CO_U = 4, CI_U = 2, NACC = CO_U * CI_U * T;
+  const long tid = static_cast<long>(blockIdx.x) * 256 + threadIdx.x;
+  const long total = static_cast<long>(npairs) * NACC * 64;
+  if (tid >= total) return;
+  const int lane = static_cast<int>(tid & 63);
+  const long r = tid >> 6;
+  const int i = static_cast<int>(r % NACC);
+  const int pair = static_cast<int>(r / NACC);
+  f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+  const long slab = static_cast<long>(npairs) * NACC * 256;
+  const float *p = ws + (static_cast<long>(pair) * NACC + i) * 256 + 4 * lane;
+  for (int k = 0; k < nsplit; ++k) s += *reinterpret_cast<const f32x4 *>(p + k * slab);
+  const int per_g = nco_b * nci_b;
+  const int g = pair / per_g, rem = pair - g * per_g;
+  const int cob = rem / nci_b, cib = rem - cob * nci_b;
+  const int t = i % T, mu = i / T;
+  const int m = mu / CI_U, u = mu - m * CI_U;
+  const int ci = cib * 16 * CI_U + 16 * u + (lane & 15);
+  const int co = g * Cog + cob * 16 * CO_U + 16 * m + 4 * (lane >> 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float *d = dw + (static_cast<long>(co + j) * T + t) * Cg + ci;
+    *d += alpha * s[j];
+  }
+}
+
+template <int H, int W, int KS, int IPS>
+int launch_wd(const bf16_t *x, const bf16_t *dy, float *dw, float *ws, long ws_floats, int N, int C, int ldy, int Cg,
+              int Cog, int groups, int splits, float alpha, hipStream_t s) {
+  using G = Wd<H, W, KS, IPS>;
+  const int nci_b = Cg / 32, nco_b = Cog / 64;
+  const int npairs = groups * nci_b * nco_b;
+  const int nstages = (N + IPS - 1) / IPS;
+  int S = splits > 0 ? splits : 256 / npairs;
+  S = S < 1 ? 1 : (S > nstages ? nstages : S);
+  const int per = (nstages + S - 1) / S;
+  S = (nstages + per - 1) / per;  // every split holds at least one stage
+  const long need = static_cast<long>(S) * npairs * G::NACC * 256;
+  if (ws_floats < need) return -4;
+  CXN_LAUNCH((conv_wgrad_direct<H, W, KS, IPS>), dim3(static_cast<unsigned>(npairs * S)), dim3(256), 0, s, x, dy, ws,
+             N, C, ldy, Cg, Cog, npairs, nci_b, nco_b, per, nstages);
+  const long threads = static_cast<long>(npairs) * G::NACC * 64;
+  CXN_LAUNCH((conv_wgrad_direct_reduce<G::T>), dim3(static_cast<unsigned>((threads + 255) / 256)), dim3(256), 0, s, ws,
+             dw, S, npairs, nci_b, nco_b, Cg, Cog, alpha);
+  return 0;
+}
+
+// workspace floats for a launch (0 when the shape is not served)
+template <int H, int W, int KS, int IPS>
+long ws_wd(int N, int Cg, int Cog, int groups, int splits) {
+  using G = Wd<H, W, KS, IPS>;
+  const int npairs = groups * (Cg / 32) * (Cog / 64);
+  const int nstages = (N + IPS - 1) / IPS;
+  int S = splits > 0 ? splits : 256 / npairs;
+  S = S < 1 ? 1 : (S > nstages ? nstages : S);
+  const int per = (nstages + S - 1) / S;
+  S = (nstages + per - 1) / per;
+  return static_cast<long>(S) * npairs * G::NACC * 256;
+}
+
+}  // namespace
+
+// Served: stride 1, "same" padding (pad = (K - 1) / 2), K = 3, 13 x 13 maps; input channels per
+// group a multiple of 32, output channels per group a multiple of 64; x / dy pixel strides (C,
+// ldy) multiples of 8.  ws == nullptr: returns the workspace size in floats (0: not served).
+// Otherwise launches the kernel and the split reduction into dw (fp32 [Cout][K][K][Cg], +=
+// alpha * gradient); -1 when not served, -4 when ws is too small.
+CXN_API long cxn_conv_wgrad_direct(const void *x, const void *dy, float *dw, float *ws, long ws_floats, int N, int H,
+                                   int W, int C, int ldy, int Cg, int Cog, int groups, int KH, int KW, int pad_h,
+                                   int pad_w, int stride, int splits, float alpha, void *stream) {
+  if (stride != 1 || KH != KW || pad_h != pad_w || pad_h != (KH - 1) / 2) return ws ? -1 : 0;
+  if (Cg % 32 || Cog % 64 || C % 8 || ldy % 8 || groups < 1 || C < groups * Cg || ldy < groups * Cog) return ws ? -1 : 0;
+  if (static_cast<long>(N) * H * W * (C > ldy ? C : ldy) >= (1L << 30)) return ws ? -1 : 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bf16_t *xb = static_cast<const bf16_t *>(x), *db = static_cast<const bf16_t *>(dy);
+  if (KH == 3 && H == 13 && W == 13) {
+    if (!ws) return ws_wd<13, 13, 3, 2>(N, Cg, Cog, groups, splits);
+    const int rc = launch_wd<13, 13, 3, 2>(xb, db, dw, ws, ws_floats, N, C, ldy, Cg, Cog, groups, splits, alpha, s);
+    if (rc != 0) return rc;
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+  }
+  return ws ? -1 : 0;
+}

@@ -134,12 +134,19 @@ class Layer:
     allow_sharing = True
 
 
+    # Opt-in: a layer class sets replay_audited = True once its GPU forward / backward has been
+    # checked to launch only library kernels with step-invariant arguments.  Anything else (a
+    # new layer, a torch op in forward / backward) keeps the eager executor, where every op
+    # runs every step; a replayed plan would silently skip torch ops.
+    replay_audited = False
+
     def replay_safe(self) -> bool:
         """Whether this layer's GPU forward / backward launch only library kernels whose
         arguments are step-invariant (per-step values read from device memory), so that the
         C++ launch-list executor can record the step once and replay it (NetTrainer._list_step).
-        Layers that issue torch ops or pass per-step host values override this."""
-        return True
+        False unless the class is audited (replay_audited); audited classes with
+        configuration-dependent torch ops override this."""
+        return bool(type(self).replay_audited)
 
     def __init__(self, ctx: LayerContext):
         self.ctx = ctx

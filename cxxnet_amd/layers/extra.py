@@ -28,6 +28,7 @@ def _num_feat(node):
 
 class BiasLayer(Layer):
     """`bias` -- reference src/layer/bias_layer-inl.hpp:14-83 (self-loop on a matrix node)."""
+    replay_audited = True  # library kernels only (tests/test_launch_hygiene_gpu.py)
     type_name = "bias"
 
     def init_connection(self, nodes_in, nodes_out):
@@ -74,6 +75,7 @@ class SplitLayer(Layer):
     reads its input in forward: conv / fullc / pooling / lrn): the outputs ARE the input buffer,
     each consumer writes its data-gradient into its output node's private grad buffer, and
     backward sums those into the input node -- no forward copies."""
+    replay_audited = True  # library kernels only (tests/test_launch_hygiene_gpu.py)
     type_name = "split"
     alias = False
 
@@ -99,6 +101,7 @@ class SplitLayer(Layer):
 class ConcatLayer(Layer):
     """`concat` (dim 3) / `ch_concat` (dim 1) -- reference src/layer/concat_layer-inl.hpp:11-79,
     2-4 inputs.  On NHWC buffers ch_concat is a strided channel copy per input."""
+    replay_audited = True  # library kernels only (tests/test_launch_hygiene_gpu.py)
 
     def __init__(self, ctx, dim):
         super().__init__(ctx)
@@ -180,6 +183,7 @@ class BatchNormLayer(Layer):
     """`batch_norm` -- reference src/layer/batch_norm_layer-inl.hpp:14-197.  Batch
     statistics in both train and test (no running mean), eps default 1e-10; slope is
     visited as "wmat", bias as "bias"; the checkpoint holds slope + bias only."""
+    replay_audited = True  # library kernels only (tests/test_launch_hygiene_gpu.py)
     type_name = "batch_norm"
 
     def __init__(self, ctx):

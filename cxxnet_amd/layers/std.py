@@ -35,6 +35,7 @@ class FullConnectLayer(Layer):
     """`fullc` -- reference src/layer/fullc_layer-inl.hpp:13-146.
     out = in . W^T + b;  gW += out_g^T . in;  gb += sum_rows(out_g);  in_g = out_g . W
     """
+    replay_audited = True  # library kernels only (tests/test_launch_hygiene_gpu.py)
     type_name = "fullc"
 
     def __init__(self, ctx):
@@ -280,6 +281,7 @@ class ConvolutionLayer(Layer):
     checkpoint keeps the reference (g, Cout/g, Cin/g*KH*KW) layout in (ci, kh, kw) order.
     The im2col buffer never exists: the MFMA kernel gathers patches on the fly.
     """
+    replay_audited = True  # library kernels only (tests/test_launch_hygiene_gpu.py)
     type_name = "conv"
 
     def __init__(self, ctx):
@@ -438,6 +440,7 @@ class ActivationLayer(Layer):
     """`relu`/`sigmoid`/`tanh` -- reference src/layer/activation_layer-inl.hpp:11-40;
     `xelu` -- src/layer/xelu_layer-inl.hpp:15-50.  Applied in place on the input node
     and copied to the output node; the gradient is expressed through the output."""
+    replay_audited = True  # library kernels only (tests/test_launch_hygiene_gpu.py)
 
     def __init__(self, ctx, kind):
         super().__init__(ctx)
@@ -486,6 +489,7 @@ class PoolingLayer(Layer):
     pooled output is saved and the backward compares values (ops.pool_backward_tie_all).
     Ties only occur between bit-identical activations (e.g. windows of relu zeros, which get
     no gradient through a fused relu either way)."""
+    replay_audited = True  # library kernels only (tests/test_launch_hygiene_gpu.py)
 
     def __init__(self, ctx, mode, relu=False):
         super().__init__(ctx)
@@ -573,6 +577,7 @@ class PoolingLayer(Layer):
 # ============================================================================ LRN
 class LRNLayer(Layer):
     """`lrn` -- reference src/layer/lrn_layer-inl.hpp:12-89 (cross-channel, knorm/alpha/beta)."""
+    replay_audited = True  # library kernels only (tests/test_launch_hygiene_gpu.py)
     type_name = "lrn"
 
     def __init__(self, ctx):
@@ -616,6 +621,7 @@ class DropoutLayer(Layer):
     """`dropout` -- reference src/layer/dropout_layer-inl.hpp:12-66 (self-loop;
     mask = (u < pkeep)/pkeep).  The mask is a counter-based hash, regenerated in
     backward instead of stored."""
+    replay_audited = True  # library kernels only (tests/test_launch_hygiene_gpu.py)
     type_name = "dropout"
 
     def __init__(self, ctx):
@@ -648,6 +654,7 @@ class DropoutLayer(Layer):
 class FlattenLayer(Layer):
     """`flatten` -- reference src/layer/flatten_layer-inl.hpp:11-40: (B,C,H,W) -> (B,1,1,CHW)
     in NCHW feature order (so fullc weights keep the reference meaning)."""
+    replay_audited = True  # library kernels only (tests/test_launch_hygiene_gpu.py)
     type_name = "flatten"
 
     def init_connection(self, nodes_in, nodes_out):
@@ -681,6 +688,7 @@ class LossLayerBase(Layer):
     """reference src/layer/loss/loss_layer_base-inl.hpp:11-133.  Self-loop on a matrix
     node; gradient (pred - target) scaled by grad_scale / (batch_size * update_period)
     with the GLOBAL batch size.  Computed on device (no host round trip)."""
+    replay_audited = True  # library kernels only (tests/test_launch_hygiene_gpu.py)
     kind = "softmax"
 
     def __init__(self, ctx):

@@ -129,8 +129,9 @@ _SIGS = {
     "cxn_rec_replay_many": [_P, _I, _P],
     "cxn_rec_free": [_P],
     "cxn_copy_d2d": [_P, _P, _L, _P],
+    "cxn_conv_wgrad_direct": [_P, _P, _P, _P, _L] + [_I] * 14 + [_F, _P],
 }
-_RESTYPE = {"cxn_rec_end": ctypes.c_void_p, "cxn_rec_free": None}
+_RESTYPE = {"cxn_rec_end": ctypes.c_void_p, "cxn_rec_free": None, "cxn_conv_wgrad_direct": ctypes.c_long}
 
 
 def kernel_lib_path() -> str:

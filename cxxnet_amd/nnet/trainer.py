@@ -640,6 +640,10 @@ class NetTrainer:
         net, red = self.net, self.reducer
         if not (self.cuda_graph != 0 and net.ctx.is_gpu and self.update_period == 1 and red is not None):
             return False
+        if red.active and not red.handles_update:
+            # data parallel without the overlapped update: the collectives (and, sharded, the
+            # owned-range update + parameter gather) live in the eager step only
+            return False
         # (fullc_gather layers issue their all-gathers through ctx.graph_cut: eager calls between
         # graph segments, like the bucket collectives)
         if self.cuda_graph < 0:
@@ -741,6 +745,8 @@ class NetTrainer:
         net, red = self.net, self.reducer
         if self.launch_replay == 0 or not net.ctx.is_gpu or self.update_period != 1 or red is None:
             return False
+        if red.active and not red.handles_update:
+            return False  # as _graph_eligible: the reduction runs in the eager step only
         if self._graph_eligible():
             return False
         if not all(c.layer.replay_safe() for c in net.connections):
@@ -815,6 +821,9 @@ class NetTrainer:
         optimizer and the per-bucket updates skip them); their device schedule row is
         refreshed first."""
         net, red = self.net, self.reducer
+        # a planned step reduces gradients only through the overlapped per-bucket update; the
+        # eligibility rules (_graph_eligible / _list_eligible) keep every other DP mode eager
+        assert red.handles_update or not red.active, "planned step under DP without the overlapped update"
         if fused:
             net.updater.stage_hyper(self.epoch_counter)
             net.updater.fused_offsets.update(fused)

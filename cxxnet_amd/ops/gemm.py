@@ -743,6 +743,44 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False, wt_
     return False
 
 
+# Direct small-map weight gradient (conv_wgrad_direct.hip: gap-slot K walk, resident x / dy
+# stages, partial tiles reduced in a fixed order -- no atomics, deterministic).  "1" / "auto":
+# use it wherever it serves the shape; "0": off (the split-K GEMMs run).
+_WGD = os.environ.get("CXXNET_WGRAD_DIRECT", "auto")
+_wgd_ws = {}
+
+
+def _wgd_workspace(n, device):
+    buf = _wgd_ws.get(str(device))
+    if buf is None or buf.numel() < n:
+        from .mode import retire
+        retire(buf)  # a recorded / captured step may still point at it
+        buf = _wgd_ws[str(device)] = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=device)
+    return buf
+
+
+def conv_wgrad_direct(x, dy, dw, g: ConvGeom, splits: int = 0) -> bool:
+    """dw += the weight gradient on the direct small-map kernel; False when it does not serve
+    the shape (or is switched off)."""
+    if _WGD == "0" or _glds_cfg["tile"] >= 0 or not _native_t(x) or g.Ho != g.H or g.Wo != g.W:
+        return False  # (a forced LDS-DMA tile id means a test / probe wants that kernel)
+    if not (x.is_contiguous() or x.stride(-1) == 1) or dy.stride(-1) != 1:
+        return False
+    k = native.kernels()
+    args = (g.N, g.H, g.W, _pix(x), _pix(dy), g.cg_in, g.cg_out, g.groups, g.KH, g.KW, g.pad_y, g.pad_x, g.stride,
+            int(splits))
+    need = int(k.cxn_conv_wgrad_direct(None, None, None, None, 0, *args, 1.0, None))
+    if need <= 0:
+        return False
+    ws = _wgd_workspace(need, dw.device)
+    rc = int(k.cxn_conv_wgrad_direct(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), ws.data_ptr(), ws.numel(), *args,
+                                     1.0, _stream()))
+    if rc == -1:
+        return False
+    native.check(rc, "conv_wgrad_direct")
+    return True
+
+
 def conv_backward_weight(x, dy, dw, g: ConvGeom):
     """dw += sum over pixels of dy (x) im2col(x).  dw fp32 [Cout][KH][KW][Cg].
     (Folding the bias gradient into this GEMM was measured a wash on GoogLeNet and its
@@ -778,6 +816,8 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
         key = ("cws", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
         return reg_run(_tuned_tile(key, reg_run, o, reg_default, cands=_wgrad_cands(kd, g.cg_out, g.groups, P)), o)
     rowrun = va != 8 and rowrun_ok(g)
+    if conv_wgrad_direct(x, dy, dw, g):  # deterministic as well: no atomics, fixed split order
+        return
     if _DET["on"] and not (rowrun and cg % va):
         # one fp32 slab per K slice, summed in slice order into dw: bitwise reproducible
         tile = _pick(WGRAD_TILES, kd, g.cg_out, g.groups, min_blocks=1)
