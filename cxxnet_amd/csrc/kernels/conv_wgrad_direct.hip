@@ -111,7 +111,7 @@ __device__ __forceinline__ int slot_pixel(int lin) {
   return (img * H + row) * W + col;
 }
 
-template <int H, int W, int KS, int IPS>
+template <int H, int W, int KS, int IPS, int V>
 __global__ void __launch_bounds__(256, 1)
 conv_wgrad_direct(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, float *__restrict__ ws, int N, int C,
                   int ldy, int Cg, int Cog, int npairs, int nci_b, int nco_b, int per, int nstages) {
@@ -150,20 +150,31 @@ conv_wgrad_direct(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, f
     const int pix = slot_pixel<H, W, KS, IPS>(32 * sg + (lane >> 1) - G::XLEAD);
     vx[i] = (q < CI_U * NX && pix >= 0) ? static_cast<uint32_t>((pix * C + 16 * u + 8 * (lane & 1)) * 2) : OOB;
   }
-  // stage st -> buffer b: every DMA of this wave (descriptors cover the stage's whole images; a
-  // missing last image is out of range, so its slots read as zeros)
-  auto issue = [&](int st, int b) __attribute__((always_inline)) {
+  // stage st -> buffer b: the DMAs of this wave (descriptors cover the stage's whole images; a
+  // missing last image is out of range, so its slots read as zeros).  DMA i < NQD is dy
+  // instruction wave + 4 i, the rest x instructions.
+  constexpr int NDMA = NQD + NQX;
+  rsrc_t rd, rx;
+  auto prep = [&](int st) __attribute__((always_inline)) {
     const int n0 = st * IPS;
     const int nimg = min(IPS, N - n0);
     const long pd = static_cast<long>(n0) * HW;
-    const rsrc_t rd = make_rsrc(dy + pd * ldy + co0, static_cast<uint32_t>((nimg * HW * static_cast<long>(ldy) - co0) * 2));
-    const rsrc_t rx = make_rsrc(x + pd * C + ci0, static_cast<uint32_t>((nimg * HW * static_cast<long>(C) - ci0) * 2));
+    rd = make_rsrc(dy + pd * ldy + co0, static_cast<uint32_t>((nimg * HW * static_cast<long>(ldy) - co0) * 2));
+    rx = make_rsrc(x + pd * C + ci0, static_cast<uint32_t>((nimg * HW * static_cast<long>(C) - ci0) * 2));
+  };
+  auto issue_one = [&](auto ic, int b) __attribute__((always_inline)) {
+    constexpr int i = decltype(ic)::value;
     const uint32_t base = lds0 + b * BUF + wave * 1024;  // wave-uniform LDS byte address
-#pragma unroll
-    for (int i = 0; i < NQD; ++i) dma16d(rd, base + i * 4096, vd[i]);
-#pragma unroll
-    for (int i = 0; i < NQX; ++i)
-      if (wave + 4 * i < CI_U * NX) dma16d(rx, base + DYB + i * 4096, vx[i]);
+    if constexpr (i < NQD) {
+      dma16d(rd, base + i * 4096, vd[i]);
+    } else {
+      constexpr int k = i - NQD;
+      if (wave + 4 * k < CI_U * NX) dma16d(rx, base + DYB + k * 4096, vx[k]);
+    }
+  };
+  auto issue = [&](int st, int b) __attribute__((always_inline)) {
+    prep(st);
+    static_for<NDMA>([&](auto ic) { issue_one(ic, b); });
   };
 
   // ---- fragment read bases: lane (l16, g4) = (4 q + p, g4) reads slot sl(hl) bytes 8p..8p+7
@@ -194,13 +205,14 @@ conv_wgrad_direct(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, f
       fa[set][m] = frag_d(smem + bd[b][0] + off, smem + bd[b][1] + off);
     }
   };
-  auto read_b = [&](int set, int b, int j, int t) __attribute__((always_inline)) {
+  auto read_bu = [&](int set, int b, int j, int t, int u) __attribute__((always_inline)) {
     const int kh = t / KS, kw = t - kh * KS;
+    const int off = (u * NXS + 128 * j + kh * PW + kw) * 32;
+    fb[set][u] = frag_d(smem + bx[b][0] + off, smem + bx[b][1] + off);
+  };
+  auto read_b = [&](int set, int b, int j, int t) __attribute__((always_inline)) {
 #pragma unroll
-    for (int u = 0; u < CI_U; ++u) {
-      const int off = (u * NXS + 128 * j + kh * PW + kw) * 32;
-      fb[set][u] = frag_d(smem + bx[b][0] + off, smem + bx[b][1] + off);
-    }
+    for (int u = 0; u < CI_U; ++u) read_bu(set, b, j, t, u);
   };
 
   // prologue: stage sb
@@ -219,7 +231,11 @@ conv_wgrad_direct(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, f
   auto stage = [&](auto bc, int st) __attribute__((always_inline)) {
     constexpr int B = decltype(bc)::value;
     const bool next = st + 1 < se;
-    if (next) issue(st + 1, B ^ 1);
+    if constexpr (V & 1) {
+      if (next) prep(st + 1);  // the DMAs ride on K-step 0's taps
+    } else {
+      if (next) issue(st + 1, B ^ 1);
+    }
     __builtin_amdgcn_sched_barrier(0);
     static_for<KW4>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
@@ -245,9 +261,25 @@ conv_wgrad_direct(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, f
           constexpr int m = q / CI_U, u = q % CI_U;
           constexpr int ai = (m * CI_U + u) * T + t;
           mfma_d<(ai < NAGPR_ACC)>(acc[ai], fa[ja][m], fb[sb3][u]);
-          if constexpr (q == 1) {
-            if constexpr (t + 2 < T) read_b((gt + 2) % 3, B, j, t + 2);
-            else if (more) read_b((gt + 2) % 3, B, j + 1, t + 2 - T);
+          if constexpr ((V & 1) && j == 0 && q == 4) {
+            static_for<NDMA>([&](auto ic) {
+              constexpr int i = decltype(ic)::value;
+              if constexpr (i * T / NDMA == t) {
+                if (next) issue_one(ic, B ^ 1);
+              }
+            });
+          }
+          // the next reads: both x fragments of tap t + 2 after MFMA 1 (64: one after MFMA 1, one
+          // after MFMA 3 -- at most two ds_reads per MFMA gap)
+          constexpr int q0 = (V & 2) ? 5 : 1;
+          if constexpr ((V & 64) ? (q == q0 || q == q0 + 2) : q == q0) {
+            constexpr int uu = (V & 64) ? (q - q0) / 2 : -1;
+            auto rd = [&](int jj, int tt) __attribute__((always_inline)) {
+              if constexpr (uu < 0) read_b((gt + 2) % 3, B, jj, tt);
+              else read_bu((gt + 2) % 3, B, jj, tt, uu);
+            };
+            if constexpr (t + 2 < T) rd(j, t + 2);
+            else if (more) rd(j + 1, t + 2 - T);
           }
           if constexpr (q == 3 && t == T - 2) {
             if (more) read_a(ja ^ 1, B, j + 1);
@@ -352,8 +384,11 @@ int launch_wd(const bf16_t *x, const bf16_t *dy, float *dw, float *ws, long ws_f
   S = (nstages + per - 1) / per;  // every split holds at least one stage
   const long need = static_cast<long>(S) * npairs * G::NACC * 256;
   if (ws_floats < need) return -4;
-  CXN_LAUNCH((conv_wgrad_direct<H, W, KS, IPS>), dim3(static_cast<unsigned>(npairs * S)), dim3(256), 0, s, x, dy, ws,
-             N, C, ldy, Cg, Cog, npairs, nci_b, nco_b, per, nstages);
+  // schedule 65 (bits: 1 = the next stage's DMAs ride on K-step 0's taps, 64 = the two x
+  // fragments of tap t + 2 issued after MFMAs 1 and 3 of tap t); measured against the plain
+  // schedule (DMAs at the stage start, 101.6 -> ~100 / 112 -> 101 us on conv3, r5_wgrad_direct_*)
+  CXN_LAUNCH((conv_wgrad_direct<H, W, KS, IPS, 65>), dim3(static_cast<unsigned>(npairs * S)), dim3(256), 0, s, x, dy,
+             ws, N, C, ldy, Cg, Cog, npairs, nci_b, nco_b, per, nstages);
   const long threads = static_cast<long>(npairs) * G::NACC * 64;
   CXN_LAUNCH((conv_wgrad_direct_reduce<G::T>), dim3(static_cast<unsigned>((threads + 255) / 256)), dim3(256), 0, s, ws,
              dw, S, npairs, nci_b, nco_b, Cg, Cog, alpha);
