@@ -57,6 +57,12 @@ __device__ __forceinline__ void mfma_d(f32x4 &acc, const bf16x8 &a, const bf16x8
   if constexpr (AGPR) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
   else asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
 }
+// bias-gradient MFMA: its B operand (the ones fragment) lives in VGPRs that hipcc may have just
+// (re)written with a VALU move; "s_nop 1" covers the VALU-write -> MFMA-operand wait states hipcc
+// does not insert for inline asm
+__device__ __forceinline__ void mfma_db(f32x4 &acc, const bf16x8 &a, const bf16x8 &b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+}
 template <bool AGPR>
 __device__ __forceinline__ void pin_d(f32x4 &acc) {
   if constexpr (AGPR) asm volatile("" : "+a"(acc));
@@ -114,7 +120,7 @@ __device__ __forceinline__ int slot_pixel(int lin) {
 template <int H, int W, int KS, int IPS, int V>
 __global__ void __launch_bounds__(256, 1)
 conv_wgrad_direct(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, float *__restrict__ ws, int N, int C,
-                  int ldy, int Cg, int Cog, int npairs, int nci_b, int nco_b, int per, int nstages) {
+                  int ldy, int Cg, int Cog, int npairs, int nci_b, int nco_b, int per, int nstages, int want_db) {
   using G = Wd<H, W, KS, IPS>;
   constexpr int T = G::T, NK = G::NK, KW4 = G::KW4, NKS = G::NKS, NX = G::NX, NXS = G::NXS, PW = G::PW;
   constexpr int CO_U = G::CO_U, CI_U = G::CI_U, BUF = G::BUF, DYB = G::DYB, NQD = G::NQD, NQX = G::NQX;
@@ -196,6 +202,19 @@ conv_wgrad_direct(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, f
 #pragma unroll
   for (int i = 0; i < G::NACC; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 fa[2][CO_U], fb[3][CI_U];
+  // bias gradient (want_db): db[co] = sum over pixels of dy, as MFMAs of the dy fragments with a
+  // ones operand.  K-step k (= wave + 4 j of every stage) of co block cob is summed by the block
+  // with ci block k % nci_b, so each pixel counts once and the extra MFMAs (4 per summed K-step)
+  // are spread over the ci blocks (< 1 % of the MFMAs).
+  f32x4 accb[CO_U];
+#pragma unroll
+  for (int m = 0; m < CO_U; ++m) accb[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bool dbj[KW4];
+#pragma unroll
+  for (int j = 0; j < KW4; ++j) dbj[j] = want_db && (wave + 4 * j) % nci_b == cib;
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  bf16x8 ones = __builtin_bit_cast(bf16x8, s16x8{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80});
+  asm volatile("" : "+v"(ones));  // opaque: not re-materialised next to its MFMAs
 
   // K-step j (0..KW4-1) of this wave in buffer b: slots 32 (wave + 4 j) ..
   auto read_a = [&](int set, int b, int j) __attribute__((always_inline)) {
@@ -284,6 +303,12 @@ conv_wgrad_direct(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, f
           if constexpr (q == 3 && t == T - 2) {
             if (more) read_a(ja ^ 1, B, j + 1);
           }
+          if constexpr (q == CO_U * CI_U - 1 && t == T - 1) {
+            if (dbj[j]) {
+#pragma unroll
+              for (int mm = 0; mm < CO_U; ++mm) mfma_db(accb[mm], fa[ja][mm], ones);
+            }
+          }
           __builtin_amdgcn_sched_barrier(0);
         });
       });
@@ -310,6 +335,8 @@ conv_wgrad_direct(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, f
     constexpr int i = decltype(ic)::value;
     pin_d<(i < NAGPR_ACC)>(acc[i]);
   });
+#pragma unroll
+  for (int m = 0; m < CO_U; ++m) pin_d<false>(accb[m]);
 
   // ---- the four waves' partial tiles meet through LDS (both stage buffers are free: the last
   // stage ended with a barrier), CH accumulators at a time so that no more than a few sums are
@@ -336,6 +363,22 @@ conv_wgrad_direct(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, f
     }
     block_barrier();
   });
+  if (want_db) {
+    // every column of the ones-product holds the row sum: lanes of column 0 hand over their 16
+    // channels (16 m + 4 g4 + j) per wave, wave 0 sums the four waves and stores 64 partials
+    float *sdb = reinterpret_cast<float *>(smem);
+    if (l16 == 0) {
+#pragma unroll
+      for (int m = 0; m < CO_U; ++m)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sdb[wave * 64 + 16 * m + 4 * g4 + j] = accb[m][j];
+    }
+    block_barrier();
+    if (wave == 0) {
+      const float v = sdb[lane] + sdb[64 + lane] + sdb[128 + lane] + sdb[192 + lane];
+      ws[static_cast<long>(gridDim.x) * (NACC * 256) + (static_cast<long>(split) * npairs + pair) * 64 + lane] = v;
+    }
+  }
 }
 
 // dW[co][t][ci] += sum over splits of the partial tiles (fixed order).  Thread = (pair, acc i,
@@ -343,10 +386,33 @@ conv_wgrad_direct(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, f
 // (lane & 15), tap t, with i = (m CI_U + u) T + t.
 template <int T>
 __global__ void __launch_bounds__(256)
-conv_wgrad_direct_reduce(const float *__restrict__ ws, float *__restrict__ dw, int nsplit, int npairs, int nci_b,
-                         int nco_b, int Cg, int Cog, float alpha) {
+conv_wgrad_direct_reduce(const float *__restrict__ ws, float *__restrict__ dw, float *__restrict__ db, int nsplit,
+                         int npairs, int nci_b, int nco_b, int Cg, int Cog, float alpha) {
   constexpr int CO_U = 4, CI_U = 2, NACC = CO_U * CI_U * T;
-  const long tid = static_cast<long>(blockIdx.x) * 256 + threadIdx.x;
+  // the bias-gradient blocks come first (they start with the grid instead of trailing it)
+  const int nbb = db != nullptr ? (npairs / nci_b + 3) / 4 : 0;
+  if (static_cast<int>(blockIdx.x) < nbb) {
+    // bias gradient: wave = (co block of a group); lane = channel; the nsplit x nci_b partial
+    // rows are summed in a fixed order with eight loads in flight
+    const int gcb = static_cast<int>(blockIdx.x) * 4 + static_cast<int>(threadIdx.x >> 6);  // g * nco_b + cob
+    if (gcb >= npairs / nci_b) return;
+    const int cl = threadIdx.x & 63;
+    const float *pdb = ws + static_cast<long>(nsplit) * npairs * NACC * 256 + static_cast<long>(gcb) * nci_b * 64 + cl;
+    const int nr = nsplit * nci_b;  // partial row r = (split r / nci_b, ci block r % nci_b)
+    auto row = [&](int r) { return pdb[(static_cast<long>(r / nci_b) * npairs + r % nci_b) * 64]; };
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int r = 0;
+    for (; r + 8 <= nr; r += 8) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += row(r + e);
+    }
+    for (int e = 0; r < nr; ++r, ++e) v[e] += row(r);
+    const float tot = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+    const int g = gcb / nco_b, cob = gcb - g * nco_b;
+    db[g * Cog + cob * 64 + cl] += alpha * tot;
+    return;
+  }
+  const long tid = static_cast<long>(blockIdx.x - nbb) * 256 + threadIdx.x;
   const long total = static_cast<long>(npairs) * NACC * 64;
   if (tid >= total) return;
   const int lane = static_cast<int>(tid & 63);
@@ -372,8 +438,8 @@ conv_wgrad_direct_reduce(const float *__restrict__ ws, float *__restrict__ dw, i
 }
 
 template <int H, int W, int KS, int IPS>
-int launch_wd(const bf16_t *x, const bf16_t *dy, float *dw, float *ws, long ws_floats, int N, int C, int ldy, int Cg,
-              int Cog, int groups, int splits, float alpha, hipStream_t s) {
+int launch_wd(const bf16_t *x, const bf16_t *dy, float *dw, float *db, float *ws, long ws_floats, int N, int C, int ldy,
+              int Cg, int Cog, int groups, int splits, float alpha, hipStream_t s) {
   using G = Wd<H, W, KS, IPS>;
   const int nci_b = Cg / 32, nco_b = Cog / 64;
   const int npairs = groups * nci_b * nco_b;
@@ -382,16 +448,16 @@ int launch_wd(const bf16_t *x, const bf16_t *dy, float *dw, float *ws, long ws_f
   S = S < 1 ? 1 : (S > nstages ? nstages : S);
   const int per = (nstages + S - 1) / S;
   S = (nstages + per - 1) / per;  // every split holds at least one stage
-  const long need = static_cast<long>(S) * npairs * G::NACC * 256;
+  const long need = static_cast<long>(S) * npairs * (G::NACC * 256 + 64);
   if (ws_floats < need) return -4;
   // schedule 65 (bits: 1 = the next stage's DMAs ride on K-step 0's taps, 64 = the two x
   // fragments of tap t + 2 issued after MFMAs 1 and 3 of tap t); measured against the plain
   // schedule (DMAs at the stage start, 101.6 -> ~100 / 112 -> 101 us on conv3, r5_wgrad_direct_*)
   CXN_LAUNCH((conv_wgrad_direct<H, W, KS, IPS, 65>), dim3(static_cast<unsigned>(npairs * S)), dim3(256), 0, s, x, dy,
-             ws, N, C, ldy, Cg, Cog, npairs, nci_b, nco_b, per, nstages);
-  const long threads = static_cast<long>(npairs) * G::NACC * 64;
-  CXN_LAUNCH((conv_wgrad_direct_reduce<G::T>), dim3(static_cast<unsigned>((threads + 255) / 256)), dim3(256), 0, s, ws,
-             dw, S, npairs, nci_b, nco_b, Cg, Cog, alpha);
+             ws, N, C, ldy, Cg, Cog, npairs, nci_b, nco_b, per, nstages, db != nullptr ? 1 : 0);
+  const long blocks = (static_cast<long>(npairs) * G::NACC * 64 + 255) / 256 + (db != nullptr ? (npairs / nci_b + 3) / 4 : 0);
+  CXN_LAUNCH((conv_wgrad_direct_reduce<G::T>), dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, ws, dw, db, S,
+             npairs, nci_b, nco_b, Cg, Cog, alpha);
   return 0;
 }
 
@@ -405,7 +471,7 @@ long ws_wd(int N, int Cg, int Cog, int groups, int splits) {
   S = S < 1 ? 1 : (S > nstages ? nstages : S);
   const int per = (nstages + S - 1) / S;
   S = (nstages + per - 1) / per;
-  return static_cast<long>(S) * npairs * G::NACC * 256;
+  return static_cast<long>(S) * npairs * (G::NACC * 256 + 64);
 }
 
 }  // namespace
@@ -414,18 +480,20 @@ long ws_wd(int N, int Cg, int Cog, int groups, int splits) {
 // group a multiple of 32, output channels per group a multiple of 64; x / dy pixel strides (C,
 // ldy) multiples of 8.  ws == nullptr: returns the workspace size in floats (0: not served).
 // Otherwise launches the kernel and the split reduction into dw (fp32 [Cout][K][K][Cg], +=
-// alpha * gradient); -1 when not served, -4 when ws is too small.
-CXN_API long cxn_conv_wgrad_direct(const void *x, const void *dy, float *dw, float *ws, long ws_floats, int N, int H,
+// alpha * gradient) and, when db is given, the bias gradient (fp32 [Cout], += alpha * sum of dy
+// over pixels); -1 when not served, -4 when ws is too small.
+CXN_API long cxn_conv_wgrad_direct(const void *x, const void *dy, float *dw, float *db, float *ws, long ws_floats,
+                                   int N, int H,
                                    int W, int C, int ldy, int Cg, int Cog, int groups, int KH, int KW, int pad_h,
                                    int pad_w, int stride, int splits, float alpha, void *stream) {
   if (stride != 1 || KH != KW || pad_h != pad_w || pad_h != (KH - 1) / 2) return ws ? -1 : 0;
   if (Cg % 32 || Cog % 64 || C % 8 || ldy % 8 || groups < 1 || C < groups * Cg || ldy < groups * Cog) return ws ? -1 : 0;
   if (static_cast<long>(N) * H * W * (C > ldy ? C : ldy) >= (1L << 30)) return ws ? -1 : 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const bf16_t *xb = static_cast<const bf16_t *>(x), *db = static_cast<const bf16_t *>(dy);
+  const bf16_t *xb = static_cast<const bf16_t *>(x), *dyb = static_cast<const bf16_t *>(dy);
   if (KH == 3 && H == 13 && W == 13) {
     if (!ws) return ws_wd<13, 13, 3, 2>(N, Cg, Cog, groups, splits);
-    const int rc = launch_wd<13, 13, 3, 2>(xb, db, dw, ws, ws_floats, N, C, ldy, Cg, Cog, groups, splits, alpha, s);
+    const int rc = launch_wd<13, 13, 3, 2>(xb, dyb, dw, db, ws, ws_floats, N, C, ldy, Cg, Cog, groups, splits, alpha, s);
     if (rc != 0) return rc;
     return hipGetLastError() == hipSuccess ? 0 : -3;
   }

@@ -1394,8 +1394,13 @@ __global__ void splitk_accumulate(const float *__restrict__ ws, int nsplit, long
   }
 }
 
+__device__ __forceinline__ uint32_t hash_u32(uint32_t x, uint32_t seed);
+// DROP: the dropout layer behind a fused fc -> relu is applied here as well (keep iff
+// hash(seed, flat index) < thresh, kept values * scale), with dropout_apply's mask
+template <bool DROP>
 __global__ void splitk_finalize(const float *__restrict__ ws, int nsplit, long slab, bf16_t *out, long rows,
-                                int cols, const float *__restrict__ bias, int relu, int mask_relu) {
+                                int cols, const float *__restrict__ bias, int relu, int mask_relu, uint32_t seed0,
+                                const int *counter, uint32_t thresh, float scale) {
   // grid: blockIdx.y = row, x over 8-column groups (no 64-bit division per element)
   {
     const long r = blockIdx.y;
@@ -1420,6 +1425,12 @@ __global__ void splitk_finalize(const float *__restrict__ ws, int nsplit, long s
       if (bias) f[e] += bias[c0 + e];
       if (relu) f[e] = fmaxf(f[e], 0.f);
       if (mask_relu && !(old[e] > 0.f)) f[e] = 0.f;
+    }
+    if constexpr (DROP) {
+      const uint32_t seed = counter ? hash_u32(static_cast<uint32_t>(*counter), seed0) : seed0;
+      const uint32_t i0 = static_cast<uint32_t>(r * cols + c0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = hash_u32(i0 + e, seed) < thresh ? f[e] * scale : 0.f;
     }
     *reinterpret_cast<uint4 *>(dst) = pack8(f);
   }
@@ -2109,7 +2120,20 @@ CXN_API int cxn_splitk_finalize(const float *ws, int nsplit, long slab, void *ou
                                 const float *bias, int relu, int mask_relu, void *stream) {
   if (cols % 8) return -2;
   dim3 grid(cdiv(cols / 8, NT), static_cast<unsigned>(rows));
-  CXN_LAUNCH((splitk_finalize), grid, NT, 0, S_, ws, nsplit, slab, (bf16_t *)out, rows, cols, bias, relu, mask_relu);
+  CXN_LAUNCH((splitk_finalize<false>), grid, NT, 0, S_, ws, nsplit, slab, (bf16_t *)out, rows, cols, bias, relu,
+             mask_relu, 0u, (const int *)nullptr, 0u, 1.f);
+  RET;
+}
+// the same with the dropout of a fused fc -> relu -> dropout (mask as cxn_dropout)
+CXN_API int cxn_splitk_finalize_dropout(const float *ws, int nsplit, long slab, void *out, long rows, int cols,
+                                        const float *bias, int relu, unsigned seed, const int *counter, float pkeep,
+                                        void *stream) {
+  if (cols % 8 || static_cast<double>(rows) * cols >= 4294967296.0) return -2;
+  dim3 grid(cdiv(cols / 8, NT), static_cast<unsigned>(rows));
+  const double t = static_cast<double>(pkeep) * 4294967296.0;  // as cxn_dropout
+  const uint32_t thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : static_cast<uint32_t>(t);
+  CXN_LAUNCH((splitk_finalize<true>), grid, NT, 0, S_, ws, nsplit, slab, (bf16_t *)out, rows, cols, bias, relu, 0,
+             static_cast<uint32_t>(seed), counter, thresh, 1.f / pkeep);
   RET;
 }
 CXN_API int cxn_cast_f32_bf16(const float *x, void *y, long n, void *stream) {

@@ -42,6 +42,8 @@ class FullConnectLayer(Layer):
         super().__init__(ctx)
         self.fullc_gather = -1  # 1 on, 0 off, -1 auto (_gathering)
         self.fuse_relu = False
+        self.fuse_dropout = None  # the DropoutLayer behind a fused relu (NeuralNet._fuse_dropout)
+        self.grad_alpha = 1.0     # data-gradient scale: 1 / pkeep of a fused dropout in front
         self._dx = None
         self._rows = 0
         self._gbuf = {}      # persistent gather sources / outputs (graph-capturable)
@@ -149,7 +151,9 @@ class FullConnectLayer(Layer):
             def gather_x():
                 self._xwork = dist.all_gather_into_tensor(out, src, async_op=True)
             self._collective(gather_x)
-        ops.fc_forward(x, self.w.wb, bias, nodes_out[0].mat(), relu=self.fuse_relu)
+        d = self.fuse_dropout
+        drop = (d.seed, self.ctx.step_counter, 1.0 - d.threshold) if (d is not None and is_train) else None
+        ops.fc_forward(x, self.w.wb, bias, nodes_out[0].mat(), relu=self.fuse_relu, drop=drop)
 
     def _fused_sgd(self, x, dy, prop_grad, nodes_in, xw=None, dyw=None) -> bool:
         """SGD step of the weights fused into the weight-gradient GEMM (ctx.sgd_fuse = the
@@ -182,7 +186,8 @@ class FullConnectLayer(Layer):
                 self._xs = torch.empty_like(x)
             ops.copy_(self._xs, x)  # a library copy: recorded launch lists repeat it
             if prop_grad:
-                ops.fc_backward_data(dy, spec.wb, nodes_in[0].gmat(), mask_relu=self.grad_mask_relu)
+                ops.fc_backward_data(dy, spec.wb, nodes_in[0].gmat(), mask_relu=self.grad_mask_relu,
+                                     alpha=self.grad_alpha)
             ready = torch.cuda.Event()
             ready.record()
             side.wait_event(ready)
@@ -205,7 +210,7 @@ class FullConnectLayer(Layer):
             if self._dx is None or self._dx.shape[0] < x.shape[0] or self._dx.shape[1] != x.shape[1]:
                 self._dx = torch.empty_like(x)
             gx = self._dx[:x.shape[0]]
-            ops.fc_backward_data(dy, spec.wb, gx)
+            ops.fc_backward_data(dy, spec.wb, gx, alpha=self.grad_alpha)
         xg, dyg = (x, dy) if xw is None else (xw, dyw)
         if ops.fc_backward_weight_sgd(xg, dyg, spec.w, m, spec.wb, lr, wd, mom, clip, hyp):
             upd.fused_offsets.add(spec.offset)
@@ -245,7 +250,8 @@ class FullConnectLayer(Layer):
         if self.b is not None:
             self.ctx.bias_grad(dy, self.b.g)
         if prop_grad:
-            ops.fc_backward_data(dy, self.w.wb, nodes_in[0].gmat(), mask_relu=self.grad_mask_relu)
+            ops.fc_backward_data(dy, self.w.wb, nodes_in[0].gmat(), mask_relu=self.grad_mask_relu,
+                                 alpha=self.grad_alpha)
 
     def save_model(self, fo: BinWriter):
         fo.write(self.lp.to_bytes())
@@ -397,10 +403,11 @@ class ConvolutionLayer(Layer):
         self.geo.N = x.shape[0]
         xw, geo = self._padded(x, getattr(self, "_xpad_stale", False))
         self._xpad_stale = False
-        ops.conv_backward_weight(xw, dy, self.w.g, geo)
+        want_db = self.b is not None and not self.bias_done and self.ctx.is_gpu
+        db_done = ops.conv_backward_weight(xw, dy, self.w.g, geo, db=self.b.g if want_db else None)
         if self.bias_done:  # summed by the max-pool behind this conv (NeuralNet._fuse_pool_bias)
             self.bias_done = False
-        elif self.b is not None:
+        elif self.b is not None and not db_done:  # (db_done: summed by the weight-gradient kernel)
             self.ctx.bias_grad(_pixel_rows(dy), self.b.g)
         if prop_grad:
             ready = self.ctx.flipped is not None and id(self) in self.ctx.flipped
@@ -639,13 +646,15 @@ class DropoutLayer(Layer):
         _check(nodes_in[0] is nodes_out[0], "DropoutLayer is an self-loop Layer")
         _check(0.0 <= self.threshold < 1.0, "DropoutLayer: invalid dropout threshold")
 
+    fused_into_producer = False  # NeuralNet._fuse_dropout: the fc around it applies the mask
+
     def forward(self, is_train, nodes_in, nodes_out):
-        if is_train and self.threshold > 0:
+        if is_train and self.threshold > 0 and not self.fused_into_producer:
             x = nodes_in[0].data
             ops.dropout_apply(x, x, self.seed, 1.0 - self.threshold, self.ctx.step_counter)
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
-        if self.threshold > 0:
+        if self.threshold > 0 and not self.fused_into_producer:
             x = nodes_in[0].data
             ops.dropout_apply(x, x, self.seed, 1.0 - self.threshold, self.ctx.step_counter)
 

@@ -90,6 +90,7 @@ _SIGS = {
     "cxn_ins_pool_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _U, _P, _P],
     "cxn_ins_pool_bwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _U, _P, _P],
     "cxn_splitk_finalize": [_P, _I, _L, _P, _L, _I, _P, _I, _I, _P],
+    "cxn_splitk_finalize_dropout": [_P, _I, _L, _P, _L, _I, _P, _I, _U, _P, _F, _P],
     "cxn_splitk_accumulate": [_P, _I, _L, _P, _P],
     "cxn_set_deterministic": [_I],
     "cxn_pool_bwd_tie_all": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
@@ -129,7 +130,7 @@ _SIGS = {
     "cxn_rec_replay_many": [_P, _I, _P],
     "cxn_rec_free": [_P],
     "cxn_copy_d2d": [_P, _P, _L, _P],
-    "cxn_conv_wgrad_direct": [_P, _P, _P, _P, _L] + [_I] * 14 + [_F, _P],
+    "cxn_conv_wgrad_direct": [_P, _P, _P, _P, _P, _L] + [_I] * 14 + [_F, _P],
 }
 _RESTYPE = {"cxn_rec_end": ctypes.c_void_p, "cxn_rec_free": None, "cxn_conv_wgrad_direct": ctypes.c_long}
 

@@ -189,10 +189,28 @@ class NeuralNet:
             conn.layer.fused_into_producer = True
             cj.layer.grad_mask_relu = True
             self.aliases[id(b)] = a
+            self._fuse_dropout(p, [self.connections[k] for k in loops], cj)
+
         self._fuse_concat(producers, consumers)
         self._fuse_split(producers, consumers)
         self._fuse_pool_bias(producers, consumers)
         self._fuse_dgrad_bias(producers, consumers)
+
+    def _fuse_dropout(self, p, loops, cj):
+        """fc -> relu -> dropout -> fc (AlexNet fc6 / fc7): the producer's forward applies the
+        dropout mask on the way out (the split-K finalize, ops.fc_forward(drop=...)) and the
+        consumer's data-gradient scales by 1 / pkeep: the stored activation is relu(z) * mask /
+        pkeep, so the relu'-mask the consumer already applies (old value > 0) is exactly the
+        dropout mask as well -- the dropout layer launches nothing in either direction.
+        CXXNET_FUSE_DROPOUT=0 keeps the separate dropout kernels."""
+        if os.environ.get("CXXNET_FUSE_DROPOUT", "1") == "0" or len(loops) != 1:
+            return
+        d = loops[0]
+        if p.type != K_FULLC or cj.type != K_FULLC or d.shared or not 0.0 < d.layer.threshold < 1.0:
+            return
+        p.layer.fuse_dropout = d.layer
+        cj.layer.grad_alpha = 1.0 / (1.0 - d.layer.threshold)
+        d.layer.fused_into_producer = True
 
     def _fuse_dgrad_bias(self, producers, consumers):
         """Bias gradient of a conv whose output (through a fused relu) is read by one other conv

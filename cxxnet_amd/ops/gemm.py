@@ -441,41 +441,67 @@ def _effective_split(kdim, split):
     return -(-kt // per)
 
 
-def _gemm_bf16_out(a, b, amode, bmode, out, ldc, *, bias=None, relu=False, mask_relu=False):
-    """out (bf16, [rows_j][ldc]) = epilogue(A . B) for a single-group GEMM, with split-K
+def _finalize(ws, split, slab, out, rows, ldc, bias, relu, mask_relu, drop):
+    """out = epilogue(sum of the split-K fp32 slabs); drop = (seed, counter, pkeep): the dropout
+    of a fused fc -> relu -> dropout applied on the way out (same mask as ops.dropout_apply)."""
+    k = native.kernels()
+    bp = bias.data_ptr() if bias is not None else None
+    if drop is not None:
+        seed, counter, pkeep = drop
+        native.check(k.cxn_splitk_finalize_dropout(ws.data_ptr(), split, slab, out.data_ptr(), rows, ldc, bp, int(relu),
+                                                   seed & 0xFFFFFFFF,
+                                                   counter.data_ptr() if counter is not None else None,
+                                                   float(pkeep), _stream()), "splitk_finalize_dropout")
+        return
+    native.check(k.cxn_splitk_finalize(ws.data_ptr(), split, slab, out.data_ptr(), rows, ldc, bp, int(relu),
+                                       int(mask_relu), _stream()), "splitk_finalize")
+
+
+def _gemm_bf16_out(a, b, amode, bmode, out, ldc, *, bias=None, relu=False, mask_relu=False, alpha=1.0,
+                   drop=None) -> bool:
+    """out (bf16, [rows_j][ldc]) = epilogue(alpha * A . B) for a single-group GEMM, with split-K
     through fp32 slabs + one finalize pass when the output tile grid is too small to
-    fill the chip (the FC layers at batch 256: 64 tiles of 128x128 for fc6)."""
+    fill the chip (the FC layers at batch 256: 64 tiles of 128x128 for fc6).  drop: see
+    _finalize; returns True when the dropout was applied (only the split-K path fuses it)."""
     # fc data-grad (A MN-major) stays on the register-staged kernel: its LDS-DMA form measured
     # slower on AlexNet's fc6-8 (profiles/r14_glds_tiles.jsonl)
-    if bmode == DIRECT_K and amode == DIRECT_K and _use("fc") and \
-            _fc_glds(a, b, GL_K, out, ldc, bias, relu, mask_relu):
-        return
+    if bmode == DIRECT_K and amode == DIRECT_K and alpha == 1.0 and _use("fc"):
+        r = _fc_glds(a, b, GL_K, out, ldc, bias, relu, mask_relu, drop)
+        if r is not None:
+            return r
     tile = _pick(FC_TILES, a.rows, b.rows, 1, min_blocks=1)
     split = _auto_split(a.rows, b.rows, 1, a.kdim, tile, min_ktiles=8)
     if split > 1 and a.kdim >= 2048 and ldc % 8 == 0 and ldc == a.rows:
         split = _effective_split(a.kdim, split)
         slab = b.rows * ldc
         ws = torch.empty((split, slab), dtype=torch.float32, device=out.device)
-        _gemm(a, b, amode, bmode, 8, 8, ws, 0, ldc, epi=EPI_F32, ksplit=split, tile=tile, kstride=slab)
-        native.check(native.kernels().cxn_splitk_finalize(
-            ws.data_ptr(), split, slab, out.data_ptr(), b.rows, ldc,
-            bias.data_ptr() if bias is not None else None, int(relu), int(mask_relu), _stream()), "splitk_finalize")
-        return
-    _gemm(a, b, amode, bmode, 8, 8, out, 0, ldc, bias=bias, relu=relu, mask_relu=mask_relu, epi=EPI_BF16,
+        _gemm(a, b, amode, bmode, 8, 8, ws, 0, ldc, alpha=alpha, epi=EPI_F32, ksplit=split, tile=tile, kstride=slab)
+        _finalize(ws, split, slab, out, b.rows, ldc, bias, relu, mask_relu, drop)
+        return drop is not None
+    _gemm(a, b, amode, bmode, 8, 8, out, 0, ldc, alpha=alpha, bias=bias, relu=relu, mask_relu=mask_relu, epi=EPI_BF16,
           tile=tile)
+    return False
 
 
-def _fc_glds(a, b, amode, out, ldc, bias, relu, mask_relu) -> bool:
-    """fc forward (A = W, K-major) / data-grad (A = W, MN-major) on the LDS-DMA kernel."""
+def _fc_glds(a, b, amode, out, ldc, bias, relu, mask_relu, drop=None):
+    """fc forward (A = W, K-major) / data-grad (A = W, MN-major) on the LDS-DMA kernel.  None
+    when the kernel does not serve the shape; else whether the dropout (drop) was applied."""
     key = ("fc", amode, a.rows, b.rows, a.kdim, ldc)
-    run = lambda t, o: _fc_glds_tile(a, b, amode, o, ldc, bias, relu, mask_relu, t)  # noqa: E731
+    got = {}
+
+    def run(t, o):
+        r = _fc_glds_tile(a, b, amode, o, ldc, bias, relu, mask_relu, t, drop)
+        got["drop"] = r == 2
+        return bool(r)
     tile = _tuned_tile(key, run, out, lambda: 1 if amode == GL_MN else _pick_glds(a.rows, b.rows, 1))
-    return run(tile, out)
+    if not run(tile, out):
+        return None
+    return got["drop"]
 
 
-def _fc_glds_tile(a, b, amode, out, ldc, bias, relu, mask_relu, tile) -> bool:
+def _fc_glds_tile(a, b, amode, out, ldc, bias, relu, mask_relu, tile, drop=None) -> int:
     """split-K through fp32 slabs when the output tile grid cannot fill the chip (fc6 at
-    batch 256: 32 tiles of 128x256)."""
+    batch 256: 32 tiles of 128x256).  0: not served, 1: done, 2: done with the dropout."""
     bm, bn = GLDS_TILES[tile]
     tiles = _cdiv(a.rows, bm) * _cdiv(b.rows, bn)
     ktiles = _cdiv(a.kdim, 64)
@@ -485,12 +511,10 @@ def _fc_glds_tile(a, b, amode, out, ldc, bias, relu, mask_relu, tile) -> bool:
         slab = b.rows * ldc
         ws = torch.empty((split, slab), dtype=torch.float32, device=out.device)
         if not _glds(a, b, amode, GL_K, ws, 0, ldc, epi=EPI_F32, ksplit=split, kstride=slab, tile=tile):
-            return False
-        native.check(native.kernels().cxn_splitk_finalize(
-            ws.data_ptr(), split, slab, out.data_ptr(), b.rows, ldc,
-            bias.data_ptr() if bias is not None else None, int(relu), int(mask_relu), _stream()), "splitk_finalize")
-        return True
-    return _glds(a, b, amode, GL_K, out, 0, ldc, bias=bias, relu=relu, mask_relu=mask_relu, tile=tile)
+            return 0
+        _finalize(ws, split, slab, out, b.rows, ldc, bias, relu, mask_relu, drop)
+        return 2 if drop is not None else 1
+    return int(_glds(a, b, amode, GL_K, out, 0, ldc, bias=bias, relu=relu, mask_relu=mask_relu, tile=tile))
 
 
 def _auto_split(rows_i, rows_j, groups, kdim, tile=0, target=2 * NUM_CU, min_ktiles=4):
@@ -759,9 +783,10 @@ def _wgd_workspace(n, device):
     return buf
 
 
-def conv_wgrad_direct(x, dy, dw, g: ConvGeom, splits: int = 0) -> bool:
-    """dw += the weight gradient on the direct small-map kernel; False when it does not serve
-    the shape (or is switched off)."""
+def conv_wgrad_direct(x, dy, dw, g: ConvGeom, splits: int = 0, db=None) -> bool:
+    """dw += the weight gradient on the direct small-map kernel (and db += the bias gradient,
+    the sum of dy over pixels, when db is given); False when it does not serve the shape (or is
+    switched off)."""
     if _WGD == "0" or _glds_cfg["tile"] >= 0 or not _native_t(x) or g.Ho != g.H or g.Wo != g.W:
         return False  # (a forced LDS-DMA tile id means a test / probe wants that kernel)
     if not (x.is_contiguous() or x.stride(-1) == 1) or dy.stride(-1) != 1:
@@ -769,20 +794,22 @@ def conv_wgrad_direct(x, dy, dw, g: ConvGeom, splits: int = 0) -> bool:
     k = native.kernels()
     args = (g.N, g.H, g.W, _pix(x), _pix(dy), g.cg_in, g.cg_out, g.groups, g.KH, g.KW, g.pad_y, g.pad_x, g.stride,
             int(splits))
-    need = int(k.cxn_conv_wgrad_direct(None, None, None, None, 0, *args, 1.0, None))
+    need = int(k.cxn_conv_wgrad_direct(None, None, None, None, None, 0, *args, 1.0, None))
     if need <= 0:
         return False
     ws = _wgd_workspace(need, dw.device)
-    rc = int(k.cxn_conv_wgrad_direct(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), ws.data_ptr(), ws.numel(), *args,
-                                     1.0, _stream()))
+    rc = int(k.cxn_conv_wgrad_direct(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), db.data_ptr() if db is not None else None,
+                                     ws.data_ptr(), ws.numel(), *args, 1.0, _stream()))
     if rc == -1:
         return False
     native.check(rc, "conv_wgrad_direct")
     return True
 
 
-def conv_backward_weight(x, dy, dw, g: ConvGeom):
-    """dw += sum over pixels of dy (x) im2col(x).  dw fp32 [Cout][KH][KW][Cg].
+def conv_backward_weight(x, dy, dw, g: ConvGeom, db=None) -> bool:
+    """dw += sum over pixels of dy (x) im2col(x).  dw fp32 [Cout][KH][KW][Cg].  db (fp32 [Cout],
+    optional): the kernel may also add the bias gradient (sum of dy over pixels); returns True
+    when it did (else the caller sums dy itself).
     (Folding the bias gradient into this GEMM was measured a wash on GoogLeNet and its
     extra registers slowed every weight-grad kernel by 5-25%: profiles/r2_inception_bias_fold.md,
     profiles/r2_ab_bias_fold_regression.md.)"""
@@ -816,8 +843,8 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
         key = ("cws", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
         return reg_run(_tuned_tile(key, reg_run, o, reg_default, cands=_wgrad_cands(kd, g.cg_out, g.groups, P)), o)
     rowrun = va != 8 and rowrun_ok(g)
-    if conv_wgrad_direct(x, dy, dw, g):  # deterministic as well: no atomics, fixed split order
-        return
+    if conv_wgrad_direct(x, dy, dw, g, db=db):  # deterministic as well: no atomics, fixed split order
+        return db is not None
     if _DET["on"] and not (rowrun and cg % va):
         # one fp32 slab per K slice, summed in slice order into dw: bitwise reproducible
         tile = _pick(WGRAD_TILES, kd, g.cg_out, g.groups, min_blocks=1)
@@ -882,8 +909,10 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom):
 
 
 # ----------------------------------------------------------------------------- fully connected
-def fc_forward(x, w, bias, y, relu=False, out_fp32=False):
-    """y[B][nout] = x[B][nin] . w[nout][nin]^T + bias."""
+def fc_forward(x, w, bias, y, relu=False, out_fp32=False, drop=None):
+    """y[B][nout] = x[B][nin] . w[nout][nin]^T + bias.  drop = (seed, counter, pkeep): then
+    y = dropout(y) as ops.dropout_apply(y, y, seed, pkeep, counter) (fused into the split-K
+    finalize where the GEMM takes that path)."""
     if not _native_t(x):
         out = x @ w.t()
         if bias is not None:
@@ -891,6 +920,9 @@ def fc_forward(x, w, bias, y, relu=False, out_fp32=False):
         if relu:
             out = out.clamp_min(0)
         y.copy_(out)
+        if drop is not None:
+            from .nn import dropout_apply
+            dropout_apply(y, y, drop[0], drop[2], drop[1])
         return
     Bn, nin = x.shape
     nout = w.shape[0]
@@ -898,14 +930,22 @@ def fc_forward(x, w, bias, y, relu=False, out_fp32=False):
     Bo = _op(x, 0, nin, Bn, nin)
     if out_fp32:
         _gemm(A, Bo, DIRECT_K, DIRECT_K, 8, 8, y, 0, nout, bias=bias, relu=relu, epi=EPI_F32)
+        done = False
     else:
-        _gemm_bf16_out(A, Bo, DIRECT_K, DIRECT_K, y, nout, bias=bias, relu=relu)
+        done = _gemm_bf16_out(A, Bo, DIRECT_K, DIRECT_K, y, nout, bias=bias, relu=relu, drop=drop)
+    if drop is not None and not done:
+        from .nn import dropout_apply
+        dropout_apply(y, y, drop[0], drop[2], drop[1])
 
 
-def fc_backward_data(dy, w, dx, mask_relu=False):
-    """dx[B][nin] = dy[B][nout] . w[nout][nin]  (mask_relu: see conv_backward_data)."""
+def fc_backward_data(dy, w, dx, mask_relu=False, alpha=1.0):
+    """dx[B][nin] = alpha * dy[B][nout] . w[nout][nin]  (mask_relu: see conv_backward_data;
+    with the dropout of a fused fc -> relu -> dropout in front, alpha = 1 / pkeep: dx already
+    holds the dropped-out activation, so relu'-masking by it applies the dropout mask too)."""
     if not _native_t(dy):
         out = dy @ w
+        if alpha != 1.0:
+            out = out * alpha
         if mask_relu:
             out = out * (dx > 0).to(out.dtype)
         dx.copy_(out)
@@ -914,7 +954,7 @@ def fc_backward_data(dy, w, dx, mask_relu=False):
     nin = w.shape[1]
     A = _op(w, 0, nin, nin, nout)
     Bo = _op(dy, 0, nout, Bn, nout)
-    _gemm_bf16_out(A, Bo, DIRECT_MN, DIRECT_K, dx, nin, mask_relu=mask_relu)
+    _gemm_bf16_out(A, Bo, DIRECT_MN, DIRECT_K, dx, nin, mask_relu=mask_relu, alpha=alpha)
 
 
 def fc_backward_weight_sgd(x, dy, w, m, wb, lr, wd, mom, clip, hyp=None) -> bool:

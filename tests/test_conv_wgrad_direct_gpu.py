@@ -19,6 +19,7 @@ CASES = [
     (7, 64, 64, 1, 3),     # one channel pair, forced splits over 4 stages
     (2, 32, 128, 1, 1),    # two co blocks, one split
     (32, 256, 384, 1, 0),  # the per-GPU batch of 8-GPU strong scaling
+    (4, 64, 192, 1, 2),    # three co blocks, 2 ci blocks: bias K-steps k % 2 per ci block
 ]
 
 
@@ -44,15 +45,23 @@ def test_wgrad_direct(case):
     x = _rnd((N, 13, 13, C), 1)
     dy = _rnd((N, 13, 13, Cout), 2)
     dw = torch.full((Cout, 3, 3, C // groups), 0.5, device=DEV)
-    assert gemm.conv_wgrad_direct(x, dy, dw, g, splits=splits)
+    db = torch.full((Cout,), 0.25, device=DEV)
+    assert gemm.conv_wgrad_direct(x, dy, dw, g, splits=splits, db=db)
     torch.cuda.synchronize()
     got = (dw - 0.5).permute(0, 3, 1, 2)
     err = _err(got, _ref(x, dy, groups))
     assert err < 1e-5, err  # fp32 accumulation of bf16 products: only the summation order differs
+    dbref = dy.float().sum((0, 1, 2))
+    assert _err(db - 0.25, dbref) < 1e-5
     dw2 = torch.full_like(dw, 0.5)
-    assert gemm.conv_wgrad_direct(x, dy, dw2, g, splits=splits)
+    db2 = torch.full_like(db, 0.25)
+    assert gemm.conv_wgrad_direct(x, dy, dw2, g, splits=splits, db=db2)
     torch.cuda.synchronize()
-    assert torch.equal(dw, dw2)  # fixed split order, no atomics
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)  # fixed split order, no atomics
+    dw3 = torch.full_like(dw, 0.5)
+    assert gemm.conv_wgrad_direct(x, dy, dw3, g, splits=splits)  # without the bias: same dW
+    torch.cuda.synchronize()
+    assert torch.equal(dw, dw3)
 
 
 def test_wgrad_direct_dy_slice_and_accumulate():

@@ -403,3 +403,46 @@ def test_rand_fill_host_statistics_and_determinism():
     assert abs(a.mean().item()) < 3e-4 and abs(a.std().item() / 0.02 - 1) < 1e-2
     u = rand_fill(torch.empty(100000), 7, "uniform", -1.0, 1.0)
     assert u.min().item() >= -1.0 and u.max().item() < 1.0 and abs(u.mean().item()) < 1e-2
+
+
+DROP_NET = """
+netconfig=start
+layer[0->1] = flatten
+layer[1->2] = fullc:f1
+  nhidden = 24
+layer[2->3] = relu
+layer[3->3] = dropout
+  threshold = 0.5
+layer[3->4] = fullc:f2
+  nhidden = 16
+layer[4->5] = relu
+layer[5->5] = dropout
+  threshold = 0.25
+layer[5->6] = fullc:f3
+  nhidden = 5
+layer[6->6] = softmax
+netconfig=end
+input_shape = 2,3,4
+"""
+
+
+def test_fused_fc_relu_dropout_matches_unfused(monkeypatch):
+    """NeuralNet._fuse_dropout: the fc forward applies the dropout mask and the next fc's
+    data-gradient scales by 1 / pkeep under the relu'-mask -- the same gradients as the
+    separate relu and dropout layers (CPU executor with fusion forced on, CXXNET_FUSE=2)."""
+    B = 6
+    x = torch.randn(B, 2, 3, 4)
+    y = torch.randint(0, 5, (B, 1)).float()
+    out = {}
+    for mode in ("0", "2"):
+        monkeypatch.setenv("CXXNET_FUSE", mode)
+        torch.manual_seed(0)
+        tr = make(DROP_NET, B, [("seed", "7")])
+        if mode == "2":
+            fused = [c.layer for c in tr.net.connections if type(c.layer).__name__ == "DropoutLayer"]
+            assert all(d.fused_into_producer for d in fused)
+        out[mode] = grads_of(tr, x, y)
+        out[mode + "p"] = tr.net.nodes[-1].data.clone()
+    for k in out["0"]:
+        assert torch.allclose(out["0"][k], out["2"][k], rtol=1e-5, atol=1e-6), k
+    assert torch.allclose(out["0p"], out["2p"], rtol=1e-5, atol=1e-6)
