@@ -324,7 +324,7 @@ int launch_halo(const GOperand &A, const GOperand &B, const GEpi &E, hipStream_t
   return 0;
 }
 
-// Persistent form for ONE output-channel block (tiles 132-133: VGG conv1_2 forward / data-
+// Persistent form for ONE output-channel block (tile 133: VGG conv1_2 forward / data-
 // gradient, conv2_1 forward, conv2_2).  With one or two channel blocks the kernel above stages
 // its first halo, runs its K-tiles and writes out with nothing overlapping the first halo's HBM
 // fetch or the epilogue inside the block; conv1_2 ran at ~590 TFLOP/s against ~1,000 for the
@@ -447,20 +447,6 @@ conv_halo_ps(GOperand A, GOperand B, GEpi E, int tiles_w, int tiles_h, uint32_t 
   for (int f = 0; f < NF; ++f) read_frag(0, f, 0, 0, 0, 0);
   __builtin_amdgcn_sched_barrier(0);
 
-  // BM = 64 (one half): the epilogue's 8 row-segment stores per lane are deferred into taps 0-3 of
-  // the next item, two per tap after that tap's DMAs, as fixed-count buffer stores (OOB = dropped)
-  // counted in the waits -- a store ahead of a DMA would make every later wait for that DMA wait
-  // for the store as well (vmcnt retires in issue order); past the last item they are flushed
-  constexpr bool DEFER = NR == 4;
-  const rsrc_t ro = make_rsrc(E.out, 0x80000000u);
-  uint4 pq[8];
-  uint32_t poff[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    pq[k] = make_uint4(0, 0, 0, 0);
-    poff[k] = OOB;
-  }
-  typedef int v4i __attribute__((ext_vector_type(4)));
   int hb = 0, cb = 0;
   uint32_t tn = t;
   int h0n = h0, w0n = w0, imgn = img;
@@ -496,7 +482,6 @@ conv_halo_ps(GOperand A, GOperand B, GEpi E, int tiles_w, int tiles_h, uint32_t 
       constexpr int tap = decltype(tc)::value;
       constexpr int st = tap % 3;
       constexpr int NQ = NA + (tap < 7 ? NHK : 0);
-      constexpr int ST = (DEFER && tap < 4) ? 2 : 0, STP = (DEFER && tap >= 1 && tap < 5) ? 2 : 0;
       wait_lgkm_h<0>();
       __builtin_amdgcn_sched_barrier(0);
       static_for<PER>([&](auto uc) {
@@ -504,11 +489,6 @@ conv_halo_ps(GOperand A, GOperand B, GEpi E, int tiles_w, int tiles_h, uint32_t 
         if constexpr (u == 0) {  // weights of K-tile t + 2: this item's, or taps 0-1 of the next
           if constexpr (tap + 2 < 9) issue_A(true, cb, tap + 2, (tap + 2) % 3);
           else issue_A(more, cbn, tap + 2 - 9, (tap + 2) % 3);
-        }
-        if constexpr (ST > 0 && u == PER - 1) {  // the previous patch's stores, after this tap's DMAs
-#pragma unroll
-          for (int k = 2 * tap; k < 2 * tap + 2; ++k)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, pq[k]), ro, poff[k], 0, 0);
         }
         static_for<NHK>([&](auto jc) {
           constexpr int j = decltype(jc)::value;
@@ -526,7 +506,7 @@ conv_halo_ps(GOperand A, GOperand B, GEpi E, int tiles_w, int tiles_h, uint32_t 
         __builtin_amdgcn_sched_barrier(0);
       });
       wait_lgkm_h<0>();
-      wait_vmcnt<NQ + ST + STP>();  // all but this tap's DMAs and the stores after the last waited DMA
+      wait_vmcnt<NQ>();  // all but this tap's DMAs
       block_barrier();
       static_for<PER>([&](auto uc) {
         constexpr int u = decltype(uc)::value;
@@ -608,17 +588,9 @@ conv_halo_ps(GOperand A, GOperand B, GEpi E, int tiles_w, int tiles_h, uint32_t 
             }
           }
         }
-        if constexpr (DEFER) {
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            pq[k] = q[k];
-            poff[k] = row[k] >= 0 ? static_cast<uint32_t>(row[k] * 2) : OOB;
-          }
-        } else {
-#pragma unroll
-          for (int k = 0; k < 8; ++k)
-            if (row[k] >= 0) *reinterpret_cast<uint4 *>(out + row[k]) = q[k];
-        }
+        for (int k = 0; k < 8; ++k)
+          if (row[k] >= 0) *reinterpret_cast<uint4 *>(out + row[k]) = q[k];
       });
       block_barrier();  // staging reads done before the item after next streams into this buffer
       if (!more) break;
@@ -631,10 +603,6 @@ conv_halo_ps(GOperand A, GOperand B, GEpi E, int tiles_w, int tiles_h, uint32_t 
     }
     cb = cbn;
     hb ^= 1;
-  }
-  if constexpr (DEFER) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, pq[k]), ro, poff[k], 0, 0);
   }
   wait_vmcnt<0>();
 }
@@ -655,8 +623,6 @@ int launch_halo_ps(const GOperand &A, const GOperand &B, const GEpi &E, hipStrea
   const int tiles_w = cdiv(B.W, WT), tiles_h = cdiv(B.H, HaloCfg<BM, WT, true>::R);
   const long nt = static_cast<long>(tiles_w) * tiles_h * N;
   if (nt >= (1L << 31)) return -1;
-  // BM = 64 defers its stores as buffer stores with 32-bit byte offsets (OOB = 2^31)
-  if (HaloCfg<BM, WT, true>::NR == 4 && static_cast<long>(N) * B.H * B.W * E.ldc * 2 >= (1L << 31)) return -1;
   // one block per CU, a multiple of 8 (one share per XCD), no more than 8 x the patches per XCD
   long g = num_cu_h() / 8 * 8;
   const long per_xcd = (nt + 7) / 8;
@@ -670,8 +636,8 @@ int launch_halo_ps(const GOperand &A, const GOperand &B, const GEpi &E, hipStrea
 }  // namespace
 
 namespace cxg {
-// 130: 64 output channels per block, 131: 128; 132 / 133: the persistent forms of 130 / 131
-// (one output-channel block only).  The operands are the implicit-GEMM ones of a
+// 130: 64 output channels per block, 131: 128; 133: the persistent form of 131 (one
+// output-channel block only; its 64-channel form 132 was measured and retired).  The operands are the implicit-GEMM ones of a
 // conv forward or stride-1 data-gradient (A: weights [rows][9 Cg], B: K_GATHER of an NHWC map);
 // served: one group, 3 x 3, stride 1, pad 1, same-size output, Cg % 64 == 0, whole pixels of the
 // B map addressable in 31 bits.  -1 otherwise (the caller falls back).
@@ -711,13 +677,8 @@ int dispatch_halo(int amode, int bmode, int epi, int tile, GOperand A, GOperand 
     return dbl ? launch_halo<128, 16, true>(A, B, E, s) : launch_halo<128, 16, false>(A, B, E, s);
   }
   // persistent item walk: one output-channel block
-  if (tile == 132 || tile == 133) {
-    if (A.rows % 8 != 0) return -1;  // whole 16-byte output segments
-    if (tile == 132) {
-      if (A.rows > 64) return -1;
-      return wide ? launch_halo_ps<64, 32>(A, B, E, s) : launch_halo_ps<64, 16>(A, B, E, s);
-    }
-    if (A.rows > 128) return -1;
+  if (tile == 133) {
+    if (A.rows % 8 != 0 || A.rows > 128) return -1;  // whole 16-byte output segments
     return wide ? launch_halo_ps<128, 32>(A, B, E, s) : launch_halo_ps<128, 16>(A, B, E, s);
   }
   return -1;

@@ -381,25 +381,21 @@ static bool fast_ok(int bmode, const GOperand &A, const GOperand &B) {
   return true;
 }
 
-// 110: 256x256, 111: 256x128, 112: 128x256, 114: 128x128, 115: 64x256 (16x16x32); 113: 256x256 (32x32x16)
+// 114: 128x128 (16x16x32 MFMA), conv forward / data-gradient gathers
 int dispatch_4w(int amode, int bmode, int epi, int tile, const GOperand &A, const GOperand &B, const GEpi &E,
                 int groups, int ksplit, hipStream_t s) {
   if (amode != K_DIRECT || !fast_ok(bmode, A, B)) return -1;
 #define CX4(BMV, EPV)                                                                \
   if (bmode == BMV && epi == EPV) {                                                  \
     switch (tile) {                                                                  \
-      case 110: launch_4f<256, 256, BMV, EPV, 16>(A, B, E, groups, ksplit, s); return 0; \
-      case 111: launch_4f<256, 128, BMV, EPV, 16>(A, B, E, groups, ksplit, s); return 0; \
-      case 112: launch_4f<128, 256, BMV, EPV, 16>(A, B, E, groups, ksplit, s); return 0; \
-      case 113: launch_4f<256, 256, BMV, EPV, 32>(A, B, E, groups, ksplit, s); return 0; \
       case 114: launch_4f<128, 128, BMV, EPV, 16>(A, B, E, groups, ksplit, s); return 0; \
-      case 115: launch_4f<64, 256, BMV, EPV, 16>(A, B, E, groups, ksplit, s); return 0;  \
       default: return -1;                                                            \
     }                                                                                \
   }
+  // (tiles 110-113 / 115 -- 256x256 in 16x16x32 and 32x32x16 form, 256x128, 128x256, 64x256 -- and
+  // the K_DIRECT instantiations were measured and retired: no table entry uses them,
+  // docs/performance.md "MFMA shape")
   CX4(K_GATHER, EPI_BF16)  // conv fwd / dgrad
-  CX4(K_DIRECT, EPI_BF16)  // fc fwd, square GEMMs
-  CX4(K_DIRECT, EPI_F32)   // fc fwd split-K
 #undef CX4
   return -1;
 }

@@ -446,269 +446,19 @@ int launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int 
 
 
 
-// (A variant with waves 4-7 staggered half a segment behind their SIMD partners -- two
-// barriers per segment -- measured 5-25% slower on every shape: profiles/r2_sweep_segmented.jsonl.)
-template <int BM, int BN, int AMODE, int BMODE, int EPI>
-__global__ void __launch_bounds__(512, 1)
-gemm_seg(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_tiles, int ktiles_total) {
-  constexpr int NW = 8, WGM = 2, WGN = 4;
-  constexpr int WM = BM / WGM, WN = BN / WGN;
-  constexpr int MR = WM / 16, NR = WN / 16;
-  using OA = SegOp<AMODE, BM>;
-  using OB = SegOp<BMODE, BN>;
-  constexpr int NPH = OA::NI + OB::NI;         // DMA instructions per wave per segment
-  constexpr int A_BYTES = BM * 64, SLOT = (BM + BN) * 64;
-  constexpr int EPI_BYTES = NW * 16 * (WM + 4) * 4;
-  constexpr int SMEM = 4 * SLOT > EPI_BYTES ? 4 * SLOT : EPI_BYTES;
-  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
-  const uint32_t ntile = static_cast<uint32_t>(tiles_i) * tiles_j;
-  const GemmBlock wb = gemm_block(ntile);
-  const int g = wb.g;
-  const uint32_t tile = wb.tile;
-  int ti, tj;
-  tile_ij(tile, tiles_i, tiles_j, E.group_i, ti, tj);
-  const int i0 = ti * BM, j0 = tj * BN;
-  const int kt_beg = wb.slice * ksplit_tiles;
-  const int kt_end = min(kt_beg + ksplit_tiles, ktiles_total);
-  if (kt_beg >= kt_end) return;
-  const int nseg = 2 * (kt_end - kt_beg);
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const rsrc_t rA = make_rsrc(A.ptr, A.nbytes);
-  const rsrc_t rB = make_rsrc(B.ptr, B.nbytes);
-  const uint32_t goA = static_cast<uint32_t>(g * A.gstride) * 2u;
-  const uint32_t goB = static_cast<uint32_t>(g * B.gstride) * 2u;
-  OA oa;
-  OB ob;
-  oa.init(A, i0, goA, wave, lane);
-  ob.init(B, j0, goB, wave, lane);
-
-  // all DMAs of segment `seg` into slot seg & 3 (all-OOB dummies past the slice)
-  auto issue = [&](int seg) {
-    const int kt = kt_beg + (seg >> 1), half = seg & 1;
-    const typename OA::Prep pa = oa.prep(A, kt, half, kt_end, goA);
-    const typename OB::Prep pb = ob.prep(B, kt, half, kt_end, goB);
-    char *sl = smem + (seg & 3) * SLOT;
-    static_for<OA::NI>([&](auto sc) {
-      constexpr int q = decltype(sc)::value;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void *)(sl + (wave + NW * q) * 1024), 16,
-                                               oa.template offset<q>(A, pa), 0, 0, 0);
-    });
-    static_for<OB::NI>([&](auto sc) {
-      constexpr int q = decltype(sc)::value;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void *)(sl + A_BYTES + (wave + NW * q) * 1024), 16,
-                                               ob.template offset<q>(B, pb), 0, 0, 0);
-    });
-  };
-
-  const int wi_ = wave % WGM, wj_ = wave / WGM;
-  f32x4 acc[MR][NR];
-#pragma unroll
-  for (int m = 0; m < MR; ++m)
-#pragma unroll
-    for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  issue(0);
-  issue(1);
-  issue(2);
-  for (int seg = 0; seg < nseg; ++seg) {
-    wait_vmcnt<2 * NPH>();                         // this wave's DMAs of segment `seg` landed
-    __builtin_amdgcn_s_waitcnt(0xc07f);            // lgkmcnt(0): its reads of segment seg-1 returned
-    block_barrier();                               // ... for every wave
-    issue(seg + 3);                                // into slot (seg - 1) & 3, released just now
-    const char *sa = smem + (seg & 3) * SLOT;
-    const char *sb = sa + A_BYTES;
-    bf16x8 fa[MR], fb[NR];
-#pragma unroll
-    for (int n = 0; n < NR; ++n) fb[n] = seg_frag(sb, wj_ * WN + n * 16, lane);
-#pragma unroll
-    for (int m = 0; m < MR; ++m) fa[m] = seg_frag(sa, wi_ * WM + m * 16, lane);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int m = 0; m < MR; ++m)
-#pragma unroll
-      for (int n = 0; n < NR; ++n)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  }
-  wait_vmcnt<0>();
-  __syncthreads();  // slots are reused by the epilogue
-
-  seg_epilogue<EPI, MR, NR, WM>(acc, smem, E, g, wb.slice, A.rows, B.rows, i0 + wi_ * WM, j0 + wj_ * WN, wave, lane);
-}
-
-template <int BM, int BN, int AMODE, int BMODE, int EPI>
-void launch_seg(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int ksplit, hipStream_t s) {
-  const int ti = cdiv(A.rows, BM), tj = cdiv(B.rows, BN);
-  const int ktiles = cdiv(A.kdim, BK);
-  ksplit = ksplit < 1 ? 1 : (ksplit > ktiles ? ktiles : ksplit);
-  const int per = cdiv(ktiles, ksplit);
-  ksplit = cdiv(ktiles, per);
-  dim3 grid(ti * tj, ksplit, groups);
-  CXN_LAUNCH((gemm_seg<BM, BN, AMODE, BMODE, EPI>), grid, dim3(512), 0, s, A, B, E, ti, tj, per, ktiles);
-}
-
-// ======================================================================================
-// Ping-pong 8-wave pipeline (tiles 60 / 61: 256 x 256 with 4 / 5 k-half LDS slots, K-major
-// operands -- conv forward / data-grad, fc forward).
-//
-// The two waves that share a SIMD belong to different wave GROUPS (group = wave >> 2, which
-// is also the wave's half of the A rows), and group 1 runs one s_barrier behind group 0.
-// Every PHASE is   wait vmcnt -> issue 2 DMAs -> fragment reads -> barrier -> MFMAs -> barrier,
-// so while one group computes, the other issues its DMAs and LDS reads: the MFMA pipe of each
-// SIMD alternates between its two waves instead of idling through both waves' load phases at
-// the same time (the cdna guide's 8-phase template).
-//   * LDS: NS k-half slots (segment u = 32 k of the block's K range, slot u % NS) of
-//     [256 A rows + 256 B rows] x 64 B -- the gemm_seg image (SegOp DMAs, seg_frag reads);
-//   * segment u = two phases: P0 reads B n-frags 0-3 and A m-frags 0-3 and runs 16 MFMAs,
-//     P1 reads A m-frags 4-7 and runs the other 16 (per wave 128 x 64 outputs, 48 fragment
-//     VGPRs live at most);
-//   * P0 issues the B DMAs and P1 the A DMAs of segment u + NS - 1.  With the one-barrier lag
-//     a slot may be re-filled two phases after its last read, and a DMA must be retired by a
-//     wait one phase before its first read: `s_waitcnt vmcnt(2 (2 NS - 5))` at the top of every
-//     phase (the DMAs of the 2 NS - 5 most recent phases stay in flight) satisfies both;
-//   * past the end of the K slice the DMAs are all-OOB dummies, so the count never changes.
-template <int AMODE, int BMODE, int EPI, int NS>
-__global__ void __launch_bounds__(512, 1)
-gemm_pp(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_tiles, int ktiles_total) {
-  constexpr int BM = 256, BN = 256, NW = 8;
-  constexpr int WM = 128, WN = 64, MR = 8, NR = 4;
-  using OA = SegOp<AMODE, BM>;
-  using OB = SegOp<BMODE, BN>;
-  static_assert(OA::NI == 2 && OB::NI == 2, "2 DMAs per wave per operand and segment");
-  constexpr int A_BYTES = BM * 64, SLOT = (BM + BN) * 64;
-  constexpr int EPI_BYTES = NW * 16 * (WM + 4) * 4;
-  constexpr int SMEM = NS * SLOT > EPI_BYTES ? NS * SLOT : EPI_BYTES;
-  static_assert(NS == 4 || NS == 5, "4 or 5 k-half slots");
-  // segment u is issued at segment u - (NS - 1); its first read (phase 2u) needs it retired by the
-  // wait of phase 2u - 1, which may leave the DMAs of the 2NS - 5 phases before it in flight
-  constexpr int VM = 2 * (2 * NS - 5);
-  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-
-  const uint32_t ntile = static_cast<uint32_t>(tiles_i) * tiles_j;
-  const GemmBlock wb = gemm_block(ntile);
-  const int g = wb.g;
-  const uint32_t tile = wb.tile;
-  int ti, tj;
-  tile_ij(tile, tiles_i, tiles_j, E.group_i, ti, tj);
-  const int i0 = ti * BM, j0 = tj * BN;
-  const int kt_beg = wb.slice * ksplit_tiles;
-  const int kt_end = min(kt_beg + ksplit_tiles, ktiles_total);
-  if (kt_beg >= kt_end) return;
-  const int nseg = 2 * (kt_end - kt_beg);
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wave >> 2, wc = wave & 3;  // group = A-row half; B column quarter
-  const rsrc_t rA = make_rsrc(A.ptr, A.nbytes);
-  const rsrc_t rB = make_rsrc(B.ptr, B.nbytes);
-  const uint32_t goA = static_cast<uint32_t>(g * A.gstride) * 2u;
-  const uint32_t goB = static_cast<uint32_t>(g * B.gstride) * 2u;
-  OA oa;
-  OB ob;
-  oa.init(A, i0, goA, wave, lane);
-  ob.init(B, j0, goB, wave, lane);
-
-  auto issue_a = [&](int seg) {
-    const typename OA::Prep pa = oa.prep(A, kt_beg + (seg >> 1), seg & 1, kt_end, goA);
-    char *sl = smem + (seg % NS) * SLOT;
-    static_for<OA::NI>([&](auto sc) {
-      constexpr int q = decltype(sc)::value;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void *)(sl + (wave + NW * q) * 1024), 16,
-                                               oa.template offset<q>(A, pa), 0, 0, 0);
-    });
-  };
-  auto issue_b = [&](int seg) {
-    const typename OB::Prep pb = ob.prep(B, kt_beg + (seg >> 1), seg & 1, kt_end, goB);
-    char *sl = smem + (seg % NS) * SLOT + A_BYTES;
-    static_for<OB::NI>([&](auto sc) {
-      constexpr int q = decltype(sc)::value;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void *)(sl + (wave + NW * q) * 1024), 16,
-                                               ob.template offset<q>(B, pb), 0, 0, 0);
-    });
-  };
-
-  f32x4 acc[MR][NR];
-#pragma unroll
-  for (int m = 0; m < MR; ++m)
-#pragma unroll
-    for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // prologue: segments 0 .. NS-2 in full; segment 0 landed for every wave before anyone reads it
-#pragma unroll
-  for (int u = 0; u < NS - 1; ++u) {
-    issue_a(u);
-    issue_b(u);
-  }
-  wait_vmcnt<4 * (NS - 2)>();
-  block_barrier();
-  if (wr == 1) block_barrier();  // group 1 runs one barrier behind group 0
-
-  bf16x8 fa[MR], fb[NR];
-  for (int seg = 0; seg < nseg; ++seg) {
-    const char *sa = smem + (seg % NS) * SLOT;
-    const char *sb = sa + A_BYTES;
-    // ---- phase 0: B fragments and A m-frags 0-3; B DMAs of segment seg + NS - 1; 16 MFMAs
-    // (segment seg was retired by every wave's wait in the previous phase)
-#pragma unroll
-    for (int n = 0; n < NR; ++n) fb[n] = seg_frag(sb, wc * WN + n * 16, lane);
-#pragma unroll
-    for (int m = 0; m < MR / 2; ++m) fa[m] = seg_frag(sa, wr * WM + m * 16, lane);
-    issue_b(seg + NS - 1);
-    block_barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int m = 0; m < MR / 2; ++m)
-#pragma unroll
-      for (int n = 0; n < NR; ++n)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    block_barrier();
-    // ---- phase 1: A m-frags 4-7; A DMAs of segment seg + NS - 1; retire segment seg + 1; 16 MFMAs
-#pragma unroll
-    for (int m = MR / 2; m < MR; ++m) fa[m] = seg_frag(sa, wr * WM + m * 16, lane);
-    wait_vmcnt<VM>();
-    issue_a(seg + NS - 1);
-    block_barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int m = MR / 2; m < MR; ++m)
-#pragma unroll
-      for (int n = 0; n < NR; ++n)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m], fb[n], acc[m][n], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    block_barrier();
-  }
-  if (wr == 0) block_barrier();  // equal barrier counts for both groups
-  wait_vmcnt<0>();
-  __syncthreads();  // slots are reused by the epilogue
-
-  seg_epilogue<EPI, MR, NR, WM>(acc, smem, E, g, wb.slice, A.rows, B.rows, i0 + wr * WM, j0 + wc * WN, wave, lane);
-}
-
-template <int AMODE, int BMODE, int EPI, int NS>
-void launch_pp(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int ksplit, hipStream_t s) {
-  const int ti = cdiv(A.rows, 256), tj = cdiv(B.rows, 256);
-  const int ktiles = cdiv(A.kdim, BK);
-  ksplit = ksplit < 1 ? 1 : (ksplit > ktiles ? ktiles : ksplit);
-  const int per = cdiv(ktiles, ksplit);
-  ksplit = cdiv(ktiles, per);
-  dim3 grid(ti * tj, ksplit, groups);
-  CXN_LAUNCH((gemm_pp<AMODE, BMODE, EPI, NS>), grid, dim3(512), 0, s, A, B, E, ti, tj, per, ktiles);
-}
-
-// Tile ids (BM x BN, wave grid, stages); MN-major operands need a 128-wide tile side:
-//   0: 128x256 (1x4) 3      1: 128x128 (1x4) 2      2: 128x128 (2x2) 3      7: 64x128 (1x4) 2
-//  10: 128x64 (2x2) 2      13: 128x128 (1x4) 3     15: 64x64 (2x2) 3       17: 128x128 (2x2) 2
-// 8 waves, two per SIMD (half the DMA bytes per MFMA of a 128x128 tile):
-//  20: 128x512 (1x8) 2     21: 256x256 (2x4) 2     23: 128x128 (2x4) 3     25: 64x512 (1x8) 2
-// (as plain 2-stage loops they tie the 4-wave tiles on AlexNet shapes: profiles/r15_glds_8wave.jsonl)
-// 96-row tiles (70: 96x256 1x4, 71: 96x128 1x4, 72: 96x128 2x2) and the 160-row / 96-column
-// probes 73-75: the round-1 96-row tiles gave wrong outputs (profiles/r16_t96_tiles.jsonl) because
-// the epilogue's intra-wave LDS hand-off was unfenced (wave_lds_handoff); fixed, they are correct
-// and 72 ties the 128-row tile on AlexNet conv1 (the row gather, not the idle MFMA rows, bounds it).
+// Tile ids (BM x BN, wave grid, stages): only the tiles some shipped table entry uses
+// (ops/glds_tune_gfx950.json) or a default pick (ops.gemm._pick_glds: 1 / 7 / 10 / 15; fc
+// weight-grad 1) are compiled -- tests/test_tile_table_cpu.py checks both directions.
+//   1: 128x128 (1x4) 2      2: 128x128 (2x2) 3      7: 64x128 (1x4) 2       10: 128x64 (2x2) 2
+//  15: 64x64 (2x2) 3       17: 128x128 (2x2) 2
+// 8 waves, two per SIMD: 21: 256x256 (2x4) 2   23: 128x128 (2x4) 3   25: 64x512 (1x8) 2
+// PIPE variants (setprio around the MFMA clusters, both k-steps' fragments read ahead): 30, 31, 34,
+// 37-41; 96-row 72 (96x128) / 96-column 75 (64x96); 32-row 76-78; 48 of 64 staged rows 79 (AlexNet
+// conv2's 48-channel data-gradient); 82: 256x192 against wave quantisation (AlexNet conv3 dgrad).
+// Tiles measured and retired (no table entry, rounds 2-4): 0, 13, 20, 33, 35, 36, 70, 71, 73, 74,
+// 80, 81, 83, the segmented (50 / 51) and ping-pong (60 / 61) 8-wave pipelines, the MN-major 4w
+// weight-gradient (120), 4w tiles 110-113 / 115 and the persistent 64-channel halo (132).
 #define CXG_T(ID, BM, BN, WGM, WGN, ST) \
   case ID: return launch<BM, BN, WGM, WGN, ST, AM, BMo, EP>(A, B, E, groups, ksplit, s);
 #define CXG_TP(ID, BM, BN, WGM, WGN, ST, PIPE) \
@@ -717,31 +467,19 @@ void launch_pp(const GOperand &A, const GOperand &B, const GEpi &E, int groups, 
   case ID: return launch<BM, BN, WGM, WGN, ST, AM, BMo, EP, 0, BMC>(A, B, E, groups, ksplit, s);
 #define CXG_KK_TILES                                                                                      \
   switch (tile) {                                                                                         \
-    CXG_T(0, 128, 256, 1, 4, 3) CXG_T(1, 128, 128, 1, 4, 2) CXG_T(2, 128, 128, 2, 2, 3)                   \
-    CXG_T(7, 64, 128, 1, 4, 2) CXG_T(10, 128, 64, 2, 2, 2) CXG_T(15, 64, 64, 2, 2, 3)                     \
-    CXG_T(20, 128, 512, 1, 8, 2) CXG_T(21, 256, 256, 2, 4, 2) CXG_T(25, 64, 512, 1, 8, 2)                 \
-    CXG_TP(30, 128, 256, 2, 4, 3, 0) CXG_TP(31, 128, 256, 2, 4, 3, 3) CXG_TP(33, 128, 256, 1, 4, 3, 3)    \
-    CXG_TP(34, 256, 256, 2, 4, 2, 3) CXG_TP(35, 64, 256, 1, 4, 3, 0) CXG_TP(36, 128, 128, 2, 4, 3, 3)     \
+    CXG_T(1, 128, 128, 1, 4, 2) CXG_T(7, 64, 128, 1, 4, 2) CXG_T(10, 128, 64, 2, 2, 2)                    \
+    CXG_T(15, 64, 64, 2, 2, 3) CXG_T(21, 256, 256, 2, 4, 2) CXG_T(25, 64, 512, 1, 8, 2)                   \
+    CXG_TP(30, 128, 256, 2, 4, 3, 0) CXG_TP(31, 128, 256, 2, 4, 3, 3) CXG_TP(34, 256, 256, 2, 4, 2, 3)    \
     CXG_TP(37, 64, 128, 1, 4, 2, 3) CXG_TP(38, 128, 256, 2, 4, 2, 3) CXG_TP(39, 64, 256, 2, 4, 3, 3)      \
-    CXG_TP(70, 96, 256, 1, 4, 2, 3) CXG_TP(71, 96, 128, 1, 4, 2, 3) CXG_TP(72, 96, 128, 2, 2, 2, 0)       \
-    CXG_TP(73, 160, 128, 1, 4, 2, 0) CXG_TP(74, 128, 96, 2, 2, 2, 0) CXG_TP(75, 64, 96, 2, 2, 2, 0)       \
+    CXG_TP(72, 96, 128, 2, 2, 2, 0) CXG_TP(75, 64, 96, 2, 2, 2, 0)                                        \
     CXG_T(76, 32, 128, 1, 4, 2) CXG_T(77, 32, 64, 1, 4, 3) CXG_T(78, 32, 256, 1, 4, 2)                    \
-    CXG_TC(79, 64, 48, 128, 1, 4, 2) CXG_TC(80, 64, 48, 256, 1, 4, 2) CXG_TC(81, 64, 48, 64, 1, 4, 3)     \
-    CXG_TP(82, 256, 192, 2, 4, 2, 3) CXG_TP(83, 192, 256, 2, 4, 2, 3)                                     \
-    default: return -1;                                                                                   \
-  }
-#define CXG_MK_TILES  /* A MN-major (BM = 128), B K-major */                                              \
-  switch (tile) {                                                                                         \
-    CXG_T(0, 128, 256, 1, 4, 3) CXG_T(1, 128, 128, 1, 4, 2) CXG_T(2, 128, 128, 2, 2, 3)                   \
-    CXG_T(10, 128, 64, 2, 2, 2) CXG_T(13, 128, 128, 1, 4, 3) CXG_T(17, 128, 128, 2, 2, 2)                 \
-    CXG_T(20, 128, 512, 1, 8, 2)                                                                          \
+    CXG_TC(79, 64, 48, 128, 1, 4, 2) CXG_TP(82, 256, 192, 2, 4, 2, 3)                                     \
     default: return -1;                                                                                   \
   }
 #define CXG_MM_TILES  /* both MN-major (128 x 128) */                                                     \
   switch (tile) {                                                                                         \
-    CXG_T(1, 128, 128, 1, 4, 2) CXG_T(2, 128, 128, 2, 2, 3) CXG_T(13, 128, 128, 1, 4, 3)                  \
-    CXG_T(17, 128, 128, 2, 2, 2) CXG_T(23, 128, 128, 2, 4, 3)                                             \
-    CXG_TP(36, 128, 128, 2, 4, 3, 3) CXG_TP(40, 128, 128, 1, 4, 2, 3) CXG_TP(41, 128, 128, 2, 2, 2, 3)    \
+    CXG_T(1, 128, 128, 1, 4, 2) CXG_T(2, 128, 128, 2, 2, 3) CXG_T(17, 128, 128, 2, 2, 2)                  \
+    CXG_T(23, 128, 128, 2, 4, 3) CXG_TP(40, 128, 128, 1, 4, 2, 3) CXG_TP(41, 128, 128, 2, 2, 2, 3)        \
     default: return -1;                                                                                   \
   }
 #define CXG_CASE(AMV, BMV, EPV, TILES)                       \
@@ -752,45 +490,12 @@ void launch_pp(const GOperand &A, const GOperand &B, const GEpi &E, int groups, 
 
 int dispatch(int amode, int bmode, int epi, int tile, const GOperand &A, const GOperand &B, const GEpi &E,
              int groups, int ksplit, hipStream_t s) {
-  // segmented 8-wave pipeline: 50 = 256x256, 51 = 128x256 (K-major A and B)
-#define CXG_SEG(AMV, BMV, EPV)                                                                      \
-  if (amode == AMV && bmode == BMV && epi == EPV) {                                                 \
-    if (tile == 50) { launch_seg<256, 256, AMV, BMV, EPV>(A, B, E, groups, ksplit, s); return 0; }  \
-    if (tile == 51) { launch_seg<128, 256, AMV, BMV, EPV>(A, B, E, groups, ksplit, s); return 0; }  \
-  }
-  // (99 is the Python-side pseudo-tile of the register kernel, never passed here)
-  if (tile >= 110 && tile <= 119) return cxg::dispatch_4w(amode, bmode, epi, tile, A, B, E, groups, ksplit, s);
-  if (tile >= 130 && tile <= 133) return cxg::dispatch_halo(amode, bmode, epi, tile, A, B, E, groups, ksplit, s);
-  if (tile == 120) return cxg::dispatch_4m(amode, bmode, epi, tile, A, B, E, groups, ksplit, s);
-  if (tile >= 140 && tile <= 142) return cxg::dispatch_wgrad_halo(amode, bmode, epi, tile, A, B, E, groups, s);
-  if (tile >= 50 && tile <= 51) {
-    CXG_SEG(K_DIRECT, K_GATHER, EPI_BF16)
-    CXG_SEG(K_DIRECT, K_DIRECT, EPI_BF16)
-    CXG_SEG(K_DIRECT, K_DIRECT, EPI_F32)
-    return -1;
-  }
-#undef CXG_SEG
-  // ping-pong 8-wave pipeline, 256x256 (K-major A and B): 60 = 4 k-half slots, 61 = 5
-#define CXG_PP(AMV, BMV, EPV)                                                                         \
-  if (amode == AMV && bmode == BMV && epi == EPV) {                                                   \
-    if (tile == 60) { launch_pp<AMV, BMV, EPV, 4>(A, B, E, groups, ksplit, s); return 0; }            \
-    if (tile == 61) { launch_pp<AMV, BMV, EPV, 5>(A, B, E, groups, ksplit, s); return 0; }            \
-  }
-  if (tile == 60 || tile == 61) {
-    CXG_PP(K_DIRECT, K_GATHER, EPI_BF16)
-    CXG_PP(K_DIRECT, K_DIRECT, EPI_BF16)
-    CXG_PP(K_DIRECT, K_DIRECT, EPI_F32)
-    return -1;
-  }
-#undef CXG_PP
   CXG_CASE(K_DIRECT, K_GATHER, EPI_BF16, CXG_KK_TILES)    // conv fwd / dgrad
   CXG_CASE(K_DIRECT, K_GATHER, EPI_BF16_DB, CXG_KK_TILES)  // conv dgrad + the lower conv's bias gradient
   CXG_CASE(K_DIRECT, K_ROWGATHER, EPI_BF16, CXG_KK_TILES)  // conv fwd, few input channels (conv1)
   CXG_CASE(K_DIRECT, K_DIRECT, EPI_BF16, CXG_KK_TILES)    // fc fwd
   CXG_CASE(K_DIRECT, K_DIRECT, EPI_F32, CXG_KK_TILES)     // fc fwd split-K
   CXG_CASE(MN_GATHER, MN_DIRECT, EPI_F32_ATOMIC, CXG_MM_TILES)  // conv wgrad
-  CXG_CASE(MN_DIRECT, K_DIRECT, EPI_BF16, CXG_MK_TILES)   // fc dgrad
-  CXG_CASE(MN_DIRECT, K_DIRECT, EPI_F32, CXG_MK_TILES)    // fc dgrad split-K
   CXG_CASE(MN_DIRECT, MN_DIRECT, EPI_F32, CXG_MM_TILES)   // fc wgrad (store)
   CXG_CASE(MN_DIRECT, MN_DIRECT, EPI_F32_ACC, CXG_MM_TILES)  // fc wgrad (+=)
   CXG_CASE(MN_DIRECT, MN_DIRECT, EPI_F32_SGD, CXG_MM_TILES)  // fc wgrad fused with the SGD step
@@ -798,7 +503,6 @@ int dispatch(int amode, int bmode, int epi, int tile, const GOperand &A, const G
 }
 #undef CXG_CASE
 #undef CXG_MM_TILES
-#undef CXG_MK_TILES
 #undef CXG_KK_TILES
 #undef CXG_T
 #undef CXG_TC

@@ -578,13 +578,10 @@ __device__ __forceinline__ void seg_epilogue(f32x4 (&acc)[MR][NR], char *smem, c
   }
 }
 
-// the one-wave-per-SIMD address-free tiles (gemm_4w.hip): tiles 110-115; -1 when unsupported
+// the one-wave-per-SIMD address-free tile (gemm_4w.hip): tile 114; -1 when unsupported
 int dispatch_4w(int amode, int bmode, int epi, int tile, const GOperand &A, const GOperand &B, const GEpi &E,
                 int groups, int ksplit, hipStream_t s);
-// one-wave-per-SIMD MN-major tile (gemm_4w_mn.hip, conv weight-gradients): tile 120; -1 when unsupported
-int dispatch_4m(int amode, int bmode, int epi, int tile, const GOperand &A, const GOperand &B, const GEpi &E,
-                int groups, int ksplit, hipStream_t s);
-// direct 3x3 convolution on a resident input halo (conv_halo.hip): tiles 130-131; -1 when unsupported
+// direct 3x3 convolution on a resident input halo (conv_halo.hip): tiles 130, 131, 133; -1 when unsupported
 int dispatch_halo(int amode, int bmode, int epi, int tile, GOperand A, GOperand B, const GEpi &E, int groups,
                   int ksplit, hipStream_t s);
 // direct 3x3 weight-gradient on resident halo / dy tiles (conv_wgrad_halo.hip): tiles 140-142

@@ -261,6 +261,34 @@ __global__ void conv_weight_flip_multi(FlipTable tab) {
   const int col = threadIdx.x & 63;
   const unsigned short *w = reinterpret_cast<const unsigned short *>(sg.w);
   unsigned short *wt = reinterpret_cast<unsigned short *>(sg.wt);
+  if ((sg.Co & 7) == 0 && (sg.Ci & 7) == 0) {
+    // 16-byte accesses: lane (r8, c8) moves 8 consecutive channels of one row (the 2-byte form
+    // below issued 8x the memory instructions: AlexNet's 7.5 MB of conv weights took 12 us)
+    unsigned short *tl = reinterpret_cast<unsigned short *>(tile);  // [64][130] bf16 (pitch 65 words)
+    const int c8 = (threadIdx.x & 7) * 8, r8 = threadIdx.x >> 3;
+    for (int r = r8; r < 64; r += NT / 8) {
+      const int co = co0 + r, ci = ci0 + c8;
+      if (co < sg.Co && ci < sg.Ci) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(w + (((g * sg.Co + co) * sg.KH + kh) * sg.KW + kw) * sg.Ci + ci);
+        const unsigned short *e = reinterpret_cast<const unsigned short *>(&v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) tl[r * 130 + c8 + k] = e[k];
+      }
+    }
+    __syncthreads();
+    for (int r = r8; r < 64; r += NT / 8) {  // r = ci within the tile, c8 = first co
+      const int ci = ci0 + r, co = co0 + c8;
+      if (co < sg.Co && ci < sg.Ci) {
+        uint4 v;
+        unsigned short *e = reinterpret_cast<unsigned short *>(&v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) e[k] = tl[(c8 + k) * 130 + r];
+        *reinterpret_cast<uint4 *>(wt + (((g * sg.Ci + ci) * sg.KH + (sg.KH - 1 - kh)) * sg.KW + (sg.KW - 1 - kw)) * sg.Co +
+                                   co) = v;
+      }
+    }
+    return;
+  }
   for (int r = threadIdx.x >> 6; r < 64; r += NT / 64) {
     const int co = co0 + r, ci = ci0 + col;
     if (co < sg.Co && ci < sg.Ci) tile[r][col] = w[(((g * sg.Co + co) * sg.KH + kh) * sg.KW + kw) * sg.Ci + ci];
@@ -1044,6 +1072,207 @@ __global__ void lrn_bwd_shfl(const bf16_t *x, const bf16_t *__restrict__ dy, bf1
     if (mask_relu && !(xv[e] > 0.f)) out[e] = 0.f;
   }
   *reinterpret_cast<uint4 *>(dx + off) = pack8(out);
+}
+
+// ------------------------------------------------------------------ fused max-pool -> LRN
+// AlexNet's pool1 -> lrn1 and pool2 -> lrn2 (reference pooling_layer-inl.hpp:45-86 and
+// lrn_layer-inl.hpp:53-74) as one kernel per direction.  Lanes are laid out as the shuffle LRN
+// (whole pooled pixels per wave, C / 8 lanes each), so the cross-channel window sums stay in
+// registers.
+//   forward : the 3x3 / 2 max window (first max, offset byte, relu' bit as pool_fwd_rows) ->
+//             pooled P and the LRN output Y in one pass: P is written (the LRN backward reads it)
+//             but not read back;
+//   backward: per 2x2 input cell (pool_bwd_s2k3's formulation) the LRN data-gradient of the
+//             four windows that cover it is recomputed from (P, dY) and routed by the offsets:
+//             the pooled gradient is never stored.  relu' of the routed pixel comes from bit 7
+//             of the offset.  With dbias the conv-bias gradient behind a relu'd pool (the
+//             _fuse_pool_bias sum of the pooled gradient, masked by bit 7) is summed on the way:
+//             window (ho, wo) counts in cell (ho, wo) only; per-block partial rows.
+template <int H>
+__global__ void pool_lrn_fwd(const bf16_t *__restrict__ x, bf16_t *__restrict__ P, uint8_t *__restrict__ arg,
+                             bf16_t *__restrict__ Y, int N, int Hin, int Win, int C, int Ho, int Wo, int relu,
+                             float salpha, float beta, float knorm) {
+  const long npix = static_cast<long>(N) * Ho * Wo;
+  const LrnLane L = lrn_lane(npix, C);
+  float pv[8];
+  uint32_t am[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    pv[q] = 0.f;
+    am[q] = 0;
+  }
+  long o = 0;
+  if (L.active) {
+    const int n = static_cast<int>(L.pix / (static_cast<long>(Ho) * Wo));
+    const int rem = static_cast<int>(L.pix - static_cast<long>(n) * Ho * Wo);
+    const int ho = rem / Wo, wo = rem - (rem / Wo) * Wo;
+    const int hs = 2 * ho, ws = 2 * wo;
+    const bf16_t *xb = x + static_cast<long>(n) * Hin * Win * C + L.cv * 8;
+    uint4 raw[9];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int h = min(hs + kh, Hin - 1), w = min(ws + kw, Win - 1);
+        raw[kh * 3 + kw] = *reinterpret_cast<const uint4 *>(xb + (static_cast<long>(h) * Win + w) * C);
+      }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) pv[q] = -INFINITY;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        if (hs + kh >= Hin || ws + kw >= Win) continue;
+        float v[8];
+        unpack8(raw[kh * 3 + kw], v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float a = (relu & 1) ? fmaxf(v[q], 0.f) : v[q];
+          if (a > pv[q]) {
+            pv[q] = a;
+            am[q] = static_cast<uint32_t>(kh * 3 + kw);
+          }
+        }
+      }
+    if (relu & 2)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) am[q] |= pv[q] > 0.f ? 0u : 0x80u;
+    o = L.pix * C + L.cv * 8;
+    const uint4 pk = pack8(pv);
+    *reinterpret_cast<uint4 *>(P + o) = pk;
+    *reinterpret_cast<uint2 *>(arg + o) =
+        make_uint2(am[0] | am[1] << 8 | am[2] << 16 | am[3] << 24, am[4] | am[5] << 8 | am[6] << 16 | am[7] << 24);
+    unpack8(pk, pv);  // the LRN reads the stored (bf16) P, as the separate kernel would
+  }
+  float sq[8], sw[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sq[e] = pv[e] * pv[e];
+  lrn_window_sum<H>(sq, L, sw);
+  if (!L.active) return;
+  float out[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) out[e] = pv[e] * exp2f(-beta * __log2f(knorm + salpha * sw[e]));
+  *reinterpret_cast<uint4 *>(Y + o) = pack8(out);
+}
+
+template <int H>
+__global__ void lrn_pool_bwd(const bf16_t *__restrict__ P, const bf16_t *__restrict__ dY,
+                             const uint8_t *__restrict__ arg, bf16_t *__restrict__ dx, int N, int Hin, int Win, int C,
+                             int Ho, int Wo, int HC, int WC, int relu_bit, float salpha, float beta, float knorm,
+                             float *__restrict__ dbias_part) {
+  const long ncell = static_cast<long>(N) * HC * WC;
+  const LrnLane L = lrn_lane(ncell, C);
+  int n = 0, ci = 0, cj = 0;
+  if (L.active) {
+    n = static_cast<int>(L.pix / (static_cast<long>(HC) * WC));
+    const int rem = static_cast<int>(L.pix - static_cast<long>(n) * HC * WC);
+    ci = rem / WC;
+    cj = rem - ci * WC;
+  }
+  float g[4][8], bsum[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) bsum[k] = 0.f;
+  uint2 a[4];
+  bool ok[4];
+#pragma unroll
+  for (int pq = 0; pq < 4; ++pq) {
+    const int p = pq >> 1, q = pq & 1;
+    const int ho = ci - 1 + p, wo = cj - 1 + q;
+    ok[pq] = L.active && ho >= 0 && ho < Ho && wo >= 0 && wo < Wo;
+    float xv[8], gv[8];
+    a[pq] = make_uint2(0u, 0u);
+    if (ok[pq]) {
+      const long o = ((static_cast<long>(n) * Ho + ho) * Wo + wo) * C + L.cv * 8;
+      unpack8(*reinterpret_cast<const uint4 *>(P + o), xv);
+      unpack8(*reinterpret_cast<const uint4 *>(dY + o), gv);
+      a[pq] = *reinterpret_cast<const uint2 *>(arg + o);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xv[e] = gv[e] = 0.f;
+    }
+    // LRN data-gradient of window (ho, wo) (as lrn_bwd_shfl; every lane takes part in the shuffles)
+    float sq[8], s[8], t[8], ts[8], ng[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sq[e] = xv[e] * xv[e];
+    lrn_window_sum<H>(sq, L, s);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float lg = __log2f(knorm + salpha * s[e]);
+      const float pw = exp2f(-beta * lg);
+      ng[e] = gv[e] * pw;
+      t[e] = gv[e] * xv[e] * pw * exp2f(-lg);
+    }
+    lrn_window_sum<H>(t, L, ts);
+    float gp[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gp[e] = ng[e] - 2.f * beta * salpha * xv[e] * ts[e];
+    // the stored pooled gradient is bf16 in the unfused pair: round the same way
+    const uint4 gpk = pack8(gp);
+    unpack8(gpk, gp);
+    const uint32_t ab[8] = {a[pq].x & 0xff, (a[pq].x >> 8) & 0xff, (a[pq].x >> 16) & 0xff, a[pq].x >> 24,
+                            a[pq].y & 0xff, (a[pq].y >> 8) & 0xff, (a[pq].y >> 16) & 0xff, a[pq].y >> 24};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float gm = (relu_bit && (ab[e] & 0x80u)) ? 0.f : gp[e];
+      g[pq][e] = gm;
+      if (pq == 3 && ok[pq]) bsum[e] += gm;  // window (ci, cj): counted by this cell only
+    }
+  }
+  if (L.active) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int sx = 0; sx < 2; ++sx) {
+        const int h = 2 * ci + r, w = 2 * cj + sx;
+        if (h >= Hin || w >= Win) continue;
+        float out[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) out[k] = 0.f;
+#pragma unroll
+        for (int pq = 0; pq < 4; ++pq) {
+          const int p = pq >> 1, q = pq & 1;
+          const int kh = 2 + r - 2 * p, kw = 2 + sx - 2 * q;  // tap of (h, w) in window (ci-1+p, cj-1+q)
+          if (kh > 2 || kw > 2 || !ok[pq]) continue;
+          const uint32_t off = static_cast<uint32_t>(kh * 3 + kw);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            out[k] += (((a[pq].x >> (8 * k)) & 0x7f) == off) ? g[pq][k] : 0.f;
+            out[k + 4] += (((a[pq].y >> (8 * k)) & 0x7f) == off) ? g[pq][k + 4] : 0.f;
+          }
+        }
+        *reinterpret_cast<uint4 *>(dx + ((static_cast<long>(n) * Hin + h) * Win + w) * C + L.cv * 8) = pack8(out);
+      }
+  }
+  if (dbias_part != nullptr) {
+    __shared__ float red[512];
+    for (int c = threadIdx.x; c < C; c += blockDim.x) red[c] = 0.f;
+    __syncthreads();
+    if (L.active)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) atomicAdd(&red[L.cv * 8 + k], bsum[k]);
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) dbias_part[static_cast<long>(blockIdx.x) * C + c] = red[c];
+  }
+}
+
+// db[c] += sum_r part[r][c] over nrows fp32 partial rows of C columns: 32 columns x 8 row groups
+// per block over a chunk of 256 rows, one atomic per column per chunk
+__global__ void part_rows_colsum(const float *__restrict__ part, int nrows, int C, float *__restrict__ db) {
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const int rg = threadIdx.x >> 5;
+  const int r0 = blockIdx.y * 256, r1 = min(nrows, r0 + 256);
+  float acc = 0.f;
+  if (c < C)
+    for (int r = r0 + rg; r < r1; r += 8) acc += part[static_cast<long>(r) * C + c];
+  __shared__ float red[8][33];
+  red[rg][threadIdx.x & 31] = acc;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t += red[q][threadIdx.x & 31];
+    atomicAdd(db + c, t);
+  }
 }
 
 __global__ void lrn_bwd(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, bf16_t *__restrict__ dx,
@@ -1958,6 +2187,61 @@ CXN_API int cxn_lrn_fwd(const void *x, void *y, long npix, int C, int nsize, flo
   CXN_LAUNCH((lrn_fwd), nblocks(npix * C / 8), NT, 0, S_, (const bf16_t *)x, (bf16_t *)y, npix, C, nsize / 2, alpha / nsize,
                                                  beta, knorm);
   RET;
+}
+// fused max-pool (3x3 / 2, pad 0) -> LRN; see pool_lrn_fwd / lrn_pool_bwd.  -1: not served.
+CXN_API int cxn_pool_lrn_fwd(const void *x, void *P, void *arg, void *Y, int N, int Hin, int Win, int C, int Ho, int Wo,
+                             int relu, int nsize, float alpha, float beta, float knorm, void *stream) {
+  const int tpp = C / 8, half = nsize / 2;
+  if (C % 8 || tpp > 64 || half > 4 || Hin < 3 || Win < 3) return -1;
+  if (Ho != min(Hin - 2, Hin - 1) / 2 + 1 || Wo != min(Win - 2, Win - 1) / 2 + 1) return -1;  // ceil-mode 3x3 / 2
+  const long npix = static_cast<long>(N) * Ho * Wo;
+  const long waves = (npix + 64 / tpp - 1) / (64 / tpp);
+  const int blocks = static_cast<int>((waves + NT / 64 - 1) / (NT / 64));
+  const float sa = alpha / nsize;
+#define CXN_PLF(HV) CXN_LAUNCH((pool_lrn_fwd<HV>), blocks, NT, 0, S_, (const bf16_t *)x, (bf16_t *)P, (uint8_t *)arg, \
+                               (bf16_t *)Y, N, Hin, Win, C, Ho, Wo, relu, sa, beta, knorm)
+  switch (half) {
+    case 0: CXN_PLF(0); break;
+    case 1: CXN_PLF(1); break;
+    case 2: CXN_PLF(2); break;
+    case 3: CXN_PLF(3); break;
+    default: CXN_PLF(4); break;
+  }
+#undef CXN_PLF
+  RET;
+}
+// dbias_part: fp32 [blocks][C] per-block partial sums of the masked pooled gradient (null: no
+// bias sum); part_rows < 0: only return the block count.  Returns the block count (>= 0), -1
+// when not served, -4 when part_rows is too small.  The caller sums the partial rows.
+CXN_API int cxn_lrn_pool_bwd(const void *P, const void *dY, const void *arg, void *dx, int N, int Hin, int Win, int C,
+                             int Ho, int Wo, int relu_bit, int nsize, float alpha, float beta, float knorm,
+                             float *dbias, float *dbias_part, long part_rows, void *stream) {
+  const int tpp = C / 8, half = nsize / 2;
+  if (C % 8 || tpp > 64 || C > 512 || half > 4 || Hin < 3 || Win < 3) return -1;
+  if (Ho != min(Hin - 2, Hin - 1) / 2 + 1 || Wo != min(Win - 2, Win - 1) / 2 + 1) return -1;
+  const int HC = (Hin + 1) / 2, WC = (Win + 1) / 2;
+  const long ncell = static_cast<long>(N) * HC * WC;
+  const long waves = (ncell + 64 / tpp - 1) / (64 / tpp);
+  const int blocks = static_cast<int>((waves + NT / 64 - 1) / (NT / 64));
+  if (part_rows < 0) return blocks;  // query
+  const float sa = alpha / nsize;
+  float *part = dbias != nullptr ? dbias_part : nullptr;
+  if (dbias != nullptr && (part == nullptr || part_rows < blocks)) return -4;
+#define CXN_PLB(HV) CXN_LAUNCH((lrn_pool_bwd<HV>), blocks, NT, 0, S_, (const bf16_t *)P, (const bf16_t *)dY,   \
+                               (const uint8_t *)arg, (bf16_t *)dx, N, Hin, Win, C, Ho, Wo, HC, WC, relu_bit, sa, \
+                               beta, knorm, part)
+  switch (half) {
+    case 0: CXN_PLB(0); break;
+    case 1: CXN_PLB(1); break;
+    case 2: CXN_PLB(2); break;
+    case 3: CXN_PLB(3); break;
+    default: CXN_PLB(4); break;
+  }
+#undef CXN_PLB
+  if (part != nullptr)
+    CXN_LAUNCH((part_rows_colsum), dim3((C + 31) / 32, (blocks + 255) / 256), NT, 0, S_, part, blocks, C, dbias);
+  if (hipGetLastError() != hipSuccess) return -3;
+  return blocks;
 }
 CXN_API int cxn_lrn_bwd(const void *x, const void *dy, void *dx, long npix, int C, int nsize, float alpha, float beta,
                         float knorm, int mask_relu, void *stream) {

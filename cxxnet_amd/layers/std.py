@@ -509,6 +509,9 @@ class PoolingLayer(Layer):
         # the conv in front whose bias gradient this pool's backward provides (executor fusion,
         # NeuralNet._fuse_pool_bias); None = not fused
         self.bias_of = None
+        # (LRN layer, its output node) run inside this pool's kernels (NeuralNet._fuse_pool_lrn)
+        self.fused_lrn = None
+        self._dbpart = None
 
     def set_param(self, name, val):
         super().set_param(name, val)
@@ -544,6 +547,17 @@ class PoolingLayer(Layer):
 
     def forward(self, is_train, nodes_in, nodes_out):
         lp = self.lp
+        if self.fused_lrn is not None:
+            lrn, yout = self.fused_lrn
+            st = self._state(nodes_out[0])  # (also in eval: the fused kernel always writes offsets)
+            flags = int(bool(self.relu)) | (2 if self._mask_in_state() else 0)
+            if ops.pool_lrn_forward(nodes_in[0].data, nodes_out[0].data, st, yout.data, flags, lrn.nsize, lrn.alpha,
+                                    lrn.beta, lrn.knorm):
+                return
+            ops.pool_forward(nodes_in[0].data, nodes_out[0].data, st, lp.kernel_height, lp.kernel_width, lp.stride,
+                             lp.pad_y, self.mode, self.relu, mark_mask=self._mask_in_state())
+            ops.lrn_forward(nodes_out[0].data, yout.data, lrn.nsize, lrn.alpha, lrn.beta, lrn.knorm)
+            return
         st = self._state(nodes_out[0]) if is_train else None
         ops.pool_forward(nodes_in[0].data, nodes_out[0].data, st, lp.kernel_height, lp.kernel_width, lp.stride,
                          lp.pad_y, self.mode, self.relu, mark_mask=self._mask_in_state())
@@ -570,6 +584,8 @@ class PoolingLayer(Layer):
             return
         if relu and self._mask_in_state():
             relu = 2  # relu' of the argmax was recorded by the forward: no read of x
+        if self.fused_lrn is not None and self._fused_backprop(nodes_in, nodes_out, relu):
+            return
         conv = self.bias_of
         if conv is not None and conv.b is not None and relu in (0, 2) and self.ctx.is_gpu and not deterministic():
             # the conv's bias gradient from this pool's output gradient (before it is consumed)
@@ -579,6 +595,32 @@ class PoolingLayer(Layer):
             conv.bias_done = True
         ops.pool_backward(x, self.state, nodes_out[0].data, nodes_in[0].gdst, lp.kernel_height, lp.kernel_width, lp.stride,
                           lp.pad_y, self.mode, relu)
+
+    def _fused_backprop(self, nodes_in, nodes_out, relu) -> bool:
+        """Backward of the fused pool -> LRN pair: the LRN's output gradient (held by its output
+        node) straight to this pool's input gradient.  When the fused kernel declines, the LRN
+        backward runs here into the pooled gradient and False sends the caller down the plain
+        pool backward."""
+        lrn, yout = self.fused_lrn
+        pooled = nodes_out[0].data  # still the pooled output: the LRN layer's backprop did nothing
+        if relu in (0, 2):
+            conv = self.bias_of
+            db = None
+            part = None
+            if conv is not None and conv.b is not None and self.ctx.is_gpu and not deterministic():
+                rows = ops.lrn_pool_backward_rows(nodes_in[0].data.shape, pooled.shape, lrn.nsize)
+                C = pooled.shape[-1]
+                if rows > 0:
+                    if self._dbpart is None or self._dbpart.shape[0] < rows or self._dbpart.shape[1] != C:
+                        self._dbpart = torch.empty((rows, C), dtype=torch.float32, device=pooled.device)
+                    db, part = conv.b.g, self._dbpart
+            if ops.lrn_pool_backward(pooled, yout.data, self.state, nodes_in[0].gdst, int(relu == 2), lrn.nsize,
+                                     lrn.alpha, lrn.beta, lrn.knorm, dbias=db, part=part):
+                if db is not None:
+                    conv.bias_done = True
+                return True
+        ops.lrn_backward(pooled, yout.data, nodes_out[0].gdst, lrn.nsize, lrn.alpha, lrn.beta, lrn.knorm)
+        return False
 
 
 # ============================================================================ LRN
@@ -611,11 +653,15 @@ class LRNLayer(Layer):
         _check(nodes_in[0] is not nodes_out[0], "LRNLayer: input and output must be different nodes")
         nodes_out[0].set_shape(*nodes_in[0].shape, cp=nodes_in[0].cp)
 
+    fused_with_pool = False  # NeuralNet._fuse_pool_lrn: the max-pool in front runs this layer
+
     def forward(self, is_train, nodes_in, nodes_out):
+        if self.fused_with_pool:
+            return
         ops.lrn_forward(nodes_in[0].data, nodes_out[0].data, self.nsize, self.alpha, self.beta, self.knorm)
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
-        if not prop_grad:
+        if not prop_grad or self.fused_with_pool:
             return
         x = nodes_in[0].data
         # in place: the LDS-staged kernel reads a pixel's whole channel row before writing it

@@ -195,6 +195,36 @@ class NeuralNet:
         self._fuse_split(producers, consumers)
         self._fuse_pool_bias(producers, consumers)
         self._fuse_dgrad_bias(producers, consumers)
+        self._fuse_pool_lrn(producers, consumers)
+
+    def _fuse_pool_lrn(self, producers, consumers):
+        """Max-pool (3x3 / 2, pad 0) -> LRN (AlexNet pool1 -> lrn1, pool2 -> lrn2): one kernel per
+        direction (ops.pool_lrn_forward / ops.lrn_pool_backward).  The pool's forward also writes
+        the LRN output, and its backward takes the LRN's output gradient straight to the pool's
+        input gradient (the LRN layer launches nothing): the pooled output is not re-read in
+        forward and the pooled gradient never goes to memory.  The pool's output must be read by
+        the LRN alone.  CXXNET_FUSE_POOL_LRN=0 keeps the two layers apart."""
+        if os.environ.get("CXXNET_FUSE_POOL_LRN", "1") == "0" or not self.ctx.is_gpu:
+            return
+        for conn in self.connections:
+            lay = conn.layer
+            if conn.type not in (K_MAXPOOL, K_RELU_MAXPOOL) or conn.shared or len(conn.nodes_in) != 1:
+                continue
+            lp = lay.lp
+            if (getattr(lay, "mode", None) != "max" or lay.tie_all or lp.kernel_height != 3 or lp.kernel_width != 3
+                    or lp.stride != 2 or lp.pad_y != 0 or lp.pad_x != 0):
+                continue
+            out = conn.nodes_out[0]
+            cons = consumers.get(id(out), [])
+            if len(cons) != 1 or cons[0][1]:
+                continue
+            cj = self.connections[cons[0][0]]
+            if cj.type != K_LRN or cj.shared or cj.nodes_in[0] is not out or cj.layer.grad_mask_relu:
+                continue
+            if out.cp % 8 or cj.layer.nsize // 2 > 4:
+                continue
+            lay.fused_lrn = (cj.layer, cj.nodes_out[0])
+            cj.layer.fused_with_pool = True
 
     def _fuse_dropout(self, p, loops, cj):
         """fc -> relu -> dropout -> fc (AlexNet fc6 / fc7): the producer's forward applies the

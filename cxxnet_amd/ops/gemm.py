@@ -132,38 +132,31 @@ def _pick(candidates, rows_i, rows_j, groups, min_blocks=2 * NUM_CU):
 
 # ----------------------------------------------------------------------------- LDS-DMA kernel
 # gemm_glds.hip: both operands K-major (conv fwd / dgrad, fc fwd), 4 waves, one block per CU.
-GLDS_TILES = {0: (128, 256), 1: (128, 128), 2: (128, 128), 4: (192, 256), 5: (64, 256), 6: (256, 128),
-              7: (64, 128), 8: (192, 128), 9: (96, 128), 10: (128, 64), 11: (64, 128), 12: (64, 128),
-              13: (128, 128), 14: (128, 64), 15: (64, 64), 16: (192, 64), 17: (128, 128),
-              20: (128, 512), 21: (256, 256), 23: (128, 128), 25: (64, 512),
+# Only the tiles the shipped table (glds_tune_gfx950.json) or a default pick uses are compiled;
+# tests/test_tile_table_cpu.py checks this dict against the kernels' dispatch switches.  Tiles
+# measured and retired in rounds 2-5 are listed in gemm_glds.hip's dispatch comment.
+GLDS_TILES = {1: (128, 128), 2: (128, 128), 7: (64, 128), 10: (128, 64), 15: (64, 64), 17: (128, 128),
+              # 8 waves, two per SIMD
+              21: (256, 256), 23: (128, 128), 25: (64, 512),
               # pipelined variants (gemm_glds.hip PIPE: setprio around the MFMA clusters, both
               # k-steps' fragments read ahead of the MFMAs) and 8-wave 128x256 / 64x256 tiles
-              30: (128, 256), 31: (128, 256), 33: (128, 256), 34: (256, 256), 35: (64, 256), 36: (128, 128),
-              37: (64, 128), 38: (128, 256), 39: (64, 256), 40: (128, 128), 41: (128, 128),
-              # segmented 8-wave pipeline (gemm_seg): k-half LDS slots, two k-halves of DMAs in
-              # flight across every barrier
-              50: (256, 256), 51: (128, 256),
-              # ping-pong 8-wave pipeline (gemm_pp): the two wave groups one barrier apart
-              60: (256, 256), 61: (256, 256),
-              # 96-row tiles (K-major A): 96-output-channel convs (AlexNet conv1) without idle rows
-              70: (96, 256), 71: (96, 128), 72: (96, 128), 73: (160, 128), 74: (128, 96), 75: (64, 96),
+              30: (128, 256), 31: (128, 256), 34: (256, 256), 37: (64, 128), 38: (128, 256), 39: (64, 256),
+              40: (128, 128), 41: (128, 128),
+              # 96-row / 96-column tiles: 96-channel convs (AlexNet conv1) without idle rows
+              72: (96, 128), 75: (64, 96),
               # 32-row tiles (K-major A): convs with 16..48 output channels (GoogLeNet's 5x5-reduce and
               # pool-projection layers) and their data-gradients onto 16..48 input channels
               76: (32, 128), 77: (32, 64), 78: (32, 256),
               # 48 computed rows on 64 staged (AlexNet conv2's data-gradient: 48 channels per group)
-              79: (48, 128), 80: (48, 256), 81: (48, 64),
-              # 8-wave 3/4-width tiles against wave quantisation: AlexNet conv3's data-gradient has
+              79: (48, 128),
+              # 8-wave 3/4-width tile against wave quantisation: AlexNet conv3's data-gradient has
               # 169 256x256 tiles for 256 CUs, 226 of 256x192
-              82: (256, 192), 83: (192, 256),
-              # one wave per SIMD, address-free DMA issue (gemm_4w.hip): 113 = 32x32x16 MFMA
-              110: (256, 256), 111: (256, 128), 112: (128, 256), 113: (256, 256), 114: (128, 128),
-              115: (64, 256),
-              # one wave per SIMD, MN-major operands (gemm_4w_mn.hip): conv weight-gradients
-              120: (128, 128),
-              # direct 3x3 halo convolution (conv_halo.hip): output channels x 256-pixel patch
-              130: (64, 256), 131: (128, 256),
-              # ... its persistent patch walk for one input / one output channel block (132 / 133)
-              132: (64, 256), 133: (128, 256),
+              82: (256, 192),
+              # one wave per SIMD, address-free DMA issue (gemm_4w.hip)
+              114: (128, 128),
+              # direct 3x3 halo convolution (conv_halo.hip): output channels x 256-pixel patch, and
+              # the persistent patch walk for one 128-channel output block (133)
+              130: (64, 256), 131: (128, 256), 133: (128, 256),
               # direct 3x3 weight-gradient on resident halo / dy tiles (conv_wgrad_halo.hip): 64 x 64
               # channel pairs, persistent over 128-pixel patches (140 auto width, 141 16, 142 32)
               140: (64, 64), 141: (64, 64), 142: (64, 64)}
@@ -182,11 +175,11 @@ _glds_cfg = {"on": os.environ.get("CXXNET_GEMM_GLDS", "1") != "0",
 # row-run weight-grad for few-channel convs ("cwr", conv1) is 3% faster as a kernel but its
 # padded-buffer zero + fold-back pass makes the whole step 1.1% slower (profiles/r15_ab_cwr.jsonl)
 # Autotuning candidates: the 2-stage tiles that run 2-5 blocks per CU measured best on every
-# AlexNet shape (profiles/r14_glds_tiles.jsonl); 2 and 0 cover wide-i GEMMs (fc); the 8-wave
+# AlexNet shape (profiles/r14_glds_tiles.jsonl); 2 covers the fc weight-gradients; the 8-wave
 # 128x256 / 64x256 tiles and the pipelined variants (30-41) win conv2/conv3 forward, fc6 forward
 # and several VGG shapes (profiles/r2_sweep_tiles.jsonl).
-GLDS_CANDS = (1, 7, 10, 15, 2, 0, 13, 17, 21, 25, 30, 31, 34, 37, 38, 39, 40, 41, 50, 51, 72, 76, 77, 78, 79, 80,
-              81, 82, 83, 110, 111, 112, 113, 114, 115, 130, 131, 132, 133)
+GLDS_CANDS = (1, 7, 10, 15, 2, 17, 21, 25, 30, 31, 34, 37, 38, 39, 40, 41, 72, 75, 76, 77, 78, 79,
+              82, 114, 130, 131, 133)
 # the halo data-gradient tiles (130 / 131) hand over the lower conv's bias gradient from their
 # epilogue (EPI_BF16_DB) instead of a separate column-sum pass; CXXNET_HALO_DB=0 turns that off
 _HALO_DB = os.environ.get("CXXNET_HALO_DB", "1") != "0"

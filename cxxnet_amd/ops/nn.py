@@ -233,6 +233,53 @@ def pool_backward(x, state, dy, dx, KH, KW, S, P, mode: str, relu=False, dbias=N
                                    _stream()), "pool_bwd")
 
 
+def pool_lrn_forward(x, pooled, state, y, relu_flags, nsize, alpha, beta, knorm) -> bool:
+    """Fused max-pool (3x3 / 2, pad 0, ceil mode) -> LRN: pooled = pool(x) with the first-max
+    offsets in state (bit 7 = relu' of the max when relu_flags & 2), y = lrn(pooled).  Same
+    values as pool_forward + lrn_forward.  False when the fused kernel does not serve the
+    shape (nothing was done)."""
+    N, H, W, C = x.shape
+    Ho, Wo = pooled.shape[1], pooled.shape[2]
+    if not _native_t(x):
+        return False
+    rc = _k().cxn_pool_lrn_fwd(x.data_ptr(), pooled.data_ptr(), state.data_ptr(), y.data_ptr(), N, H, W, C, Ho, Wo,
+                               int(relu_flags), int(nsize), float(alpha), float(beta), float(knorm), _stream())
+    if rc == -1:
+        return False
+    native.check(rc, "pool_lrn_fwd")
+    return True
+
+
+def lrn_pool_backward(pooled, dy, state, dx, relu_bit, nsize, alpha, beta, knorm, dbias=None, part=None) -> bool:
+    """Backward of the fused max-pool -> LRN: dx = unpool(lrn'(pooled, dy)) routed by state
+    (relu_bit: a window whose bit 7 is set routes nothing), without storing the pooled
+    gradient.  dbias (+= the masked pooled gradient's column sums, the bias gradient of the
+    conv in front) needs part, an fp32 scratch of at least lrn_pool_backward_rows(...) x C.
+    False when the fused kernel does not serve the shape (nothing was done)."""
+    N, H, W, C = dx.shape
+    Ho, Wo = pooled.shape[1], pooled.shape[2]
+    if not _native_t(dy):
+        return False
+    rc = _k().cxn_lrn_pool_bwd(pooled.data_ptr(), dy.data_ptr(), state.data_ptr(), dx.data_ptr(), N, H, W, C, Ho, Wo,
+                               int(relu_bit), int(nsize), float(alpha), float(beta), float(knorm),
+                               dbias.data_ptr() if dbias is not None else None,
+                               part.data_ptr() if part is not None else None,
+                               part.shape[0] if part is not None else 0, _stream())
+    if rc == -1:
+        return False
+    if rc < 0:
+        native.check(rc, "lrn_pool_bwd")
+    return True
+
+
+def lrn_pool_backward_rows(x_shape, pooled_shape, nsize) -> int:
+    """Partial rows lrn_pool_backward needs for its bias sum (0: not served)."""
+    N, H, W, C = x_shape
+    rc = _k().cxn_lrn_pool_bwd(None, None, None, None, N, H, W, C, pooled_shape[1], pooled_shape[2], 1, int(nsize),
+                               0.0, 0.0, 1.0, None, None, -1, None)
+    return max(int(rc), 0)
+
+
 def pool_backward_tie_all(x, y, dy, dx, KH, KW, S, P, relu=False):
     """Max-unpool with the reference tie rule (pooling_layer-inl.hpp:55-86): every input
     equal to its window's max y gets that window's gradient; relu: max over relu(x), the

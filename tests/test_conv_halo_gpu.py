@@ -105,7 +105,7 @@ def test_halo_declines_other_convs():
 
 # persistent forms (one output-channel block; any number of 64-channel input blocks):
 # (N, H, W, C, Cout)
-PS_TILES = {132: 64, 133: 128}
+PS_TILES = {133: 128}
 PS_CASES = [
     (2, 16, 64, 64, 64),     # two 32-wide x 8-row patches per row band, whole patches
     (3, 20, 48, 64, 64),     # 16-wide patches, bottom edge cut
@@ -164,18 +164,18 @@ def test_halo_persistent_data_grad(tile, mask, cin):
 
 
 def test_halo_persistent_declines_two_output_blocks():
-    """128 output channels on the 64-channel persistent block: 132 declines."""
-    geo = _geom(2, 16, 32, 64, 128)
+    """256 output channels on the 128-channel persistent block: 133 declines."""
+    geo = _geom(2, 16, 32, 64, 256)
     x = _rnd((2, 16, 32, 64), 1.0, 16)
-    w = _rnd((128, 3, 3, 64), 0.05, 17)
-    y = torch.empty(2, 16, 32, 128, dtype=torch.bfloat16, device=DEV)
-    gemm.set_glds(tile=132)
+    w = _rnd((256, 3, 3, 64), 0.05, 17)
+    y = torch.empty(2, 16, 32, 256, dtype=torch.bfloat16, device=DEV)
+    gemm.set_glds(tile=133)
     gemm.LAST_GLDS[0] = None
     try:
         ops.conv_forward(x, w, None, y, geo)
     finally:
         gemm.set_glds(tile=-1)
-    assert gemm.LAST_GLDS[0] != 132
+    assert gemm.LAST_GLDS[0] != 133
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, padding=1)
     assert _rel(y, ref.permute(0, 2, 3, 1)) < 1e-2
 

@@ -283,7 +283,7 @@ def test_alexnet_trajectory_gpu_vs_cpu_fp32():
     print(f"\nloss cpu {l_cpu}\nloss gpu {l_gpu}\nrel loss err {err_loss:.3g} (floor {floor_loss:.3g})\n"
           f"weight err per layer {[round(v, 4) for v in err_w]}\nfloor {[round(v, 4) for v in floor_w]}")
     assert l_gpu[-1] < l_gpu[0]  # it trains
-    # measured on MI355X (tools/gpu_r2h.sh): loss error 4.7x the floor (0.0075 vs 0.0016); per
+    # measured on MI355X (round 2): loss error 4.7x the floor (0.0075 vs 0.0016); per
     # layer weight error 1.0-1.4x the floor (e.g. conv3 0.165 vs 0.140, fc7 0.264 vs 0.218)
     assert err_loss < 8 * floor_loss
     for e, f in zip(err_w, floor_w):

@@ -1,7 +1,7 @@
-"""The one-wave-per-SIMD address-free GEMM tiles (csrc/kernels/gemm_4w.hip, ids 110-113) against
-fp32 torch on the ops that route to them: conv forward (implicit-im2col gather, padding taps,
-groups, stride 2, 1x1), the stride-1 conv data-gradient, fc forward (split-K fp32 slabs) and a
-square GEMM.  Each case asserts that the forced tile really ran (gemm.LAST_GLDS): a tile that
+"""The one-wave-per-SIMD address-free GEMM tile (csrc/kernels/gemm_4w.hip, id 114; the other
+4w tiles were retired in round 5) against fp32 torch on the ops that route to it: conv forward
+(implicit-im2col gather, padding taps, groups, stride 2, 1x1) and the stride-1 conv
+data-gradient; fc forward declines it (K-direct operands are not compiled) and falls back.  Each case asserts that the forced tile really ran (gemm.LAST_GLDS): a tile that
 returns "unsupported" would otherwise pass on a fallback kernel."""
 import pytest
 import torch
@@ -13,7 +13,7 @@ from cxxnet_amd.ops.gemm import ConvGeom, conv_out_size
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-TILES = (110, 111, 112, 113, 114, 115)
+TILES = (114,)
 
 
 def _rnd(shape, scale, seed):
@@ -81,20 +81,19 @@ def test_conv_data_grad(tile, case):
     assert _rel(dx, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", TILES)
-@pytest.mark.parametrize("nin,nout,B", [(4096, 1000, 96), (1024, 1024, 1024), (9216, 4096, 200)])
-def test_fc_forward(tile, nin, nout, B):
+@pytest.mark.parametrize("nin,nout,B", [(4096, 1000, 96), (1024, 1024, 1024)])
+def test_fc_forward_declines(nin, nout, B):
     x = _rnd((B, nin), 1.0, 7)
     w = _rnd((nout, nin), 0.02, 8)
     b = torch.randn(nout, device=DEV) * 0.1
     y = torch.empty(B, nout, dtype=torch.bfloat16, device=DEV)
-    gemm.set_glds(tile=tile)
+    gemm.set_glds(tile=114)
     gemm.LAST_GLDS[0] = None
     try:
         ops.fc_forward(x, w, b, y)
     finally:
         gemm.set_glds(tile=-1)
-    assert gemm.LAST_GLDS[0] == tile
+    assert gemm.LAST_GLDS[0] != 114
     assert _rel(y, x.float() @ w.float().t() + b) < 1e-2
 
 
@@ -105,12 +104,12 @@ def test_unsupported_shapes_fall_back():
     x = _rnd((g.N, g.H, g.W, g.C), 1.0, 5)
     w = _rnd((g.Cout, g.KH, g.KW, g.cg_in), 0.05, 6)
     y = torch.empty(g.N, g.Ho, g.Wo, g.Cout, dtype=torch.bfloat16, device=DEV)
-    gemm.set_glds(tile=110)
+    gemm.set_glds(tile=114)
     gemm.LAST_GLDS[0] = None
     try:
         ops.conv_forward(x, w, None, y, g)
     finally:
         gemm.set_glds(tile=-1)
-    assert gemm.LAST_GLDS[0] != 110
+    assert gemm.LAST_GLDS[0] != 114
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, padding=1).permute(0, 2, 3, 1)
     assert _rel(y, ref) < 1e-2

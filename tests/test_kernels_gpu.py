@@ -733,7 +733,9 @@ def test_conv_weight_flip_multi_matches_single():
     from cxxnet_amd.ops import gemm as G
     torch.manual_seed(5)
     geos = [ConvGeom(2, 13, 13, 384, 13, 13, 256, 3, 3, 1, 1, 1, 2), ConvGeom(2, 27, 27, 96, 27, 27, 256, 5, 5, 1, 2, 2, 2),
-            ConvGeom(2, 28, 28, 192, 28, 28, 64, 1, 1, 1, 0, 0, 1), ConvGeom(2, 7, 7, 8, 7, 7, 16, 3, 3, 1, 1, 1, 1)]
+            ConvGeom(2, 28, 28, 192, 28, 28, 64, 1, 1, 1, 0, 0, 1), ConvGeom(2, 7, 7, 8, 7, 7, 16, 3, 3, 1, 1, 1, 1),
+            ConvGeom(2, 7, 7, 12, 7, 7, 20, 3, 3, 1, 1, 1, 1),  # channels not multiples of 8: 2-byte path
+            ConvGeom(2, 14, 14, 160, 14, 14, 72, 3, 3, 1, 1, 1, 1)]  # partial 64 x 64 tiles, 16-byte path
     items, refs = [], []
     for g in geos:
         w = torch.randn(g.Cout, g.KH, g.KW, g.cg_in, device=DEV).to(torch.bfloat16)

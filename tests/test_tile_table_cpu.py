@@ -27,8 +27,41 @@ def test_every_entry_names_a_known_tile():
 
 def test_tuning_candidates_are_known_tiles():
     assert set(G.GLDS_CANDS) <= set(G.GLDS_TILES)
-    for t in (82, 83, 110, 114, 115, 130, 131):  # wave-quantisation (r3), one-wave-per-SIMD, halo (r4)
+    for t in (82, 114, 130, 131, 133):  # wave-quantisation (r3), one-wave-per-SIMD, halo (r4)
         assert t in G.GLDS_CANDS
+
+
+def _compiled_tiles():
+    """Tile ids the kernels' dispatch code accepts, read from the HIP sources."""
+    import os
+    import re
+    kdir = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(G.__file__))), "csrc", "kernels")
+    src = lambda f: open(os.path.join(kdir, f)).read()
+    tiles = set()
+    glds = src("gemm_glds.hip")
+    body = glds[glds.index("#define CXG_KK_TILES"):glds.index("#define CXG_CASE")]
+    tiles |= {int(m) for m in re.findall(r"CXG_T[PC]?\((\d+),", body)}
+    tiles |= {int(m) for m in re.findall(r"case (\d+): launch_4f", src("gemm_4w.hip"))}
+    halo = src("conv_halo.hip")
+    tiles |= {int(m) for m in re.findall(r"tile == (\d+)", halo[halo.index("int dispatch_halo"):])}
+    wg = src("conv_wgrad_halo.hip")
+    tiles |= {int(m) for m in re.findall(r"tile [!=]= (\d+)", wg[wg.index("int dispatch_wgrad_halo"):])}
+    return tiles
+
+
+def test_tile_dict_matches_compiled_kernels():
+    """Every tile the Python side can name is compiled, and no compiled tile is orphaned."""
+    compiled = _compiled_tiles()
+    assert set(G.GLDS_TILES) == compiled, (sorted(set(G.GLDS_TILES) - compiled), sorted(compiled - set(G.GLDS_TILES)))
+
+
+def test_every_compiled_tile_is_used():
+    """A compiled tile is in the shipped table, a default pick, or the fc weight-grad set."""
+    used = {t for k, t in _table().items() if k.split("|")[0] != "cws"}
+    used |= {1, 7, 10, 15}  # _pick_glds defaults
+    used |= {141, 142}  # forced patch widths of the 140 kernel (same template instances)
+    unused = sorted(_compiled_tiles() - used)
+    assert not unused, unused
 
 
 def test_signature_keys_are_well_formed():
