@@ -30,8 +30,12 @@ __device__ __forceinline__ void unpack8(const uint4 &v, float *f) {
   f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
   f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
 }
+// Two floats -> one v_cvt_pk_bf16_f32 (the scalar form, f2bf | f2bf << 16, cost two converts
+// plus three re-packing ops per pair: the compiler pairs the converts across the wrong operands)
+typedef float cxn_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 cxn_bf16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return static_cast<uint32_t>(f2bf(a)) | (static_cast<uint32_t>(f2bf(b)) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((cxn_f32x2){a, b}, cxn_bf16x2));
 }
 __device__ __forceinline__ uint4 pack8(const float *f) {
   return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));

@@ -234,176 +234,8 @@ int launch(const bf16_t *x, long x_bytes, const bf16_t *w, const float *bias, bf
 }
 
 
-// ------------------------------------------------------------------------------------------
-// Weight gradient: dW[co][c] += sum_p dy[p][co] X[p][c] with c = (kh, jj) over the kernel rows'
-// runs (c < KH*LP) and p = output pixels.  The implicit GEMM form (MN-gather of x, split-K over
-// pixels) reads the overlapping runs ~7.6x and dy once per 128-column tile (AlexNet conv1:
-// 1.3 GB through L2, 159 us).  Here a block walks work items of WR output rows of one image and
-// stages, by LDS-DMA into a 3-deep ring (two items in flight ahead of the MFMAs), the item's
-// input span and its dy rows as 64 pixel slots per row of DPB bytes (slots past Wo, rows past Ho
-// and the slot pad load as zeros).  Both MFMA operands are [pixel][column] images read with
-// ds_read_b64_tr_b16 (T10): the K dimension of the product is the pixel, so lane quad p of a
-// 16-lane group supplies four consecutive columns of one pixel row:
-//   * A (16 co x 32 pixels): dy slots, columns co;
-//   * B (16 columns c x 32 pixels): four 4-column quads (kh, jj..jj+3) of the staged input rows
-//     -- a pixel row is the run at x row S*r + kh, offset wo*S*C, 8-byte aligned reads;
-// 8 waves, each owning CFH x KF 16x16 tiles of dW (co half x column quarter) for the whole grid
-// sweep in its accumulators; one fp32 atomic add per element per block at the end.
-constexpr int WR = 2;    // output rows per weight-grad work item
-constexpr int WS = 64;   // pixel slots per output row (Wo <= 64)
-
-template <int CFH, int KF>
-__global__ void __launch_bounds__(NT, 1)
-conv_rowrun_wgrad(const bf16_t *__restrict__ x, long x_bytes, const bf16_t *__restrict__ dy, long dy_bytes,
-                  float *__restrict__ dw, int N, int H, int W, int C, int Ho, int Wo, int KH, int LP, int S, int KR,
-                  int XB, int ndma_x, int DB, int ndma_d) {
-  constexpr int COUT = 32 * CFH;
-  constexpr int NWV = NT / 64;
-  // dy slot pitch: 32 * odd bytes (COUT/8 data chunks + 2), so the 8 consecutive slots a 32-lane
-  // half reads land on 8 distinct 8-dword bank ranges (conflict-free transposed reads)
-  constexpr int DCH = COUT / 8 + 2;
-  constexpr int DPB = DCH * 16;
-  static_assert((DPB / 32) % 2 == 1, "slot pitch 32 * odd bytes");
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int pitch = W * C * 2;
-  const int pxs = S * C * 2;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int g4 = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
-  const rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t *>(x), (short)0,
-                                                      static_cast<int>(x_bytes), 0x00020000);
-  const rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t *>(dy), (short)0,
-                                                      static_cast<int>(dy_bytes), 0x00020000);
-  const int groups_per_img = (Ho + WR - 1) / WR;
-  const long items = static_cast<long>(N) * groups_per_img;
-  const int stage = XB + DB;
-  char *scratch = smem + 3 * stage;  // 1 KiB sink of the dummy DMAs that keep per-wave counts equal
-  const int nx = (ndma_x + NWV - 1) / NWV, nd = (ndma_d + NWV - 1) / NWV;
-  // every wave issues exactly nx + nd DMAs per item (past the tensors / the item: zeros)
-  auto issue = [&](long it, int buf) {
-    const bool live = it < items;
-    const int n = live ? static_cast<int>(it / groups_per_img) : 0;
-    const int grp = live ? static_cast<int>(it - static_cast<long>(n) * groups_per_img) : 0;
-    const long xs = (static_cast<long>(n) * H + static_cast<long>(grp) * WR * S) * pitch;
-    char *dx = smem + buf * stage;
-    for (int i = 0; i < nx; ++i) {
-      const int q = wave + NWV * i;
-      const long off = xs + q * 1024 + lane * 16;
-      const uint32_t o = (live && q < ndma_x && off < x_bytes) ? static_cast<uint32_t>(off) : 0x80000000u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_void *)(q < ndma_x ? dx + q * 1024 : scratch), 16, o, 0, 0, 0);
-    }
-    char *dd = dx + XB;
-    for (int i = 0; i < nd; ++i) {
-      const int q = wave + NWV * i;
-      const int m = q * 64 + lane;  // LDS chunk
-      const int slot = m / DCH, part = m - slot * DCH;
-      const int r = slot / WS, wo = slot - r * WS;
-      const int ho = grp * WR + r;
-      uint32_t o = 0x80000000u;
-      if (live && q < ndma_d && part < DCH - 2 && wo < Wo && r < WR && ho < Ho)
-        o = static_cast<uint32_t>((((static_cast<long>(n) * Ho + ho) * Wo + wo) * COUT) * 2 + part * 16);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rd, (lds_void *)(q < ndma_d ? dd + q * 1024 : scratch), 16, o, 0, 0, 0);
-    }
-  };
-  long it = blockIdx.x;
-  issue(it, 0);
-  issue(it + gridDim.x, 1);
-
-  const int ch = wave & 1, kq = wave >> 1;  // co half, column quarter
-  int qoff[KF];  // this lane's quad (columns 4*p4 .. +3) of each of its KF 16-column fragments
-#pragma unroll
-  for (int kf = 0; kf < KF; ++kf) {
-    int c = ((kq * KF + kf) * 16 + 4 * p4);
-    if (c >= KR) c = KR - 4;  // pad columns: any in-range quad, never stored
-    const int quad = c >> 2, qpr = LP >> 2;
-    const int kh = quad / qpr, jj = 4 * (quad - kh * qpr);
-    qoff[kf] = kh * pitch + jj * 2;
-  }
-  // per k-step s (32 slots = half an output row) the lane's 8 K values are pixels 4*g4 + q4 (lo
-  // read) and + 16 (hi read): each read instruction's 32-lane half takes 8 consecutive pixels,
-  // whose x runs (24-byte steps) span < 256 bytes (shared words broadcast) and whose dy slots
-  // fall on distinct banks
-  const int w_lo = 4 * g4 + q4;
-  f32x4 acc[CFH][KF];
-#pragma unroll
-  for (int cf = 0; cf < CFH; ++cf)
-#pragma unroll
-    for (int kf = 0; kf < KF; ++kf) acc[cf][kf] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int buf = 0;
-  for (; it < items; it += gridDim.x) {
-    vm_wait(nx + nd);  // this item's DMAs landed (the next item's stay in flight)
-    __syncthreads();   // ... for every wave; every wave is done with the buffer refilled next
-    issue(it + 2L * gridDim.x, buf == 0 ? 2 : buf - 1);
-    const char *sx = smem + buf * stage;
-    const char *sd = sx + XB;
-#pragma unroll
-    for (int s = 0; s < WR * WS / 32; ++s) {
-      bf16x8 a[CFH], b[KF];
-      const int r = s / (WS / 32), w0 = (s % (WS / 32)) * 32 + w_lo;
-      const char *xlo = sx + r * S * pitch + w0 * pxs;
-      const char *xhi = xlo + 16 * pxs;
-      const char *dlo = sd + (s * 32 + w_lo) * DPB + 8 * p4;
-      const char *dhi = dlo + 16 * DPB;
-      typedef short s16x8 __attribute__((ext_vector_type(8)));
-#pragma unroll
-      for (int cf = 0; cf < CFH; ++cf) {
-        const int co = (ch * CFH + cf) * 32;  // byte offset of the fragment's 16 columns
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(dlo + co));
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(dhi + co));
-        const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        a[cf] = __builtin_bit_cast(bf16x8, v);
-      }
-#pragma unroll
-      for (int kf = 0; kf < KF; ++kf) {
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(xlo + qoff[kf]));
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(xhi + qoff[kf]));
-        const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        b[kf] = __builtin_bit_cast(bf16x8, v);
-      }
-#pragma unroll
-      for (int cf = 0; cf < CFH; ++cf)
-#pragma unroll
-        for (int kf = 0; kf < KF; ++kf)
-          acc[cf][kf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[cf], b[kf], acc[cf][kf], 0, 0, 0);
-    }
-    buf = buf == 2 ? 0 : buf + 1;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // D row = co (4*g4 + j of the fragment), column = c (i16)
-#pragma unroll
-  for (int cf = 0; cf < CFH; ++cf)
-#pragma unroll
-    for (int kf = 0; kf < KF; ++kf) {
-      const int c = (kq * KF + kf) * 16 + i16;
-      if (c < KR) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          atomicAdd(dw + static_cast<long>((ch * CFH + cf) * 16 + 4 * g4 + j) * KR + c, acc[cf][kf][j]);
-      }
-    }
-}
-
-template <int CFH, int KF>
-int launch_wgrad(const bf16_t *x, long x_bytes, const bf16_t *dy, long dy_bytes, float *dw, int N, int H, int W, int C,
-                 int Ho, int Wo, int KH, int LP, int S, hipStream_t s) {
-  const int KR = KH * LP;
-  const long span = static_cast<long>(S * (WR - 1) + KH) * W * C * 2 + 16;
-  const int ndma_x = static_cast<int>((span + 1023) / 1024);
-  const int XB = ndma_x * 1024;
-  const int dch = 32 * CFH / 8 + 2;
-  const int ndma_d = (WR * WS * dch + 63) / 64;
-  const int DB = ndma_d * 1024;
-  const long lds = 3L * (XB + DB) + 1024;
-  if (lds > 160 * 1024 || Wo > WS) return -1;
-  if ((ndma_x + 7) / 8 + (ndma_d + 7) / 8 > 15) return -1;
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void *>(conv_rowrun_wgrad<CFH, KF>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  if (attr != hipSuccess) return -1;  // once per instantiation (thread-safe static); -1: caller falls back
-  const long items = static_cast<long>(N) * ((Ho + WR - 1) / WR);
-  const int grid = static_cast<int>(items < 256 ? items : 256);
-  CXN_LAUNCH((conv_rowrun_wgrad<CFH, KF>), dim3(grid), dim3(NT), static_cast<size_t>(lds), s, x, x_bytes, dy,
-                     dy_bytes, dw, N, H, W, C, Ho, Wo, KH, LP, S, KR, XB, ndma_x, DB, ndma_d);
-  return 0;
-}
+// (A direct weight-gradient over the staged kernel-row runs lived here until round 5: 169-189 us
+// against the split-K GEMM's 159 on AlexNet conv1, profiles/r3_conv1_direct.md -- never shipped.)
 
 }  // namespace
 
@@ -435,26 +267,3 @@ CXN_API int cxn_conv_rowrun_fwd(const void *x, long x_bytes, const void *w, cons
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-// dw [Cout][KH*LP] fp32 += the weight gradient over kernel-row runs (columns (kh, jj), jj < LP:
-// positions past a row's KW*C elements get the products with the next pixels' values, which
-// the caller drops).  x as for cxn_conv_rowrun_fwd; dy: contiguous [N][Ho][Wo][Cout] bf16.
-// Served: (Cout, ceil(KH*LP/64)) in {(96, 7), (64, 4), (32, 2), (128, 3)}; -1 otherwise.
-CXN_API int cxn_conv_rowrun_wgrad(const void *x, long x_bytes, const void *dy, long dy_bytes, float *dw, int N, int H,
-                                  int W, int C, int Ho, int Wo, int Cout, int KH, int LP, int S, void *stream) {
-  if (LP % 8 || S < 1 || (S * C * 2) % 8 || (W * C * 2) % 8 || x_bytes >= (1L << 31) || dy_bytes >= (1L << 31))
-    return -1;
-  if ((Ho - 1) * S + KH > H || Wo < 1 || (reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(dy) & 15))
-    return -1;
-  if (dy_bytes != static_cast<long>(N) * Ho * Wo * Cout * 2) return -1;
-  const bf16_t *xb = static_cast<const bf16_t *>(x);
-  const bf16_t *db = static_cast<const bf16_t *>(dy);
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const int kf = (KH * LP + 63) / 64;
-  int rc = -1;
-  if (Cout == 96 && kf == 7) rc = launch_wgrad<3, 7>(xb, x_bytes, db, dy_bytes, dw, N, H, W, C, Ho, Wo, KH, LP, S, s);
-  else if (Cout == 64 && kf == 4) rc = launch_wgrad<2, 4>(xb, x_bytes, db, dy_bytes, dw, N, H, W, C, Ho, Wo, KH, LP, S, s);
-  else if (Cout == 32 && kf == 2) rc = launch_wgrad<1, 2>(xb, x_bytes, db, dy_bytes, dw, N, H, W, C, Ho, Wo, KH, LP, S, s);
-  else if (Cout == 128 && kf == 3) rc = launch_wgrad<4, 3>(xb, x_bytes, db, dy_bytes, dw, N, H, W, C, Ho, Wo, KH, LP, S, s);
-  if (rc != 0) return rc;
-  return hipGetLastError() == hipSuccess ? 0 : -3;
-}

@@ -490,6 +490,9 @@ int launch(const GOperand &A, const GOperand &B, const GEpi &E, int groups, int 
 
 int dispatch(int amode, int bmode, int epi, int tile, const GOperand &A, const GOperand &B, const GEpi &E,
              int groups, int ksplit, hipStream_t s) {
+  if (tile == 114) return cxg::dispatch_4w(amode, bmode, epi, tile, A, B, E, groups, ksplit, s);
+  if (tile >= 130 && tile <= 133) return cxg::dispatch_halo(amode, bmode, epi, tile, A, B, E, groups, ksplit, s);
+  if (tile >= 140 && tile <= 142) return cxg::dispatch_wgrad_halo(amode, bmode, epi, tile, A, B, E, groups, s);
   CXG_CASE(K_DIRECT, K_GATHER, EPI_BF16, CXG_KK_TILES)    // conv fwd / dgrad
   CXG_CASE(K_DIRECT, K_GATHER, EPI_BF16_DB, CXG_KK_TILES)  // conv dgrad + the lower conv's bias gradient
   CXG_CASE(K_DIRECT, K_ROWGATHER, EPI_BF16, CXG_KK_TILES)  // conv fwd, few input channels (conv1)

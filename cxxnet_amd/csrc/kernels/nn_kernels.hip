@@ -39,8 +39,8 @@ __global__ void nchw_f32_to_nhwc_bf16(const float *__restrict__ x, bf16_t *__res
       float v[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) v[c] = c < C ? src[static_cast<long>(c) * H * W] * scale : 0.f;
-      *reinterpret_cast<uint2 *>(dst) = make_uint2(static_cast<uint32_t>(f2bf(v[0])) | static_cast<uint32_t>(f2bf(v[1])) << 16,
-                                                   static_cast<uint32_t>(f2bf(v[2])) | static_cast<uint32_t>(f2bf(v[3])) << 16);
+      *reinterpret_cast<uint2 *>(dst) = make_uint2(pack2(v[0], v[1]),
+                                                   pack2(v[2], v[3]));
       continue;
     }
     for (int c = 0; c < Cp; ++c) dst[c] = c < C ? f2bf(src[static_cast<long>(c) * H * W] * scale) : 0;
@@ -94,8 +94,8 @@ __global__ void image_u8_to_nhwc_bf16(const uint8_t *__restrict__ pix, const int
   }
   bf16_t *dst = y + (static_cast<long>(row) * Wp + x) * Cp;
   if (Cp == 4) {  // one 8-byte store per pixel
-    *reinterpret_cast<uint2 *>(dst) = make_uint2(static_cast<uint32_t>(f2bf(v[0])) | static_cast<uint32_t>(f2bf(v[1])) << 16,
-                                                 static_cast<uint32_t>(f2bf(v[2])) | static_cast<uint32_t>(f2bf(v[3])) << 16);
+    *reinterpret_cast<uint2 *>(dst) = make_uint2(pack2(v[0], v[1]),
+                                                 pack2(v[2], v[3]));
   } else {
     for (int c = 0; c < Cp; ++c) dst[c] = c < 8 ? f2bf(v[c]) : static_cast<bf16_t>(0);
   }
@@ -176,8 +176,8 @@ __global__ void image_u8c3_nhwc3p(const uint32_t *__restrict__ pix, long ndw, co
     uint2 *dst = y + (static_cast<long>(row) * Wp + x0) * 3 / 4;  // 4 pixels = 24 bytes = three uint2
 #pragma unroll
     for (int t = 0; t < 3; ++t)
-      dst[t] = make_uint2(static_cast<uint32_t>(f2bf(out[4 * t])) | static_cast<uint32_t>(f2bf(out[4 * t + 1])) << 16,
-                          static_cast<uint32_t>(f2bf(out[4 * t + 2])) | static_cast<uint32_t>(f2bf(out[4 * t + 3])) << 16);
+      dst[t] = make_uint2(pack2(out[4 * t], out[4 * t + 1]),
+                          pack2(out[4 * t + 2], out[4 * t + 3]));
   }
 }
 
@@ -864,6 +864,11 @@ __global__ void pool_bwd_s2k3(const bf16_t *__restrict__ x, const uint8_t *__res
 }
 
 // ------------------------------------------------------------------ LRN
+// The norm's powers: norm = k + alpha / n * sum(x^2) >= k > 0 (k = 1 in every shipped net), so the
+// raw v_log_f32 / v_exp_f32 give exp2f / __log2f's values without their denormal-range fix-ups
+// (a compare, a select and a scale per call: a third of the fused pool -> LRN backward's VALU).
+__device__ __forceinline__ float lrn_log2(float x) { return __builtin_amdgcn_logf(x); }
+__device__ __forceinline__ float lrn_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 // norm[c] = knorm + alpha/n * sum_{c' in [c-h, c+h] clipped} x[c']^2 ; y = x * norm^-beta
 // One thread per (pixel, 8 channels); halo of up to 8 channels each side via three 16-B loads.
 __device__ __forceinline__ void load_window(const bf16_t *row, int C, int c0, float *buf /*[24]*/) {
@@ -902,7 +907,7 @@ __global__ void lrn_fwd(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, lo
         s += v * v;
       }
       const float norm = knorm + salpha * s;
-      out[e] = xb[8 + e] * exp2f(-beta * __log2f(norm));
+      out[e] = xb[8 + e] * lrn_exp2(-beta * lrn_log2(norm));
     }
     *reinterpret_cast<uint4 *>(y + pix * C + c0) = pack8(out);
   }
@@ -952,10 +957,10 @@ __global__ void lrn_bwd_lds(const bf16_t *x, const bf16_t *dy, bf16_t *dx, long 
         const float v = xs[c + d];
         s += v * v;
       }
-      const float lg = __log2f(knorm + salpha * s);
-      const float p = exp2f(-beta * lg);         // norm^-b
+      const float lg = lrn_log2(knorm + salpha * s);
+      const float p = lrn_exp2(-beta * lg);         // norm^-b
       ng[e] = gv[e] * p;
-      ts[c] = gv[e] * xv[e] * p * exp2f(-lg);    // g x norm^(-b-1)
+      ts[c] = gv[e] * xv[e] * p * lrn_exp2(-lg);    // g x norm^(-b-1)
     }
   }
   __syncthreads();
@@ -1034,7 +1039,7 @@ __global__ void lrn_fwd_shfl(const bf16_t *__restrict__ x, bf16_t *__restrict__ 
   if (!L.active) return;
   float out[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) out[e] = xv[e] * exp2f(-beta * __log2f(knorm + salpha * s[e]));
+  for (int e = 0; e < 8; ++e) out[e] = xv[e] * lrn_exp2(-beta * lrn_log2(knorm + salpha * s[e]));
   *reinterpret_cast<uint4 *>(y + off) = pack8(out);
 }
 
@@ -1058,10 +1063,10 @@ __global__ void lrn_bwd_shfl(const bf16_t *x, const bf16_t *__restrict__ dy, bf1
   float ng[8], t[8], ts[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const float lg = __log2f(knorm + salpha * s[e]);
-    const float p = exp2f(-beta * lg);  // norm^-b
+    const float lg = lrn_log2(knorm + salpha * s[e]);
+    const float p = lrn_exp2(-beta * lg);  // norm^-b
     ng[e] = gv[e] * p;
-    t[e] = gv[e] * xv[e] * p * exp2f(-lg);  // g x norm^(-b-1)
+    t[e] = gv[e] * xv[e] * p * lrn_exp2(-lg);  // g x norm^(-b-1)
   }
   lrn_window_sum<H>(t, L, ts);
   if (!L.active) return;
@@ -1082,12 +1087,14 @@ __global__ void lrn_bwd_shfl(const bf16_t *x, const bf16_t *__restrict__ dy, bf1
 //   forward : the 3x3 / 2 max window (first max, offset byte, relu' bit as pool_fwd_rows) ->
 //             pooled P and the LRN output Y in one pass: P is written (the LRN backward reads it)
 //             but not read back;
-//   backward: per 2x2 input cell (pool_bwd_s2k3's formulation) the LRN data-gradient of the
-//             four windows that cover it is recomputed from (P, dY) and routed by the offsets:
-//             the pooled gradient is never stored.  relu' of the routed pixel comes from bit 7
-//             of the offset.  With dbias the conv-bias gradient behind a relu'd pool (the
-//             _fuse_pool_bias sum of the pooled gradient, masked by bit 7) is summed on the way:
-//             window (ho, wo) counts in cell (ho, wo) only; per-block partial rows.
+//   backward: a block owns a band of R cell rows (2x2 input cells, pool_bwd_s2k3's
+//             formulation) of one image.  Phase 1 computes the LRN data-gradient of the band's
+//             windows (plus the row above, recomputed) from (P, dY) into LDS, masked by relu'
+//             (bit 7 of the offset) and rounded to bf16 as the separate layers store it; phase 2
+//             routes it from LDS to each cell's four pixels: the pooled gradient never reaches
+//             HBM.  With dbias the conv-bias gradient behind a relu'd pool (the _fuse_pool_bias
+//             sum of the pooled gradient) is summed over the band's own windows; per-block
+//             partial rows in a fixed order.
 template <int H>
 __global__ void pool_lrn_fwd(const bf16_t *__restrict__ x, bf16_t *__restrict__ P, uint8_t *__restrict__ arg,
                              bf16_t *__restrict__ Y, int N, int Hin, int Win, int C, int Ho, int Wo, int relu,
@@ -1151,116 +1158,164 @@ __global__ void pool_lrn_fwd(const bf16_t *__restrict__ x, bf16_t *__restrict__ 
   if (!L.active) return;
   float out[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) out[e] = pv[e] * exp2f(-beta * __log2f(knorm + salpha * sw[e]));
+  for (int e = 0; e < 8; ++e) out[e] = pv[e] * lrn_exp2(-beta * lrn_log2(knorm + salpha * sw[e]));
   *reinterpret_cast<uint4 *>(Y + o) = pack8(out);
 }
 
 template <int H>
-__global__ void lrn_pool_bwd(const bf16_t *__restrict__ P, const bf16_t *__restrict__ dY,
-                             const uint8_t *__restrict__ arg, bf16_t *__restrict__ dx, int N, int Hin, int Win, int C,
-                             int Ho, int Wo, int HC, int WC, int relu_bit, float salpha, float beta, float knorm,
-                             float *__restrict__ dbias_part) {
-  const long ncell = static_cast<long>(N) * HC * WC;
-  const LrnLane L = lrn_lane(ncell, C);
-  int n = 0, ci = 0, cj = 0;
-  if (L.active) {
-    n = static_cast<int>(L.pix / (static_cast<long>(HC) * WC));
-    const int rem = static_cast<int>(L.pix - static_cast<long>(n) * HC * WC);
-    ci = rem / WC;
-    cj = rem - ci * WC;
-  }
-  float g[4][8], bsum[8];
+__global__ void __launch_bounds__(NT)
+lrn_pool_bwd(const bf16_t *__restrict__ P, const bf16_t *__restrict__ dY, const uint8_t *__restrict__ arg,
+             bf16_t *__restrict__ dx, int Hin, int Win, int C, int Ho, int Wo, int HC, int WC, int R, int nband,
+             int relu_bit, float salpha, float beta, float knorm, float *__restrict__ dbias_part) {
+  extern __shared__ __attribute__((aligned(16))) char plds[];
+  const int tpp = C / 8, ppw = 64 / tpp;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int pl = lane / tpp, cv = lane - pl * tpp;
+  const bool lane_ok = pl < ppw;
+  LrnLane L;  // lrn_window_sum's view: channel block cv of a pixel of tpp lanes
+  L.tpp = tpp;
+  L.cv = cv;
+  L.pix = 0;
+  L.active = lane_ok;
+  const int n = blockIdx.x / nband, band = blockIdx.x - n * nband;
+  const int c0 = band * R;                                            // first cell row
+  const int h_lo = max(c0 - 1, 0), h_hi = min(c0 + R - 1, Ho - 1);    // window rows it reads
+  const int nwin = (h_hi - h_lo + 1) * Wo;
+  bf16_t *const gl = reinterpret_cast<bf16_t *>(plds);                          // [window][C] gradient
+  uint8_t *const al = reinterpret_cast<uint8_t *>(plds + static_cast<size_t>(R + 1) * Wo * C * 2);  // offsets
+  const int step = (NT / 64) * ppw;
+  // per-image bases (64-bit once); offsets inside one image fit 32 bits (checked by the launcher)
+  const long pimg = static_cast<long>(n) * Ho * Wo * C;
+  const bf16_t *const Pn = P + pimg;
+  const bf16_t *const dYn = dY + pimg;
+  const uint8_t *const an = arg + pimg;
+  bf16_t *const dxn = dx + static_cast<long>(n) * Hin * Win * C;
+  float bsum[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) bsum[k] = 0.f;
-  uint2 a[4];
-  bool ok[4];
-#pragma unroll
-  for (int pq = 0; pq < 4; ++pq) {
-    const int p = pq >> 1, q = pq & 1;
-    const int ho = ci - 1 + p, wo = cj - 1 + q;
-    ok[pq] = L.active && ho >= 0 && ho < Ho && wo >= 0 && wo < Wo;
+  // phase 1: the LRN data-gradient of every window of the band (and of the row above it), masked
+  // by relu', rounded to bf16 as the separate layers store it, into LDS with the offsets
+  // (window row, column) of this lane's window, advanced by `step` windows per pass (no divides)
+  int wr = (wave * ppw + pl) / Wo, wc = (wave * ppw + pl) - wr * Wo;
+  for (int base = 0; base < nwin; base += step) {
+    const int wi = base + wave * ppw + pl;
+    const bool ok = lane_ok && wi < nwin;
+    const int ho = h_lo + wr, wo = wc;
+    wc += step;
+    while (wc >= Wo) {
+      wc -= Wo;
+      ++wr;
+    }
     float xv[8], gv[8];
-    a[pq] = make_uint2(0u, 0u);
-    if (ok[pq]) {
-      const long o = ((static_cast<long>(n) * Ho + ho) * Wo + wo) * C + L.cv * 8;
-      unpack8(*reinterpret_cast<const uint4 *>(P + o), xv);
-      unpack8(*reinterpret_cast<const uint4 *>(dY + o), gv);
-      a[pq] = *reinterpret_cast<const uint2 *>(arg + o);
+    uint2 a = make_uint2(0u, 0u);
+    if (ok) {
+      const int o = (ho * Wo + wo) * C + cv * 8;
+      unpack8(*reinterpret_cast<const uint4 *>(Pn + o), xv);
+      unpack8(*reinterpret_cast<const uint4 *>(dYn + o), gv);
+      a = *reinterpret_cast<const uint2 *>(an + o);
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) xv[e] = gv[e] = 0.f;
     }
-    // LRN data-gradient of window (ho, wo) (as lrn_bwd_shfl; every lane takes part in the shuffles)
-    float sq[8], s[8], t[8], ts[8], ng[8];
+    float sq[8], sw[8], t[8], ts[8], ng[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) sq[e] = xv[e] * xv[e];
-    lrn_window_sum<H>(sq, L, s);
+    lrn_window_sum<H>(sq, L, sw);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float lg = __log2f(knorm + salpha * s[e]);
-      const float pw = exp2f(-beta * lg);
+    for (int e = 0; e < 8; ++e) {  // as lrn_bwd_shfl
+      const float lg = lrn_log2(knorm + salpha * sw[e]);
+      const float pw = lrn_exp2(-beta * lg);
       ng[e] = gv[e] * pw;
-      t[e] = gv[e] * xv[e] * pw * exp2f(-lg);
+      t[e] = gv[e] * xv[e] * pw * lrn_exp2(-lg);
     }
     lrn_window_sum<H>(t, L, ts);
+    if (!ok) continue;
     float gp[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) gp[e] = ng[e] - 2.f * beta * salpha * xv[e] * ts[e];
-    // the stored pooled gradient is bf16 in the unfused pair: round the same way
-    const uint4 gpk = pack8(gp);
-    unpack8(gpk, gp);
-    const uint32_t ab[8] = {a[pq].x & 0xff, (a[pq].x >> 8) & 0xff, (a[pq].x >> 16) & 0xff, a[pq].x >> 24,
-                            a[pq].y & 0xff, (a[pq].y >> 8) & 0xff, (a[pq].y >> 16) & 0xff, a[pq].y >> 24};
+    unpack8(pack8(gp), gp);
+    const uint32_t ab[8] = {a.x & 0xff, (a.x >> 8) & 0xff, (a.x >> 16) & 0xff, a.x >> 24,
+                            a.y & 0xff, (a.y >> 8) & 0xff, (a.y >> 16) & 0xff, a.y >> 24};
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float gm = (relu_bit && (ab[e] & 0x80u)) ? 0.f : gp[e];
-      g[pq][e] = gm;
-      if (pq == 3 && ok[pq]) bsum[e] += gm;  // window (ci, cj): counted by this cell only
-    }
+    for (int e = 0; e < 8; ++e) gp[e] = (relu_bit && (ab[e] & 0x80u)) ? 0.f : gp[e];
+    if (ho >= c0)  // rows c0.. are this band's own windows (row c0 - 1 belongs to the band above)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bsum[e] += gp[e];
+    *reinterpret_cast<uint4 *>(gl + static_cast<long>(wi) * C + cv * 8) = pack8(gp);
+    *reinterpret_cast<uint2 *>(al + static_cast<long>(wi) * C + cv * 8) =
+        make_uint2(a.x & 0x7f7f7f7fu, a.y & 0x7f7f7f7fu);
   }
-  if (L.active) {
+  __syncthreads();
+  // phase 2: per 2x2 input cell the four windows that cover it (pool_bwd_s2k3's formulation)
+  const int ncell = (min(c0 + R, HC) - c0) * WC;
+  int cr = (wave * ppw + pl) / WC, cc = (wave * ppw + pl) - cr * WC;
+  for (int base = 0; base < ncell; base += step) {
+    const int ce = base + wave * ppw + pl;
+    const int ci = c0 + cr, cj = cc;
+    cc += step;
+    while (cc >= WC) {
+      cc -= WC;
+      ++cr;
+    }
+    if (!lane_ok || ce >= ncell) continue;
+    uint4 g[4];
+    uint2 a[4];
+    bool okw[4];
 #pragma unroll
-    for (int r = 0; r < 2; ++r)
+    for (int pq = 0; pq < 4; ++pq) {
+      const int ho = ci - 1 + (pq >> 1), wo = cj - 1 + (pq & 1);
+      okw[pq] = ho >= 0 && ho < Ho && wo >= 0 && wo < Wo;
+      const int wi = okw[pq] ? (ho - h_lo) * Wo + wo : 0;
+      g[pq] = *reinterpret_cast<const uint4 *>(gl + static_cast<long>(wi) * C + cv * 8);
+      a[pq] = *reinterpret_cast<const uint2 *>(al + static_cast<long>(wi) * C + cv * 8);
+    }
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr)
 #pragma unroll
       for (int sx = 0; sx < 2; ++sx) {
-        const int h = 2 * ci + r, w = 2 * cj + sx;
+        const int h = 2 * ci + rr, w = 2 * cj + sx;
         if (h >= Hin || w >= Win) continue;
         float out[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) out[k] = 0.f;
 #pragma unroll
         for (int pq = 0; pq < 4; ++pq) {
-          const int p = pq >> 1, q = pq & 1;
-          const int kh = 2 + r - 2 * p, kw = 2 + sx - 2 * q;  // tap of (h, w) in window (ci-1+p, cj-1+q)
-          if (kh > 2 || kw > 2 || !ok[pq]) continue;
+          const int kh = 2 + rr - 2 * (pq >> 1), kw = 2 + sx - 2 * (pq & 1);  // tap of (h, w) in the window
+          if (kh > 2 || kw > 2 || !okw[pq]) continue;
           const uint32_t off = static_cast<uint32_t>(kh * 3 + kw);
+          float gv[8];
+          unpack8(g[pq], gv);
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            out[k] += (((a[pq].x >> (8 * k)) & 0x7f) == off) ? g[pq][k] : 0.f;
-            out[k + 4] += (((a[pq].y >> (8 * k)) & 0x7f) == off) ? g[pq][k + 4] : 0.f;
+            out[k] += ((a[pq].x >> (8 * k)) & 0xff) == off ? gv[k] : 0.f;
+            out[k + 4] += ((a[pq].y >> (8 * k)) & 0xff) == off ? gv[k + 4] : 0.f;
           }
         }
-        *reinterpret_cast<uint4 *>(dx + ((static_cast<long>(n) * Hin + h) * Win + w) * C + L.cv * 8) = pack8(out);
+        *reinterpret_cast<uint4 *>(dxn + (h * Win + w) * C + cv * 8) = pack8(out);
       }
   }
-  if (dbias_part != nullptr) {
-    __shared__ float red[512];
-    for (int c = threadIdx.x; c < C; c += blockDim.x) red[c] = 0.f;
-    __syncthreads();
-    if (L.active)
+  if (dbias_part != nullptr) {  // the block's column sums in a fixed order (wave, pixel): no atomics
+    __shared__ float red[NT / 64][64][9];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) atomicAdd(&red[L.cv * 8 + k], bsum[k]);
+    for (int k = 0; k < 8; ++k) red[wave][lane][k] = lane_ok ? bsum[k] : 0.f;
     __syncthreads();
-    for (int c = threadIdx.x; c < C; c += blockDim.x) dbias_part[static_cast<long>(blockIdx.x) * C + c] = red[c];
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      const int cc = c >> 3, k = c & 7;
+      float acc = 0.f;
+      for (int w = 0; w < NT / 64; ++w)
+        for (int j = 0; j < ppw; ++j) acc += red[w][j * tpp + cc][k];
+      dbias_part[static_cast<long>(blockIdx.x) * C + c] = acc;
+    }
   }
 }
 
 // db[c] += sum_r part[r][c] over nrows fp32 partial rows of C columns: 32 columns x 8 row groups
-// per block over a chunk of 256 rows, one atomic per column per chunk
-__global__ void part_rows_colsum(const float *__restrict__ part, int nrows, int C, float *__restrict__ db) {
+// per block over a chunk of `chunk` rows, one atomic per column per chunk (one chunk: a fixed
+// summation order, the deterministic mode)
+__global__ void part_rows_colsum(const float *__restrict__ part, int nrows, int C, float *__restrict__ db, int chunk) {
   const int c = blockIdx.x * 32 + (threadIdx.x & 31);
   const int rg = threadIdx.x >> 5;
-  const int r0 = blockIdx.y * 256, r1 = min(nrows, r0 + 256);
+  const int r0 = blockIdx.y * chunk, r1 = min(nrows, r0 + chunk);
   float acc = 0.f;
   if (c < C)
     for (int r = r0 + rg; r < r1; r += 8) acc += part[static_cast<long>(r) * C + c];
@@ -1301,7 +1356,7 @@ __global__ void lrn_bwd(const bf16_t *__restrict__ x, const bf16_t *__restrict__
       }
       const float norm = knorm + salpha * s;
       normv[j] = norm;
-      tv[j] = gb[j] * xb[j] * exp2f((-beta - 1.f) * __log2f(norm));
+      tv[j] = gb[j] * xb[j] * lrn_exp2((-beta - 1.f) * lrn_log2(norm));
     }
     float out[8];
 #pragma unroll
@@ -1309,7 +1364,7 @@ __global__ void lrn_bwd(const bf16_t *__restrict__ x, const bf16_t *__restrict__
       const int j = 8 + e;
       float s = 0.f;
       for (int d = -half; d <= half; ++d) s += tv[j + d];
-      out[e] = gb[j] * exp2f(-beta * __log2f(normv[j])) - 2.f * beta * salpha * xb[j] * s;
+      out[e] = gb[j] * lrn_exp2(-beta * lrn_log2(normv[j])) - 2.f * beta * salpha * xb[j] * s;
       if (mask_relu && !(xb[j] > 0.f)) out[e] = 0.f;
     }
     *reinterpret_cast<uint4 *>(dx + pix * C + c0) = pack8(out);
@@ -2212,23 +2267,33 @@ CXN_API int cxn_pool_lrn_fwd(const void *x, void *P, void *arg, void *Y, int N, 
 }
 // dbias_part: fp32 [blocks][C] per-block partial sums of the masked pooled gradient (null: no
 // bias sum); part_rows < 0: only return the block count.  Returns the block count (>= 0), -1
-// when not served, -4 when part_rows is too small.  The caller sums the partial rows.
+// when not served, -4 when part_rows is too small.  det: the partial rows summed in one fixed
+// order (else 256-row chunks added atomically).
 CXN_API int cxn_lrn_pool_bwd(const void *P, const void *dY, const void *arg, void *dx, int N, int Hin, int Win, int C,
                              int Ho, int Wo, int relu_bit, int nsize, float alpha, float beta, float knorm,
-                             float *dbias, float *dbias_part, long part_rows, void *stream) {
+                             float *dbias, float *dbias_part, long part_rows, int det, void *stream) {
   const int tpp = C / 8, half = nsize / 2;
-  if (C % 8 || tpp > 64 || C > 512 || half > 4 || Hin < 3 || Win < 3) return -1;
+  if (C % 8 || tpp > 64 || half > 4 || Hin < 3 || Win < 3 || N < 1) return -1;
   if (Ho != min(Hin - 2, Hin - 1) / 2 + 1 || Wo != min(Win - 2, Win - 1) / 2 + 1) return -1;
   const int HC = (Hin + 1) / 2, WC = (Win + 1) / 2;
-  const long ncell = static_cast<long>(N) * HC * WC;
-  const long waves = (ncell + 64 / tpp - 1) / (64 / tpp);
-  const int blocks = static_cast<int>((waves + NT / 64 - 1) / (NT / 64));
+  // cell rows per block: the band's windows (R + 1 rows: one row recomputed) staged in LDS as bf16
+  // gradient + offset byte, within 56 KiB of dynamic LDS (the bias partials take 9 KiB more)
+  const long row_bytes = static_cast<long>(Wo) * C * 3;
+  int R = 4;
+  while (R > 1 && (R + 1) * row_bytes > 56 * 1024) --R;
+  if ((R + 1) * row_bytes > 56 * 1024) return -1;
+  if (static_cast<long>(Hin) * Win * C >= (1L << 31)) return -1;  // 32-bit offsets inside an image
+  const int nband = (HC + R - 1) / R;
+  const long blocks_l = static_cast<long>(N) * nband;
+  if (blocks_l >= (1L << 31)) return -1;
+  const int blocks = static_cast<int>(blocks_l);
   if (part_rows < 0) return blocks;  // query
   const float sa = alpha / nsize;
   float *part = dbias != nullptr ? dbias_part : nullptr;
   if (dbias != nullptr && (part == nullptr || part_rows < blocks)) return -4;
-#define CXN_PLB(HV) CXN_LAUNCH((lrn_pool_bwd<HV>), blocks, NT, 0, S_, (const bf16_t *)P, (const bf16_t *)dY,   \
-                               (const uint8_t *)arg, (bf16_t *)dx, N, Hin, Win, C, Ho, Wo, HC, WC, relu_bit, sa, \
+  const size_t lds = static_cast<size_t>((R + 1) * row_bytes);
+#define CXN_PLB(HV) CXN_LAUNCH((lrn_pool_bwd<HV>), blocks, NT, lds, S_, (const bf16_t *)P, (const bf16_t *)dY,        \
+                               (const uint8_t *)arg, (bf16_t *)dx, Hin, Win, C, Ho, Wo, HC, WC, R, nband, relu_bit, sa, \
                                beta, knorm, part)
   switch (half) {
     case 0: CXN_PLB(0); break;
@@ -2238,8 +2303,11 @@ CXN_API int cxn_lrn_pool_bwd(const void *P, const void *dY, const void *arg, voi
     default: CXN_PLB(4); break;
   }
 #undef CXN_PLB
-  if (part != nullptr)
-    CXN_LAUNCH((part_rows_colsum), dim3((C + 31) / 32, (blocks + 255) / 256), NT, 0, S_, part, blocks, C, dbias);
+  if (part != nullptr) {
+    const int chunk = det ? blocks : 256;
+    CXN_LAUNCH((part_rows_colsum), dim3((C + 31) / 32, (blocks + chunk - 1) / chunk), NT, 0, S_, part, blocks, C,
+               dbias, chunk);
+  }
   if (hipGetLastError() != hipSuccess) return -3;
   return blocks;
 }

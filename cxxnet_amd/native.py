@@ -78,7 +78,6 @@ _SIGS = {
     "cxn_zero": [_P, _L, _P],
     "cxn_add_rows_f32": [_P, _P, _L, _I, _I, _P],
     "cxn_conv_rowrun_fwd": [_P, _L, _P, _P, _P] + [_I] * 12 + [_P],
-    "cxn_conv_rowrun_wgrad": [_P, _L, _P, _L, _P] + [_I] * 10 + [_P],
     "cxn_conv_fewc_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "cxn_chan_reduce": [_P, _P, _P, _P, _L, _I, _I, _P],
     "cxn_bn_stats": [_P, _P, _P, _P, _L, _I, _F, _P],
@@ -106,7 +105,7 @@ _SIGS = {
     "cxn_lrn_fwd": [_P, _P, _L, _I, _I, _F, _F, _F, _P],
     "cxn_lrn_bwd": [_P, _P, _P, _L, _I, _I, _F, _F, _F, _I, _P],
     "cxn_pool_lrn_fwd": [_P, _P, _P, _P] + [_I] * 8 + [_F, _F, _F, _P],
-    "cxn_lrn_pool_bwd": [_P, _P, _P, _P] + [_I] * 8 + [_F, _F, _F, _P, _P, _L, _P],
+    "cxn_lrn_pool_bwd": [_P, _P, _P, _P] + [_I] * 8 + [_F, _F, _F, _P, _P, _L, _I, _P],
     "cxn_act_fwd": [_P, _P, _P, _L, _I, _F, _P],
     "cxn_act_bwd": [_P, _P, _P, _L, _I, _F, _P],
     "cxn_dropout": [_P, _P, _L, _U, _P, _F, _P],

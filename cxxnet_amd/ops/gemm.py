@@ -607,7 +607,6 @@ _FEWC = os.environ.get("CXXNET_FEWC", "1") != "0"
 # direct row-run forward (conv_rowrun.hip: input rows staged once per 4 output rows) for the
 # few-channel pad-0 first layer (AlexNet conv1) instead of the K_ROWGATHER GEMM
 _ROWRUN_DIRECT = os.environ.get("CXXNET_ROWRUN_DIRECT", "1") != "0"
-_ROWRUN_WGRAD = os.environ.get("CXXNET_ROWRUN_WGRAD", "0") == "1"
 
 
 def fewc_ok(x, g: ConvGeom) -> bool:
@@ -882,17 +881,6 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom, db=None) -> bool:
         key = ("cwr", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride)
         from .nn import zero_
         zero_(ws)  # library memset / add below: a replayed launch list repeats them (torch ops it would not)
-        if _ROWRUN_WGRAD and not _DET["on"] and x.is_contiguous() and dy.is_contiguous():
-            # conv_rowrun.hip: input rows and dy rows staged once per 2 output rows (off by default:
-            # 169-189 us against the split-K GEMM's 159 on AlexNet conv1, profiles/r3_conv1_direct.md)
-            rc = native.kernels().cxn_conv_rowrun_wgrad(
-                x.data_ptr(), x.numel() * x.element_size(), dy.data_ptr(), dy.numel() * dy.element_size(), ws.data_ptr(),
-                g.N, g.H, g.W, g.C, g.Ho, g.Wo, g.Cout, g.KH, lp, g.stride, _stream())
-            if rc == 0:
-                _add_rows(ws, dw, g.Cout * g.KH, g.KW * g.C, lp)
-                return
-            if rc != -1:
-                native.check(rc, "conv_rowrun_wgrad")
         if run(_tuned_tile(key, run, ws, lambda: 1), ws):
             _add_rows(ws, dw, g.Cout * g.KH, g.KW * g.C, lp)
             return

@@ -264,7 +264,7 @@ def lrn_pool_backward(pooled, dy, state, dx, relu_bit, nsize, alpha, beta, knorm
                                int(relu_bit), int(nsize), float(alpha), float(beta), float(knorm),
                                dbias.data_ptr() if dbias is not None else None,
                                part.data_ptr() if part is not None else None,
-                               part.shape[0] if part is not None else 0, _stream())
+                               part.shape[0] if part is not None else 0, int(_det()), _stream())
     if rc == -1:
         return False
     if rc < 0:
@@ -276,7 +276,7 @@ def lrn_pool_backward_rows(x_shape, pooled_shape, nsize) -> int:
     """Partial rows lrn_pool_backward needs for its bias sum (0: not served)."""
     N, H, W, C = x_shape
     rc = _k().cxn_lrn_pool_bwd(None, None, None, None, N, H, W, C, pooled_shape[1], pooled_shape[2], 1, int(nsize),
-                               0.0, 0.0, 1.0, None, None, -1, None)
+                               0.0, 0.0, 1.0, None, None, -1, 0, None)
     return max(int(rc), 0)
 
 

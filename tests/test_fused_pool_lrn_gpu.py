@@ -1,5 +1,6 @@
 """Max-pool -> LRN fused (NeuralNet._fuse_pool_lrn; ops.pool_lrn_forward / lrn_pool_backward) on
-AlexNet against the separate layers (CXXNET_FUSE_POOL_LRN=0): after one training step every
+AlexNet against the separate layers (CXXNET_FUSE_POOL_LRN=0), both in deterministic mode:
+after one training step every
 parameter is bitwise the same, except the biases of conv1 / conv2, whose gradient the fused
 backward sums in another order (fp32 partial rows instead of the column-sum pass); and the
 fused kernels' outputs against fp32 torch pooling + LRN."""
@@ -19,8 +20,9 @@ def _alexnet(batch, fuse, monkeypatch):
     monkeypatch.setenv("CXXNET_FUSE_POOL_LRN", fuse)
     tr = NetTrainer()
     base = [(k, v) for k, v in load_conf("alexnet", []) if not k.startswith("metric")]
+    # deterministic: the split-K weight-gradients' fp32 atomics would differ run to run
     for k, v in base + [("batch_size", str(batch)), ("dev", "gpu"), ("eval_train", "0"), ("silent", "1"),
-                        ("seed", "11")]:
+                        ("seed", "11"), ("deterministic", "1")]:
         tr.set_param(k, v)
     tr.init_model()
     pools = [c.layer for c in tr.net.connections if type(c.layer).__name__ == "PoolingLayer"]
@@ -85,3 +87,30 @@ def test_pool_lrn_kernels_vs_torch(H, C, relu):
     assert err < 2e-2, err
     dbr = gp.sum((0, 2, 3))
     assert ((db - dbr).norm() / dbr.norm()).item() < 2e-2
+
+
+def test_pool_lrn_bias_sum_deterministic():
+    """Deterministic mode: the fused backward's conv-bias sum (per-block rows in a fixed order,
+    then one ordered pass over the rows) is bitwise repeatable; 64 images of AlexNet pool1 give
+    448 partial rows (more than one 256-row chunk)."""
+    from cxxnet_amd.ops import gemm
+    N, H, C, n = 64, 55, 96, 5
+    torch.manual_seed(0)
+    x = torch.randn(N, H, H, C, device="cuda").clamp_min(0).to(torch.bfloat16)
+    Ho = (H - 3) // 2 + 1
+    P = torch.empty(N, Ho, Ho, C, device="cuda", dtype=torch.bfloat16)
+    st = torch.empty(N, Ho, Ho, C, device="cuda", dtype=torch.uint8)
+    Y = torch.empty_like(P)
+    assert ops.pool_lrn_forward(x, P, st, Y, 2, n, 1e-4, 0.75, 1.0)
+    dY = torch.randn_like(Y)
+    dx = torch.empty_like(x)
+    rows = ops.lrn_pool_backward_rows(x.shape, P.shape, n)
+    assert rows > 256
+    part = torch.empty(rows, C, device="cuda")
+    gemm.set_deterministic(True)
+    out = []
+    for _ in range(3):
+        db = torch.zeros(C, device="cuda")
+        assert ops.lrn_pool_backward(P, dY, st, dx, 1, n, 1e-4, 0.75, 1.0, dbias=db, part=part)
+        out.append(db)
+    assert torch.equal(out[0], out[1]) and torch.equal(out[0], out[2])

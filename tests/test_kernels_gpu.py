@@ -452,32 +452,6 @@ def test_conv_rowrun_direct_forward(N, H, W, C, Cout, K, S, relu):
     assert relerr(y.permute(0, 3, 1, 2), ref) < 1e-2
 
 
-@pytest.mark.parametrize("N,H,W,C,Cout,K,S", [(2, 227, 228, 3, 96, 11, 4), (16, 227, 228, 3, 96, 11, 4),
-                                               (40, 227, 228, 3, 96, 11, 4),  # several work items per block
-                                               (3, 35, 36, 4, 64, 7, 2), (2, 43, 44, 3, 128, 7, 4),
-                                               (5, 30, 32, 3, 32, 5, 4)])
-def test_conv_rowrun_direct_wgrad(N, H, W, C, Cout, K, S):
-    """conv_rowrun.hip weight gradient (tr16-read [pixel][column] images of the staged input rows
-    and dy slots) called directly -- rc 0, no GEMM fallback -- against fp32 torch; the run
-    columns past KW*C (products with the next pixels) are dropped as the caller does."""
-    from cxxnet_amd import native
-    torch.manual_seed(N + 3 * K)
-    x = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16)
-    Ho, Wo = (H - K) // S + 1, (W - K) // S + 1
-    dy = torch.randn(N, Ho, Wo, Cout, device=DEV).to(torch.bfloat16)
-    lp = (K * C + 7) // 8 * 8
-    ws = torch.zeros(Cout, K * lp, device=DEV)
-    rc = native.kernels().cxn_conv_rowrun_wgrad(x.data_ptr(), x.numel() * 2, dy.data_ptr(), dy.numel() * 2,
-                                                ws.data_ptr(), N, H, W, C, Ho, Wo, Cout, K, lp, S,
-                                                torch.cuda.current_stream().cuda_stream)
-    assert rc == 0
-    torch.cuda.synchronize()
-    dw = ws.view(Cout, K, lp)[:, :, :K * C].reshape(Cout, K, K, C)
-    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (Cout, C, K, K), dy.float().permute(0, 3, 1, 2),
-                                      stride=S)
-    assert relerr(dw.permute(0, 3, 1, 2), ref) < 1e-2
-
-
 def test_conv1_three_channel_row_runs_deterministic():
     """Deterministic mode (left on by a trainer with deterministic = 1) keeps the 3-channel
     row-run weight-gradient: one K slice, bitwise equal on a repeat, and still exact."""
