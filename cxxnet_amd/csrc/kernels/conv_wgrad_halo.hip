@@ -19,8 +19,9 @@
 //   * 4 waves (one per SIMD), wave w owns input channels 16w..16w+15 of the pair: per K-step
 //     it reads 4 dy fragments and 9 halo fragments (one per tap) and issues 36 MFMAs into
 //     4 x 9 accumulators pinned in AGPRs (144 registers) that live across all its patches;
-//   * double-buffered: the next patch's 46 DMAs are issued (12 per wave) as a patch starts, one
-//     barrier per patch, at its end; fragment reads of K-step r + 1 ride on the MFMAs of K-step r;
+//   * double-buffered: the next patch's 46 DMAs are issued (12 per wave, inline asm: see dma16w)
+//     as a patch starts, one barrier per patch, at its end; fragment reads of K-step r + 1 ride on
+//     the MFMAs of K-step r;
 //   * persistent split over pixels: (pairs x splits) ~ one block per CU, consecutive blocks
 //     (one XCD) share a pixel range so its x / dy bytes are fetched into that XCD's L2 once;
 //   * epilogue: one fp32 atomic per accumulator element (the split-K kernels do the same).
@@ -30,8 +31,16 @@ using namespace cxg;
 
 namespace {
 
-__device__ __forceinline__ void dma16w(rsrc_t r, char *dst, uint32_t voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void *)dst, 16, voff, 0, 0, 0);
+// One 1-KiB LDS-DMA (16 bytes per lane) as inline asm.  With the builtin, hipcc cannot tell the
+// next patch's LDS bytes from the ones the current patch's ds_reads touch and puts a vmcnt(0)
+// before the first ds_read after the DMAs: every patch then waited for all of the next patch's
+// HBM loads at its first K-step instead of letting them land under its 144 MFMAs.  Completion
+// is counted by hand (wait_vmcnt + barrier at the patch end).  M0 is saved and restored inside
+// the statement (compiler-reserved).
+__device__ __forceinline__ void dma16w(rsrc_t r, uint32_t lds_addr, uint32_t voff) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(r), "s"(lds_addr) : "memory");
 }
 
 template <int N>
@@ -95,6 +104,7 @@ conv_wgrad_halo(GOperand X, GOperand D, GEpi E, int npairs, int ncib, int per, i
   const int Hx = X.H, Wx = X.W, Ho = X.Ho, Wo = X.Wo;
   const rsrc_t rx = make_rsrc(X.ptr, X.nbytes), rd = make_rsrc(D.ptr, D.nbytes);
   const uint32_t xpb = static_cast<uint32_t>(X.C) * 2u, dpb = static_cast<uint32_t>(D.ld) * 2u;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void *)smem)));
 
   // this wave's DMA slots s: s < 8 halo group G = wave + 4 s (G < NGH), s >= 8 dy group
   // q = wave + 4 (s - 8).  Per lane only the column and the swizzled chunk offset are kept;
@@ -149,7 +159,7 @@ conv_wgrad_halo(GOperand X, GOperand D, GEpi E, int npairs, int ncib, int per, i
     const int gr = r0 + drow, gc = c0 + dcol[s];
     const bool ok = static_cast<unsigned>(gr) < static_cast<unsigned>(HH) && static_cast<unsigned>(gc) < static_cast<unsigned>(WW);
     const uint32_t pix = static_cast<uint32_t>((img * HH + gr) * WW + gc);
-    dma16w(rs, smem + b * BUF + dst, ok ? pix * pb + loff[s] : OOB);
+    dma16w(rs, lds0 + static_cast<uint32_t>(b * BUF + dst), ok ? pix * pb + loff[s] : OOB);
   };
 
   // fragment read bases (bytes) per buffer: lane (l16, g4) reads k-rows pk and pk + 4
