@@ -38,15 +38,16 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--model", default="alexnet")
     ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--graph", type=int, default=0)
+    ap.add_argument("--graph", type=int, default=-1, help="cuda_graph (-1: the trainer's default, launch lists)")
     a = ap.parse_args()
     from cxxnet_amd.io.data import DataBatch
     from cxxnet_amd.models import load_conf
     from cxxnet_amd.nnet import NetTrainer
     from cxxnet_amd.parallel import init_distributed
     init_distributed()
-    pairs = load_conf(a.model, [("batch_size", str(a.batch)), ("eval_train", "0"), ("dev", "gpu"), ("silent", "1"),
-                                ("cuda_graph", str(a.graph))])
+    extra = [("cuda_graph", str(a.graph))] if a.graph >= 0 else []
+    pairs = load_conf(a.model, [("batch_size", str(a.batch)), ("eval_train", "0"), ("dev", "gpu"), ("silent", "1")]
+                      + extra)
     tr = NetTrainer()
     for k, v in pairs:
         if not k.startswith("metric"):
