@@ -6,7 +6,11 @@ import os
 import sys
 from collections import defaultdict
 
-MATCH = os.environ.get("PMC_MATCH", "gemm")  # kernel-name substring (hipBLASLt: Cijk)
+MATCH = os.environ.get("PMC_MATCH", "gemm")  # kernel-name substrings, '|'-separated (hipBLASLt: Cijk)
+
+
+def _hit(name):
+    return any(m in name for m in MATCH.split("|"))
 
 
 def read(d):
@@ -14,12 +18,12 @@ def read(d):
     durs = []
     for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(p)):
-            if MATCH not in r.get("Kernel_Name", ""):
+            if not _hit(r.get("Kernel_Name", "")):
                 continue
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
     for p in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(p)):
-            if MATCH in r.get("Kernel_Name", ""):
+            if _hit(r.get("Kernel_Name", "")):
                 durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0)
     return {k: sum(v) / len(v) for k, v in vals.items()}, (sum(durs) / len(durs) if durs else 0.0)
 
