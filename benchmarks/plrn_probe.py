@@ -47,7 +47,7 @@ def main():
         rows = ops.lrn_pool_backward_rows(x.shape, P.shape, n)
         part = torch.empty(rows, C, device="cuda")
         arms = {
-            "fused_fwd": lambda: ops.pool_lrn_forward(x, P, st, Y, 2, n, alpha, beta, k),
+            "fused_fwd": lambda: ops.pool_lrn_forward(x, P, st, Y, 6, n, alpha, beta, k),
             "sep_pool_fwd": lambda: ops.pool_forward(x, P, st, 3, 3, 2, 0, "max", relu=False, mark_mask=True),
             "sep_lrn_fwd": lambda: ops.lrn_forward(P, Y, n, alpha, beta, k),
             "fused_bwd": lambda: ops.lrn_pool_backward(P, dY, st, dx, 1, n, alpha, beta, k),

@@ -1095,7 +1095,12 @@ __global__ void lrn_bwd_shfl(const bf16_t *x, const bf16_t *__restrict__ dy, bf1
 //             HBM.  With dbias the conv-bias gradient behind a relu'd pool (the _fuse_pool_bias
 //             sum of the pooled gradient) is summed over the band's own windows; per-block
 //             partial rows in a fixed order.
-template <int H>
+// NN: the input is known to be >= 0 (a relu output: relu fused into the producing conv).  Then
+// bf16 bits order as unsigned integers, and the first max of a window is one v_max_u32 per
+// element over keys (bits << 16 | 15 - tap) -- the larger key is the larger value, then the
+// earlier tap -- instead of unpack + compare + two selects.  The sign bit is cleared first: a
+// relu of -0 may have stored -0 (0x8000), which must rank as 0.
+template <int H, bool NN>
 __global__ void pool_lrn_fwd(const bf16_t *__restrict__ x, bf16_t *__restrict__ P, uint8_t *__restrict__ arg,
                              bf16_t *__restrict__ Y, int N, int Hin, int Win, int C, int Ho, int Wo, int relu,
                              float salpha, float beta, float knorm) {
@@ -1123,24 +1128,49 @@ __global__ void pool_lrn_fwd(const bf16_t *__restrict__ x, bf16_t *__restrict__ 
         const int h = min(hs + kh, Hin - 1), w = min(ws + kw, Win - 1);
         raw[kh * 3 + kw] = *reinterpret_cast<const uint4 *>(xb + (static_cast<long>(h) * Win + w) * C);
       }
+    if constexpr (NN) {
+      uint32_t best[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) pv[q] = -INFINITY;
+      for (int q = 0; q < 8; ++q) best[q] = 0u;  // below every real key (>= 7)
 #pragma unroll
-    for (int kh = 0; kh < 3; ++kh)
+      for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        if (hs + kh >= Hin || ws + kw >= Win) continue;
-        float v[8];
-        unpack8(raw[kh * 3 + kw], v);
+        for (int kw = 0; kw < 3; ++kw) {
+          if (hs + kh >= Hin || ws + kw >= Win) continue;
+          const uint32_t t = 15u - static_cast<uint32_t>(kh * 3 + kw);
+          const uint4 r = raw[kh * 3 + kw];
+          const uint32_t wd[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const float a = (relu & 1) ? fmaxf(v[q], 0.f) : v[q];
-          if (a > pv[q]) {
-            pv[q] = a;
-            am[q] = static_cast<uint32_t>(kh * 3 + kw);
+          for (int q = 0; q < 4; ++q) {
+            best[2 * q] = max(best[2 * q], ((wd[q] << 16) & 0x7fff0000u) | t);
+            best[2 * q + 1] = max(best[2 * q + 1], (wd[q] & 0x7fff0000u) | t);
           }
         }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        pv[q] = __uint_as_float(best[q] & 0x7fff0000u);
+        am[q] = 15u - (best[q] & 15u);
       }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) pv[q] = -INFINITY;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          if (hs + kh >= Hin || ws + kw >= Win) continue;
+          float v[8];
+          unpack8(raw[kh * 3 + kw], v);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float a = (relu & 1) ? fmaxf(v[q], 0.f) : v[q];
+            if (a > pv[q]) {
+              pv[q] = a;
+              am[q] = static_cast<uint32_t>(kh * 3 + kw);
+            }
+          }
+        }
+    }
     if (relu & 2)
 #pragma unroll
       for (int q = 0; q < 8; ++q) am[q] |= pv[q] > 0.f ? 0u : 0x80u;
@@ -2253,8 +2283,13 @@ CXN_API int cxn_pool_lrn_fwd(const void *x, void *P, void *arg, void *Y, int N, 
   const long waves = (npix + 64 / tpp - 1) / (64 / tpp);
   const int blocks = static_cast<int>((waves + NT / 64 - 1) / (NT / 64));
   const float sa = alpha / nsize;
-#define CXN_PLF(HV) CXN_LAUNCH((pool_lrn_fwd<HV>), blocks, NT, 0, S_, (const bf16_t *)x, (bf16_t *)P, (uint8_t *)arg, \
-                               (bf16_t *)Y, N, Hin, Win, C, Ho, Wo, relu, sa, beta, knorm)
+  // relu bit 2 (4): the input is a relu output (>= 0): the integer-key max (pool_lrn_fwd NN)
+  const bool nn = (relu & 4) != 0 && (relu & 1) == 0;
+#define CXN_PLF(HV)                                                                                            \
+  if (nn) CXN_LAUNCH((pool_lrn_fwd<HV, true>), blocks, NT, 0, S_, (const bf16_t *)x, (bf16_t *)P, (uint8_t *)arg, \
+                     (bf16_t *)Y, N, Hin, Win, C, Ho, Wo, relu, sa, beta, knorm);                                    \
+  else CXN_LAUNCH((pool_lrn_fwd<HV, false>), blocks, NT, 0, S_, (const bf16_t *)x, (bf16_t *)P, (uint8_t *)arg,  \
+                  (bf16_t *)Y, N, Hin, Win, C, Ho, Wo, relu, sa, beta, knorm)
   switch (half) {
     case 0: CXN_PLF(0); break;
     case 1: CXN_PLF(1); break;

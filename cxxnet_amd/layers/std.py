@@ -550,7 +550,8 @@ class PoolingLayer(Layer):
         if self.fused_lrn is not None:
             lrn, yout = self.fused_lrn
             st = self._state(nodes_out[0])  # (also in eval: the fused kernel always writes offsets)
-            flags = int(bool(self.relu)) | (2 if self._mask_in_state() else 0)
+            # bit 2: the input is a fused conv -> relu output (>= 0), read as integer keys
+            flags = int(bool(self.relu)) | (2 if self._mask_in_state() else 0) | (4 if self.grad_mask_relu else 0)
             if ops.pool_lrn_forward(nodes_in[0].data, nodes_out[0].data, st, yout.data, flags, lrn.nsize, lrn.alpha,
                                     lrn.beta, lrn.knorm):
                 return

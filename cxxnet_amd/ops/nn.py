@@ -236,7 +236,8 @@ def pool_backward(x, state, dy, dx, KH, KW, S, P, mode: str, relu=False, dbias=N
 def pool_lrn_forward(x, pooled, state, y, relu_flags, nsize, alpha, beta, knorm) -> bool:
     """Fused max-pool (3x3 / 2, pad 0, ceil mode) -> LRN: pooled = pool(x) with the first-max
     offsets in state (bit 7 = relu' of the max when relu_flags & 2), y = lrn(pooled).  Same
-    values as pool_forward + lrn_forward.  False when the fused kernel does not serve the
+    values as pool_forward + lrn_forward.  relu_flags & 1: max over relu(x); & 4: x is known to
+    be >= 0 (a fused conv -> relu output; the kernel then takes the max on integer keys).  False when the fused kernel does not serve the
     shape (nothing was done)."""
     N, H, W, C = x.shape
     Ho, Wo = pooled.shape[1], pooled.shape[2]

@@ -51,7 +51,7 @@ def test_alexnet_step_fused_pool_lrn_matches(monkeypatch):
             assert torch.equal(a, b), key
 
 
-@pytest.mark.parametrize("H,C,relu", [(55, 96, 2), (27, 256, 2), (13, 64, 0), (8, 32, 2)])
+@pytest.mark.parametrize("H,C,relu", [(55, 96, 2), (55, 96, 6), (27, 256, 6), (27, 256, 2), (13, 64, 0), (8, 32, 6)])
 def test_pool_lrn_kernels_vs_torch(H, C, relu):
     N, n, alpha, beta, k = 3, 5, 1e-3, 0.75, 1.0
     torch.manual_seed(H)
@@ -72,7 +72,7 @@ def test_pool_lrn_kernels_vs_torch(H, C, relu):
     db = torch.zeros(C, device="cuda")
     rows = ops.lrn_pool_backward_rows(x.shape, P.shape, n)
     part = torch.empty(rows, C, device="cuda")
-    assert ops.lrn_pool_backward(P, dY, st, dx, int(relu == 2), n, alpha, beta, k, dbias=db, part=part)
+    assert ops.lrn_pool_backward(P, dY, st, dx, int((relu & 2) != 0), n, alpha, beta, k, dbias=db, part=part)
     xv = xr.clone().requires_grad_(True)
     pv = F.max_pool2d(xv, 3, 2, ceil_mode=True)
     pv.retain_grad()
@@ -80,7 +80,7 @@ def test_pool_lrn_kernels_vs_torch(H, C, relu):
     yv.backward(dY.float().permute(0, 3, 1, 2))
     gx = xv.grad
     gp = pv.grad
-    if relu == 2:
+    if relu & 2:
         gx = gx * (xr > 0).float()
         gp = gp * (pv.detach() > 0).float()
     err = ((dx.float().permute(0, 3, 1, 2) - gx).norm() / gx.norm()).item()
@@ -114,3 +114,23 @@ def test_pool_lrn_bias_sum_deterministic():
         assert ops.lrn_pool_backward(P, dY, st, dx, 1, n, 1e-4, 0.75, 1.0, dbias=db, part=part)
         out.append(db)
     assert torch.equal(out[0], out[1]) and torch.equal(out[0], out[2])
+
+
+def test_pool_lrn_integer_key_max_matches_float_compare():
+    """The non-negative-input path (flag 4: integer keys) against the float-compare path on
+    inputs full of ties and signed zeros: same maxima, same first-max offsets, same LRN."""
+    N, H, C, n = 4, 27, 64, 5
+    g = torch.Generator(device="cuda").manual_seed(3)
+    vals = torch.tensor([0.0, -0.0, 1.0, 2.0, 0.5], device="cuda")
+    x = vals[torch.randint(0, 5, (N, H, H, C), generator=g, device="cuda")].to(torch.bfloat16)
+    Ho = (H - 3) // 2 + 1
+    out = {}
+    for flags in (2, 6):
+        P = torch.empty(N, Ho, Ho, C, device="cuda", dtype=torch.bfloat16)
+        st = torch.empty(N, Ho, Ho, C, device="cuda", dtype=torch.uint8)
+        Y = torch.empty_like(P)
+        assert ops.pool_lrn_forward(x, P, st, Y, flags, n, 1e-4, 0.75, 1.0)
+        out[flags] = (P.float(), st.clone(), Y.float())
+    assert torch.equal(out[2][0], out[6][0])
+    assert torch.equal(out[2][1], out[6][1])
+    assert torch.equal(out[2][2], out[6][2])
