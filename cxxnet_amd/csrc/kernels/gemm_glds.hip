@@ -215,6 +215,13 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
       const int il = il_b;
       const int i = ibase + il;
       const bool vec_store = ((E.ldc & 7) == 0) && (i + 8 <= Mi);
+      // second destination (E.out2): this lane's 8 columns lie on one side of split_i
+      int ldc = E.ldc, ic = i;
+      if (E.out2 != nullptr && i >= E.split_i) {
+        out = reinterpret_cast<bf16_t *>(E.out2);
+        ldc = E.ldc2;
+        ic = i - E.split_i;
+      }
       // relu'-mask: the fragment's old values are all loaded before its first store (a load
       // issued after a store waits for it: vmcnt counts both in issue order)
       constexpr int NIT = (16 + RPI - 1) / RPI;
@@ -225,7 +232,7 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
         for (int k = 0; k < NIT; ++k) {
           const int jl = jl0 + k * RPI;
           if (jl < 16 && jbase + n * 16 + jl < Nj && i < Mi)
-            oldv[k] = *reinterpret_cast<const uint4 *>(out + static_cast<long>(jbase + n * 16 + jl) * E.ldc + i);
+            oldv[k] = *reinterpret_cast<const uint4 *>(out + static_cast<long>(jbase + n * 16 + jl) * ldc + ic);
         }
       }
 #pragma unroll
@@ -241,7 +248,7 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
             f[e] = f[e] * E.alpha + bias8[e];
             if (E.relu) f[e] = fmaxf(f[e], 0.f);
           }
-          bf16_t *dst = out + static_cast<long>(j) * E.ldc + i;
+          bf16_t *dst = out + static_cast<long>(j) * ldc + ic;
           if (vec_store) {
             if (E.mask_relu) {
               float old[8];
@@ -602,6 +609,33 @@ CXN_API int cxn_gemm_glds(const CxnOperandG *a, const CxnOperandG *b, int amode,
          nullptr, nullptr, nullptr, 0.f, 0.f, 0.f, 0.f, dws, dws_ld, dws_elems, dbias, g_gemm_group_i};
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int rc = dispatch(amode, bmode, epi, tile, A, B, E, groups < 1 ? 1 : groups, ksplit < 1 ? 1 : ksplit, s);
+  if (rc != 0) return rc;
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// cxn_gemm_glds with two bf16 destinations: output columns [0, split_i) to out (row stride
+// ldc), [split_i, rows of A) to out2 (row stride ldc2) -- the sibling 1x1 convs of an inception
+// module as one GEMM (NeuralNet._fuse_siblings).  Only the gemm_glds tiles of the dispatch switch
+// (not 114 / 130-142, whose epilogues have one destination); EPI_BF16, no split-K.
+CXN_API int cxn_gemm_glds_split(const CxnOperandG *a, const CxnOperandG *b, int amode, int bmode, void *out, int ldc,
+                                void *out2, int ldc2, int split_i, const float *bias, int relu, int tile,
+                                void *stream) {
+  if (a->kdim != b->kdim || split_i <= 0 || split_i % 8 != 0 || split_i >= a->rows || (ldc & 7) || (ldc2 & 7))
+    return -1;
+  if (tile == 114 || (tile >= 130 && tile <= 142)) return -1;
+  if ((kmajor(amode) || kmajor(bmode)) && a->kdim % 8 != 0) return -1;
+  if (!supported(a, amode) || !supported(b, bmode)) return -1;
+  if (b->rows <= 0 || a->kdim <= 0) return 0;
+  GOperand A{}, B{};
+  fill(A, a, amode);
+  fill(B, b, bmode);
+  GEpi E{out, 0, ldc, 1.f, bias, 0, relu, 0, 0,
+         nullptr, nullptr, nullptr, 0.f, 0.f, 0.f, 0.f, nullptr, 0, 0, nullptr, g_gemm_group_i};
+  E.out2 = out2;
+  E.ldc2 = ldc2;
+  E.split_i = split_i;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int rc = dispatch(amode, bmode, EPI_BF16, tile, A, B, E, 1, 1, s);
   if (rc != 0) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

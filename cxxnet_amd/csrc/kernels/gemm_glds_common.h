@@ -53,6 +53,11 @@ struct GEpi {
   // EPI_F32_SGD: when set, (lr, wd, mom, clip) are read from this device array instead of the
   // fields above -- a recorded / captured step then takes each replay's schedule values
   const float *sgd_hyp;
+  // bf16 epilogues of gemm_glds (tiles of its dispatch switch): output columns i >= split_i go
+  // to out2 (row stride ldc2) at column i - split_i instead (sibling 1x1 convs sharing one
+  // GEMM, NeuralNet._fuse_siblings); out2 == nullptr: one destination.  split_i % 8 == 0.
+  void *out2;
+  int ldc2, split_i;
 };
 
 }  // namespace cxg

@@ -492,8 +492,13 @@ static inline dim3 partials_grid(int nb, int C) {
 // spend most of their issue slots on 64-bit divisions).  Same semantics, including the
 // relu' bit.
 // SS / KS > 0: stride / square kernel fixed at compile time (3x3/2, 3x3/1, 2x2/2 -- every
-// pooling of the model zoo): constant divisions and fully unrolled windows
-template <int SS, int KS>
+// pooling of the model zoo): constant divisions and fully unrolled windows.
+// NN (max mode, fixed window, relu & 4 and not relu & 1): the input is a relu output (>= 0), so
+// bf16 bits order as unsigned integers and the first max is one v_max_u32 per element over keys
+// (bits << 16 | 15 - tap; see pool_lrn_fwd) instead of unpack + compare + two selects.
+__device__ __forceinline__ uint32_t nn_key_lo(uint32_t w, uint32_t t) { return ((w << 16) & 0x7fff0000u) | t; }
+__device__ __forceinline__ uint32_t nn_key_hi(uint32_t w, uint32_t t) { return (w & 0x7fff0000u) | t; }
+template <int SS, int KS, bool NN = false>
 __global__ void pool_fwd_rows(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, uint8_t *__restrict__ arg, int H,
                               int W, int C, int Ho, int Wo, int KHr, int KWr, int Sr, int P, int mode, int relu,
                               FastDiv fd_cv, FastDiv fd_row, FastDiv fd_h, uint32_t total) {
@@ -545,12 +550,37 @@ __global__ void pool_fwd_rows(const bf16_t *__restrict__ x, bf16_t *__restrict__
         const int h = min(max(hs + kh, 0), H - 1), w = min(max(ws + kw, 0), W - 1);
         raw[kh * KS + kw] = *reinterpret_cast<const uint4 *>(xb + (static_cast<long>(h) * W + w) * C);
       }
+    if constexpr (NN) {
+      uint32_t best[8];
 #pragma unroll
-    for (int kh = 0; kh < KS; ++kh)
+      for (int q = 0; q < 8; ++q) best[q] = 0u;
 #pragma unroll
-      for (int kw = 0; kw < KS; ++kw)
-        if (hs + kh >= 0 && hs + kh < he && ws + kw >= 0 && ws + kw < we)
-          take(raw[kh * KS + kw], static_cast<uint32_t>(kh * KW + kw));
+      for (int kh = 0; kh < KS; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < KS; ++kw)
+          if (hs + kh >= 0 && hs + kh < he && ws + kw >= 0 && ws + kw < we) {
+            const uint32_t t = 15u - static_cast<uint32_t>(kh * KS + kw);
+            const uint4 r = raw[kh * KS + kw];
+            const uint32_t wd[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              best[2 * q] = max(best[2 * q], nn_key_lo(wd[q], t));
+              best[2 * q + 1] = max(best[2 * q + 1], nn_key_hi(wd[q], t));
+            }
+          }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        acc[q] = __uint_as_float(best[q] & 0x7fff0000u);
+        am[q] = 15u - (best[q] & 15u);
+      }
+    } else {
+#pragma unroll
+      for (int kh = 0; kh < KS; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < KS; ++kw)
+          if (hs + kh >= 0 && hs + kh < he && ws + kw >= 0 && ws + kw < we)
+            take(raw[kh * KS + kw], static_cast<uint32_t>(kh * KW + kw));
+    }
   } else {
     for (int h = max(hs, 0); h < he; ++h)
       for (int w = max(ws, 0); w < we; ++w)
@@ -647,7 +677,9 @@ __global__ void pool_bwd_rows(const bf16_t *__restrict__ x, const uint8_t *__res
 // thread: each input row of the strip is read once as a 3-tap row maximum (value + kw), and every
 // output row takes the row maxima of its three input rows -- (R + 2) * 3 loads per R outputs
 // instead of 9 per output.  Same first-max order (kh, then kw) and relu flags as pool_fwd_rows.
-template <int R>
+// NN: integer keys as pool_fwd_rows (row key bits << 16 | 3 - kw; the output key adds 12 - 3 kh,
+// giving bits << 16 | 15 - (3 kh + kw)).
+template <int R, bool NN = false>
 __global__ void pool_fwd_s1k3(const bf16_t *__restrict__ x, bf16_t *__restrict__ y, uint8_t *__restrict__ arg,
                               int H, int W, int C, int Ho, int Wo, int P, int relu, FastDiv fd_cv, FastDiv fd_row,
                               FastDiv fd_hs, uint32_t total) {
@@ -670,6 +702,53 @@ __global__ void pool_fwd_s1k3(const bf16_t *__restrict__ x, bf16_t *__restrict__
       acc[o][q] = -INFINITY;
       am[o][q] = 0;
     }
+  if constexpr (NN) {
+    uint32_t best[R][8];
+#pragma unroll
+    for (int o = 0; o < R; ++o)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) best[o][q] = 0u;
+#pragma unroll
+    for (int r = 0; r < R + 2; ++r) {
+      const int h = h0 + r;
+      if (h < 0 || h >= H) continue;
+      uint4 raw[3];
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int w = min(max(ws + kw, 0), W - 1);
+        raw[kw] = *reinterpret_cast<const uint4 *>(xb + (static_cast<long>(h) * W + w) * C);
+      }
+      uint32_t rk[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) rk[q] = 0u;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        if (ws + kw < 0 || ws + kw >= W) continue;
+        const uint32_t t = 3u - static_cast<uint32_t>(kw);
+        const uint32_t wd[4] = {raw[kw].x, raw[kw].y, raw[kw].z, raw[kw].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          rk[2 * q] = max(rk[2 * q], nn_key_lo(wd[q], t));
+          rk[2 * q + 1] = max(rk[2 * q + 1], nn_key_hi(wd[q], t));
+        }
+      }
+#pragma unroll
+      for (int o = 0; o < R; ++o) {
+        const int kh = r - o;
+        if (kh < 0 || kh > 2) continue;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)  // (every row has a valid tap: rk >= 1)
+          best[o][q] = max(best[o][q], rk[q] + static_cast<uint32_t>(12 - 3 * kh));
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < R; ++o)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        acc[o][q] = __uint_as_float(best[o][q] & 0x7fff0000u);
+        am[o][q] = 15u - (best[o][q] & 15u);
+      }
+  } else {
 #pragma unroll
   for (int r = 0; r < R + 2; ++r) {
     const int h = h0 + r;
@@ -713,6 +792,7 @@ __global__ void pool_fwd_s1k3(const bf16_t *__restrict__ x, bf16_t *__restrict__
           am[o][q] = static_cast<uint32_t>(kh * 3) + hk[q];
         }
     }
+  }
   }
 #pragma unroll
   for (int o = 0; o < R; ++o) {
@@ -2160,25 +2240,39 @@ CXN_API int cxn_pool_fwd(const void *x, void *y, void *arg, int N, int H, int W,
   if (C % 8 == 0) {
     const long total = static_cast<long>(N) * Ho * Wo * (C / 8);
     if (total >= (1L << 31)) return -2;  // fdiv (mulhi + n) stays exact below 2^31
-#define CXN_POOL_FWD(SSV, KSV)                                                                              \
-  CXN_LAUNCH((pool_fwd_rows<SSV, KSV>), cdiv(total, NT), NT, 0, S_,                                                   \
+    // relu & 4: the input is a relu output (>= 0): integer-key max (NN forms)
+    const bool nn = mode == 0 && (relu & 4) != 0 && (relu & 1) == 0;
+#define CXN_POOL_FWD_T(SSV, KSV, NNV)                                                                        \
+  CXN_LAUNCH((pool_fwd_rows<SSV, KSV, NNV>), cdiv(total, NT), NT, 0, S_,                                     \
       (const bf16_t *)x, (bf16_t *)y, (uint8_t *)arg, H, W, C, Ho, Wo, KH, KW, S, P, mode, relu,             \
       make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(Wo * (C / 8))),        \
       make_fastdiv(static_cast<uint32_t>(Ho)), static_cast<uint32_t>(total))
+#define CXN_POOL_FWD(SSV, KSV)                   \
+  do {                                           \
+    if (nn) CXN_POOL_FWD_T(SSV, KSV, true);      \
+    else CXN_POOL_FWD_T(SSV, KSV, false);        \
+  } while (0)
     const int sq = KH == KW ? KH : 0;
     if (S == 1 && sq == 3 && mode == 0 && P <= 2 && pool_strips) {
       constexpr int R = 4;
       const int HS = (Ho + R - 1) / R;
       const long tot = static_cast<long>(N) * HS * Wo * (C / 8);
-      CXN_LAUNCH((pool_fwd_s1k3<R>), cdiv(tot, NT), NT, 0, S_, 
-          (const bf16_t *)x, (bf16_t *)y, (uint8_t *)arg, H, W, C, Ho, Wo, P, relu,
-          make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(Wo * (C / 8))),
-          make_fastdiv(static_cast<uint32_t>(HS)), static_cast<uint32_t>(tot));
+      if (nn)
+        CXN_LAUNCH((pool_fwd_s1k3<R, true>), cdiv(tot, NT), NT, 0, S_, (const bf16_t *)x, (bf16_t *)y, (uint8_t *)arg,
+                   H, W, C, Ho, Wo, P, relu, make_fastdiv(static_cast<uint32_t>(C / 8)),
+                   make_fastdiv(static_cast<uint32_t>(Wo * (C / 8))), make_fastdiv(static_cast<uint32_t>(HS)),
+                   static_cast<uint32_t>(tot));
+      else
+        CXN_LAUNCH((pool_fwd_s1k3<R, false>), cdiv(tot, NT), NT, 0, S_, (const bf16_t *)x, (bf16_t *)y, (uint8_t *)arg,
+                   H, W, C, Ho, Wo, P, relu, make_fastdiv(static_cast<uint32_t>(C / 8)),
+                   make_fastdiv(static_cast<uint32_t>(Wo * (C / 8))), make_fastdiv(static_cast<uint32_t>(HS)),
+                   static_cast<uint32_t>(tot));
     } else if (S == 2 && sq == 3) CXN_POOL_FWD(2, 3);
     else if (S == 1 && sq == 3) CXN_POOL_FWD(1, 3);
     else if (S == 2 && sq == 2) CXN_POOL_FWD(2, 2);
-    else CXN_POOL_FWD(0, 0);
+    else CXN_POOL_FWD_T(0, 0, false);
 #undef CXN_POOL_FWD
+#undef CXN_POOL_FWD_T
   } else {
     CXN_LAUNCH((pool_fwd<1>), nblocks(static_cast<long>(N) * Ho * Wo * C), NT, 0, S_, 
         (const bf16_t *)x, (bf16_t *)y, (uint8_t *)arg, N, H, W, C, Ho, Wo, KH, KW, S, P, mode, relu);

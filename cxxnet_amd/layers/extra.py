@@ -78,6 +78,7 @@ class SplitLayer(Layer):
     replay_audited = True  # library kernels only (tests/test_launch_hygiene_gpu.py)
     type_name = "split"
     alias = False
+    skip_grads = frozenset()
 
     def init_connection(self, nodes_in, nodes_out):
         _check(len(nodes_in) == 1 and len(nodes_out) >= 1, "SplitLayer: only support 1-n connection")
@@ -94,8 +95,11 @@ class SplitLayer(Layer):
         if not prop_grad:
             return
         # the output gradients summed in one pass (fp32 accumulation, one rounding); masked by
-        # relu' when the input is a zero-copy concat of relu outputs (NeuralNet._fuse_concat)
-        ops.sum_into(nodes_in[0].gdst, [o.gdst for o in nodes_out], mask_relu=self.grad_mask_relu)
+        # relu' when the input is a zero-copy concat of relu outputs (NeuralNet._fuse_concat).
+        # skip_grads: outputs whose consumer's data-gradient a fused sibling wrote into another
+        # output's slot (NeuralNet._fuse_siblings)
+        skip = self.skip_grads
+        ops.sum_into(nodes_in[0].gdst, [o.gdst for o in nodes_out if id(o) not in skip], mask_relu=self.grad_mask_relu)
 
 
 class ConcatLayer(Layer):

@@ -301,6 +301,10 @@ class ConvolutionLayer(Layer):
         # the conv below whose bias gradient this conv's data-gradient epilogue sums
         # (NeuralNet._fuse_dgrad_bias); None = not fused
         self.bias_below = None
+        # sibling group (NeuralNet._fuse_siblings): the lead holds the group (dict), the other
+        # members compute nothing themselves
+        self.sib = None
+        self.sib_member = False
 
     def init_connection(self, nodes_in, nodes_out):
         _check(len(nodes_in) == 1 and len(nodes_out) == 1, "ConvolutionLayer: only support 1-1 connection")
@@ -385,9 +389,21 @@ class ConvolutionLayer(Layer):
             ops.pad_interior(x, xp, g.pad_y, g.pad_x)
         return xp, ConvGeom(N, H2, W2, g.C, g.Ho, g.Wo, g.Cout, g.KH, g.KW, g.stride, 0, 0, g.groups)
 
+    def _sib_geo(self, cout):
+        g = self.geo
+        return ConvGeom(g.N, g.H, g.W, g.C, g.Ho, g.Wo, cout, 1, 1, 1, 0, 0, 1)
+
     def forward(self, is_train, nodes_in, nodes_out):
         self.geo.N = nodes_in[0].data.shape[0]
+        if self.sib_member:  # computed by the group's lead
+            return
         bias = self.b.w if self.b is not None else None
+        S = self.sib
+        if S is not None:  # all siblings as one GEMM: [0, C1) to this output, the rest to H
+            N = self.geo.N
+            ops.gemm.conv_forward_split(nodes_in[0].data, S["w_all"], S["b_all"], nodes_out[0].data, S["H"][:N],
+                                        S["c1"], self._sib_geo(S["ctot"]), relu=self.fuse_relu)
+            return
         # few-channel stride-1 first layers (VGG conv1_1): the direct kernel pads on the
         # fly; the zero-bordered copy is then built by the weight-gradient pass that needs it
         if ops.gemm.fewc_preferred(self.geo) and ops.gemm.conv_forward_fewc(
@@ -399,8 +415,22 @@ class ConvolutionLayer(Layer):
         ops.conv_forward(x, self.w.wb, bias, nodes_out[0].data, geo, relu=self.fuse_relu)
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
+        if self.sib_member:  # the group's lead runs this layer's backward with its own
+            return
         x, dy = nodes_in[0].data, nodes_out[0].data
         self.geo.N = x.shape[0]
+        S = self.sib
+        if S is not None:
+            # the other siblings: their dy is H itself (their consumers wrote it into the slices)
+            N = x.shape[0]
+            H = S["H"][:N]
+            gbc = self._sib_geo(S["cbc"])
+            ops.conv_backward_weight(x, H, S["wbc_g"], gbc)
+            if S["bbc_g"] is not None:
+                self.ctx.bias_grad(_pixel_rows(H), S["bbc_g"])
+            if prop_grad:
+                ready = self.ctx.flipped is not None and id(self) in self.ctx.flipped
+                ops.conv_backward_data(H, S["wbc_wb"], S["dx_node"].gdst, gbc, S["wt_bc"], wt_ready=ready)
         xw, geo = self._padded(x, getattr(self, "_xpad_stale", False))
         self._xpad_stale = False
         want_db = self.b is not None and not self.bias_done and self.ctx.is_gpu
@@ -418,6 +448,13 @@ class ConvolutionLayer(Layer):
             if ops.conv_backward_data(dy, self.w.wb, nodes_in[0].gdst, self.geo, self.flip_target()[1],
                                       mask_relu=self.grad_mask_relu, wt_ready=ready, dbias=db):
                 below.bias_done = True
+
+    def extra_flip_targets(self):
+        """Flip items besides flip_target(): a sibling group's stacked non-lead weights."""
+        S = self.sib
+        if S is None:
+            return []
+        return [(S["wbc_wb"], S["wt_bc"], self._sib_geo(S["cbc"]))]
 
     def flip_target(self):
         """(weights, flipped-weights buffer, geometry) of the data-gradient GEMM."""
@@ -511,6 +548,8 @@ class PoolingLayer(Layer):
         self.bias_of = None
         # (LRN layer, its output node) run inside this pool's kernels (NeuralNet._fuse_pool_lrn)
         self.fused_lrn = None
+        # the input can only hold values >= 0 (NeuralNet._mark_nonneg): max on integer keys
+        self.input_nonneg = False
         self._dbpart = None
 
     def set_param(self, name, val):
@@ -550,18 +589,18 @@ class PoolingLayer(Layer):
         if self.fused_lrn is not None:
             lrn, yout = self.fused_lrn
             st = self._state(nodes_out[0])  # (also in eval: the fused kernel always writes offsets)
-            # bit 2: the input is a fused conv -> relu output (>= 0), read as integer keys
-            flags = int(bool(self.relu)) | (2 if self._mask_in_state() else 0) | (4 if self.grad_mask_relu else 0)
+            # bit 2: the input can only be >= 0 (NeuralNet._mark_nonneg): max on integer keys
+            flags = int(bool(self.relu)) | (2 if self._mask_in_state() else 0) | (4 if self.input_nonneg else 0)
             if ops.pool_lrn_forward(nodes_in[0].data, nodes_out[0].data, st, yout.data, flags, lrn.nsize, lrn.alpha,
                                     lrn.beta, lrn.knorm):
                 return
             ops.pool_forward(nodes_in[0].data, nodes_out[0].data, st, lp.kernel_height, lp.kernel_width, lp.stride,
-                             lp.pad_y, self.mode, self.relu, mark_mask=self._mask_in_state())
+                             lp.pad_y, self.mode, self.relu, mark_mask=self._mask_in_state(), nonneg=self.input_nonneg)
             ops.lrn_forward(nodes_out[0].data, yout.data, lrn.nsize, lrn.alpha, lrn.beta, lrn.knorm)
             return
         st = self._state(nodes_out[0]) if is_train else None
         ops.pool_forward(nodes_in[0].data, nodes_out[0].data, st, lp.kernel_height, lp.kernel_width, lp.stride,
-                         lp.pad_y, self.mode, self.relu, mark_mask=self._mask_in_state())
+                         lp.pad_y, self.mode, self.relu, mark_mask=self._mask_in_state(), nonneg=self.input_nonneg)
         if is_train and self._tie_all():
             y = nodes_out[0].data
             if self.ysave is None or self.ysave.shape != y.shape:

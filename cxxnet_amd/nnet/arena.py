@@ -30,8 +30,15 @@ class ParamArena:
         self.total = 0
         self.w = self.g = self.m1 = self.m2 = self.wb = None
 
-    def build(self, layer_specs: Sequence[tuple]):
-        """layer_specs: [(layer_index, [ParamSpec, ...]), ...] in forward order."""
+    def build(self, layer_specs: Sequence[tuple], groups: Sequence[Sequence[int]] = ()):
+        """layer_specs: [(layer_index, [ParamSpec, ...]), ...] in forward order.
+
+        groups: layer-index lists (forward order) whose weights must be ONE matrix and whose
+        biases one vector (sibling convs computed as one GEMM, NeuralNet._fuse_siblings): the
+        group is laid out at its first layer's place, weights back to back in the listed order,
+        then the biases, 8-element aligned inside (ALIGN after).  Every member spec gets
+        grad_li / fwd_li = the first layer: its gradient is final after that layer's backprop and
+        that layer's forward reads it (data-parallel buckets and forward gating)."""
         from ..parallel.dp import world_info
         # a multiple of world*ALIGN, so that sharded buckets split into equal,
         # aligned per-rank chunks (parallel/dp.py, update_on_server); a segment whose gradient
@@ -40,7 +47,25 @@ class ParamArena:
         q = ALIGN * world_info()[1]
         off = 0
         self.specs = []
+        by_li = dict(layer_specs)
+        lead_of = {li: g[0] for g in groups for li in g}
+        group_of = {g[0]: list(g) for g in groups}
         for li, specs in sorted(layer_specs, key=lambda t: -t[0]):
+            if li in lead_of and lead_of[li] != li:
+                continue  # laid out with its group's first layer
+            if li in group_of:
+                members = group_of[li]
+                for kind in (0, 1):  # weights, then biases
+                    for m in members:
+                        ps = by_li[m]
+                        if kind < len(ps):
+                            s = ps[kind]
+                            s.offset = off
+                            s.grad_li = s.fwd_li = li
+                            self.specs.append((m, s))
+                            off += (s.numel + 7) // 8 * 8
+                off = (off + ALIGN - 1) // ALIGN * ALIGN
+                continue
             for s in specs:
                 nr = getattr(s, "no_reduce", False)
                 if nr:

@@ -143,6 +143,7 @@ class NeuralNet:
 
     def _fuse(self):
         if not self.fuse:
+            self._mark_nonneg()
             return
         producers: Dict[int, list] = {}
         consumers: Dict[int, list] = {}
@@ -193,9 +194,36 @@ class NeuralNet:
 
         self._fuse_concat(producers, consumers)
         self._fuse_split(producers, consumers)
+        self._fuse_siblings(producers, consumers)
         self._fuse_pool_bias(producers, consumers)
         self._fuse_dgrad_bias(producers, consumers)
         self._fuse_pool_lrn(producers, consumers)
+        self._mark_nonneg()
+
+    def _mark_nonneg(self):
+        """Nodes that can only hold values >= 0 (relu outputs -- fused into their producer or
+        not -- and what max-pool / LRN / dropout / split / concat make of them); a max-pool
+        reading one gets input_nonneg, and its kernels then take the window maximum on integer
+        keys of the bf16 bits (ops.pool_forward(nonneg=True))."""
+        nn = set()
+        for conn in self.connections:
+            lay, t = conn.layer, conn.type
+            ins = conn.nodes_in
+            if t == K_RELU or (t in (K_CONV, K_FULLC) and getattr(lay, "fuse_relu", False)):
+                ok = True
+            elif t in (K_MAXPOOL, K_RELU_MAXPOOL):
+                ok = t == K_RELU_MAXPOOL or bool(getattr(lay, "relu", False)) or all(id(n) in nn for n in ins)
+                lay.input_nonneg = all(id(n) in nn for n in ins)
+            elif t in (K_LRN, K_DROPOUT, K_SPLIT, K_CHCONCAT, K_CONCAT):
+                ok = all(id(n) in nn for n in ins)
+            else:
+                ok = False
+            if ok:
+                for n in conn.nodes_out:
+                    nn.add(id(n))
+        for b, a in getattr(self, "aliases", {}).items():  # b = fused relu(a): a holds relu(z) too
+            if b in nn:
+                nn.add(id(a))
 
     def _fuse_pool_lrn(self, producers, consumers):
         """Max-pool (3x3 / 2, pad 0) -> LRN (AlexNet pool1 -> lrn1, pool2 -> lrn2): one kernel per
@@ -369,17 +397,117 @@ class NeuralNet:
             for o in conn.nodes_out:
                 self.split_alias[id(o)] = a
 
+    def _fuse_siblings(self, producers, consumers):
+        """Sibling 1x1 convs (an inception module's 1x1, 3x3_reduce and 5x5_reduce: same input
+        through a zero-copy split, 1x1 / stride 1 / pad 0, relu fused) as ONE GEMM per direction
+        where the data allow.  The first sibling (the lead) computes all of them: output
+        channels [0, C1) to its own output (a concat slice), the others to channel slices of one
+        new buffer H [pixels][C2 + C3 + ...] (ops.conv_forward_split); backward, the lead's own
+        part as before plus one weight-gradient and one data-gradient GEMM over all of H (its
+        dy is H itself, since the consumers of the slices write their input gradient into
+        them).  The arena lays the group's weights out as one matrix and its biases as one
+        vector (ParamArena.build groups); checkpoints stay per layer.  The split sums one
+        gradient fewer per extra sibling.  Reference: src/layer/split_layer-inl.hpp:29-41,
+        src/layer/convolution_layer-inl.hpp:70-106.  CXXNET_FUSE_SIBLINGS=0 turns it off."""
+        self.sib_groups = []
+        self.sib_views = {}
+        if (os.environ.get("CXXNET_FUSE_SIBLINGS", "1") == "0" or not self.ctx.is_gpu
+                or os.environ.get("CXXNET_DGRAD_BIAS", "0") == "1"):
+            return
+        views = getattr(self, "concat_views", {})
+        for conn in self.connections:
+            if conn.type != K_SPLIT or conn.shared or not getattr(conn.layer, "alias", False):
+                continue
+            x = conn.nodes_in[0]
+            if x.cp % 8:
+                continue
+            mem = []
+            for o in conn.nodes_out:
+                cons = consumers.get(id(o), [])
+                if len(cons) != 1 or cons[0][1]:
+                    continue
+                j = cons[0][0]
+                cj = self.connections[j]
+                lay = cj.layer
+                if cj.type != K_CONV or cj.shared or not getattr(lay, "fuse_relu", False):
+                    continue
+                lp = lay.lp
+                if (lp.kernel_height != 1 or lp.kernel_width != 1 or lp.stride != 1 or lp.pad_y or lp.pad_x
+                        or lp.num_group != 1 or lp.num_channel % 8 or getattr(lay, "_prepad_on", False)):
+                    continue
+                mem.append((j, o))
+            mem.sort(key=lambda t: t[0])
+            if len(mem) < 2 or len({self.connections[j].layer.lp.no_bias for j, _ in mem}) != 1:
+                continue
+            rest = [(j, o) for j, o in mem[1:] if id(self.connections[j].nodes_out[0]) not in views]
+            if not rest:
+                continue
+            lead_j = mem[0][0]
+            gi = len(self.sib_groups)
+            group = [lead_j] + [j for j, _ in rest]
+            self.sib_groups.append(group)
+            off = 0
+            for j, _ in rest:
+                a = self.connections[j].nodes_out[0]
+                self.sib_views[id(a)] = (a, gi, off, a.cp)
+                off += a.cp
+                self.connections[j].layer.sib_member = True
+            lead = self.connections[lead_j].layer
+            lead.sib = {"gi": gi, "layers": [self.connections[j].layer for j in group], "cbc": off,
+                        "dx_node": rest[0][1]}
+            # the data-gradient of every sibling after the lead lands in the first one's slot
+            conn.layer.skip_grads = {id(o) for _, o in rest[1:]}
+
+    def _sibling_views(self):
+        """Arena views of each sibling group (after _build_arena): the stacked weights (compute
+        copy), the non-lead part's weights / gradient, and the biases."""
+        a = self.arena
+        wb = a.wb if a.wb is not None else a.w
+        for conn in self.connections:
+            S = getattr(conn.layer, "sib", None)
+            if not S:
+                continue
+            lays = S["layers"]
+            cin = lays[0].geo.C
+            ctot = sum(l.lp.num_channel for l in lays)
+            c1 = lays[0].lp.num_channel
+            w0, w1 = lays[0].w.offset, lays[1].w.offset
+            S["ctot"], S["c1"] = ctot, c1
+            S["w_all"] = wb[w0:w0 + ctot * cin].view(ctot, 1, 1, cin)
+            S["wbc_wb"] = wb[w1:w1 + S["cbc"] * cin].view(S["cbc"], 1, 1, cin)
+            S["wbc_g"] = a.g[w1:w1 + S["cbc"] * cin].view(S["cbc"], 1, 1, cin)
+            S["wt_bc"] = torch.empty_like(S["wbc_wb"])
+            if lays[0].b is not None:
+                b0, b1 = lays[0].b.offset, lays[1].b.offset
+                S["b_all"] = a.w[b0:b0 + ctot]
+                S["bbc_g"] = a.g[b1:b1 + S["cbc"]]
+            else:
+                S["b_all"] = S["bbc_g"] = None
+
     def _alloc_nodes(self):
         dt = self.ctx.act_dtype
         aliases = dict(getattr(self, "aliases", {}))
         splits = getattr(self, "split_alias", {})
         aliases.update(splits)
         views = getattr(self, "concat_views", {})
+        sibs = getattr(self, "sib_views", {})
         for n in self.nodes:
-            if id(n) not in aliases and id(n) not in views:
+            if id(n) not in aliases and id(n) not in views and id(n) not in sibs:
                 n.alloc(self.device, dt)
         for a, out, off, c in views.values():  # conv outputs that are channel slices of a concat
             a.data = out.data[..., off:off + c]
+        # sibling conv outputs: channel slices of their group's buffer H (NeuralNet._fuse_siblings)
+        hbuf = {}
+        for a, gi, off, c in sibs.values():
+            if gi not in hbuf:
+                cbc = sum(cc for _, g2, _, cc in sibs.values() if g2 == gi)
+                b, _, h, w = a.shape
+                hbuf[gi] = torch.zeros((b, h, w, cbc), device=self.device, dtype=dt)
+            a.data = hbuf[gi][..., off:off + c]
+        for conn in self.connections:
+            S = getattr(conn.layer, "sib", None)
+            if S:
+                S["H"] = hbuf[S["gi"]]
         pending = [n for n in self.nodes if id(n) in aliases]
         for _ in range(len(pending) + 1):  # resolve chains (split of a relu alias, ...)
             left = []
@@ -409,7 +537,8 @@ class NeuralNet:
             if not conn.shared:
                 specs.append((i, conn.layer.declare_params()))
         self.arena = ParamArena(self.device, torch.bfloat16 if self.ctx.is_gpu else None)
-        self.arena.build(specs)
+        self.arena.build(specs, groups=getattr(self, "sib_groups", ()))
+        self._sibling_views()
 
     def _init_updater(self):
         self.updater = ArenaUpdater(self.cfg.updater_type, self.arena, self.arena.segments(), self.cfg.defcfg,
@@ -552,9 +681,12 @@ class NeuralNet:
             flips, seen = [], set()
             for i, conn in enumerate(self.connections):
                 lay = conn.layer
+                if getattr(lay, "sib_member", False):
+                    continue
                 if hasattr(lay, "flip_target") and (i != 0 or prop_to_input) and id(lay) not in seen:
                     seen.add(id(lay))
                     flips.append(lay.flip_target())
+                    flips.extend(lay.extra_flip_targets())
             from ..ops.gemm import conv_weight_flip_multi
             conv_weight_flip_multi(flips)
             self.ctx.flipped = seen

@@ -651,7 +651,9 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
         raise ValueError(f"conv: channels per group ({cg}) must be a multiple of 4 on the GPU path")
     kd = g.kdim
     A = _op(w, g.cg_out * kd, kd, g.cg_out, kd)
-    B = _op(x, cg, 0, g.N * g.Ho * g.Wo, kd, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW,
+    # C = the input's pixel stride: a channel slice of a wider buffer (sibling outputs,
+    # NeuralNet._fuse_siblings) is read in place
+    B = _op(x, cg, 0, g.N * g.Ho * g.Wo, kd, H=g.H, W=g.W, C=_pix(x), Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW,
             stride=g.stride, pad_h=g.pad_y, pad_w=g.pad_x, dil=1, Cg=cg)
     def reg(o):
         tile = _pick(CONV_FWD_TILES if va == 8 else CONV_FWD_TILES_V4, g.cg_out, g.N * g.Ho * g.Wo, g.groups)
@@ -690,6 +692,48 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
     if cg % va:
         raise RuntimeError(f"conv: no GPU kernel for {cg} channels per group ({g})")
     reg(y)
+
+
+# gemm_glds tiles whose epilogue takes a second destination (cxn_gemm_glds_split)
+SPLIT_CANDS = tuple(t for t in GLDS_CANDS if t not in (114, 130, 131, 133))
+
+
+def conv_forward_split(x, w, bias, y, y2, split, g: ConvGeom, relu=False):
+    """One GEMM for convs that read the same input (the sibling 1x1 convs of an inception
+    module, NeuralNet._fuse_siblings): w [Cout][KH][KW][Cin] stacks their weights, output
+    channels [0, split) go to y and [split, Cout) to y2 (each NHWC, any pixel stride)."""
+    if not _native_t(x):
+        t = torch.empty(y.shape[:-1] + (g.Cout,), dtype=y.dtype, device=y.device)
+        conv_forward(x, w, bias, t, g, relu=relu)
+        y.copy_(t[..., :split])
+        y2.copy_(t[..., split:])
+        return
+    cg = g.cg_in
+    kd = g.kdim
+    A = _op(w, g.cg_out * kd, kd, g.cg_out, kd)
+    B = _op(x, cg, 0, g.N * g.Ho * g.Wo, kd, H=g.H, W=g.W, C=_pix(x), Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW,
+            stride=g.stride, pad_h=g.pad_y, pad_w=g.pad_x, dil=1, Cg=cg)
+
+    def run(t, o):
+        if t == REG or not _glds_cfg["on"]:
+            return False
+        rc = native.kernels().cxn_gemm_glds_split(
+            A, B, GL_K, GL_KG, o.data_ptr(), _pix(o), y2.data_ptr(), _pix(y2), int(split),
+            bias.data_ptr() if bias is not None else None, int(relu), t, _stream())
+        if rc == -1:
+            return False
+        native.check(rc, "gemm_glds_split")
+        LAST_GLDS[0] = t
+        return True
+    key = ("cfs", g.N, g.H, g.W, g.C, g.Cout, split)
+    if cg % 8 == 0 and g.groups == 1 and _use("cf"):
+        t = _tuned_tile(key, run, y, lambda: _pick_glds(A.rows, B.rows, 1), cands=SPLIT_CANDS)
+        if run(t, y):
+            return
+    # no two-destination tile for this shape: the two channel ranges as two GEMMs
+    for lo, hi, o in ((0, split, y), (split, g.Cout, y2)):
+        gi = ConvGeom(g.N, g.H, g.W, g.C, g.Ho, g.Wo, hi - lo, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, 1)
+        conv_forward(x, w[lo:hi], bias[lo:hi] if bias is not None else None, o, gi, relu=relu)
 
 
 def conv_weight_flip_multi(items):
@@ -737,20 +781,20 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False, wt_
             KW=g.KW, stride=1, pad_h=g.KH - 1 - g.pad_y, pad_w=g.KW - 1 - g.pad_x, dil=g.stride, Cg=cg_out)
     def reg(o):
         tile = _pick(CONV_FWD_TILES, cg_in, g.N * g.H * g.W, g.groups)
-        _gemm(A, B, DIRECT_K, GATHER_K, 8, 8, o, cg_in, g.C, epi=EPI_BF16, groups=g.groups, mask_relu=mask_relu,
+        _gemm(A, B, DIRECT_K, GATHER_K, 8, 8, o, cg_in, _pix(o), epi=EPI_BF16, groups=g.groups, mask_relu=mask_relu,
               tile=tile)
         return True
     if g.stride == 1 and _use("cd"):
         def run(t, o):
             if t == REG:
                 return reg(o)
-            return _glds(A, B, GL_K, GL_KG, o, cg_in, g.C, groups=g.groups, mask_relu=mask_relu, tile=t)
+            return _glds(A, B, GL_K, GL_KG, o, cg_in, _pix(o), groups=g.groups, mask_relu=mask_relu, tile=t)
         key = ("cd", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
         t = _tuned_tile(key, run, dx, lambda: _pick_glds(A.rows, B.rows, g.groups), extra=(REG,))
         if dbias is not None and t != REG and (t not in (130, 131) or _HALO_DB):
             from .nn import _workspace
             ws = _workspace((-(-B.rows // 16) + 8) * g.C, dx.device)  # >= tiles_j * waves_j rows
-            if _glds(A, B, GL_K, GL_KG, dx, cg_in, g.C, groups=g.groups, mask_relu=mask_relu, tile=t,
+            if _glds(A, B, GL_K, GL_KG, dx, cg_in, _pix(dx), groups=g.groups, mask_relu=mask_relu, tile=t,
                      epi=EPI_BF16_DB_G, bias_gstride=cg_in, dbias=dbias, dws=ws, dws_ld=g.C):
                 return True
         if run(t, dx):
@@ -816,7 +860,7 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom, db=None) -> bool:
     va = 8 if cg % 8 == 0 else 4
     kd = g.kdim
     P = g.N * g.Ho * g.Wo
-    A = _op(x, cg, 0, kd, P, H=g.H, W=g.W, C=g.C, Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW, stride=g.stride,
+    A = _op(x, cg, 0, kd, P, H=g.H, W=g.W, C=_pix(x), Ho=g.Ho, Wo=g.Wo, KH=g.KH, KW=g.KW, stride=g.stride,
             pad_h=g.pad_y, pad_w=g.pad_x, dil=1, Cg=cg)
     B = _op(dy, g.cg_out, _pix(dy), g.cg_out, P)
 

@@ -162,10 +162,11 @@ def _pool_ref(x, KH, KW, S, P, mode, relu, Ho, Wo):
     return out.permute(0, 2, 3, 1), arg
 
 
-def pool_forward(x, y, state, KH, KW, S, P, mode: str, relu=False, mark_mask=False):
+def pool_forward(x, y, state, KH, KW, S, P, mode: str, relu=False, mark_mask=False, nonneg=False):
     """y = pool(x).  state: uint8 [N][Ho][Wo][C] first-max window offsets (max mode, may be None).
     mark_mask (GPU, max mode, window < 128): also record relu'(max) in bit 7 of the
-    offsets so that pool_backward(relu=2) needs no input read."""
+    offsets so that pool_backward(relu=2) needs no input read.  nonneg: x can only hold values
+    >= 0 (a relu output); the max is then taken on integer keys of the bf16 bits."""
     N, H, W, C = x.shape
     Ho, Wo = y.shape[1], y.shape[2]
     m = POOL_MODE[mode]
@@ -178,6 +179,7 @@ def pool_forward(x, y, state, KH, KW, S, P, mode: str, relu=False, mark_mask=Fal
             state.copy_(arg)
         return
     flags = int(bool(relu)) | (2 if (mark_mask and m == 0 and KH * KW < 128 and state is not None) else 0)
+    flags |= 4 if nonneg else 0
     native.check(_k().cxn_pool_fwd(x.data_ptr(), y.data_ptr(),
                                    state.data_ptr() if (state is not None and m == 0) else None,
                                    N, H, W, C, Ho, Wo, KH, KW, S, P, m, flags, _stream()), "pool_fwd")

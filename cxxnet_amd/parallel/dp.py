@@ -108,6 +108,7 @@ class GradReducer:
     def _plain_buckets(self, limit):
         cur_start, cur_end, cur_li = None, 0, None
         for li, spec in self.arena.specs:  # arena order = reverse layer order
+            li = getattr(spec, "grad_li", li)  # the layer after whose backprop the gradient is final
             s, e = spec.offset, spec.offset + spec.numel
             if getattr(spec, "no_reduce", False):  # fullc_gather: gradient is already global
                 self.extra_ranges.append((s, e))
@@ -119,9 +120,9 @@ class GradReducer:
                 cur_start, cur_li = s, li
             if e - cur_start > limit and cur_end > cur_start:
                 self.buckets.append(Bucket(cur_start, cur_end, cur_li))
-                cur_start = s
+                cur_start, cur_li = s, li
             cur_end = e
-            cur_li = li
+            cur_li = min(cur_li, li)
         if cur_start is not None and cur_end > cur_start:
             self.buckets.append(Bucket(cur_start, cur_end, cur_li))
 
@@ -133,7 +134,7 @@ class GradReducer:
         q = ALIGN * max(self.world, 1)
         total = self.arena.total
         assert total % q == 0, "arena must be padded to world*ALIGN"
-        segs = [(spec.offset, spec.offset + spec.numel, li) for li, spec in self.arena.specs
+        segs = [(spec.offset, spec.offset + spec.numel, getattr(spec, "grad_li", li)) for li, spec in self.arena.specs
                 if not getattr(spec, "no_reduce", False)]
         # fullc_gather segments (q-aligned by the arena) hold a global gradient: every rank
         # updates them whole, they are cut out of the reduced runs
@@ -173,6 +174,7 @@ class GradReducer:
         """layer index -> buckets holding (part of) that layer's parameters."""
         self.layer_buckets = {}
         for li, spec in self.arena.specs:
+            li = getattr(spec, "fwd_li", li)  # the layer whose forward reads it
             s, e = spec.offset, spec.offset + spec.numel
             for bi, b in enumerate(self.buckets):
                 if b.start < e and s < b.end:

@@ -1,0 +1,74 @@
+"""Max pooling on integer keys for inputs that can only be >= 0 (NeuralNet._mark_nonneg ->
+PoolingLayer.input_nonneg -> ops.pool_forward(nonneg=True)): which pools qualify (CPU) and
+bitwise equality with the float-compare kernels on tie-heavy inputs with signed zeros (GPU)."""
+import pytest
+import torch
+
+from cxxnet_amd import ops
+from cxxnet_amd.models import load_conf
+from cxxnet_amd.nnet import NetTrainer
+
+
+def _net(model, batch):
+    tr = NetTrainer()
+    for k, v in load_conf(model, [("batch_size", str(batch)), ("dev", "cpu")]):
+        if not k.startswith("metric"):
+            tr.set_param(k, v)
+    tr.init_model()
+    return tr.net
+
+
+@pytest.mark.parametrize("model", ["alexnet", "inception_v1", "vgg16"])
+def test_every_max_pool_after_relu_is_marked(model):
+    net = _net(model, 2)
+    pools = [c.layer for c in net.connections if type(c.layer).__name__ == "PoolingLayer" and c.layer.mode == "max"]
+    assert pools and all(p.input_nonneg for p in pools)
+
+
+def test_pool_on_unrectified_input_is_not_marked():
+    from cxxnet_amd import native
+    conf = """
+netconfig=start
+layer[0->1] = conv:c1
+  kernel_size = 3
+  nchannel = 8
+layer[1->2] = max_pooling
+  kernel_size = 2
+  stride = 2
+layer[2->3] = relu
+layer[3->4] = max_pooling
+  kernel_size = 2
+  stride = 2
+layer[4->5] = flatten
+layer[5->6] = fullc:f
+  nhidden = 4
+layer[6->6] = softmax
+netconfig=end
+input_shape = 3,12,12
+"""
+    tr = NetTrainer()
+    for k, v in list(native.rt().parse_config(conf)) + [("batch_size", "2"), ("dev", "cpu")]:
+        tr.set_param(k, v)
+    tr.init_model()
+    pools = [c.layer for c in tr.net.connections if type(c.layer).__name__ == "PoolingLayer"]
+    assert [p.input_nonneg for p in pools] == [False, True]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,S,P,H", [(3, 2, 0, 27), (3, 1, 1, 14), (2, 2, 0, 28), (3, 2, 0, 13)])
+def test_integer_key_pool_matches_float_compare(K, S, P, H):
+    N, C = 3, 64
+    g = torch.Generator(device="cuda").manual_seed(K * 10 + H)
+    vals = torch.tensor([0.0, -0.0, 1.0, 2.0, 0.5], device="cuda")
+    x = vals[torch.randint(0, 5, (N, H, H, C), generator=g, device="cuda")].to(torch.bfloat16)
+    Ho = (H + 2 * P - K) // S + 1
+    if S > 1:
+        Ho = min(H + 2 * P - K + S - 1, H + 2 * P - 1) // S + 1  # the layer's ceil mode
+    out = {}
+    for nn in (False, True):
+        y = torch.empty(N, Ho, Ho, C, device="cuda", dtype=torch.bfloat16)
+        st = torch.empty(N, Ho, Ho, C, device="cuda", dtype=torch.uint8)
+        ops.pool_forward(x, y, st, K, K, S, P, "max", mark_mask=True, nonneg=nn)
+        out[nn] = (y.float(), st.clone())
+    assert torch.equal(out[False][0], out[True][0])
+    assert torch.equal(out[False][1], out[True][1])

@@ -16,7 +16,7 @@ def test_every_entry_names_a_known_tile():
         op = key.split("|")[0]
         if op == "cws":  # register weight-grad: tile * 100000 + K-split slices
             ok = tile // 100000 in G.TILES and tile % 100000 >= 1
-        elif op in ("cf", "cd", "cw"):
+        elif op in ("cf", "cd", "cw", "cfs"):
             ok = tile in G.GLDS_TILES or tile == G.REG
         else:  # cr, cwr, fc, fw, fws: LDS-DMA tiles only
             ok = tile in G.GLDS_TILES
@@ -65,7 +65,7 @@ def test_every_compiled_tile_is_used():
 
 
 def test_signature_keys_are_well_formed():
-    width = {"cf": 11, "cd": 11, "cw": 11, "cws": 11, "cr": 8, "cwr": 8, "fc": 5, "fw": 3, "fws": 3}
+    width = {"cf": 11, "cfs": 6, "cd": 11, "cw": 11, "cws": 11, "cr": 8, "cwr": 8, "fc": 5, "fw": 3, "fws": 3}
     for key in _table():
         parts = key.split("|")
         assert parts[0] in width, key
