@@ -121,10 +121,26 @@ def test_shipped_table_entry(op, sig):
     elif op == "fws":
         nin, nout, B = sig
         err = check_fc_sgd(nin, nout, B)
+    elif op == "cfs":
+        err = check_conv_split(sig)
     else:
         nin, nout, B = sig
         err = check_fc("fw", nin, nout, B)
     assert err < 1e-2, (op, sig, gemm._TUNE.get("|".join([op] + [str(v) for v in sig])), err)
+
+
+def check_conv_split(sig):
+    """Sibling 1x1 convs as one two-destination GEMM (key "cfs": N, H, W, C, Cout, split):
+    channels [0, split) into a slice of a wider buffer, the rest into a second buffer."""
+    N, H, W, C, Cout, split = sig
+    x = _rnd((N, H, W, C), 1.0, 21)
+    w = _rnd((Cout, 1, 1, C), 0.05, 22)
+    b = torch.randn(Cout, device=DEV) * 0.1
+    big = torch.zeros(N, H, W, split + 64, device=DEV, dtype=torch.bfloat16)
+    y, y2 = big[..., 32:32 + split], torch.empty(N, H, W, Cout - split, device=DEV, dtype=torch.bfloat16)
+    ops.gemm.conv_forward_split(x, w, b, y, y2, split, ConvGeom(N, H, W, C, H, W, Cout, 1, 1, 1, 0, 0, 1), relu=True)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b).clamp_min(0).permute(0, 2, 3, 1)
+    return _relnorm(torch.cat([y.float(), y2.float()], -1), ref)
 
 
 def check_fc_sgd(nin, nout, B):
