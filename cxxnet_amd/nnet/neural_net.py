@@ -551,11 +551,18 @@ class NeuralNet:
         self._fuse()
         self._alloc_nodes()
         self._build_arena()
-        for li, spec in self.arena.specs:
-            # drawn where the arena lives (device RNG kernel on the GPU), in logical layout
-            t = torch.zeros(spec.shape, dtype=torch.float32, device=self.device)
-            spec.init(t)
-            spec.w.copy_(t)
+        # drawn in reverse layer order, each layer's tensors in declaration order -- not in arena
+        # order, which sibling groups (ParamArena.build groups) rearrange: a seed gives the same
+        # initial weights with and without the groups
+        for i in range(len(self.connections) - 1, -1, -1):
+            conn = self.connections[i]
+            if conn.shared:
+                continue
+            for spec in conn.layer.params:
+                # drawn where the arena lives (device RNG kernel on the GPU), in logical layout
+                t = torch.zeros(spec.shape, dtype=torch.float32, device=self.device)
+                spec.init(t)
+                spec.w.copy_(t)
         self.arena.sync_shadow()
         self._init_updater()
 

@@ -53,6 +53,10 @@ def _step(batch, fuse, monkeypatch):
 
 @pytest.mark.parametrize("batch", [256, 8])
 def test_fused_dropout_bitwise(batch, monkeypatch):
+    # the heuristic tile for every shape (no per-process timing): both nets then run the same
+    # split-K decomposition, whatever the timing of the first one's shapes said
+    from cxxnet_amd.ops import gemm
+    monkeypatch.setitem(gemm._glds_cfg, "tune", False)
     a = _step(batch, "0", monkeypatch)
     b = _step(batch, "1", monkeypatch)
     assert torch.equal(a, b), (a - b).abs().max().item()

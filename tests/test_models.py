@@ -67,7 +67,9 @@ def test_model_one_step_gpu_vs_cpu(model, batch, ncls):
     cpu = _trainer(pairs)
     gpu = _trainer([(k, "gpu" if k == "dev" else v) for k, v in pairs])
     cpu.net.arena.w.copy_(cpu.net.arena.w.to(torch.bfloat16).float())
-    for (_, sc), (_, sg) in zip(cpu.net.arena.specs, gpu.net.arena.specs):
+    src = {(li, sc.tag): sc for li, sc in cpu.net.arena.specs}  # (the GPU arena may group siblings)
+    for li, sg in gpu.net.arena.specs:
+        sc = src[(li, sg.tag)]
         sg.w.zero_()
         sg.w[..., : sc.shape[-1]].copy_(sc.w)  # padded first-layer input channels
     gpu.net.arena.sync_shadow()
