@@ -37,7 +37,8 @@ def _step(batch, fuse, monkeypatch):
     monkeypatch.setenv("CXXNET_FUSE_DROPOUT", fuse)
     tr = NetTrainer()
     for k, v in list(native.rt().parse_config(NET)) + [("batch_size", str(batch)), ("dev", "gpu"), ("seed", "3"),
-                                                       ("eval_train", "0"), ("silent", "1"), ("eta", "0.1")]:
+                                                       ("eval_train", "0"), ("silent", "1"), ("eta", "0.1"),
+                                                       ("deterministic", "1")]:
         tr.set_param(k, v)
     tr.init_model()
     drops = [c.layer for c in tr.net.connections if type(c.layer).__name__ == "DropoutLayer"]

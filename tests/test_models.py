@@ -82,7 +82,9 @@ def test_model_one_step_gpu_vs_cpu(model, batch, ncls):
     assert torch.isfinite(pg).all()
     assert _rel(pg, pc) < 0.05, _rel(pg, pc)
     worst = 0.0
-    for (li, sc), (_, sg) in zip(cpu.net.arena.specs, gpu.net.arena.specs):
+    gsp = {(li, sg.tag): sg for li, sg in gpu.net.arena.specs}
+    for li, sc in cpu.net.arena.specs:
+        sg = gsp[(li, sc.tag)]
         mc = cpu.net.arena.m1[sc.offset:sc.offset + sc.numel].view(sc.shape)
         mg = gpu.net.arena.m1[sg.offset:sg.offset + sg.numel].view(sg.shape)[..., : sc.shape[-1]]
         if mc.abs().max() < 1e-12:
