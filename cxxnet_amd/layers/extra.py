@@ -116,6 +116,10 @@ class ConcatLayer(Layer):
         self.grad_mask_inputs = set()
         # the inputs are channel slices of the output buffer (NeuralNet._fuse_concat): no copies
         self.zero_copy = False
+        # zero-copy inputs that moved into a sibling group's buffer H (NeuralNet._fuse_siblings):
+        # (group, H channel offset, output channel offset, channels); h_copies: with H bound
+        self.copy_from_h = []
+        self.h_copies = []
 
     def init_connection(self, nodes_in, nodes_out):
         _check(len(nodes_in) > 1 and len(nodes_out) == 1, "Concat layer only support n-1 connection")
@@ -147,6 +151,9 @@ class ConcatLayer(Layer):
 
     def forward(self, is_train, nodes_in, nodes_out):
         if self.zero_copy:
+            out = nodes_out[0].data
+            for H, hoff, coff, c in self.h_copies:  # sibling outputs computed into H
+                ops.channel_copy(H[: out.shape[0]], hoff, out, coff, c)
             return
         if self.dim == 1:
             if ops.concat_channels([n.data for n in nodes_in], nodes_out[0].data):
@@ -164,7 +171,12 @@ class ConcatLayer(Layer):
                 off += wi
 
     def backprop(self, prop_grad, nodes_in, nodes_out):
-        if not prop_grad or self.zero_copy:
+        if not prop_grad:
+            return
+        if self.zero_copy:
+            out = nodes_out[0].data
+            for H, hoff, coff, c in self.h_copies:  # the slice's gradient back into H, times relu'
+                ops.channel_copy(out, coff, H[: out.shape[0]], hoff, c, mask_relu=True)
             return
         if self.dim == 1:
             if ops.concat_channels([n.gdst for n in nodes_in], nodes_out[0].data, backward=True,

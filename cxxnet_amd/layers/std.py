@@ -399,10 +399,9 @@ class ConvolutionLayer(Layer):
             return
         bias = self.b.w if self.b is not None else None
         S = self.sib
-        if S is not None:  # all siblings as one GEMM: [0, C1) to this output, the rest to H
-            N = self.geo.N
-            ops.gemm.conv_forward_split(nodes_in[0].data, S["w_all"], S["b_all"], nodes_out[0].data, S["H"][:N],
-                                        S["c1"], self._sib_geo(S["ctot"]), relu=self.fuse_relu)
+        if S is not None:  # all siblings as one GEMM into their group buffer H
+            ops.conv_forward(nodes_in[0].data, S["w_all"], S["b_all"], S["H"][:self.geo.N], self._sib_geo(S["ctot"]),
+                             relu=self.fuse_relu)
             return
         # few-channel stride-1 first layers (VGG conv1_1): the direct kernel pads on the
         # fly; the zero-bordered copy is then built by the weight-gradient pass that needs it
@@ -421,16 +420,16 @@ class ConvolutionLayer(Layer):
         self.geo.N = x.shape[0]
         S = self.sib
         if S is not None:
-            # the other siblings: their dy is H itself (their consumers wrote it into the slices)
-            N = x.shape[0]
-            H = S["H"][:N]
-            gbc = self._sib_geo(S["cbc"])
-            ops.conv_backward_weight(x, H, S["wbc_g"], gbc)
-            if S["bbc_g"] is not None:
-                self.ctx.bias_grad(_pixel_rows(H), S["bbc_g"])
+            # every sibling at once: their dy is H itself (the consumers of the slices wrote it)
+            H = S["H"][:x.shape[0]]
+            gall = self._sib_geo(S["ctot"])
+            ops.conv_backward_weight(x, H, S["w_g"], gall)
+            if S["b_g"] is not None:
+                self.ctx.bias_grad(_pixel_rows(H), S["b_g"])
             if prop_grad:
                 ready = self.ctx.flipped is not None and id(self) in self.ctx.flipped
-                ops.conv_backward_data(H, S["wbc_wb"], S["dx_node"].gdst, gbc, S["wt_bc"], wt_ready=ready)
+                ops.conv_backward_data(H, S["w_all"], S["dx_node"].gdst, gall, S["wt"], wt_ready=ready)
+            return
         xw, geo = self._padded(x, getattr(self, "_xpad_stale", False))
         self._xpad_stale = False
         want_db = self.b is not None and not self.bias_done and self.ctx.is_gpu
@@ -450,11 +449,11 @@ class ConvolutionLayer(Layer):
                 below.bias_done = True
 
     def extra_flip_targets(self):
-        """Flip items besides flip_target(): a sibling group's stacked non-lead weights."""
+        """Flip items besides flip_target(): a sibling group's stacked weights."""
         S = self.sib
         if S is None:
             return []
-        return [(S["wbc_wb"], S["wt_bc"], self._sib_geo(S["cbc"]))]
+        return [(S["w_all"], S["wt"], self._sib_geo(S["ctot"]))]
 
     def flip_target(self):
         """(weights, flipped-weights buffer, geometry) of the data-gradient GEMM."""

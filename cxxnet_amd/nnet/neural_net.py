@@ -399,15 +399,17 @@ class NeuralNet:
 
     def _fuse_siblings(self, producers, consumers):
         """Sibling 1x1 convs (an inception module's 1x1, 3x3_reduce and 5x5_reduce: same input
-        through a zero-copy split, 1x1 / stride 1 / pad 0, relu fused) as ONE GEMM per direction
-        where the data allow.  The first sibling (the lead) computes all of them: output
-        channels [0, C1) to its own output (a concat slice), the others to channel slices of one
-        new buffer H [pixels][C2 + C3 + ...] (ops.conv_forward_split); backward, the lead's own
-        part as before plus one weight-gradient and one data-gradient GEMM over all of H (its
-        dy is H itself, since the consumers of the slices write their input gradient into
-        them).  The arena lays the group's weights out as one matrix and its biases as one
-        vector (ParamArena.build groups); checkpoints stay per layer.  The split sums one
-        gradient fewer per extra sibling.  Reference: src/layer/split_layer-inl.hpp:29-41,
+        through a zero-copy split, 1x1 / stride 1 / pad 0, relu fused) as ONE GEMM per
+        direction.  Their outputs become channel slices of one buffer H [pixels][C1 + C2 + ...]:
+        the first sibling (the lead) computes all of them in one forward GEMM, the consumers of
+        the slices read them in place (strided NHWC) and write their input gradients back into
+        them, so H's gradient is contiguous and one weight-gradient and one data-gradient GEMM
+        over all of H replace one per sibling.  A sibling whose output was a zero-copy concat
+        slice (the 1x1) moves into H; the concat copies that slice in (forward) and its gradient
+        back (backward, relu'-masked) -- two small copies instead of two GEMMs.  The arena lays
+        each group's weights out as one matrix and its biases as one vector (ParamArena.build
+        groups); checkpoints stay per layer.  The split sums one gradient per group instead of
+        one per sibling.  Reference: src/layer/split_layer-inl.hpp:29-41,
         src/layer/convolution_layer-inl.hpp:70-106.  CXXNET_FUSE_SIBLINGS=0 turns it off."""
         self.sib_groups = []
         self.sib_views = {}
@@ -435,32 +437,48 @@ class NeuralNet:
                 if (lp.kernel_height != 1 or lp.kernel_width != 1 or lp.stride != 1 or lp.pad_y or lp.pad_x
                         or lp.num_group != 1 or lp.num_channel % 8 or getattr(lay, "_prepad_on", False)):
                     continue
+                a = cj.nodes_out[0]
+                if id(a) in views:  # a zero-copy concat slice: movable if it is a ch_concat input
+                    cc = self._concat_of(a, consumers)
+                    if cc is None:
+                        continue
                 mem.append((j, o))
             mem.sort(key=lambda t: t[0])
             if len(mem) < 2 or len({self.connections[j].layer.lp.no_bias for j, _ in mem}) != 1:
                 continue
-            rest = [(j, o) for j, o in mem[1:] if id(self.connections[j].nodes_out[0]) not in views]
-            if not rest:
-                continue
-            lead_j = mem[0][0]
             gi = len(self.sib_groups)
-            group = [lead_j] + [j for j, _ in rest]
+            group = [j for j, _ in mem]
             self.sib_groups.append(group)
             off = 0
-            for j, _ in rest:
+            for j, _ in mem:
                 a = self.connections[j].nodes_out[0]
+                if id(a) in views:  # the concat copies this slice from H instead
+                    _, out, coff, c = views.pop(id(a))
+                    cc = self._concat_of(a, consumers)
+                    cc.layer.copy_from_h.append((gi, off, coff, a.cp))
                 self.sib_views[id(a)] = (a, gi, off, a.cp)
                 off += a.cp
+            for j, _ in mem[1:]:
                 self.connections[j].layer.sib_member = True
-            lead = self.connections[lead_j].layer
-            lead.sib = {"gi": gi, "layers": [self.connections[j].layer for j in group], "cbc": off,
-                        "dx_node": rest[0][1]}
-            # the data-gradient of every sibling after the lead lands in the first one's slot
-            conn.layer.skip_grads = {id(o) for _, o in rest[1:]}
+            lead = self.connections[group[0]].layer
+            lead.sib = {"gi": gi, "layers": [self.connections[j].layer for j in group], "ctot": off,
+                        "dx_node": mem[0][1]}
+            # the data-gradient of every sibling lands in the lead's slot of the split
+            conn.layer.skip_grads = {id(o) for _, o in mem[1:]}
+
+    def _concat_of(self, a, consumers):
+        """The zero-copy ch_concat connection that a fused-relu conv output a feeds, or None."""
+        b = next((bb for bb, src in self.aliases.items() if src is a), None)  # b = relu(a) alias key
+        node = a if b is None else next((n for n in self.nodes if id(n) == b), a)
+        for j, _ in consumers.get(id(node), []):
+            cj = self.connections[j]
+            if cj.type == K_CHCONCAT and getattr(cj.layer, "zero_copy", False):
+                return cj
+        return None
 
     def _sibling_views(self):
         """Arena views of each sibling group (after _build_arena): the stacked weights (compute
-        copy), the non-lead part's weights / gradient, and the biases."""
+        copy and gradient) and biases."""
         a = self.arena
         wb = a.wb if a.wb is not None else a.w
         for conn in self.connections:
@@ -469,20 +487,17 @@ class NeuralNet:
                 continue
             lays = S["layers"]
             cin = lays[0].geo.C
-            ctot = sum(l.lp.num_channel for l in lays)
-            c1 = lays[0].lp.num_channel
-            w0, w1 = lays[0].w.offset, lays[1].w.offset
-            S["ctot"], S["c1"] = ctot, c1
+            ctot = S["ctot"]
+            w0 = lays[0].w.offset
             S["w_all"] = wb[w0:w0 + ctot * cin].view(ctot, 1, 1, cin)
-            S["wbc_wb"] = wb[w1:w1 + S["cbc"] * cin].view(S["cbc"], 1, 1, cin)
-            S["wbc_g"] = a.g[w1:w1 + S["cbc"] * cin].view(S["cbc"], 1, 1, cin)
-            S["wt_bc"] = torch.empty_like(S["wbc_wb"])
+            S["w_g"] = a.g[w0:w0 + ctot * cin].view(ctot, 1, 1, cin)
+            S["wt"] = torch.empty_like(S["w_all"])
             if lays[0].b is not None:
-                b0, b1 = lays[0].b.offset, lays[1].b.offset
+                b0 = lays[0].b.offset
                 S["b_all"] = a.w[b0:b0 + ctot]
-                S["bbc_g"] = a.g[b1:b1 + S["cbc"]]
+                S["b_g"] = a.g[b0:b0 + ctot]
             else:
-                S["b_all"] = S["bbc_g"] = None
+                S["b_all"] = S["b_g"] = None
 
     def _alloc_nodes(self):
         dt = self.ctx.act_dtype
@@ -508,6 +523,8 @@ class NeuralNet:
             S = getattr(conn.layer, "sib", None)
             if S:
                 S["H"] = hbuf[S["gi"]]
+            if getattr(conn.layer, "copy_from_h", None):
+                conn.layer.h_copies = [(hbuf[gi], hoff, coff, c) for gi, hoff, coff, c in conn.layer.copy_from_h]
         pending = [n for n in self.nodes if id(n) in aliases]
         for _ in range(len(pending) + 1):  # resolve chains (split of a relu alias, ...)
             left = []
@@ -692,7 +709,8 @@ class NeuralNet:
                     continue
                 if hasattr(lay, "flip_target") and (i != 0 or prop_to_input) and id(lay) not in seen:
                     seen.add(id(lay))
-                    flips.append(lay.flip_target())
+                    if getattr(lay, "sib", None) is None:  # (a group lead flips the stacked weights)
+                        flips.append(lay.flip_target())
                     flips.extend(lay.extra_flip_targets())
             from ..ops.gemm import conv_weight_flip_multi
             conv_weight_flip_multi(flips)
