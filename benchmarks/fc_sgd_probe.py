@@ -1,0 +1,64 @@
+"""The fc weight-gradient GEMM fused with the SGD step (ops.fc_backward_weight_sgd, table key
+"fws") on AlexNet's fc6 / fc7 at batch 256, for each MN-major tile: median time and the
+parameter stream rate (18 bytes per parameter: fp32 w and momentum read and written, the bf16
+shadow written).  Interleaved rounds in one process.
+
+    python benchmarks/fc_sgd_probe.py [--tiles 1,2,17,23,40,41] [--rounds 7]"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cxxnet_amd import ops  # noqa: E402
+from cxxnet_amd.ops import gemm as G  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tiles", default="-1,1,2,17,23,40,41")
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--groups", default="8", help="tile-order groups (ops.gemm.set_tile_group) to A/B")
+    a = ap.parse_args()
+    B = a.batch
+    for name, nin, nout in (("fc6", 9216, 4096), ("fc7", 4096, 4096)):
+        g = torch.Generator(device="cuda").manual_seed(1)
+        x = torch.randn(B, nin, device="cuda", generator=g).to(torch.bfloat16)
+        dy = torch.randn(B, nout, device="cuda", generator=g).to(torch.bfloat16)
+        w = torch.randn(nout, nin, device="cuda", generator=g) * 0.02
+        m = torch.zeros(nout, nin, device="cuda")
+        wb = w.to(torch.bfloat16)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        arms = [(int(t), int(gi)) for t in a.tiles.split(",") for gi in a.groups.split(",")]
+        times = {arm: [] for arm in arms}
+        for _ in range(a.rounds):
+            for arm in arms:
+                t, gi = arm
+                G.set_glds(True, t)
+                G.set_tile_group(gi)
+                assert ops.fc_backward_weight_sgd(x, dy, w, m, wb, 1e-6, 0.0, 0.9, 0.0)
+                torch.cuda.synchronize()
+                s.record()
+                for _ in range(a.iters):
+                    ops.fc_backward_weight_sgd(x, dy, w, m, wb, 1e-6, 0.0, 0.9, 0.0)
+                e.record()
+                e.synchronize()
+                times[arm].append(s.elapsed_time(e) * 1e3 / a.iters)
+        G.set_glds(True, -1)
+        G.set_tile_group(8)
+        rec = {"op": name, "batch": B}
+        for (t, gi), v in times.items():
+            us = statistics.median(v)
+            tag = (f"t{t}" if t >= 0 else "tdef") + f"g{gi}"
+            rec[f"{tag}_us"] = round(us, 1)
+            rec[f"{tag}_TBps"] = round(18 * nin * nout / us / 1e6, 2)
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -19,10 +19,10 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-KK = (0, 1, 2, 7, 10, 15, 20, 21, 25, 30, 31, 33, 34, 35, 36, 37, 38, 39, 50, 51, 70, 71, 72, 73, 74, 75, 76, 77,
-      78, 79, 80, 81, 82, 83, 110, 111, 112, 113, 114, 115)
-MM = (1, 2, 13, 17, 23, 36, 40, 41)
-SHORT = (0, 1, 2, 7, 10, 15, 34, 37, 38, 75, 76, 77, 78, 79, 80, 81)
+# the compiled tile sets (ops.gemm.GLDS_TILES; tests/test_tile_table_cpu.py keeps them in sync)
+KK = (1, 7, 10, 15, 21, 25, 30, 31, 34, 37, 38, 39, 72, 75, 76, 77, 78, 79, 82, 114)
+MM = (1, 2, 17, 23, 40, 41)
+SHORT = (1, 7, 10, 15, 34, 37, 38, 75, 76, 77, 78, 79)
 
 
 class LogDict(dict):
@@ -88,12 +88,12 @@ def main():
         if a.ops and op not in a.ops.split(","):
             continue
         if op in ("cf", "cd", "cr", "fc"):
-            cands = list(SHORT if a.short else KK) + ([G.REG] if op in ("cf", "cd") else [])
+            cands = list(SHORT if a.short else KK) + ([G.REG, 130, 131, 133] if op in ("cf", "cd") else [])
         elif op in ("fw", "fws", "cwr"):
             cands = list(MM)
-        elif op == "cw":  # conv weight-grad: the register split-K kernel, LDS-DMA MN tiles, tile 120,
+        elif op == "cw":  # conv weight-grad: the register split-K kernel, LDS-DMA MN tiles,
             # the direct 3x3 kernel (140; it declines other shapes and the entry then runs REG)
-            cands = [G.REG] + list(MM) + [120, 140]
+            cands = [G.REG] + list(MM) + [140]
         elif op == "cws":
             N, H, W, C, Co, KH, KW, st, py, px, g = (int(v) for v in key.split("|")[1:])
             Ho, Wo = conv_out_size(H, W, KH, KW, st, py, px)
