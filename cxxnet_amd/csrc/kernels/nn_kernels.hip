@@ -1405,7 +1405,9 @@ lrn_pool_bwd(const bf16_t *__restrict__ P, const bf16_t *__restrict__ dY, const 
       }
   }
   if (dbias_part != nullptr) {  // the block's column sums in a fixed order (wave, pixel): no atomics
-    __shared__ float red[NT / 64][64][9];
+    // (in the window buffer, done with after phase 2: no extra LDS, so no lower occupancy)
+    __syncthreads();
+    float(*red)[64][9] = reinterpret_cast<float(*)[64][9]>(plds);
 #pragma unroll
     for (int k = 0; k < 8; ++k) red[wave][lane][k] = lane_ok ? bsum[k] : 0.f;
     __syncthreads();
@@ -1420,7 +1422,8 @@ lrn_pool_bwd(const bf16_t *__restrict__ P, const bf16_t *__restrict__ dY, const 
 }
 
 // db[c] += sum_r part[r][c] over nrows fp32 partial rows of C columns: 32 columns x 8 row groups
-// per block over a chunk of `chunk` rows, one atomic per column per chunk (one chunk: a fixed
+// per block over a chunk of `chunk` rows (32: four dependent loads per thread, a few-us kernel
+// instead of 11 us at 256), one atomic per column per chunk (one chunk: a fixed
 // summation order, the deterministic mode)
 __global__ void part_rows_colsum(const float *__restrict__ part, int nrows, int C, float *__restrict__ db, int chunk) {
   const int c = blockIdx.x * 32 + (threadIdx.x & 31);
@@ -2420,7 +2423,8 @@ CXN_API int cxn_lrn_pool_bwd(const void *P, const void *dY, const void *arg, voi
   const float sa = alpha / nsize;
   float *part = dbias != nullptr ? dbias_part : nullptr;
   if (dbias != nullptr && (part == nullptr || part_rows < blocks)) return -4;
-  const size_t lds = static_cast<size_t>((R + 1) * row_bytes);
+  // (the bias partials reuse the window buffer: at least NT x 9 floats)
+  const size_t lds = std::max(static_cast<size_t>((R + 1) * row_bytes), static_cast<size_t>(NT * 9 * 4));
 #define CXN_PLB(HV) CXN_LAUNCH((lrn_pool_bwd<HV>), blocks, NT, lds, S_, (const bf16_t *)P, (const bf16_t *)dY,        \
                                (const uint8_t *)arg, (bf16_t *)dx, Hin, Win, C, Ho, Wo, HC, WC, R, nband, relu_bit, sa, \
                                beta, knorm, part)
@@ -2433,7 +2437,7 @@ CXN_API int cxn_lrn_pool_bwd(const void *P, const void *dY, const void *arg, voi
   }
 #undef CXN_PLB
   if (part != nullptr) {
-    const int chunk = det ? blocks : 256;
+    const int chunk = det ? blocks : 32;  // 4 rows per thread: latency-bound otherwise
     CXN_LAUNCH((part_rows_colsum), dim3((C + 31) / 32, (blocks + chunk - 1) / chunk), NT, 0, S_, part, blocks, C,
                dbias, chunk);
   }
