@@ -8,7 +8,8 @@ Writes N JPEG images (smooth random content, quality 90, ImageNet-like file size
 given side), packs them with im2bin into 64 MB pages, then times `iter = imgbin(x)` +
 `threadbuffer` with the AlexNet training augmentation (random 227 crop, random mirror,
 mean_value) at batch 256 for each worker count, decoding in the native C++ pool
-(decode_native), in Pillow processes (decode_process) or in Pillow threads (decode_thread).  Prints one JSON line per setting: img/s, img/s per busy host
+(decode_native), in the native pool's entropy stage + the GPU (gpu: decode_gpu, io/jpeg_stage.py),
+in Pillow processes (decode_process) or in Pillow threads (decode_thread).  Prints one JSON line per setting: img/s, img/s per busy host
 core, and the host cores one MI355X would need at its measured AlexNet training rate.
 """
 import argparse
@@ -64,12 +65,13 @@ def make_trainer(model, batch):
 
 def run(root, it_type, mode, workers, batches, batch, tr=None):
     threads, procs = (workers, 0) if mode == "thread" else (1, workers)
-    nat = "1" if mode == "native" else "0"
+    nat = "1" if mode in ("native", "gpu") else "0"
     from cxxnet_amd.io.iterators import create_iterator
     cfg = [("iter", it_type), ("image_list", os.path.join(root, "train.lst")),
            ("image_bin", os.path.join(root, "train.bin")), ("rand_crop", "1"), ("rand_mirror", "1"),
            ("mean_value", "104,117,123"), ("decode_thread", str(threads)), ("decode_process", str(procs)),
            ("decode_native", nat), ("decode_native_threads", str(workers)),
+           ("decode_gpu", "1" if mode == "gpu" else "0"),
            ("input_shape", "3,227,227"),
            ("batch_size", str(batch)), ("round_batch", "1"), ("silent", "1"), ("iter", "threadbuffer"),
            ("iter", "end")]
@@ -89,8 +91,10 @@ def run(root, it_type, mode, workers, batches, batch, tr=None):
         b = it.value()
         if tr is not None:
             tr.update(b)
+        elif mode == "gpu":  # decode only: finish the decode on the GPU
+            b.data.to_u8("cuda")
         n += 1
-    if tr is not None:
+    if tr is not None or mode == "gpu":
         import torch
         torch.cuda.synchronize()
     el = time.perf_counter() - t0
@@ -103,7 +107,7 @@ def main():
     ap.add_argument("--n", type=int, default=2048)
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--workers", default="4,8,16")
-    ap.add_argument("--modes", default="native,process,thread")
+    ap.add_argument("--modes", default="gpu,native,process,thread")
     ap.add_argument("--iters", default="imgbin,imgbinx")
     ap.add_argument("--batches", type=int, default=12)
     ap.add_argument("--batch", type=int, default=256)

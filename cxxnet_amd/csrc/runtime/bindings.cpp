@@ -27,6 +27,57 @@ static KVList ParseConfigFile(const std::string &path) {
   return ConfigTokenizer(ss.str()).ParseAll();
 }
 
+// (out_h, out_w, channels, rand_crop, rand_mirror, mirror, crop_y_start, crop_x_start,
+//  max_random_contrast, max_random_illumination, mean_mode)
+static CropConfig ParseCropConfig(py::tuple cfg) {
+  CropConfig c;
+  c.out_h = cfg[0].cast<int>();
+  c.out_w = cfg[1].cast<int>();
+  c.channels = cfg[2].cast<int>();
+  c.rand_crop = cfg[3].cast<int>();
+  c.rand_mirror = cfg[4].cast<int>();
+  c.mirror = cfg[5].cast<int>();
+  c.crop_y_start = cfg[6].cast<int>();
+  c.crop_x_start = cfg[7].cast<int>();
+  c.max_random_contrast = cfg[8].cast<float>();
+  c.max_random_illumination = cfg[9].cast<float>();
+  c.mean_mode = cfg[10].cast<int>();
+  if (c.channels < 1 || c.channels > 3) throw std::runtime_error("JpegDecodePool: 1-3 channels");
+  return c;
+}
+
+static void CheckPrmCm(py::array_t<int32_t> &prm, py::array_t<float> &cm, long B) {
+  if (prm.ndim() != 2 || prm.shape(0) != B || prm.shape(1) != 4 || cm.ndim() != 2 || cm.shape(0) != B ||
+      cm.shape(1) != 2 || !(prm.flags() & py::array::c_style) || !(cm.flags() & py::array::c_style))
+    throw std::runtime_error("JpegDecodePool: prm [B][4] int32 / cm [B][2] float32 expected");
+}
+
+// items: [(row, payload bytes-like or path str, seed)]
+static std::vector<DecodeItem> ParseItems(py::list items, long B, std::vector<py::buffer_info> &keep) {
+  std::vector<DecodeItem> its;
+  its.reserve(items.size());
+  keep.reserve(items.size());
+  for (auto h : items) {
+    py::tuple t = h.cast<py::tuple>();
+    DecodeItem d;
+    d.row = t[0].cast<int>();
+    if (d.row < 0 || d.row >= B) throw std::runtime_error("JpegDecodePool: row out of range");
+    d.seed = t[2].cast<uint64_t>();
+    py::handle pl = t[1];
+    if (py::isinstance<py::str>(pl)) {
+      d.data = nullptr;
+      d.size = 0;
+      d.path = pl.cast<std::string>();
+    } else {
+      keep.push_back(py::reinterpret_borrow<py::buffer>(pl).request());
+      d.data = static_cast<const unsigned char *>(keep.back().ptr);
+      d.size = static_cast<size_t>(keep.back().size * keep.back().itemsize);
+    }
+    its.push_back(std::move(d));
+  }
+  return its;
+}
+
 PYBIND11_MODULE(_cxxnet_rt, m) {
   m.doc() = "cxxnet_amd native runtime: config parser, NetConfig, checkpoint PODs, IO, metrics";
 
@@ -177,48 +228,14 @@ PYBIND11_MODULE(_cxxnet_rt, m) {
             // items: [(row, payload bytes-like or path str, seed)]; cfg: (out_h, out_w, channels,
             // rand_crop, rand_mirror, mirror, crop_y_start, crop_x_start, max_random_contrast,
             // max_random_illumination, mean_mode)
-            CropConfig c;
-            c.out_h = cfg[0].cast<int>();
-            c.out_w = cfg[1].cast<int>();
-            c.channels = cfg[2].cast<int>();
-            c.rand_crop = cfg[3].cast<int>();
-            c.rand_mirror = cfg[4].cast<int>();
-            c.mirror = cfg[5].cast<int>();
-            c.crop_y_start = cfg[6].cast<int>();
-            c.crop_x_start = cfg[7].cast<int>();
-            c.max_random_contrast = cfg[8].cast<float>();
-            c.max_random_illumination = cfg[9].cast<float>();
-            c.mean_mode = cfg[10].cast<int>();
-            if (c.channels < 1 || c.channels > 3) throw std::runtime_error("JpegDecodePool: 1-3 channels");
+            CropConfig c = ParseCropConfig(cfg);
             if (out.ndim() != 4 || out.shape(1) != c.out_h || out.shape(2) != c.out_w || out.shape(3) != c.channels ||
                 !(out.flags() & py::array::c_style))
               throw std::runtime_error("JpegDecodePool: out must be a C-contiguous [B][h][w][C] uint8 array");
             const long B = out.shape(0);
-            if (prm.ndim() != 2 || prm.shape(0) != B || prm.shape(1) != 4 || cm.ndim() != 2 || cm.shape(0) != B ||
-                cm.shape(1) != 2 || !(prm.flags() & py::array::c_style) || !(cm.flags() & py::array::c_style))
-              throw std::runtime_error("JpegDecodePool: prm [B][4] int32 / cm [B][2] float32 expected");
-            std::vector<DecodeItem> its;
+            CheckPrmCm(prm, cm, B);
             std::vector<py::buffer_info> keep;  // buffer views stay valid while the GIL is released
-            its.reserve(items.size());
-            keep.reserve(items.size());
-            for (auto h : items) {
-              py::tuple t = h.cast<py::tuple>();
-              DecodeItem d;
-              d.row = t[0].cast<int>();
-              if (d.row < 0 || d.row >= B) throw std::runtime_error("JpegDecodePool: row out of range");
-              d.seed = t[2].cast<uint64_t>();
-              py::handle pl = t[1];
-              if (py::isinstance<py::str>(pl)) {
-                d.data = nullptr;
-                d.size = 0;
-                d.path = pl.cast<std::string>();
-              } else {
-                keep.push_back(py::reinterpret_borrow<py::buffer>(pl).request());
-                d.data = static_cast<const unsigned char *>(keep.back().ptr);
-                d.size = static_cast<size_t>(keep.back().size * keep.back().itemsize);
-              }
-              its.push_back(std::move(d));
-            }
+            std::vector<DecodeItem> its = ParseItems(items, B, keep);
             uint8_t *o = out.mutable_data();
             int32_t *pp = prm.mutable_data();
             float *cp = cm.mutable_data();
@@ -230,7 +247,38 @@ PYBIND11_MODULE(_cxxnet_rt, m) {
             return failed;
           },
           "Decode + crop/mirror every (row, payload, seed) into out[row]; returns the rows it could not "
-          "decode (non-JPEG or unsupported JPEG: use the Pillow path for those)");
+          "decode (non-JPEG or unsupported JPEG: use the Pillow path for those)")
+      .def(
+          "decode_coef",
+          [](JpegDecodePool &pool, py::list items, py::tuple cfg, py::array_t<int16_t> coef, py::array_t<int32_t> bwin,
+             py::array_t<int32_t> meta, py::array_t<int32_t> prm, py::array_t<float> cm) {
+            CropConfig c = ParseCropConfig(cfg);
+            const long B = meta.ndim() == 3 ? meta.shape(0) : -1;
+            if (B < 0 || meta.shape(1) != 3 || meta.shape(2) != kCoefMeta || !(meta.flags() & py::array::c_style))
+              throw std::runtime_error("JpegDecodePool.decode_coef: meta must be a C-contiguous [B][3][80] int32 array");
+            if (coef.ndim() != 2 || coef.shape(1) != 64 || bwin.ndim() != 1 || bwin.shape(0) != coef.shape(0) ||
+                !(coef.flags() & py::array::c_style) || !(bwin.flags() & py::array::c_style))
+              throw std::runtime_error("JpegDecodePool.decode_coef: coef [cap][64] int16 / bwin [cap] int32 expected");
+            CheckPrmCm(prm, cm, B);
+            std::vector<py::buffer_info> keep;
+            std::vector<DecodeItem> its = ParseItems(items, B, keep);
+            CoefStage st;
+            st.coef = coef.mutable_data();
+            st.bwin = bwin.mutable_data();
+            st.meta = meta.mutable_data();
+            st.cap_blocks = coef.shape(0);
+            int32_t *pp = prm.mutable_data();
+            float *cp = cm.mutable_data();
+            std::pair<std::vector<int>, long> r;
+            {
+              py::gil_scoped_release rel;
+              r = pool.RunCoef(its, c, st, pp, cp);
+            }
+            return py::make_tuple(r.first, r.second);
+          },
+          "Entropy-decode every (row, payload, seed) into the GPU decode stage (coef blocks, their window "
+          "ids, per-row window tables; ops.jpeg_decode finishes on the GPU); returns (rows left to "
+          "decode(), blocks used)");
 
   py::class_<ImageListEntry>(m, "ImageListEntry")
       .def_readonly("index", &ImageListEntry::index)

@@ -34,6 +34,7 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 namespace cxxnet_rt {
@@ -45,9 +46,40 @@ typedef unsigned int JDIMENSION;
 typedef unsigned char JSAMPLE;
 typedef JSAMPLE *JSAMPROW;
 typedef JSAMPROW *JSAMPARRAY;
-enum { JCS_RGB = 2, JDCT_ISLOW = 0, JPEG_LIB_VERSION = 80 };
+enum { JCS_GRAYSCALE = 1, JCS_RGB = 2, JCS_YCbCr = 3, JDCT_ISLOW = 0, JPEG_LIB_VERSION = 80 };
 struct jpeg_common_struct;
 typedef jpeg_common_struct *j_common_ptr;
+typedef short JCOEF;
+typedef JCOEF JBLOCK[64];  // one 8x8 block of quantised coefficients, natural (row-major) order
+typedef JBLOCK *JBLOCKROW;
+typedef JBLOCKROW *JBLOCKARRAY;
+struct jvirt_barray_control;
+typedef jvirt_barray_control *jvirt_barray_ptr;
+
+// the memory manager's method table (only access_virt_barray is called)
+struct jpeg_memory_mgr {
+  void *alloc_small, *alloc_large, *alloc_sarray, *alloc_barray, *request_virt_sarray, *request_virt_barray,
+      *realize_virt_arrays, *access_virt_sarray;
+  JBLOCKARRAY (*access_virt_barray)(j_common_ptr, jvirt_barray_ptr, JDIMENSION start_row, JDIMENSION num_rows,
+                                    int writable);
+};
+
+struct JQUANT_TBL {
+  unsigned short quantval[64];  // natural order
+  int sent_table;
+};
+
+struct jpeg_component_info {
+  int component_id, component_index, h_samp_factor, v_samp_factor, quant_tbl_no, dc_tbl_no, ac_tbl_no;
+  JDIMENSION width_in_blocks, height_in_blocks;
+  int DCT_h_scaled_size, DCT_v_scaled_size;
+  JDIMENSION downsampled_width, downsampled_height;
+  int component_needed;
+  int MCU_width, MCU_height, MCU_blocks, MCU_sample_width, last_col_width, last_row_height;
+  JQUANT_TBL *quant_table;
+  void *dct_table;
+};
+static_assert(sizeof(jpeg_component_info) == 96, "libjpeg v8 jpeg_component_info layout");
 
 struct jpeg_error_mgr {
   void (*error_exit)(j_common_ptr);
@@ -139,6 +171,7 @@ struct Api {
   JDIMENSION (*skip_scanlines)(jpeg_decompress_struct *, JDIMENSION) = nullptr;
   void (*crop_scanline)(jpeg_decompress_struct *, JDIMENSION *, JDIMENSION *) = nullptr;
   void (*abort_decompress)(jpeg_decompress_struct *) = nullptr;
+  jvirt_barray_ptr *(*read_coefficients)(jpeg_decompress_struct *) = nullptr;
   std::string error;
   bool ok = false;
 
@@ -166,6 +199,7 @@ struct Api {
     sym(skip_scanlines, "jpeg_skip_scanlines");
     sym(crop_scanline, "jpeg_crop_scanline");
     sym(abort_decompress, "jpeg_abort_decompress");
+    sym(read_coefficients, "jpeg_read_coefficients");
     ok = all;
     if (!ok) error = "libjpeg lacks the libjpeg-turbo partial-decode entry points";
   }
@@ -222,6 +256,42 @@ struct DecodeItem {
   uint64_t seed;
 };
 
+// The crop / mirror / contrast / illumination draws of io/augment.py _augment_one, in its order,
+// from the record's own generator.  False if the crop does not fit the H x W image.
+inline bool DrawCrop(int H, int W, const CropConfig &c, uint64_t seed, int *py, int *px, bool *pmirror,
+                     float *pcontrast, float *pillum) {
+  using namespace jpg;
+  const int ch = c.out_h, cw = c.out_w;
+  Rng rng(seed);
+  int yy = H - ch, xx = W - cw;
+  if (c.rand_crop && (yy || xx)) {
+    yy = static_cast<int>(rng.below(static_cast<uint32_t>(yy + 1)));
+    xx = static_cast<int>(rng.below(static_cast<uint32_t>(xx + 1)));
+  } else {
+    yy /= 2;
+    xx /= 2;
+  }
+  if (H != ch && c.crop_y_start != -1) yy = c.crop_y_start;
+  if (W != cw && c.crop_x_start != -1) xx = c.crop_x_start;
+  if (yy < 0 || xx < 0 || yy + ch > H || xx + cw > W) return false;
+  float contrast = static_cast<float>(rng.uniform() * c.max_random_contrast * 2 - c.max_random_contrast + 1);
+  float illum = static_cast<float>(rng.uniform() * c.max_random_illumination * 2 - c.max_random_illumination);
+  bool mirror;
+  if (c.mean_mode == 0) {
+    mirror = c.rand_mirror && rng.uniform() < 0.5;
+    contrast = 1.f;
+    illum = 0.f;
+  } else {
+    mirror = (c.rand_mirror && rng.uniform() < 0.5) || c.mirror == 1;
+  }
+  *py = yy;
+  *px = xx;
+  *pmirror = mirror;
+  *pcontrast = contrast;
+  *pillum = illum;
+  return true;
+}
+
 // Decodes one record's crop into out (out_h x out_w x channels, row-major), params (y, x,
 // mirrored), (contrast, illumination).  Returns 0, or a libjpeg message code / -1 / -2.
 inline int DecodeCrop(const jpg::Api &J, const unsigned char *buf, size_t len, const CropConfig &c, uint64_t seed,
@@ -251,31 +321,12 @@ inline int DecodeCrop(const jpg::Api &J, const unsigned char *buf, size_t len, c
     J.destroy_decompress(&cinfo);
     return -2;  // the Pillow path raises the reference's message
   }
-  // the draws of io/augment.py _augment_one, in its order
-  Rng rng(seed);
-  int yy = H - ch, xx = W - cw;
-  if (c.rand_crop && (yy || xx)) {
-    yy = static_cast<int>(rng.below(static_cast<uint32_t>(yy + 1)));
-    xx = static_cast<int>(rng.below(static_cast<uint32_t>(xx + 1)));
-  } else {
-    yy /= 2;
-    xx /= 2;
-  }
-  if (H != ch && c.crop_y_start != -1) yy = c.crop_y_start;
-  if (W != cw && c.crop_x_start != -1) xx = c.crop_x_start;
-  if (yy < 0 || xx < 0 || yy + ch > H || xx + cw > W) {
+  int yy, xx;
+  bool mirror;
+  float contrast, illum;
+  if (!DrawCrop(H, W, c, seed, &yy, &xx, &mirror, &contrast, &illum)) {
     J.destroy_decompress(&cinfo);
     return -2;
-  }
-  float contrast = static_cast<float>(rng.uniform() * c.max_random_contrast * 2 - c.max_random_contrast + 1);
-  float illum = static_cast<float>(rng.uniform() * c.max_random_illumination * 2 - c.max_random_illumination);
-  bool mirror;
-  if (c.mean_mode == 0) {
-    mirror = c.rand_mirror && rng.uniform() < 0.5;
-    contrast = 1.f;
-    illum = 0.f;
-  } else {
-    mirror = (c.rand_mirror && rng.uniform() < 0.5) || c.mirror == 1;
   }
   J.start_decompress(&cinfo);
   if (cinfo.output_components != 3) {
@@ -284,11 +335,13 @@ inline int DecodeCrop(const jpg::Api &J, const unsigned char *buf, size_t len, c
     return -1;
   }
   // crop_scanline aligns the window's left edge down to an iMCU boundary but keeps its right
-  // edge where asked, and the fancy upsampler treats that edge as the image border: ask for
-  // up to 16 more columns so the crop's last column keeps its right-hand chroma context
-  // (bit-identical to a full decode then; without the margin the edge column differs by a few
-  // levels on 4:2:0 images)
-  JDIMENSION x0 = static_cast<JDIMENSION>(xx), wd = static_cast<JDIMENSION>(std::min(cw + 16, W - xx));
+  // edge where asked, and the fancy upsampler treats both window edges as the image border:
+  // ask for one column more on the left (a crop starting on an iMCU boundary then starts one
+  // iMCU earlier) and up to 16 more on the right, so the crop's edge columns keep their
+  // chroma context (bit-identical to a full decode then; without the margins an edge column
+  // differs by a few levels on subsampled images)
+  JDIMENSION x0 = static_cast<JDIMENSION>(xx > 0 ? xx - 1 : 0);
+  JDIMENSION wd = static_cast<JDIMENSION>(std::min(xx + cw + 16, W)) - x0;
   J.crop_scanline(&cinfo, &x0, &wd);  // x0 <= xx, x0 + wd >= xx + cw
   const int dx = xx - static_cast<int>(x0);
   row.resize(static_cast<size_t>(cinfo.output_width) * 3 + 64);
@@ -318,6 +371,141 @@ inline int DecodeCrop(const jpg::Api &J, const unsigned char *buf, size_t len, c
     }
   }
   // the rows below the crop are never decoded
+  J.abort_decompress(&cinfo);
+  J.destroy_decompress(&cinfo);
+  prm[0] = yy;
+  prm[1] = xx;
+  prm[2] = mirror ? 1 : 0;
+  cm[0] = contrast;
+  cm[1] = illum;
+  return 0;
+}
+
+// ---- GPU decode stage: entropy decode here, everything after it on the GPU ------------------
+//
+// The host keeps only the serial part of JPEG decoding (Huffman / arithmetic decoding of the
+// coefficients: jpeg_read_coefficients); dequantisation, the islow IDCT, the fancy chroma
+// upsampling, YCbCr->RGB, crop and mirror run in ops/jpeg_kernels.hip over the whole batch.
+// Per record only the coefficient blocks of the crop window (plus the one chroma sample of
+// upsampling context on each side) are staged, so a large photo costs what a 256px one does.
+//
+// Staging layout (one batch): coef int16 [cap][64] blocks packed by an atomic cursor (the
+// order between records depends on the threads; every record finds its blocks through its
+// window table, so the decoded batch does not), bwin int32 [cap] window id of each block
+// (row * 3 + component), meta int32 [B][3][kCoefMeta] window tables (layout below).
+constexpr int kCoefMeta = 80;
+enum CoefMetaField {
+  kBlk0 = 0,    // first block of the window in coef
+  kBw = 1,      // window width / height in blocks
+  kBh = 2,
+  kBy0 = 3,     // window origin in the component's block grid
+  kBx0 = 4,
+  kDw = 5,      // component's real sample width / height (libjpeg downsampled_width / _height)
+  kDh = 6,
+  kRh = 7,      // horizontal / vertical expansion to the luma grid (1 or 2)
+  kRv = 8,
+  kNcomp = 9,   // 1 (grayscale) or 3 (YCbCr); same in the three windows of a record
+  kValid = 10,  // 1: decoded here; 0: not this stage's row (padding / fallback / other rank)
+  kQuant = 16,  // 64 dequantisation steps, natural order
+};
+
+struct CoefStage {
+  int16_t *coef = nullptr;
+  int32_t *bwin = nullptr;
+  int32_t *meta = nullptr;
+  long cap_blocks = 0;
+  std::atomic<long> cursor{0};
+};
+
+// Entropy-decodes one record into the stage.  Returns 0, or -1 (not a layout the GPU stage
+// handles: 12-bit, CMYK / RGB-coded, 4:4:0 or exotic sampling -> the CPU decoder), -2 (crop
+// does not fit), -3 (stage full), or a libjpeg message code.
+inline int ReadCoefCrop(const jpg::Api &J, const unsigned char *buf, size_t len, const CropConfig &c, uint64_t seed,
+                        int row, CoefStage &st, int *prm, float *cm) {
+  using namespace jpg;
+  jpeg_decompress_struct cinfo;
+  ErrMgr err;
+  std::memset(&cinfo, 0, sizeof(cinfo));
+  cinfo.err = J.std_error(&err.pub);
+  err.pub.error_exit = on_error;
+  err.pub.emit_message = on_message;
+  err.code = 0;
+  volatile bool created = false;
+  if (setjmp(err.jb)) {
+    if (created) J.destroy_decompress(&cinfo);
+    return err.code > 0 ? err.code : -1;
+  }
+  J.create_decompress(&cinfo, JPEG_LIB_VERSION, sizeof(cinfo));
+  created = true;
+  J.mem_src(&cinfo, buf, static_cast<unsigned long>(len));
+  J.read_header(&cinfo, 1);
+  const int nc = cinfo.num_components;
+  const jpeg_component_info *ci = static_cast<const jpeg_component_info *>(cinfo.comp_info);
+  bool ok = cinfo.data_precision == 8 && ((nc == 3 && cinfo.jpeg_color_space == JCS_YCbCr) ||
+                                          (nc == 1 && cinfo.jpeg_color_space == JCS_GRAYSCALE));
+  const int mh = cinfo.max_h_samp_factor, mv = cinfo.max_v_samp_factor;
+  for (int k = 0; ok && k < nc; ++k) {
+    const int rh = mh / ci[k].h_samp_factor, rv = mv / ci[k].v_samp_factor;
+    ok = ci[k].h_samp_factor * rh == mh && ci[k].v_samp_factor * rv == mv && rh <= 2 && rv <= rh &&
+         (k > 0 || (rh == 1 && rv == 1));  // luma at full rate; chroma 4:4:4, 4:2:2 or 4:2:0
+  }
+  const int H = static_cast<int>(cinfo.image_height), W = static_cast<int>(cinfo.image_width);
+  if (!ok) {
+    J.destroy_decompress(&cinfo);
+    return -1;
+  }
+  if (H < c.out_h || W < c.out_w) {
+    J.destroy_decompress(&cinfo);
+    return -2;
+  }
+  int yy, xx;
+  bool mirror;
+  float contrast, illum;
+  if (!DrawCrop(H, W, c, seed, &yy, &xx, &mirror, &contrast, &illum)) {
+    J.destroy_decompress(&cinfo);
+    return -2;
+  }
+  jvirt_barray_ptr *arrays = J.read_coefficients(&cinfo);
+  ci = static_cast<const jpeg_component_info *>(cinfo.comp_info);
+  int win[3][6];  // by0, bx0, bw, bh, rh, rv
+  long total = 0;
+  for (int k = 0; k < nc; ++k) {
+    const int rh = mh / ci[k].h_samp_factor, rv = mv / ci[k].v_samp_factor;
+    const int dw = static_cast<int>(ci[k].downsampled_width), dh = static_cast<int>(ci[k].downsampled_height);
+    // samples of this component the crop reads: the covered range, widened by the one
+    // neighbour the triangle upsampling filter takes on each side
+    int r0 = yy / rv, r1 = (yy + c.out_h - 1) / rv, c0 = xx / rh, c1 = (xx + c.out_w - 1) / rh;
+    if (rv == 2) --r0, ++r1;
+    if (rh == 2) --c0, ++c1;
+    r0 = std::max(r0, 0), c0 = std::max(c0, 0), r1 = std::min(r1, dh - 1), c1 = std::min(c1, dw - 1);
+    win[k][0] = r0 / 8, win[k][1] = c0 / 8, win[k][2] = c1 / 8 - c0 / 8 + 1, win[k][3] = r1 / 8 - r0 / 8 + 1;
+    win[k][4] = rh, win[k][5] = rv;
+    total += static_cast<long>(win[k][2]) * win[k][3];
+  }
+  const long blk0 = st.cursor.fetch_add(total);
+  if (blk0 + total > st.cap_blocks) {
+    J.abort_decompress(&cinfo);
+    J.destroy_decompress(&cinfo);
+    return -3;
+  }
+  jpeg_memory_mgr *mem = static_cast<jpeg_memory_mgr *>(cinfo.mem);
+  long b = blk0;
+  for (int k = 0; k < nc; ++k) {
+    int32_t *m = st.meta + (static_cast<long>(row) * 3 + k) * kCoefMeta;
+    m[kBlk0] = static_cast<int32_t>(b);
+    m[kBw] = win[k][2], m[kBh] = win[k][3], m[kBy0] = win[k][0], m[kBx0] = win[k][1];
+    m[kDw] = static_cast<int32_t>(ci[k].downsampled_width), m[kDh] = static_cast<int32_t>(ci[k].downsampled_height);
+    m[kRh] = win[k][4], m[kRv] = win[k][5], m[kNcomp] = nc, m[kValid] = 1;
+    for (int q = 0; q < 64; ++q) m[kQuant + q] = ci[k].quant_table->quantval[q];
+    const size_t row_bytes = static_cast<size_t>(win[k][2]) * sizeof(JBLOCK);
+    for (int by = 0; by < win[k][3]; ++by) {
+      JBLOCKARRAY a = mem->access_virt_barray(reinterpret_cast<j_common_ptr>(&cinfo), arrays[k],
+                                              static_cast<JDIMENSION>(win[k][0] + by), 1, 0);
+      std::memcpy(st.coef + b * 64, a[0][win[k][1]], row_bytes);
+      std::fill(st.bwin + b, st.bwin + b + win[k][2], row * 3 + k);
+      b += win[k][2];
+    }
+  }
   J.abort_decompress(&cinfo);
   J.destroy_decompress(&cinfo);
   prm[0] = yy;
@@ -377,10 +565,59 @@ class JpegDecodePool {
                           rowbuf);
       if (rc != 0) failed_flag[i] = 1;
     };
+    Dispatch(items.size(), work);
+    std::vector<int> failed;
+    for (size_t i = 0; i < items.size(); ++i)
+      if (failed_flag[i]) failed.push_back(items[i].row);
+    return failed;
+  }
+
+  // The GPU stage's host half: every record's crop-window coefficients into the stage (see
+  // ReadCoefCrop).  Rows it reports back (non-JPEG, layouts the GPU stage does not take, a full
+  // stage) go through Run() instead.  Returns (failed rows, blocks used).
+  std::pair<std::vector<int>, long> RunCoef(const std::vector<DecodeItem> &items, const CropConfig &cfg,
+                                            CoefStage &st, int32_t *prm, float *cm) {
+    const jpg::Api &J = jpg::api();
+    if (!J.ok) throw std::runtime_error("native JPEG decoder unavailable: " + J.error);
+    std::vector<int> failed_flag(items.size(), 0);
+    st.cursor.store(0);
+    auto work = [&](size_t i, std::vector<unsigned char> &, std::string &filebuf) {
+      const DecodeItem &it = items[i];
+      const unsigned char *p = it.data;
+      size_t n = it.size;
+      if (p == nullptr) {
+        std::ifstream f(it.path, std::ios::binary);
+        if (!f) {
+          failed_flag[i] = 1;
+          return;
+        }
+        filebuf.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+        p = reinterpret_cast<const unsigned char *>(filebuf.data());
+        n = filebuf.size();
+      }
+      if (n < 4 || p[0] != 0xFF || p[1] != 0xD8) {
+        failed_flag[i] = 1;
+        return;
+      }
+      const int r = it.row;
+      if (ReadCoefCrop(J, p, n, cfg, it.seed, r, st, prm + 4 * r, cm + 2 * r) != 0) {
+        for (int k = 0; k < 3; ++k) st.meta[(static_cast<long>(r) * 3 + k) * kCoefMeta + kValid] = 0;
+        failed_flag[i] = 1;
+      }
+    };
+    Dispatch(items.size(), work);
+    std::vector<int> failed;
+    for (size_t i = 0; i < items.size(); ++i)
+      if (failed_flag[i]) failed.push_back(items[i].row);
+    return {failed, std::min(st.cursor.load(), st.cap_blocks)};
+  }
+
+ private:
+  void Dispatch(size_t n, std::function<void(size_t, std::vector<unsigned char> &, std::string &)> work) {
     {
       std::lock_guard<std::mutex> lk(mu_);
-      job_ = work;
-      njobs_ = items.size();
+      job_ = std::move(work);
+      njobs_ = n;
       next_.store(0);
       active_ = static_cast<int>(threads_.size());
       ++gen_;
@@ -392,13 +629,8 @@ class JpegDecodePool {
       done_cv_.wait(lk, [this] { return active_ == 0; });
       job_ = nullptr;
     }
-    std::vector<int> failed;
-    for (size_t i = 0; i < items.size(); ++i)
-      if (failed_flag[i]) failed.push_back(items[i].row);
-    return failed;
   }
 
- private:
   void Drain() {
     std::vector<unsigned char> rowbuf;
     std::string filebuf;

@@ -64,7 +64,7 @@ class U8Images:
 
 def dense(data) -> torch.Tensor:
     """Float NCHW view of a batch's data whatever its storage."""
-    return data.to_float() if isinstance(data, U8Images) else data
+    return data.to_float() if hasattr(data, "to_float") else data  # U8Images, io.jpeg_stage.JpegCoefImages
 
 
 @dataclass

@@ -47,7 +47,9 @@ import torch
 
 from .. import native
 from .augment import AugmentParam, DecodePool, ShmBuffer, _augment_one, default_decode_process, shm_available
+from . import jpeg_stage
 from .data import DataBatch, DataIterator, U8Images
+from .jpeg_stage import JpegCoefImages
 
 
 # ----------------------------------------------------------------------------- records
@@ -253,7 +255,9 @@ class ImageBatchIterator(DataIterator):
 
     Extra keys (new): decode_native (default 1: JPEG records without affine augmentation
     are decoded by the native C++ pool of decode_native_threads threads, default
-    min(16, host cores)), decode_process (default min(16, host cores) when there are at
+    min(16, host cores)), decode_gpu (default: on when a GPU is present; with the native
+    pool, the host only entropy-decodes and the GPU runs IDCT / upsampling / colour / crop,
+    io/jpeg_stage.py), decode_process (default min(16, host cores) when there are at
     least 4, else 0: the Pillow path decodes in that many worker processes, io/augment.py,
     writing into a shared-memory batch; 0 = use threads), decode_thread (threads when
     decode_process is 0; default min(8, cpus)), shard_decode (default 1: under
@@ -280,6 +284,7 @@ class ImageBatchIterator(DataIterator):
         self.shard_decode = 1
         self.decode_native = 1
         self.decode_native_threads = 0
+        self.decode_gpu = -1
         self._jpeg = None
         self._pool: Optional[ThreadPoolExecutor] = None
         self.mean: Optional[torch.Tensor] = None
@@ -313,6 +318,8 @@ class ImageBatchIterator(DataIterator):
             self.decode_native = int(val)
         elif name == "decode_native_threads":
             self.decode_native_threads = int(val)
+        elif name == "decode_gpu":
+            self.decode_gpu = int(val)
 
     # ------------------------------------------------------------------ setup
     def init(self):
@@ -329,6 +336,8 @@ class ImageBatchIterator(DataIterator):
             if rt.JpegDecodePool.available():
                 n = self.decode_native_threads or default_decode_process() or (os.cpu_count() or 1)
                 self._jpeg = rt.JpegDecodePool(n)
+                if self.decode_gpu < 0:
+                    self.decode_gpu = int(torch.cuda.is_available())
             elif not self.silent:
                 print(f"native JPEG decoder unavailable ({rt.JpegDecodePool.error()}): decoding with Pillow")
         if self.aug.mean_value is not None and any(v > 0 for v in self.aug.mean_value):
@@ -443,6 +452,8 @@ class ImageBatchIterator(DataIterator):
         prm = np.zeros((B, 4), dtype=np.int32)
         cm = np.zeros((B, 2), dtype=np.float32)
         cm[:, 0] = 1.0
+        if self._jpeg is not None and self.decode_gpu > 0:
+            return DataBatch(self._stage_jpeg(rows, seeds, (B, h, w, C)), label, index, padd)
         if self._jpeg is not None:
             pix = self._decode_native(rows, seeds, (B, h, w, C), prm, cm)
         elif self.decode_process > 0 and h > 1:
@@ -497,6 +508,25 @@ class ImageBatchIterator(DataIterator):
         done[[i for i, _ in rows]] = True
         pix[~done] = 0  # padding rows / other ranks' rows
         return dst
+
+    def _crop_cfg(self, h, w, C):
+        a = self.aug
+        return (h, w, C, a.rand_crop, a.rand_mirror, a.mirror, a.crop_y_start, a.crop_x_start,
+                a.max_random_contrast, a.max_random_illumination, self.mean_mode)
+
+    def _stage_jpeg(self, rows, seeds, shape) -> JpegCoefImages:
+        """decode_gpu: the native pool entropy-decodes the rows into a pinned coefficient stage
+        and the GPU finishes the decode inside the step's input stage (io/jpeg_stage.py); rows
+        the stage does not take are decoded to pixels here (native, then Pillow)."""
+        B, h, w, C = shape
+        cfg = self._crop_cfg(h, w, C)
+        items = [(i, r.payload, seeds[i]) for i, r in rows]
+        pinned = torch.cuda.is_available()
+        coef, bwin, meta, nblk, prm, cm, failed = jpeg_stage.stage_batch(self._jpeg, items, cfg, B, h, w, C, pinned)
+        fb = jpeg_stage.fallback_rows(self._jpeg, items, failed, cfg, shape, prm, cm, pinned,
+                                      lambda payload, seed: _augment_one(payload, self.aug, seed, self.mean_mode))
+        return JpegCoefImages(coef, bwin, meta, nblk, prm, cm, (h, w, C), fb, failed, self.mean, self.mean_mode,
+                              self.aug.scale)
 
     def _decode_procs(self, rows, seeds, shape, prm, cm) -> torch.Tensor:
         nbytes = int(np.prod(shape))

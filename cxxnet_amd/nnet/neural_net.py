@@ -29,6 +29,7 @@ from ..updater import ArenaUpdater
 from .arena import ParamArena
 from ..ops.mode import frozen
 from ..io.data import U8Images
+from ..io.jpeg_stage import JpegCoefImages
 
 K_CONV, K_FULLC, K_RELU, K_MAXPOOL, K_DROPOUT = 10, 1, 3, 11, 8
 K_SPLIT, K_CONCAT, K_CHCONCAT, K_SUMPOOL, K_AVGPOOL, K_LRN = 23, 18, 28, 12, 13, 15
@@ -628,7 +629,7 @@ class NeuralNet:
         b = data.shape[0]
         self.adjust_batch_size(b)
         n0 = self.nodes[0]
-        if isinstance(data, U8Images):
+        if isinstance(data, (U8Images, JpegCoefImages)):
             ops.image_to_nhwc(data, n0.data[:b])
         else:
             src = data.to(self.device, non_blocking=True)

@@ -39,9 +39,41 @@ def input_to_nhwc(x_nchw: torch.Tensor, out: torch.Tensor, scale: float = 1.0):
                                                 _stream()), "nchw_to_nhwc")
 
 
+def jpeg_decode(coef, bwin, meta, nblk: int, prm, r0: int, r1: int, h: int, w: int, C: int, dev) -> torch.Tensor:
+    """GPU half of the JPEG stage (io/jpeg_stage.py): staged coefficient blocks -> uint8
+    (r1 - r0, h, w, C) crops of rows r0..r1 on `dev` (dequantise + islow IDCT, then fancy
+    upsampling + YCbCr->RGB + crop + mirror; csrc/kernels/jpeg_kernels.hip)."""
+    B = int(meta.shape[0])
+    if not (0 <= r0 <= r1 <= B) or nblk > coef.shape[0] or tuple(meta.shape[1:]) != (3, 80):
+        raise ValueError("jpeg_decode: inconsistent stage")
+    out = torch.empty((r1 - r0, h, w, C), dtype=torch.uint8, device=dev)
+    if r1 == r0:
+        return out
+    meta_d = meta.to(dev, non_blocking=True)
+    prm_d = prm.to(dev, torch.int32, non_blocking=True).contiguous()
+    plane = torch.empty((max(nblk, 1), 64), dtype=torch.uint8, device=dev)
+    if nblk > 0:
+        coef_d = coef[:nblk].to(dev, non_blocking=True)
+        bwin_d = bwin[:nblk].to(dev, non_blocking=True)
+        if int(bwin[:nblk].max()) >= B * 3 or int(bwin[:nblk].min()) < 0:
+            raise ValueError("jpeg_decode: block window id out of range")
+    m = meta.view(B * 3, 80)
+    v = m[:, 10] != 0
+    if bool(v.any()) and int((m[v, 0] + m[v, 1] * m[v, 2]).max()) > nblk:  # blk0 + bw * bh
+        raise ValueError("jpeg_decode: window outside the staged blocks")
+        native.check(_k().cxn_jpeg_idct(coef_d.data_ptr(), bwin_d.data_ptr(), meta_d.data_ptr(), nblk,
+                                        plane.data_ptr(), _stream()), "jpeg_idct")
+    native.check(_k().cxn_jpeg_color(plane.data_ptr(), meta_d[r0:].data_ptr(), prm_d[r0:].data_ptr(), r1 - r0, h, w, C,
+                                     out.data_ptr(), _stream()), "jpeg_color")
+    return out
+
+
 def image_to_nhwc(img, out: torch.Tensor):
     """U8Images batch -> NHWC input node with the augmenter arithmetic fused
     (GPU: one kernel over uint8 pixels; CPU: the fp32 reference)."""
+    from ..io.jpeg_stage import JpegCoefImages
+    if isinstance(img, JpegCoefImages):  # finish the JPEG decode where the batch is going
+        img = img.to_u8(out.device if _native_t(out) else None)
     if not _native_t(out):
         input_to_nhwc(img.to_float(), out)
         return
