@@ -112,6 +112,9 @@ def main():
     ap.add_argument("--batches", type=int, default=12)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--dir", default="")
+    ap.add_argument("--repeat", type=int, default=1,
+                    help="pack the list this many times (a multi-page .bin from few JPEGs: the page "
+                         "reader's steady state)")
     ap.add_argument("--train", default="", help="also train this model (GPU) on the decoded batches")
     a = ap.parse_args()
     root = a.dir or tempfile.mkdtemp(prefix="cxxnet_io_")
@@ -121,6 +124,13 @@ def main():
         avg = sum(os.path.getsize(os.path.join(root, "img", f)) for f in imgs) / max(len(imgs), 1)
     else:
         avg = make_dataset(root, a.n, a.size)
+        if a.repeat > 1:
+            lines = open(os.path.join(root, "train.lst")).read().splitlines()
+            with open(os.path.join(root, "train.lst"), "w") as f:
+                for r in range(a.repeat):
+                    for i, ln in enumerate(lines):
+                        _, lab, p = ln.split("\t")
+                        f.write(f"{r * len(lines) + i}\t{lab}\t{p}\n")
         pack(os.path.join(root, "train.lst"), root + "/", os.path.join(root, "train.bin"))
     cores = os.cpu_count()
     tr = make_trainer(a.train, a.batch) if a.train else None

@@ -188,7 +188,9 @@ PYBIND11_MODULE(_cxxnet_rt, m) {
       .def("next", [](ImageBinReader &r) -> py::object {
         std::string s;
         bool ok;
-        {
+        if (r.Ready()) {  // no wait: keep the GIL (a release per record costs two thread handoffs)
+          ok = r.Next(&s);
+        } else {
           py::gil_scoped_release rel;
           ok = r.Next(&s);
         }
@@ -199,6 +201,28 @@ PYBIND11_MODULE(_cxxnet_rt, m) {
         }
         return py::bytes(s);
       })
+      .def("next_n",
+           [](ImageBinReader &r, int n) -> py::list {
+             // up to n objects (fewer at the end of the files), one call per chunk of records
+             py::list out;
+             std::string s;
+             for (int k = 0; k < n; ++k) {
+               bool ok;
+               if (r.Ready()) {
+                 ok = r.Next(&s);
+               } else {
+                 py::gil_scoped_release rel;
+                 ok = r.Next(&s);
+               }
+               if (!ok) {
+                 std::string err = r.Error();
+                 if (!err.empty()) throw std::runtime_error("ImageBinReader: " + err);
+                 break;
+               }
+               out.append(py::bytes(s));
+             }
+             return out;
+           })
       .def("next_page", [](ImageBinReader &r) -> py::object {
         std::vector<std::string> objs;
         bool ok;

@@ -77,9 +77,12 @@ class BinaryPage {
  public:
   static constexpr size_t kPageInts = 64 << 18;  // 64 MB page
   static constexpr size_t kPageBytes = kPageInts * sizeof(int32_t);
-  BinaryPage() : data_(kPageInts, 0) {}
+  // zero = false: contents left undefined (a page about to be overwritten by a file read)
+  explicit BinaryPage(bool zero = true) : data_(new int32_t[kPageInts]) {
+    if (zero) Clear();
+  }
   int32_t Size() const { return data_[0]; }
-  void Clear() { std::fill(data_.begin(), data_.end(), 0); }
+  void Clear() { std::fill(data_.get(), data_.get() + kPageInts, 0); }
   bool Push(const void *p, size_t sz) {
     if (FreeBytes() < sz + sizeof(int32_t)) return false;
     int32_t s = Size();
@@ -93,8 +96,8 @@ class BinaryPage {
     int32_t end = data_[r + 2], beg = data_[r + 1];
     return std::string(Offset(end), static_cast<size_t>(end - beg));
   }
-  char *raw() { return reinterpret_cast<char *>(data_.data()); }
-  const char *raw() const { return reinterpret_cast<const char *>(data_.data()); }
+  char *raw() { return reinterpret_cast<char *>(data_.get()); }
+  const char *raw() const { return reinterpret_cast<const char *>(data_.get()); }
   bool Valid() const {
     int32_t s = Size();
     if (s < 0 || static_cast<size_t>(s) + 2 > kPageInts) return false;
@@ -111,7 +114,7 @@ class BinaryPage {
   }
   char *Offset(int32_t pos) { return raw() + (kPageBytes - pos); }
   const char *Offset(int32_t pos) const { return raw() + (kPageBytes - pos); }
-  std::vector<int32_t> data_;
+  std::unique_ptr<int32_t[]> data_;
 };
 
 // Packs a list of files into BinaryPages (the im2bin tool; reference tools/im2bin.cpp:6-67).
@@ -155,8 +158,8 @@ class ImageBinReader {
   // Next object bytes; returns false at end of all files.
   bool Next(std::string *out) {
     while (cur_ == nullptr || cur_idx_ >= cur_->Size()) {
-      cur_.reset();
       std::unique_lock<std::mutex> lk(mu_);
+      if (cur_ != nullptr) free_.push_back(std::move(cur_));  // recycled by the loader
       cv_.wait(lk, [&] { return !queue_.empty() || done_; });
       if (queue_.empty()) return false;
       cur_ = std::move(queue_.front());
@@ -167,6 +170,9 @@ class ImageBinReader {
     *out = cur_->Get(cur_idx_++);
     return true;
   }
+  // True when Next() will not wait (the current page still has objects): callers holding an
+  // interpreter lock then need not drop it per record.
+  bool Ready() const { return cur_ != nullptr && cur_idx_ < cur_->Size(); }
   // All remaining objects of the current page (or of the next page when the current
   // one is exhausted); false at end of all files.  Used by the page-shuffling reader.
   bool NextPage(std::vector<std::string> *out) {
@@ -209,7 +215,17 @@ class ImageBinReader {
         break;
       }
       while (true) {
-        auto page = std::make_unique<BinaryPage>();
+        // a recycled page when there is one: a fresh 64 MB page costs its page faults, which
+        // made the loader (not the decoders) the limit of the whole pipeline
+        std::unique_ptr<BinaryPage> page;
+        {
+          std::lock_guard<std::mutex> lk(mu_);
+          if (!free_.empty()) {
+            page = std::move(free_.back());
+            free_.pop_back();
+          }
+        }
+        if (page == nullptr) page = std::make_unique<BinaryPage>(false);
         fi.read(page->raw(), BinaryPage::kPageBytes);
         if (fi.gcount() != static_cast<std::streamsize>(BinaryPage::kPageBytes)) break;
         if (!page->Valid()) break;
@@ -231,6 +247,7 @@ class ImageBinReader {
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<std::unique_ptr<BinaryPage>> queue_;
+  std::vector<std::unique_ptr<BinaryPage>> free_;
   std::unique_ptr<BinaryPage> cur_;
   int cur_idx_ = 0;
   bool done_ = false, stop_ = false;

@@ -1,11 +1,51 @@
 """DataBatch and the iterator interface (reference src/io/data.h:18-186)."""
 from __future__ import annotations
 
+import os
+import threading
 from dataclasses import dataclass, field
 from typing import List, Optional
 
 import numpy as np
 import torch
+
+# Held by HIP graph capture (nnet/trainer.py) and by every input prefetch: a global-mode capture
+# forbids allocations on other threads (pinned host buffers, the prefetch's device copies), so the
+# image iterator builds a whole batch under it.
+DEVICE_IO_LOCK = threading.RLock()
+_copy_streams = {}
+
+
+def input_device() -> torch.device:
+    """The GPU this process trains on (one process per GPU: LOCAL_RANK, parallel/dp.py)."""
+    return torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1))
+
+
+class DevicePrefetch:
+    """A batch's host-to-device copies issued early, from the iterator's thread, on a side
+    stream: with a thread buffer they overlap the previous training step instead of opening
+    the next one (40+ MB per AlexNet batch, about 1 ms of PCIe).  Sources should be pinned
+    (asynchronous DMA).  ``take`` orders the current stream after the copies."""
+
+    def __init__(self, tensors, dev: torch.device):
+        self.dev = dev
+        with DEVICE_IO_LOCK:
+            s = _copy_streams.get(dev.index)
+            if s is None:
+                s = _copy_streams[dev.index] = torch.cuda.Stream(dev)
+            with torch.cuda.device(dev), torch.cuda.stream(s):
+                self.tensors = [t.to(dev, non_blocking=True) for t in tensors]
+                self.event = torch.cuda.Event()
+                self.event.record(s)
+
+    def take(self, dev) -> Optional[list]:
+        if torch.device(dev) != self.dev:
+            return None
+        cur = torch.cuda.current_stream(self.dev)
+        cur.wait_event(self.event)
+        for t in self.tensors:
+            t.record_stream(cur)  # made on the copy stream, consumed on this one
+        return self.tensors
 
 
 class U8Images:
@@ -23,8 +63,17 @@ class U8Images:
     Reference: src/io/iter_augment_proc-inl.hpp:98-162.
     """
 
-    def __init__(self, pix, prm, cm, mean=None, mode=0, scale=1.0):
+    def __init__(self, pix, prm, cm, mean=None, mode=0, scale=1.0, pf=None, rows=None):
         self.pix, self.prm, self.cm, self.mean, self.mode, self.scale = pix, prm, cm, mean, mode, float(scale)
+        self.pf, self.rows = pf, rows  # DevicePrefetch of (pix, prm, cm) and the rows of it this view is
+
+    def prefetch(self, dev: torch.device):
+        self.pf, self.rows = DevicePrefetch([self.pix, self.prm, self.cm], dev), (0, self.pix.shape[0])
+
+    def on_device(self, dev):
+        """(pix, prm, cm) on `dev` from the prefetch, or None."""
+        got = self.pf.take(dev) if self.pf is not None else None
+        return None if got is None else [t[self.rows[0]:self.rows[1]] for t in got]
 
     @property
     def shape(self):
@@ -34,10 +83,16 @@ class U8Images:
     def __getitem__(self, sl):
         if not isinstance(sl, slice):
             raise TypeError("U8Images supports row slices only")
-        return U8Images(self.pix[sl], self.prm[sl], self.cm[sl], self.mean, self.mode, self.scale)
+        rows = None
+        if self.pf is not None:
+            lo, hi, step = sl.indices(self.rows[1] - self.rows[0])
+            rows = (self.rows[0] + lo, self.rows[0] + max(hi, lo)) if step == 1 else None
+        return U8Images(self.pix[sl], self.prm[sl], self.cm[sl], self.mean, self.mode, self.scale,
+                        self.pf if rows is not None else None, rows)
 
     def clone(self):
-        return U8Images(self.pix.clone(), self.prm.clone(), self.cm.clone(), self.mean, self.mode, self.scale)
+        return U8Images(self.pix.clone(), self.prm.clone(), self.cm.clone(), self.mean, self.mode, self.scale,
+                        self.pf, self.rows)
 
     def to_float(self) -> torch.Tensor:
         """fp32 NCHW batch (reference arithmetic, CPU)."""

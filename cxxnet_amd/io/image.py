@@ -48,7 +48,7 @@ import torch
 from .. import native
 from .augment import AugmentParam, DecodePool, ShmBuffer, _augment_one, default_decode_process, shm_available
 from . import jpeg_stage
-from .data import DataBatch, DataIterator, U8Images
+from .data import DEVICE_IO_LOCK, DataBatch, DataIterator, U8Images, input_device
 from .jpeg_stage import JpegCoefImages
 
 
@@ -189,11 +189,14 @@ class ImageBinSource(_Source):
     def records(self):
         reader = native.rt().ImageBinReader(self.bins, 4)
         for lst in self.lists:
-            for idx, lab, _ in _read_list(lst, self.label_width):
-                buf = reader.next()
-                if buf is None:
+            entries = _read_list(lst, self.label_width)
+            for c0 in range(0, len(entries), 64):  # objects fetched 64 at a time
+                chunk = entries[c0:c0 + 64]
+                bufs = reader.next_n(len(chunk))
+                if len(bufs) != len(chunk):
                     raise ValueError(f"image bin has fewer objects than list {lst}")
-                yield Record(idx, lab, buf)
+                for (idx, lab, _), buf in zip(chunk, bufs):
+                    yield Record(idx, lab, buf)
 
 
 class ImageBinXSource(ImageBinSource):
@@ -257,7 +260,9 @@ class ImageBatchIterator(DataIterator):
     are decoded by the native C++ pool of decode_native_threads threads, default
     min(16, host cores)), decode_gpu (default: on when a GPU is present; with the native
     pool, the host only entropy-decodes and the GPU runs IDCT / upsampling / colour / crop,
-    io/jpeg_stage.py), decode_process (default min(16, host cores) when there are at
+    io/jpeg_stage.py), prefetch_device (default: on with a GPU; the batch's host-to-device
+    copies are issued from the iterator's thread on a side stream, io/data.py DevicePrefetch),
+    decode_process (default min(16, host cores) when there are at
     least 4, else 0: the Pillow path decodes in that many worker processes, io/augment.py,
     writing into a shared-memory batch; 0 = use threads), decode_thread (threads when
     decode_process is 0; default min(8, cpus)), shard_decode (default 1: under
@@ -285,6 +290,7 @@ class ImageBatchIterator(DataIterator):
         self.decode_native = 1
         self.decode_native_threads = 0
         self.decode_gpu = -1
+        self.prefetch_device = -1
         self._jpeg = None
         self._pool: Optional[ThreadPoolExecutor] = None
         self.mean: Optional[torch.Tensor] = None
@@ -320,6 +326,8 @@ class ImageBatchIterator(DataIterator):
             self.decode_native_threads = int(val)
         elif name == "decode_gpu":
             self.decode_gpu = int(val)
+        elif name == "prefetch_device":
+            self.prefetch_device = int(val)
 
     # ------------------------------------------------------------------ setup
     def init(self):
@@ -330,6 +338,8 @@ class ImageBatchIterator(DataIterator):
             self.decode_process = default_decode_process()
         if not shm_available():
             self.decode_process = 0
+        if self.prefetch_device < 0:
+            self.prefetch_device = int(torch.cuda.is_available())
         C, h, w = self.aug.shape
         if self.decode_native and h > 1 and C <= 3 and not self.aug.need_affine():
             rt = native.rt()
@@ -433,35 +443,47 @@ class ImageBatchIterator(DataIterator):
                 padd = self._overflow
             else:
                 padd = B - len(recs)
-        self.out = self._make_batch(recs, padd)
+        if torch.cuda.is_available():  # pinned allocations: not while a HIP graph is being captured
+            with DEVICE_IO_LOCK:
+                self.out = self._make_batch(recs, padd)
+        else:
+            self.out = self._make_batch(recs, padd)
         return True
 
     def _make_batch(self, recs: List[Record], padd: int) -> DataBatch:
         B = self.batch_size
         C, h, w = self.aug.shape
         lw = self.label_width
-        label = torch.zeros((B, lw), dtype=torch.float32)
+        lab = np.zeros((B, lw), dtype=np.float32)
         index = np.zeros(B, dtype=np.uint32)
         for i, r in enumerate(recs):
-            label[i, : min(lw, len(r.label))] = torch.from_numpy(r.label[:lw])
+            lab[i, : min(lw, len(r.label))] = r.label[:lw]
             index[i] = r.index
+        label = torch.from_numpy(lab)
         lo, hi = (_dist_rows(B) if self.shard_decode else (0, B))
         rows = [(i, r) for i, r in enumerate(recs) if lo <= i < hi]
         # seeds are drawn for every record so results do not depend on the sharding
         seeds = self._seed_rng.integers(0, 2 ** 63 - 1, size=len(recs)).tolist()
-        prm = np.zeros((B, 4), dtype=np.int32)
-        cm = np.zeros((B, 2), dtype=np.float32)
-        cm[:, 0] = 1.0
+        pinned = torch.cuda.is_available()  # async host-to-device copies of the crop parameters too
+        prm_t = torch.empty((B, 4), dtype=torch.int32, pin_memory=pinned)
+        cm_t = torch.empty((B, 2), dtype=torch.float32, pin_memory=pinned)
+        prm, cm = prm_t.numpy(), cm_t.numpy()
+        prm.fill(0)
+        cm[:, 0], cm[:, 1] = 1.0, 0.0
         if self._jpeg is not None and self.decode_gpu > 0:
-            return DataBatch(self._stage_jpeg(rows, seeds, (B, h, w, C)), label, index, padd)
+            data = self._stage_jpeg(rows, seeds, (B, h, w, C))
+            if self.prefetch_device:
+                data.prefetch(input_device())
+            return DataBatch(data, label, index, padd)
         if self._jpeg is not None:
             pix = self._decode_native(rows, seeds, (B, h, w, C), prm, cm)
         elif self.decode_process > 0 and h > 1:
             pix = self._decode_procs(rows, seeds, (B, h, w, C), prm, cm)
         else:
             pix = self._decode_threads(rows, seeds, (B, h, w, C), prm, cm)
-        prm, cm = torch.from_numpy(prm), torch.from_numpy(cm)
-        data = U8Images(pix, prm, cm, self.mean, self.mean_mode, self.aug.scale)
+        data = U8Images(pix, prm_t, cm_t, self.mean, self.mean_mode, self.aug.scale)
+        if self.prefetch_device and h > 1:
+            data.prefetch(input_device())
         return DataBatch(data, label, index, padd)
 
     @staticmethod

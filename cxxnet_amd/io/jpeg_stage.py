@@ -27,7 +27,7 @@ from typing import List, Optional
 import numpy as np
 import torch
 
-from .data import U8Images
+from .data import DevicePrefetch, U8Images
 
 META = 80  # int32 per window (runtime/jpeg_decode.h CoefMetaField)
 BLK0, BW, BH, BY0, BX0, DW, DH, RH, RV, NCOMP, VALID, QUANT = 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 16
@@ -45,12 +45,18 @@ class JpegCoefImages:
     ``to_u8(device)`` finishes the decode (GPU kernels, or the numpy reference on the CPU)."""
 
     def __init__(self, coef, bwin, meta, nblk, prm, cm, hwc, fb_pix=None, fb_rows=(), mean=None, mode=0,
-                 scale=1.0, r0=0, r1=None):
+                 scale=1.0, r0=0, r1=None, pf=None):
         self.coef, self.bwin, self.meta, self.nblk = coef, bwin, meta, int(nblk)
         self.prm_all, self.cm_all, self.hwc = prm, cm, tuple(hwc)
         self.fb_pix, self.fb_rows = fb_pix, sorted(fb_rows)
         self.mean, self.mode, self.scale = mean, mode, float(scale)
         self.r0, self.r1 = r0, meta.shape[0] if r1 is None else r1
+        self.pf = pf  # DevicePrefetch of (coef[:nblk], bwin[:nblk], meta, prm[, fallback pixels])
+
+    def prefetch(self, dev: torch.device):
+        """Issue the batch's host-to-device copies now, on a side stream (the iterator's thread)."""
+        ts = [self.coef[:self.nblk], self.bwin[:self.nblk], self.meta, self.prm_all]
+        self.pf = DevicePrefetch(ts + ([self.fb_pix] if self.fb_pix is not None else []), dev)
 
     @property
     def shape(self):
@@ -67,7 +73,7 @@ class JpegCoefImages:
 
     def _view(self, r0, r1):
         return JpegCoefImages(self.coef, self.bwin, self.meta, self.nblk, self.prm_all, self.cm_all, self.hwc,
-                              self.fb_pix, self.fb_rows, self.mean, self.mode, self.scale, r0, r1)
+                              self.fb_pix, self.fb_rows, self.mean, self.mode, self.scale, r0, r1, self.pf)
 
     def __getitem__(self, sl):
         if not isinstance(sl, slice) or sl.step not in (None, 1):
@@ -81,10 +87,12 @@ class JpegCoefImages:
     def to_u8(self, device=None) -> U8Images:
         dev = torch.device(device) if device is not None else torch.device("cpu")
         h, w, C = self.hwc
+        staged = None
         if dev.type == "cuda":
             from .. import ops
+            staged = self.pf.take(dev) if self.pf is not None else None
             pix = ops.jpeg_decode(self.coef, self.bwin, self.meta, self.nblk, self.prm_all, self.r0, self.r1, h, w, C,
-                                  dev)
+                                  dev, staged[:4] if staged is not None else None)
         else:
             pix = torch.from_numpy(decode_reference(self.coef[:self.nblk].numpy(), self.bwin[:self.nblk].numpy(),
                                                     self.meta.numpy(), self.prm_all.numpy(), self.r0, self.r1,
@@ -92,9 +100,13 @@ class JpegCoefImages:
         rows = [i for i in self.fb_rows if self.r0 <= i < self.r1]
         if rows:
             idx = torch.tensor([i - self.r0 for i in rows], dtype=torch.long)
-            src = self.fb_pix[rows]
+            src = staged[4][rows] if staged is not None else self.fb_pix[rows]
             pix.index_copy_(0, idx.to(pix.device), src.to(pix.device, non_blocking=True))
-        return U8Images(pix, self.prm, self.cm, self.mean, self.mode, self.scale)
+        prm, cm = self.prm, self.cm
+        if staged is not None:  # the crop rows on the device too (the image kernel's prm)
+            prm = staged[3][self.r0:self.r1]
+            cm = cm.to(dev, non_blocking=True)
+        return U8Images(pix, prm, cm, self.mean, self.mode, self.scale)
 
     def to_float(self) -> torch.Tensor:
         return self.to_u8().to_float()
@@ -199,10 +211,12 @@ def stage_batch(pool, items, cfg, B: int, h: int, w: int, C: int, pinned: bool):
     cap = stage_capacity(B, h, w)
     coef = torch.empty((cap, 64), dtype=torch.int16, pin_memory=pinned)
     bwin = torch.empty((cap,), dtype=torch.int32, pin_memory=pinned)
-    meta = torch.zeros((B, 3, META), dtype=torch.int32, pin_memory=pinned)
-    prm = torch.zeros((B, 4), dtype=torch.int32)
-    cm = torch.zeros((B, 2), dtype=torch.float32)
-    cm[:, 0] = 1.0
+    meta = torch.empty((B, 3, META), dtype=torch.int32, pin_memory=pinned)
+    meta.numpy().fill(0)  # numpy fills: torch's parallel fill wakes its OpenMP pool, which then
+    prm = torch.empty((B, 4), dtype=torch.int32, pin_memory=pinned)  # spins against the decode threads
+    prm.numpy().fill(0)
+    cm = torch.empty((B, 2), dtype=torch.float32, pin_memory=pinned)
+    cm.numpy()[:, 0], cm.numpy()[:, 1] = 1.0, 0.0
     failed, nblk = pool.decode_coef(items, cfg, coef.numpy(), bwin.numpy(), meta.numpy(), prm.numpy(), cm.numpy())
     return coef, bwin, meta, nblk, prm, cm, list(failed)
 
@@ -211,8 +225,9 @@ def fallback_rows(pool, items, failed, cfg, shape, prm, cm, pinned: bool, pillow
     """Host pixel decode of the rows the stage reported back (CPU native decoder, then Pillow)."""
     if not failed:
         return None
-    fb = torch.zeros(shape, dtype=torch.uint8, pin_memory=pinned)
+    fb = torch.empty(shape, dtype=torch.uint8, pin_memory=pinned)
     pix = fb.numpy()
+    pix.fill(0)
     sel = [it for it in items if it[0] in set(failed)]
     again = set(pool.decode(sel, cfg, pix, prm.numpy(), cm.numpy()))
     for i, payload, seed in sel:

@@ -443,6 +443,10 @@ class NeuralNet:
                     cc = self._concat_of(a, consumers)
                     if cc is None:
                         continue
+                else:  # read in place as a strided NHWC slice of H: only convolutions can
+                    rd = consumers.get(id(self._alias_of(a)), [])
+                    if not rd or any(sl or self.connections[k].type != K_CONV for k, sl in rd):
+                        continue
                 mem.append((j, o))
             mem.sort(key=lambda t: t[0])
             if len(mem) < 2 or len({self.connections[j].layer.lp.no_bias for j, _ in mem}) != 1:
@@ -467,10 +471,14 @@ class NeuralNet:
             # the data-gradient of every sibling lands in the lead's slot of the split
             conn.layer.skip_grads = {id(o) for _, o in mem[1:]}
 
+    def _alias_of(self, a):
+        """The node that reads a fused-relu conv output a: relu(a)'s alias node, or a itself."""
+        b = next((bb for bb, src in self.aliases.items() if src is a), None)  # b = relu(a) alias key
+        return a if b is None else next((n for n in self.nodes if id(n) == b), a)
+
     def _concat_of(self, a, consumers):
         """The zero-copy ch_concat connection that a fused-relu conv output a feeds, or None."""
-        b = next((bb for bb, src in self.aliases.items() if src is a), None)  # b = relu(a) alias key
-        node = a if b is None else next((n for n in self.nodes if id(n) == b), a)
+        node = self._alias_of(a)
         for j, _ in consumers.get(id(node), []):
             cj = self.connections[j]
             if cj.type == K_CHCONCAT and getattr(cj.layer, "zero_copy", False):

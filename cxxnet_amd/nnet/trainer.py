@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 from .. import native
+from ..io.data import DEVICE_IO_LOCK
 from ..layers.base import BinReader, BinWriter
 from ..parallel.dp import GradReducer, world_info
 
@@ -935,7 +936,8 @@ class NetTrainer:
                 self._graph_warm[key] = 1
                 return False
             try:
-                gr = self._capture_plans()
+                with DEVICE_IO_LOCK:  # no input-thread allocations during a global-mode capture
+                    gr = self._capture_plans()
             except Exception as e:  # a layer that syncs with the host (e.g. pairtest): stay eager
                 if not self.silent:
                     print(f"cuda_graph: capture failed ({type(e).__name__}: {e}); running eagerly")

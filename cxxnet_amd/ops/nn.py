@@ -39,33 +39,55 @@ def input_to_nhwc(x_nchw: torch.Tensor, out: torch.Tensor, scale: float = 1.0):
                                                 _stream()), "nchw_to_nhwc")
 
 
-def jpeg_decode(coef, bwin, meta, nblk: int, prm, r0: int, r1: int, h: int, w: int, C: int, dev) -> torch.Tensor:
+def jpeg_decode(coef, bwin, meta, nblk: int, prm, r0: int, r1: int, h: int, w: int, C: int, dev,
+                staged=None) -> torch.Tensor:
     """GPU half of the JPEG stage (io/jpeg_stage.py): staged coefficient blocks -> uint8
     (r1 - r0, h, w, C) crops of rows r0..r1 on `dev` (dequantise + islow IDCT, then fancy
-    upsampling + YCbCr->RGB + crop + mirror; csrc/kernels/jpeg_kernels.hip)."""
+    upsampling + YCbCr->RGB + crop + mirror; csrc/kernels/jpeg_kernels.hip).  staged: device
+    copies of (coef[:nblk], bwin[:nblk], meta, prm) already made (io/data.py DevicePrefetch)."""
     B = int(meta.shape[0])
     if not (0 <= r0 <= r1 <= B) or nblk > coef.shape[0] or tuple(meta.shape[1:]) != (3, 80):
         raise ValueError("jpeg_decode: inconsistent stage")
     out = torch.empty((r1 - r0, h, w, C), dtype=torch.uint8, device=dev)
     if r1 == r0:
         return out
-    meta_d = meta.to(dev, non_blocking=True)
-    prm_d = prm.to(dev, torch.int32, non_blocking=True).contiguous()
-    plane = torch.empty((max(nblk, 1), 64), dtype=torch.uint8, device=dev)
-    if nblk > 0:
+    if staged is not None:
+        coef_d, bwin_d, meta_d, prm_d = staged
+    else:
+        meta_d = meta.to(dev, non_blocking=True)
+        prm_d = prm.to(dev, torch.int32, non_blocking=True).contiguous()
         coef_d = coef[:nblk].to(dev, non_blocking=True)
         bwin_d = bwin[:nblk].to(dev, non_blocking=True)
-        if int(bwin[:nblk].max()) >= B * 3 or int(bwin[:nblk].min()) < 0:
+    plane = torch.empty((max(nblk, 1), 64), dtype=torch.uint8, device=dev)
+    # host-side bounds of what the kernels will index (numpy: a torch CPU reduction would wake
+    # its OpenMP pool, whose spinning threads then slow the decode threads down)
+    if nblk > 0:
+        bw = bwin[:nblk].numpy()
+        if int(bw.max()) >= B * 3 or int(bw.min()) < 0:
             raise ValueError("jpeg_decode: block window id out of range")
-    m = meta.view(B * 3, 80)
+    m = meta.numpy().reshape(B * 3, 80)
     v = m[:, 10] != 0
-    if bool(v.any()) and int((m[v, 0] + m[v, 1] * m[v, 2]).max()) > nblk:  # blk0 + bw * bh
+    if v.any() and int((m[v, 0] + m[v, 1] * m[v, 2]).max()) > nblk:  # blk0 + bw * bh
         raise ValueError("jpeg_decode: window outside the staged blocks")
+    if nblk > 0:
         native.check(_k().cxn_jpeg_idct(coef_d.data_ptr(), bwin_d.data_ptr(), meta_d.data_ptr(), nblk,
                                         plane.data_ptr(), _stream()), "jpeg_idct")
     native.check(_k().cxn_jpeg_color(plane.data_ptr(), meta_d[r0:].data_ptr(), prm_d[r0:].data_ptr(), r1 - r0, h, w, C,
                                      out.data_ptr(), _stream()), "jpeg_color")
     return out
+
+
+_CONST = {}
+
+
+def _device_const(t: torch.Tensor, dev) -> torch.Tensor:
+    """fp32 device copy of a host tensor that does not change between batches (the iterator's
+    mean), made once: a pageable copy per step would stall the host on the stream."""
+    key = (id(t), str(dev))
+    hit = _CONST.get(key)
+    if hit is None or hit[0] is not t:
+        hit = _CONST[key] = (t, t.to(dev, torch.float32).contiguous())
+    return hit[1]
 
 
 def image_to_nhwc(img, out: torch.Tensor):
@@ -82,10 +104,14 @@ def image_to_nhwc(img, out: torch.Tensor):
     if tuple(out.shape[:2]) != (B, h) or Wp < w or Cp < C:
         raise ValueError(f"image batch {tuple(img.shape)} does not fit input node {tuple(out.shape)}")
     dev = out.device
-    pix = img.pix.to(dev, non_blocking=True).contiguous()
-    prm = img.prm.to(dev, torch.int32, non_blocking=True).contiguous()
-    cm = img.cm.to(dev, torch.float32, non_blocking=True).contiguous()
-    mean = img.mean.to(dev, torch.float32, non_blocking=True).contiguous() if img.mean is not None else None
+    got = img.on_device(dev) if hasattr(img, "on_device") else None
+    if got is not None:  # copied by the iterator's prefetch (io/data.py DevicePrefetch)
+        pix, prm, cm = (t.contiguous() for t in got)
+    else:
+        pix = img.pix.to(dev, non_blocking=True).contiguous()
+        prm = img.prm.to(dev, torch.int32, non_blocking=True).contiguous()
+        cm = img.cm.to(dev, torch.float32, non_blocking=True).contiguous()
+    mean = _device_const(img.mean, dev) if img.mean is not None else None
     Hm = Wm = 0
     if img.mode == 2:
         Hm, Wm = int(img.mean.shape[1]), int(img.mean.shape[2])
