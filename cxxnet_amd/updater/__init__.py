@@ -172,10 +172,10 @@ class ArenaUpdater:
             dev = self.arena.w.device
             pin = dev.type == "cuda"
             # a ring of pinned sources: slot k is rewritten only after the copy that read it
-            # (event), so staging never waits on the GPU in steady state
+            # (event), so staging never waits on the GPU unless the host runs 16 steps ahead
             self._hyp_host = [torch.zeros((len(self.entries), 4), dtype=torch.float32, pin_memory=pin)
-                              for _ in range(4)]
-            self._hyp_ev = [None] * 4
+                              for _ in range(16)]
+            self._hyp_ev = [None] * 16
             self._hyp_slot = 0
             self._hyp_dev = torch.zeros((len(self.entries), 4), dtype=torch.float32, device=dev)
             self._hyp_row = {spec.offset: i for i, (spec, _) in enumerate(self.entries)}
