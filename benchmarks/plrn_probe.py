@@ -31,6 +31,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--arms", default="", help="only these arms (comma list)")
     a = ap.parse_args()
     n, alpha, beta, k = 5, 1e-4, 0.75, 1.0
     for name, H, C in (("pool1", 55, 96), ("pool2", 27, 256)):
@@ -56,7 +57,12 @@ def main():
             "sep_pool_bwd": lambda: ops.pool_backward(x, st, dP, dx, 3, 3, 2, 0, "max", relu=2, dbias=db),
         }
         for arm, fn in arms.items():
-            print(json.dumps({"shape": name, "arm": arm, "us": round(timeit(fn, a.reps), 1)}), flush=True)
+            if a.arms and arm not in a.arms.split(","):
+                continue
+            rec = {"shape": name, "arm": arm, "us": round(timeit(fn, a.reps), 1)}
+            if os.environ.get("CXN_LRN_POOL_R"):
+                rec["R"] = int(os.environ["CXN_LRN_POOL_R"])
+            print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":

@@ -2411,7 +2411,13 @@ CXN_API int cxn_lrn_pool_bwd(const void *P, const void *dY, const void *arg, voi
   // cell rows per block: the band's windows (R + 1 rows: one row recomputed) staged in LDS as bf16
   // gradient + offset byte, within 56 KiB of dynamic LDS (the bias partials take 9 KiB more)
   const long row_bytes = static_cast<long>(Wo) * C * 3;
-  int R = 4;
+  static const int r_env = [] {  // CXN_LRN_POOL_R: probe override of the band height
+    const char *e = std::getenv("CXN_LRN_POOL_R");
+    return e != nullptr ? std::atoi(e) : 0;
+  }();
+  // 4 rows, 2 for wide-channel maps (AlexNet pool1 C = 96: R 4 70.4 us, R 2 77.1; pool2 C = 256:
+  // R 4 56.8 us, R 2 51.0 -- profiles/r5_lrn_pool_bwd_band_probe.jsonl)
+  int R = r_env > 0 ? r_env : (C >= 192 ? 2 : 4);
   while (R > 1 && (R + 1) * row_bytes > 56 * 1024) --R;
   if ((R + 1) * row_bytes > 56 * 1024) return -1;
   if (static_cast<long>(Hin) * Win * C >= (1L << 31)) return -1;  // 32-bit offsets inside an image
