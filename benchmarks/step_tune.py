@@ -89,6 +89,8 @@ def main():
             continue
         if op in ("cf", "cd", "cr", "fc"):
             cands = list(SHORT if a.short else KK) + ([G.REG, 130, 131, 133] if op in ("cf", "cd") else [])
+        elif op == "cfs":  # sibling-group forward (two destinations): the LDS-DMA tiles only
+            cands = [t for t in (SHORT if a.short else KK) if t in G.SPLIT_CANDS]
         elif op in ("fw", "fws", "cwr"):
             cands = list(MM)
         elif op == "cw":  # conv weight-grad: the register split-K kernel, LDS-DMA MN tiles,

@@ -192,7 +192,8 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
   // are loaded once here instead of once per output row
   constexpr int LPR_B = WM / 8;  // lanes per output row (8 bf16 per lane)
   const int il_b = (lane % LPR_B) * 8;
-  constexpr bool BF = EPI == EPI_BF16 || EPI == EPI_BF16_DB;
+  constexpr bool BF = EPI == EPI_BF16 || EPI == EPI_BF16_DB || EPI == EPI_BF16_ADD;
+  constexpr bool ADD = EPI == EPI_BF16_ADD;
   float bias8[8], bsum[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) bsum[e] = 0.f;
@@ -226,13 +227,22 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
       // issued after a store waits for it: vmcnt counts both in issue order)
       constexpr int NIT = (16 + RPI - 1) / RPI;
       const int jl0 = lane < LPR * RPI ? lane / LPR : 16;
-      uint4 oldv[NIT];
+      uint4 oldv[NIT], addv[ADD ? NIT : 1];
       if (E.mask_relu && vec_store) {
 #pragma unroll
         for (int k = 0; k < NIT; ++k) {
           const int jl = jl0 + k * RPI;
           if (jl < 16 && jbase + n * 16 + jl < Nj && i < Mi)
             oldv[k] = *reinterpret_cast<const uint4 *>(out + static_cast<long>(jbase + n * 16 + jl) * ldc + ic);
+        }
+      }
+      const bf16_t *addp = ADD ? E.add + g * E.gstride : nullptr;
+      if (ADD && vec_store) {
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) {
+          const int jl = jl0 + k * RPI;
+          if (jl < 16 && jbase + n * 16 + jl < Nj && i < Mi)
+            addv[k] = *reinterpret_cast<const uint4 *>(addp + static_cast<long>(jbase + n * 16 + jl) * ldc + ic);
         }
       }
 #pragma unroll
@@ -250,6 +260,12 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
           }
           bf16_t *dst = out + static_cast<long>(j) * ldc + ic;
           if (vec_store) {
+            if constexpr (ADD) {
+              float a8[8];
+              unpack8(addv[k], a8);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) f[e] += a8[e];
+            }
             if (E.mask_relu) {
               float old[8];
               unpack8(oldv[k], old);
@@ -266,6 +282,7 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
             }
           } else {
             for (int e = 0; e < 8 && i + e < Mi; ++e) {
+              if constexpr (ADD) f[e] += bf2f(addp[static_cast<long>(j) * ldc + ic + e]);
               if (E.mask_relu && !(bf2f(dst[e]) > 0.f)) f[e] = 0.f;
               dst[e] = f2bf(f[e]);
               if constexpr (EPI == EPI_BF16_DB) bsum[e] += bf2f(dst[e]);
@@ -502,6 +519,7 @@ int dispatch(int amode, int bmode, int epi, int tile, const GOperand &A, const G
   if (tile >= 140 && tile <= 142) return cxg::dispatch_wgrad_halo(amode, bmode, epi, tile, A, B, E, groups, s);
   CXG_CASE(K_DIRECT, K_GATHER, EPI_BF16, CXG_KK_TILES)    // conv fwd / dgrad
   CXG_CASE(K_DIRECT, K_GATHER, EPI_BF16_DB, CXG_KK_TILES)  // conv dgrad + the lower conv's bias gradient
+  CXG_CASE(K_DIRECT, K_GATHER, EPI_BF16_ADD, CXG_KK_TILES)  // conv dgrad + a second gradient (split sum)
   CXG_CASE(K_DIRECT, K_ROWGATHER, EPI_BF16, CXG_KK_TILES)  // conv fwd, few input channels (conv1)
   CXG_CASE(K_DIRECT, K_DIRECT, EPI_BF16, CXG_KK_TILES)    // fc fwd
   CXG_CASE(K_DIRECT, K_DIRECT, EPI_F32, CXG_KK_TILES)     // fc fwd split-K
@@ -609,6 +627,30 @@ CXN_API int cxn_gemm_glds(const CxnOperandG *a, const CxnOperandG *b, int amode,
          nullptr, nullptr, nullptr, 0.f, 0.f, 0.f, 0.f, dws, dws_ld, dws_elems, dbias, g_gemm_group_i};
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int rc = dispatch(amode, bmode, epi, tile, A, B, E, groups < 1 ? 1 : groups, ksplit < 1 ? 1 : ksplit, s);
+  if (rc != 0) return rc;
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// cxn_gemm_glds with a second bf16 source added in the epilogue: out = mask(acc + add), add laid out
+// like out (row stride ldc, group stride out_gstride).  The gemm_glds tiles of the dispatch switch
+// only (not 114 / 130-142, whose epilogues do not read it); conv data-gradient operands (K_DIRECT
+// weights x K_GATHER dy), no bias, no split-K.
+CXN_API int cxn_gemm_glds_add(const CxnOperandG *a, const CxnOperandG *b, int amode, int bmode, void *out,
+                              long out_gstride, int ldc, const void *add, int mask_relu, int tile, int groups,
+                              void *stream) {
+  if (a->kdim != b->kdim || add == nullptr || (ldc & 7) || tile == 114 || (tile >= 130 && tile <= 142)) return -1;
+  if ((kmajor(amode) || kmajor(bmode)) && a->kdim % 8 != 0) return -1;
+  if (!supported(a, amode) || !supported(b, bmode)) return -1;
+  if (a->rows <= 0 || b->rows <= 0 || a->kdim <= 0) return 0;
+  GOperand A{}, B{};
+  fill(A, a, amode);
+  fill(B, b, bmode);
+  GEpi E{out, out_gstride, ldc, 1.f, nullptr, 0, 0, mask_relu, 0,
+         nullptr, nullptr, nullptr, 0.f, 0.f, 0.f, 0.f, nullptr, 0, 0, nullptr, g_gemm_group_i};
+  E.add = static_cast<const bf16_t *>(add);
+  if (amode != K_DIRECT || bmode != K_GATHER) return -1;  // the one instantiated form
+  const int rc = dispatch(amode, bmode, EPI_BF16_ADD, tile, A, B, E, groups < 1 ? 1 : groups, 1,
+                          static_cast<hipStream_t>(stream));
   if (rc != 0) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

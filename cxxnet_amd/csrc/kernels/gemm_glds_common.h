@@ -18,7 +18,9 @@ enum { K_DIRECT = 0, K_GATHER = 1, MN_DIRECT = 2, MN_GATHER = 3, K_ROWGATHER = 4
 // as one row of a partials workspace (row = j-tile x wave column, no atomics: one fp32 atomic per
 // column per wave put ~10^5 adders on each of VGG conv1_1's 64 addresses and ran 3.7x slower),
 // and db_partials_reduce adds the rows into dbias.
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_ACC = 2, EPI_F32_ATOMIC = 3, EPI_F32_SGD = 4, EPI_BF16_DB = 5 };
+// EPI_BF16_ADD: EPI_BF16 plus a second bf16 source summed before the store (GEpi.add; its own
+// instantiation, so the plain bf16 epilogue carries none of its registers)
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_ACC = 2, EPI_F32_ATOMIC = 3, EPI_F32_SGD = 4, EPI_BF16_DB = 5, EPI_BF16_ADD = 6 };
 
 struct GOperand {
   const bf16_t *ptr;
@@ -58,6 +60,10 @@ struct GEpi {
   // GEMM, NeuralNet._fuse_siblings); out2 == nullptr: one destination.  split_i % 8 == 0.
   void *out2;
   int ldc2, split_i;
+  // EPI_BF16_ADD epilogue of the gemm_glds tiles: out = f(acc + add) with add a bf16 matrix laid
+  // out like out (same gstride / ldc) -- a data-gradient GEMM summing a second gradient into its
+  // node instead of a separate add pass (the split after a sibling group, NeuralNet._fuse_siblings)
+  const bf16_t *add;
 };
 
 }  // namespace cxg

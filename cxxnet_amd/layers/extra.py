@@ -79,6 +79,7 @@ class SplitLayer(Layer):
     type_name = "split"
     alias = False
     skip_grads = frozenset()
+    folded = False  # set per step by a sibling group's lead (ConvolutionLayer.backprop)
 
     def init_connection(self, nodes_in, nodes_out):
         _check(len(nodes_in) == 1 and len(nodes_out) >= 1, "SplitLayer: only support 1-n connection")
@@ -98,6 +99,8 @@ class SplitLayer(Layer):
         # relu' when the input is a zero-copy concat of relu outputs (NeuralNet._fuse_concat).
         # skip_grads: outputs whose consumer's data-gradient a fused sibling wrote into another
         # output's slot (NeuralNet._fuse_siblings)
+        if self.folded:  # the group's data-gradient GEMM summed and masked already
+            return
         skip = self.skip_grads
         ops.sum_into(nodes_in[0].gdst, [o.gdst for o in nodes_out if id(o) not in skip], mask_relu=self.grad_mask_relu)
 

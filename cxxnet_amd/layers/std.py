@@ -428,6 +428,14 @@ class ConvolutionLayer(Layer):
                 self.ctx.bias_grad(_pixel_rows(H), S["b_g"])
             if prop_grad:
                 ready = self.ctx.flipped is not None and id(self) in self.ctx.flipped
+                fold = S.get("fold")  # the split's sum folded into this GEMM (NeuralNet._fuse_siblings)
+                if fold is not None:
+                    sp = fold["split"]
+                    dst, add = fold["dst"].gdst[:x.shape[0]], fold["add"].gdst[:x.shape[0]]
+                    sp.folded = ops.gemm.conv_backward_data_add(H, S["w_all"], dst, add, gall, S["wt"],
+                                                                mask_relu=sp.grad_mask_relu, wt_ready=ready)
+                    if sp.folded:
+                        return
                 ops.conv_backward_data(H, S["w_all"], S["dx_node"].gdst, gall, S["wt"], wt_ready=ready)
             return
         xw, geo = self._padded(x, getattr(self, "_xpad_stale", False))

@@ -71,6 +71,8 @@ _SIGS = {
                           _P, _I, _P],
     "cxn_gemm_set_group": [_I],
     "cxn_set_kernel_variant": [_I, _I],
+    "cxn_gemm_glds_add": [ctypes.POINTER(CxnOperand), ctypes.POINTER(CxnOperand), _I, _I, _P, _L, _I, _P, _I, _I, _I,
+                          _P],
     "cxn_gemm_glds_split": [ctypes.POINTER(CxnOperand), ctypes.POINTER(CxnOperand), _I, _I, _P, _I, _P, _I, _I, _P,
                             _I, _I, _P],
     "cxn_gemm_glds": [ctypes.POINTER(CxnOperand), ctypes.POINTER(CxnOperand), _I, _I, _P, _L, _I, _F, _P, _L, _I,

@@ -470,6 +470,13 @@ class NeuralNet:
                         "dx_node": mem[0][1]}
             # the data-gradient of every sibling lands in the lead's slot of the split
             conn.layer.skip_grads = {id(o) for _, o in mem[1:]}
+            # one other split output (the pool branch) whose backward runs before the lead's: the
+            # lead's data-gradient GEMM adds its gradient and writes the split's input gradient
+            # (relu'-masked as the split would), and the split's sum is skipped
+            others = [o for o in conn.nodes_out if id(o) not in {id(m) for _, m in mem}]
+            if (len(others) == 1 and os.environ.get("CXXNET_FOLD_SPLIT_SUM", "1") != "0"
+                    and all(j > group[0] for j, _ in consumers.get(id(others[0]), []))):
+                lead.sib["fold"] = {"split": conn.layer, "dst": conn.nodes_in[0], "add": others[0]}
 
     def _alias_of(self, a):
         """The node that reads a fused-relu conv output a: relu(a)'s alias node, or a itself."""

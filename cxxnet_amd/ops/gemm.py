@@ -803,6 +803,42 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False, wt_
     return False
 
 
+def conv_backward_data_add(dy, w, dx, add, g: ConvGeom, wt_buf, mask_relu=False, wt_ready=False) -> bool:
+    """dx = mask(conv_transpose(dy, w) + add): the data gradient with a second gradient `add`
+    (laid out like dx) summed in the GEMM epilogue -- the split after a sibling group folds its
+    gradient sum into the group's data-gradient GEMM (NeuralNet._fuse_siblings).  Only on a tuned
+    LDS-DMA tile of this signature ("cd" table entry); False (nothing done) otherwise, and the
+    caller takes the separate data-gradient + sum path."""
+    if not _native_t(dy) or g.stride != 1 or not _use("cd") or g.cg_out % 8 or _pix(add) != _pix(dx):
+        return False
+    if tuple(add.shape) != tuple(dx.shape) or not _glds_cfg["on"]:
+        return False
+    key = "|".join(str(k) for k in ("cd", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x,
+                                    g.groups))
+    cg_in, cg_out = g.cg_in, g.cg_out
+    kd = g.KH * g.KW * cg_out
+    A = _op(wt_buf, cg_in * kd, kd, cg_in, kd)
+    B = _op(dy, cg_out, 0, g.N * g.H * g.W, kd, H=g.Ho, W=g.Wo, C=_pix(dy), Ho=g.H, Wo=g.W, KH=g.KH,
+            KW=g.KW, stride=1, pad_h=g.KH - 1 - g.pad_y, pad_w=g.KW - 1 - g.pad_x, dil=g.stride, Cg=cg_out)
+    t = _glds_cfg["tile"] if _glds_cfg["tile"] >= 0 else _TUNE.get(key)
+    if t is None:  # not tuned yet: the plain path tunes it; with tuning off, its default pick
+        if _glds_cfg["tune"] and not frozen():
+            return False
+        t = _pick_glds(A.rows, B.rows, g.groups)
+    if t == REG or t == 114 or 130 <= t <= 142:
+        return False
+    if not wt_ready:
+        native.check(native.kernels().cxn_conv_weight_flip(w.data_ptr(), wt_buf.data_ptr(), g.groups, cg_out, g.KH,
+                                                           g.KW, cg_in, _stream()), "conv_weight_flip")
+    rc = native.kernels().cxn_gemm_glds_add(A, B, GL_K, GL_KG, dx.data_ptr(), cg_in, _pix(dx), add.data_ptr(),
+                                            int(mask_relu), t, g.groups, _stream())
+    if rc == -1:  # (a flip done here is repeated by the caller's path: the same values)
+        return False
+    native.check(rc, "gemm_glds_add")
+    LAST_GLDS[0] = t
+    return True
+
+
 # Direct small-map weight gradient (conv_wgrad_direct.hip: gap-slot K walk, resident x / dy
 # stages, partial tiles reduced in a fixed order -- no atomics, deterministic).  "1" / "auto":
 # use it wherever it serves the shape; "0": off (the split-K GEMMs run).

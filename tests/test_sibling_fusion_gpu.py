@@ -68,3 +68,74 @@ def test_conv_forward_split_vs_torch(split, cout, ldc):
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b).clamp_min(0).permute(0, 2, 3, 1)
     got = torch.cat([y.float(), y2.float()], -1)
     assert ((got - ref).norm() / ref.norm()).item() < 1e-2
+
+
+def test_fused_model_file_is_byte_identical(monkeypatch):
+    """Sibling groups change only the arena layout: from the same seed the fused net draws the
+    same initial weights, writes the same model file byte for byte, and loads the unfused
+    net's file back to the same bytes."""
+    plain, fused = _net("0", monkeypatch), _net("1", monkeypatch)
+    assert len(fused.net.sib_groups) == 9
+    a, b = plain.save_model(), fused.save_model()
+    assert a == b
+    other = _net("1", monkeypatch)
+    other.load_model(a)
+    assert other.save_model() == a
+
+
+@pytest.mark.parametrize("tile", [1, 7, 38, 79])
+def test_dgrad_with_added_gradient_vs_torch(tile):
+    """ops.gemm.conv_backward_data_add (the split's sum folded into a sibling group's
+    data-gradient GEMM): dx = relu'(x) * (conv_transpose(dy, w) + add) on a forced LDS-DMA tile,
+    against fp32 torch."""
+    from cxxnet_amd.ops import gemm as G
+    N, H, C, K = 4, 14, 192, 176
+    torch.manual_seed(tile)
+    dy = torch.randn(N, H, H, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(K, 1, 1, C, device="cuda") * 0.05).to(torch.bfloat16)
+    add = torch.randn(N, H, H, C, device="cuda").to(torch.bfloat16)
+    act = torch.randn(N, H, H, C, device="cuda").to(torch.bfloat16)  # relu output where > 0
+    g = ConvGeom(N, H, H, C, H, H, K, 1, 1, 1, 0, 0, 1)
+    for mask in (False, True):
+        dx = act.clone()
+        G.set_glds(True, tile)
+        try:
+            assert G.conv_backward_data_add(dy, w, dx, add, g, torch.empty_like(w), mask_relu=mask)
+        finally:
+            G.set_glds(True, -1)
+        assert G.LAST_GLDS[0] == tile
+        ref = torch.einsum("nhwk,kc->nhwc", dy.float(), w.float().view(K, C)) + add.float()
+        if mask:
+            ref = ref * (act.float() > 0)
+        assert ((dx.float() - ref).norm() / ref.norm()).item() < 1e-2, (tile, mask)
+
+
+def test_split_sum_folded_in_training(monkeypatch):
+    """GoogLeNet at batch 16: after the first steps tuned the data-gradient signatures, the
+    splits of the sibling modules skip their sums (folded into the groups' GEMMs), and the
+    step still matches the unfolded one (CXXNET_FOLD_SPLIT_SUM=0)."""
+    B = 16
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(B, 3, 224, 224, generator=g).cuda()
+    y = torch.randint(0, 1000, (B, 1), generator=g).float().cuda()
+    res, trs = {}, {}
+    for fold in ("0", "1"):
+        monkeypatch.setenv("CXXNET_FOLD_SPLIT_SUM", fold)
+        trs[fold] = _net("1", monkeypatch, B)
+        trs[fold].update(DataBatch(x, y))  # tunes any signature not in the table
+    torch.cuda.synchronize()
+    # the same weights and momentum for the compared step (the first steps' tile picks differ)
+    a0, a1 = trs["0"].net.arena, trs["1"].net.arena
+    a1.w.copy_(a0.w)
+    a1.m1.copy_(a0.m1)
+    a1.sync_shadow()
+    for fold, tr in trs.items():
+        w0 = {(li, s.tag): s.w.clone() for li, s in tr.net.arena.specs}
+        tr.update(DataBatch(x, y))
+        torch.cuda.synchronize()
+        res[fold] = ({(li, s.tag): s.w - w0[(li, s.tag)] for li, s in tr.net.arena.specs},
+                     sum(bool(getattr(c.layer, "folded", False)) for c in tr.net.connections))
+    assert res["0"][1] == 0 and res["1"][1] >= 1, (res["0"][1], res["1"][1])
+    for key, d0 in res["0"][0].items():
+        d1 = res["1"][0][key]
+        assert ((d1 - d0).norm() / d0.norm().clamp_min(1e-12)).item() < 5e-2, key
