@@ -92,6 +92,48 @@ hipError_t cxn_fill_bytes(void *p, int v, size_t n, hipStream_t s) {
   return hipGetLastError();
 }
 
+namespace {
+struct ZeroRanges {  // up to 16 disjoint float ranges of one buffer, zeroed by one launch
+  long off[16], len[16];
+  int n;
+};
+// blockIdx.y = range; 16 bytes per thread on the 16-byte-aligned body, floats at the edges
+__global__ void zero_ranges_k(float *base, ZeroRanges r) {
+  const int k = blockIdx.y;
+  if (k >= r.n) return;
+  float *p = base + r.off[k];
+  const long n = r.len[k];
+  const long head = min(static_cast<long>((4 - ((reinterpret_cast<uintptr_t>(p) >> 2) & 3)) & 3), n);
+  const long nv = (n - head) / 4;
+  const long tid = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const long stride = static_cast<long>(gridDim.x) * blockDim.x;
+  float4 *pv = reinterpret_cast<float4 *>(p + head);
+  for (long i = tid; i < nv; i += stride) pv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const long tail0 = head + nv * 4;
+  for (long i = tid; i < head + (n - tail0); i += stride) p[i < head ? i : tail0 + (i - head)] = 0.f;
+}
+}  // namespace
+
+// Zero n float ranges [off[i], off[i] + len[i]) of base in ONE launch (recorded like a launch): the
+// accumulated-gradient ranges of the parameter arena at the start of a backward pass.
+CXN_API int cxn_zero_ranges(float *base, const long *off, const long *len, int n, void *stream) {
+  if (n <= 0) return 0;
+  if (n > 16) return -1;
+  ZeroRanges r{};
+  long mx = 0;
+  for (int i = 0; i < n; ++i) {
+    if (off[i] < 0 || len[i] < 0) return -2;
+    r.off[i] = off[i];
+    r.len[i] = len[i];
+    mx = len[i] > mx ? len[i] : mx;
+  }
+  r.n = n;
+  const long blocks = (mx / 4 + 255) / 256 + 1;
+  CXN_LAUNCH(zero_ranges_k, dim3(static_cast<unsigned>(blocks < 1024 ? blocks : 1024), n), dim3(256), 0,
+             static_cast<hipStream_t>(stream), base, r);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 // Zero `bytes` bytes at dst on `stream` (recorded when a list is open): gradient zeroing at the
 // start of a backward pass must be part of the replayed step.
 CXN_API int cxn_zero(void *dst, long bytes, void *stream) {

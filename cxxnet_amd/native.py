@@ -100,6 +100,7 @@ _SIGS = {
     "cxn_metric_eval": [_P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "cxn_nchw_f32_to_nhwc_bf16": [_P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
     "cxn_image_u8_to_nhwc_bf16": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _F, _P, _P],
+    "cxn_zero_ranges": [_P, _P, _P, _I, _P],
     "cxn_jpeg_idct": [_P, _P, _P, _L, _P, _P],
     "cxn_jpeg_color": [_P, _P, _P, _I, _I, _I, _I, _P, _P],
     "cxn_nhwc_bf16_to_nchw_f32": [_P, _P, _I, _I, _I, _I, _I, _I, _P],

@@ -106,7 +106,10 @@ class ParamArena:
     def zero_accumulated_grads(self):
         from .. import ops  # a library memset: launch lists record it (a torch zero_ they would not)
         torch_zero = os.environ.get("CXXNET_ZERO_TORCH", "0") == "1"  # diagnostics
-        for a, b in self.accumulate_ranges():
+        rs = self.accumulate_ranges()
+        if not torch_zero and ops.zero_ranges(self.g, rs):  # every range in one launch
+            return
+        for a, b in rs:
             if torch_zero:
                 self.g[a:b].zero_()
             else:

@@ -152,6 +152,23 @@ def copy_(dst: torch.Tensor, src: torch.Tensor):
                  "copy_d2d")
 
 
+def zero_ranges(buf: torch.Tensor, ranges) -> bool:
+    """Zero the float ranges [(a, b), ...] of the contiguous fp32 buffer buf in one launch (GPU,
+    at most 16 ranges; recorded into launch lists like every library launch).  False: not
+    served (CPU tensor, other dtype, too many ranges) -- the caller zeroes them one by one."""
+    if not ranges:
+        return True
+    if not _native_t(buf) or buf.dtype != torch.float32 or not buf.is_contiguous() or len(ranges) > 16:
+        return False
+    if any(a < 0 or b > buf.numel() or b < a for a, b in ranges):
+        raise ValueError("zero_ranges: range outside the buffer")
+    import ctypes
+    offs = (ctypes.c_long * len(ranges))(*[a for a, _ in ranges])
+    lens = (ctypes.c_long * len(ranges))(*[b - a for a, b in ranges])
+    native.check(_k().cxn_zero_ranges(buf.data_ptr(), offs, lens, len(ranges), _stream()), "zero_ranges")
+    return True
+
+
 def zero_(t: torch.Tensor):
     """t <- 0 for a contiguous tensor: a library memset on the GPU (recorded into launch lists,
     so a replayed step repeats it -- a torch zero_() would run only in the recording step),
