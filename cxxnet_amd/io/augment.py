@@ -380,5 +380,18 @@ def default_decode_process() -> int:
     return min(16, n) if n >= 4 else 0
 
 
+def default_native_threads() -> int:
+    """Threads of the native decode pool: this process's share of the host cores (the cores
+    it may run on / the ranks of this node -- LOCAL_WORLD_SIZE, one process per GPU), at most
+    32 (AlexNet at ~120k img/s needs about 32 decode threads per GPU with the GPU decode stage,
+    profiles/r5_io_gpu_decode_stage.jsonl)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    ranks = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1))
+    return max(1, min(32, n // ranks))
+
+
 if __name__ == "__main__":
     _worker_main()

@@ -46,7 +46,7 @@ import numpy as np
 import torch
 
 from .. import native
-from .augment import AugmentParam, DecodePool, ShmBuffer, _augment_one, default_decode_process, shm_available
+from .augment import AugmentParam, DecodePool, ShmBuffer, _augment_one, default_decode_process, default_native_threads, shm_available
 from . import jpeg_stage
 from .data import DEVICE_IO_LOCK, DataBatch, DataIterator, U8Images, input_device
 from .jpeg_stage import JpegCoefImages
@@ -257,8 +257,8 @@ class ImageBatchIterator(DataIterator):
     """BatchAdaptIterator(AugmentIterator(<source>)) with a parallel decode stage.
 
     Extra keys (new): decode_native (default 1: JPEG records without affine augmentation
-    are decoded by the native C++ pool of decode_native_threads threads, default
-    min(16, host cores)), decode_gpu (default: on when a GPU is present; with the native
+    are decoded by the native C++ pool of decode_native_threads threads, default this
+    rank's share of the host cores, at most 32: io/augment.py default_native_threads), decode_gpu (default: on when a GPU is present; with the native
     pool, the host only entropy-decodes and the GPU runs IDCT / upsampling / colour / crop,
     io/jpeg_stage.py), prefetch_device (default: on with a GPU; the batch's host-to-device
     copies are issued from the iterator's thread on a side stream, io/data.py DevicePrefetch),
@@ -344,7 +344,7 @@ class ImageBatchIterator(DataIterator):
         if self.decode_native and h > 1 and C <= 3 and not self.aug.need_affine():
             rt = native.rt()
             if rt.JpegDecodePool.available():
-                n = self.decode_native_threads or default_decode_process() or (os.cpu_count() or 1)
+                n = self.decode_native_threads or default_native_threads()
                 self._jpeg = rt.JpegDecodePool(n)
                 if self.decode_gpu < 0:
                     self.decode_gpu = int(torch.cuda.is_available())
