@@ -201,6 +201,26 @@ PYBIND11_MODULE(_cxxnet_rt, m) {
         }
         return py::bytes(s);
       })
+      .def("next_run",
+           [](ImageBinReader &r, int n) -> py::object {
+             // up to n consecutive objects of one page: (bytes blob, [(offset, length)]) -- one copy
+             // for the run; None at the end of the files
+             std::string blob;
+             std::vector<std::pair<long, long>> spans;
+             bool ok;
+             if (r.Ready()) {
+               ok = r.NextRun(n, &blob, &spans);
+             } else {
+               py::gil_scoped_release rel;
+               ok = r.NextRun(n, &blob, &spans);
+             }
+             if (!ok) {
+               std::string err = r.Error();
+               if (!err.empty()) throw std::runtime_error("ImageBinReader: " + err);
+               return py::none();
+             }
+             return py::make_tuple(py::bytes(blob), spans);
+           })
       .def("next_n",
            [](ImageBinReader &r, int n) -> py::list {
              // up to n objects (fewer at the end of the files), one call per chunk of records

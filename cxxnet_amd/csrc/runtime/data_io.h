@@ -91,6 +91,12 @@ class BinaryPage {
     ++data_[0];
     return true;
   }
+  // object r's byte range [*a, *b) within the page
+  void Span(int r, long *a, long *b) const {
+    if (r < 0 || r >= Size()) throw std::runtime_error("BinaryPage: index exceed bound");
+    *a = static_cast<long>(kPageBytes) - data_[r + 2];
+    *b = static_cast<long>(kPageBytes) - data_[r + 1];
+  }
   std::string Get(int r) const {
     if (r < 0 || r >= Size()) throw std::runtime_error("BinaryPage: index exceed bound");
     int32_t end = data_[r + 2], beg = data_[r + 1];
@@ -173,6 +179,33 @@ class ImageBinReader {
   // True when Next() will not wait (the current page still has objects): callers holding an
   // interpreter lock then need not drop it per record.
   bool Ready() const { return cur_ != nullptr && cur_idx_ < cur_->Size(); }
+  // Up to n consecutive objects of one page as ONE contiguous byte range: (*blob, object k at
+  // [spans[k].first, +spans[k].second) of it).  Objects are packed backward from the page end,
+  // so a run of them is one span of the page (copied once instead of once per object).  False
+  // at the end of all files.
+  bool NextRun(int n, std::string *blob, std::vector<std::pair<long, long>> *spans) {
+    spans->clear();
+    blob->clear();
+    std::string first;
+    if (n <= 0) return true;
+    if (!Ready()) {  // move to the next page (Next() waits for it), then un-take its first object
+      if (!Next(&first)) return false;
+      --cur_idx_;
+    }
+    const int r0 = cur_idx_, r1 = std::min(cur_->Size(), r0 + n);
+    long lo = 0, hi = 0;
+    cur_->Span(r1 - 1, &lo, &hi);  // the run's lowest address: its last object
+    long a = 0, b = 0;
+    cur_->Span(r0, &a, &b);
+    const long base = lo, top = b;
+    blob->assign(cur_->raw() + base, static_cast<size_t>(top - base));
+    for (int r = r0; r < r1; ++r) {
+      cur_->Span(r, &a, &b);
+      spans->emplace_back(a - base, b - a);
+    }
+    cur_idx_ = r1;
+    return true;
+  }
   // All remaining objects of the current page (or of the next page when the current
   // one is exhausted); false at end of all files.  Used by the page-shuffling reader.
   bool NextPage(std::vector<std::string> *out) {

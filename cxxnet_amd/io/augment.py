@@ -104,7 +104,7 @@ class AugmentParam:
 def _open(payload):
     """Decoded RGB Pillow image (JPEG/PNG/...; other modes converted to RGB)."""
     from PIL import Image
-    im = Image.open(_io.BytesIO(payload) if isinstance(payload, (bytes, bytearray)) else payload)
+    im = Image.open(_io.BytesIO(payload) if isinstance(payload, (bytes, bytearray, memoryview)) else payload)
     if im.mode != "RGB":
         im = im.convert("RGB")
     return im

@@ -190,13 +190,16 @@ class ImageBinSource(_Source):
         reader = native.rt().ImageBinReader(self.bins, 4)
         for lst in self.lists:
             entries = _read_list(lst, self.label_width)
-            for c0 in range(0, len(entries), 64):  # objects fetched 64 at a time
-                chunk = entries[c0:c0 + 64]
-                bufs = reader.next_n(len(chunk))
-                if len(bufs) != len(chunk):
+            pos = 0
+            while pos < len(entries):  # runs of up to 64 objects, one copy per run (zero-copy views)
+                got = reader.next_run(min(64, len(entries) - pos))
+                if got is None:
                     raise ValueError(f"image bin has fewer objects than list {lst}")
-                for (idx, lab, _), buf in zip(chunk, bufs):
-                    yield Record(idx, lab, buf)
+                blob, spans = got
+                mv = memoryview(blob)
+                for (idx, lab, _), (o, n) in zip(entries[pos:pos + len(spans)], spans):
+                    yield Record(idx, lab, mv[o:o + n])
+                pos += len(spans)
 
 
 class ImageBinXSource(ImageBinSource):
