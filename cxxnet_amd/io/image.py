@@ -459,9 +459,12 @@ class ImageBatchIterator(DataIterator):
         lw = self.label_width
         lab = np.zeros((B, lw), dtype=np.float32)
         index = np.zeros(B, dtype=np.uint32)
-        for i, r in enumerate(recs):
-            lab[i, : min(lw, len(r.label))] = r.label[:lw]
-            index[i] = r.index
+        if recs and all(len(r.label) >= lw for r in recs):  # one stack, not a numpy store per record
+            lab[: len(recs)] = np.stack([r.label[:lw] for r in recs])
+        else:
+            for i, r in enumerate(recs):
+                lab[i, : min(lw, len(r.label))] = r.label[:lw]
+        index[: len(recs)] = np.fromiter((r.index for r in recs), dtype=np.uint32, count=len(recs))
         label = torch.from_numpy(lab)
         lo, hi = (_dist_rows(B) if self.shard_decode else (0, B))
         rows = [(i, r) for i, r in enumerate(recs) if lo <= i < hi]
