@@ -48,8 +48,8 @@ MODEL_NAMES = {"alexnet": "AlexNet ImageNet", "inception_v1": "GoogLeNet/Incepti
 def _args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=15)
     ap.add_argument("--batch", type=int, default=256,
                     help="weak: per-GPU batch; strong: global batch split over the ranks")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
