@@ -139,3 +139,56 @@ def test_split_sum_folded_in_training(monkeypatch):
     for key, d0 in res["0"][0].items():
         d1 = res["1"][0][key]
         assert ((d1 - d0).norm() / d0.norm().clamp_min(1e-12)).item() < 5e-2, key
+
+
+def _dp_worker(rank, port, steps, out):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+                      CXXNET_DIST_BACKEND="nccl", CXXNET_DIST_FORCE="1")
+    import torch.distributed as dist
+    from cxxnet_amd.parallel import init_distributed
+    init_distributed()
+    tr = NetTrainer()
+    base = [(k, v) for k, v in load_conf("inception_v1", []) if not k.startswith("metric")]
+    for k, v in base + [("batch_size", "8"), ("dev", "gpu"), ("eval_train", "0"), ("silent", "1"), ("seed", "5"),
+                        ("deterministic", "1"), ("dp_mode", "allreduce"), ("dp_bucket_mb", "4"),
+                        ("cuda_graph", "0")]:
+        tr.set_param(k, v)
+    tr.init_model()
+    assert tr.reducer.update_fn is not None and len(tr.net.sib_groups) == 9
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(8, 3, 224, 224, generator=g).cuda()
+    y = torch.randint(0, 1000, (8, 1), generator=g).float().cuda()
+    for _ in range(steps):
+        tr.update(DataBatch(x, y))
+    torch.cuda.synchronize()
+    assert tr.reducer.check_consistency() == 0.0
+    torch.save(tr.net.arena.w.cpu(), out)
+    dist.destroy_process_group()
+
+
+def test_inception_siblings_under_rccl_dp_match_plain(tmp_path, monkeypatch):
+    """GoogLeNet with sibling groups (and folded split sums) through the data-parallel step
+    (RCCL at world 1: per-bucket all-reduce from the backprop hooks -- buckets keyed by the
+    groups' gradient-ready layer -- side-stream updates, forward gating) against the plain step
+    of the same net, deterministic mode: the same weights after 3 steps."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "w_dp")
+    mp.spawn(_dp_worker, args=(port, 3, out), nprocs=1, join=True)
+    dp_w = torch.load(out, weights_only=True)
+    tr = _net("1", monkeypatch, 8)
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(8, 3, 224, 224, generator=g).cuda()
+    y = torch.randint(0, 1000, (8, 1), generator=g).float().cuda()
+    for _ in range(3):
+        tr.update(DataBatch(x, y))
+    torch.cuda.synchronize()
+    w = tr.net.arena.w.cpu()
+    assert dp_w.shape == w.shape
+    err = ((dp_w - w).norm() / w.norm()).item()
+    assert err < 1e-5, err
