@@ -1594,6 +1594,46 @@ __global__ void softmax_rows(const bf16_t *__restrict__ x, bf16_t *__restrict__ 
   }
 }
 
+// Rows of K <= 64 * NPL: one wave per row, one block per row (every CU gets rows), the row held in
+// registers -- all of its loads issued before the first reduction instead of three dependent
+// passes over memory (AlexNet fc8 output, 256 x 1000: 9.1 -> a few us).  Same arithmetic as
+// softmax_rows: max, sum of exp(x - max), one reciprocal.
+template <int NPL>
+__global__ void __launch_bounds__(64) softmax_rows_reg(const bf16_t *__restrict__ x, bf16_t *__restrict__ y,
+                                                       float *__restrict__ pf, int K) {
+  const int lane = threadIdx.x;
+  const long base = static_cast<long>(blockIdx.x) * K;
+  float v[NPL];
+#pragma unroll
+  for (int j = 0; j < NPL; ++j) {
+    const int k = lane + 64 * j;
+    v[j] = k < K ? bf2f(x[base + k]) : -INFINITY;
+  }
+  float m = v[0];
+#pragma unroll
+  for (int j = 1; j < NPL; ++j) m = fmaxf(m, v[j]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NPL; ++j) {
+    v[j] = lane + 64 * j < K ? __expf(v[j] - m) : 0.f;
+    s += v[j];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float inv = 1.f / s;
+#pragma unroll
+  for (int j = 0; j < NPL; ++j) {
+    const int k = lane + 64 * j;
+    if (k < K) {
+      const float p = v[j] * inv;
+      y[base + k] = f2bf(p);
+      if (pf) pf[base + k] = p;
+    }
+  }
+}
+
 // grad = (p - onehot(label)) * scale, written in place over the bf16 node.  kind 0 softmax,
 // 1 l2 (x - y), 2 multi-logistic (sigma - y, node already holds sigma).  label: fp32 [rows][lw]
 __global__ void loss_grad(const float *__restrict__ p32, bf16_t *__restrict__ node, const float *__restrict__ label,
@@ -2517,6 +2557,15 @@ CXN_API int cxn_metric_eval(const float *p, int ldp, const float *lab, int ldl, 
 }
 
 CXN_API int cxn_softmax(const void *x, void *y, float *pf, int rows, int K, void *stream) {
+  if (rows <= 0) return 0;
+  if (K <= 1024 && rows < (1 << 30)) {
+    const bf16_t *xb = (const bf16_t *)x;
+    bf16_t *yb = (bf16_t *)y;
+    if (K <= 256) CXN_LAUNCH((softmax_rows_reg<4>), rows, 64, 0, S_, xb, yb, pf, K);
+    else if (K <= 512) CXN_LAUNCH((softmax_rows_reg<8>), rows, 64, 0, S_, xb, yb, pf, K);
+    else CXN_LAUNCH((softmax_rows_reg<16>), rows, 64, 0, S_, xb, yb, pf, K);
+    RET;
+  }
   CXN_LAUNCH((softmax_rows), cdiv(rows, 4), 256, 0, S_, (const bf16_t *)x, (bf16_t *)y, pf, rows, K);
   RET;
 }
