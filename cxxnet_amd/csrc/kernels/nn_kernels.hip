@@ -2342,13 +2342,24 @@ CXN_API int cxn_pool_bwd(const void *x, const void *arg, const void *dy, void *d
       make_fastdiv(static_cast<uint32_t>(H)), static_cast<uint32_t>(total))
     const int sq = KH == KW ? KH : 0;
     if (S == 1 && sq == 3 && mode == 0 && P <= 2 && pool_strips) {
-      constexpr int R = 4;
-      const int HS = (H + R - 1) / R;
-      const long tot = static_cast<long>(N) * HS * W * (C / 8);
-      CXN_LAUNCH((pool_bwd_s1k3<R>), cdiv(tot, NT), NT, 0, S_, 
-          (const bf16_t *)x, (const uint8_t *)arg, (const bf16_t *)dy, (bf16_t *)dx, H, W, C, Ho, Wo, P, relu,
-          make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(W * (C / 8))),
-          make_fastdiv(static_cast<uint32_t>(HS)), static_cast<uint32_t>(tot));
+      static const int r_env = [] {  // CXN_POOL_S1K3_R: probe override of the strip height (2 / 4 / 8)
+        const char *e = getenv("CXN_POOL_S1K3_R");
+        return e != nullptr ? atoi(e) : 4;
+      }();
+#define CXN_S1K3(RV)                                                                                           \
+  {                                                                                                            \
+    constexpr int R = RV;                                                                                      \
+    const int HS = (H + R - 1) / R;                                                                            \
+    const long tot = static_cast<long>(N) * HS * W * (C / 8);                                                  \
+    CXN_LAUNCH((pool_bwd_s1k3<R>), cdiv(tot, NT), NT, 0, S_, (const bf16_t *)x, (const uint8_t *)arg,          \
+               (const bf16_t *)dy, (bf16_t *)dx, H, W, C, Ho, Wo, P, relu,                                     \
+               make_fastdiv(static_cast<uint32_t>(C / 8)), make_fastdiv(static_cast<uint32_t>(W * (C / 8))),   \
+               make_fastdiv(static_cast<uint32_t>(HS)), static_cast<uint32_t>(tot));                          \
+  }
+      if (r_env == 2) CXN_S1K3(2)
+      else if (r_env == 8) CXN_S1K3(8)
+      else CXN_S1K3(4)
+#undef CXN_S1K3
     } else if (S == 2 && sq == 3 && mode == 0 && pool_cells) {
       const int i0 = P / 2, j0 = P / 2;
       const int HC = (P + H - 1) / 2 - i0 + 1, WC = (P + W - 1) / 2 - j0 + 1;
