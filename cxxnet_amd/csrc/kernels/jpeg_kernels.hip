@@ -13,6 +13,8 @@
 // bwin int32 [nblk] window id (row * 3 + component), meta int32 [B][3][80] window tables.
 // Samples are written block-linear (plane[blk][64]), in the coefficient block order, so the
 // IDCT needs no geometry at all and the colour kernel finds a sample through its window.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -159,6 +161,73 @@ __global__ void __launch_bounds__(256) jpeg_color(const uint8_t *__restrict__ pl
   for (int k = 0; k < C; ++k) o[k] = static_cast<uint8_t>(rgb[k]);
 }
 
+// The same output, one thread per pair of source columns (2c, 2c + 1): the two pixels share their
+// chroma column c, so the triangle filter's row sums of c and its neighbours are loaded once for
+// both (h2v2: 6 chroma gathers per component for two pixels instead of 8), and the window / crop
+// fields are read once per two pixels.  grid (cdiv(pairs, 64), B * h), 64 threads.
+__global__ void __launch_bounds__(64) jpeg_color2(const uint8_t *__restrict__ plane, const int *__restrict__ meta,
+                                                  const int *__restrict__ prm, int h, int w, int C,
+                                                  uint8_t *__restrict__ out) {
+  const int b = blockIdx.y / h, y = blockIdx.y - b * h;
+  const int *m = meta + static_cast<long>(b) * 3 * kMeta;
+  const int xx = prm[b * 4], mir = prm[b * 4 + 2];
+  const int c = (prm[b * 4 + 1] >> 1) + static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
+  const int X0 = 2 * c, x0 = X0 - prm[b * 4 + 1];  // crop column of source column X0 (x0 + 1 for X0 + 1)
+  const bool v0 = x0 >= 0 && x0 < w, v1 = x0 + 1 >= 0 && x0 + 1 < w;
+  if (!v0 && !v1) return;
+  uint8_t *orow = out + static_cast<long>(blockIdx.y) * w * C;
+  const int o0 = mir ? w - 1 - x0 : x0, o1 = mir ? w - 2 - x0 : x0 + 1;
+  if (m[kValid] == 0) {
+    for (int k = 0; k < C; ++k) {
+      if (v0) orow[o0 * C + k] = 0;
+      if (v1) orow[o1 * C + k] = 0;
+    }
+    return;
+  }
+  (void)xx;
+  const int Y = prm[b * 4] + y;
+  const Win wl = load_win(m);
+  const int y0 = v0 ? sample(plane, wl, Y, X0) : 0, y1 = v1 ? sample(plane, wl, Y, X0 + 1) : 0;
+  uint32_t rgb0[3], rgb1[3];
+  if (m[kNcomp] == 1) {
+    rgb0[0] = rgb0[1] = rgb0[2] = static_cast<uint32_t>(y0);
+    rgb1[0] = rgb1[1] = rgb1[2] = static_cast<uint32_t>(y1);
+  } else {
+    int ch0[2], ch1[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const Win wc = load_win(m + (k + 1) * kMeta);
+      if (wc.rh == 1) {
+        ch0[k] = v0 ? sample(plane, wc, Y, X0) : 0;
+        ch1[k] = v1 ? sample(plane, wc, Y, X0 + 1) : 0;
+      } else if (wc.rv == 1) {  // h2v1: 3 * nearer + farther, edges repeat
+        const int s = sample(plane, wc, Y, c);
+        ch0[k] = c == 0 ? s : (3 * s + sample(plane, wc, Y, c - 1) + 1) >> 2;
+        ch1[k] = c == wc.dw - 1 ? s : (3 * s + sample(plane, wc, Y, c + 1) + 2) >> 2;
+      } else {  // h2v2: the column sums 3 * nearer row + farther row of c - 1, c, c + 1
+        const int cy = Y >> 1;
+        const int ny = (Y & 1) ? min(cy + 1, wc.dh - 1) : max(cy - 1, 0);
+        const int t = 3 * sample(plane, wc, cy, c) + sample(plane, wc, ny, c);
+        ch0[k] = c == 0 ? (t * 4 + 8) >> 4
+                        : (3 * t + 3 * sample(plane, wc, cy, c - 1) + sample(plane, wc, ny, c - 1) + 8) >> 4;
+        ch1[k] = c == wc.dw - 1 ? (t * 4 + 7) >> 4
+                                : (3 * t + 3 * sample(plane, wc, cy, c + 1) + sample(plane, wc, ny, c + 1) + 7) >> 4;
+      }
+    }
+    const int cb0 = ch0[0] - 128, cr0 = ch0[1] - 128, cb1 = ch1[0] - 128, cr1 = ch1[1] - 128;
+    rgb0[0] = clamp255(y0 + ((91881 * cr0 + 32768) >> 16));
+    rgb0[1] = clamp255(y0 + ((-46802 * cr0 + -22554 * cb0 + 32768) >> 16));
+    rgb0[2] = clamp255(y0 + ((116130 * cb0 + 32768) >> 16));
+    rgb1[0] = clamp255(y1 + ((91881 * cr1 + 32768) >> 16));
+    rgb1[1] = clamp255(y1 + ((-46802 * cr1 + -22554 * cb1 + 32768) >> 16));
+    rgb1[2] = clamp255(y1 + ((116130 * cb1 + 32768) >> 16));
+  }
+  for (int k = 0; k < C; ++k) {
+    if (v0) orow[o0 * C + k] = static_cast<uint8_t>(rgb0[k]);
+    if (v1) orow[o1 * C + k] = static_cast<uint8_t>(rgb1[k]);
+  }
+}
+
 }  // namespace
 
 #define S_ static_cast<hipStream_t>(stream)
@@ -178,6 +247,15 @@ CXN_API int cxn_jpeg_idct(const void *coef, const int *bwin, const int *meta, lo
 CXN_API int cxn_jpeg_color(const void *plane, const int *meta, const int *prm, int B, int h, int w, int C, void *out,
                            void *stream) {
   if (C < 1 || C > 3 || B <= 0 || h <= 0 || w <= 0) return -2;
+  static const int pairs_env = [] {  // CXN_JPEG_COLOR_PAIRS=0: the one-pixel-per-thread kernel (A/B)
+    const char *e = getenv("CXN_JPEG_COLOR_PAIRS");
+    return e != nullptr ? atoi(e) : 1;
+  }();
+  if (pairs_env) {  // w / 2 + 1 column pairs cover any crop start parity
+    CXN_LAUNCH((jpeg_color2), dim3(cdiv(w / 2 + 1, 64), B * h), 64, 0, S_, (const uint8_t *)plane, meta, prm, h, w,
+               C, (uint8_t *)out);
+    RET;
+  }
   CXN_LAUNCH((jpeg_color), dim3(cdiv(w, 256), B * h), 256, 0, S_, (const uint8_t *)plane, meta, prm, h, w, C,
              (uint8_t *)out);
   RET;
