@@ -65,7 +65,7 @@ def _args(argv=None):
                     help="replay forward/backward as HIP graphs (the optimizer and collectives stay eager). "
                          "-1 (default) = the trainer's auto rule: on under data parallelism at per-GPU batch <= 64 "
                          "(strong scaling); the 1-GPU AlexNet / GoogLeNet steps are GPU-bound, graph replay measured "
-                         "-0.4%%/+0.5%% (profiles/r16_graph_ab.jsonl)")
+                         "-0.4%%/+0.5%% (profiles/early-r16_graph_ab.jsonl)")
     ap.add_argument("--dp-mode", default="auto", choices=["auto", "shard", "allreduce"],
                     help="gradient reduction: auto = fp32 all-reduce (shard: reduce-scatter, sliced update, "
                          "bf16 all-gather)")

@@ -1,0 +1,457 @@
+// Direct stride-1 "same" convolution for small maps on the gap-slot layout, gfx950: the forward
+// y[p][co] = f(sum_{t, ci} W[co][t][ci] x[p + shift(t)][ci] + b[co]), and the data gradient as the
+// same forward over dy with the flipped weights (conv_weight_flip), its epilogue applying the relu'
+// mask of the node it writes and summing that node's bias gradient.
+// Reference: src/layer/convolution_layer-inl.hpp:70-101 (forward: im2col + gemm per group) and
+// :139-155 (backward data: gemm + col2im).
+//
+// Why.  The implicit GEMMs (gemm_glds.hip K_GATHER) rebuild each pixel's im2col address per
+// 16-byte load -- 3.5-6 VALU per MFMA on AlexNet conv2-5 (profiles/r5_pmc_alexnet_ops.md) -- and
+// fetch every input pixel once per tap through L2.  Here the taps are constant LDS offsets:
+//   * Gap slots (as conv_wgrad_direct.hip): every image row is followed by a P-wide zero gap
+//     (pitch PW = W + P) and the images of a block are stacked with P zero separator rows.  In
+//     that slot space the input under tap (kh, kw) of output slot o is staged slot
+//     o + kh * PW + kw, for every slot: padding falls on gap slots, which are zeros.
+//   * A block item = IPB whole images x 16 NF output channels of one group.  Its K loop walks
+//     the input channels in stages of 32: per stage the block stages the x halo of its images
+//     (32 channels, four 8-channel planes [plane][slot][8 ch], 16 B per slot) and the weights of
+//     all taps for its channels (one 1-KiB operand image per (tap, 16 channels), lane l's 16 B at
+//     16 l), both by LDS-DMA with per-lane source offsets fixed for the whole kernel: per stage
+//     only the buffer descriptors move, and slots off the map read zeros through out-of-range
+//     offsets.  Every fragment read is one ds_read_b128 at a constant offset from a per-lane base,
+//     conflict-free for any tap shift (16 consecutive slots of one plane per 16 lanes).
+//   * MFMA v_mfma_f32_16x16x32_bf16 with the weights as A (rows = output channels) and the
+//     shifted slots as B (columns = slots), so each lane's accumulator holds 4 consecutive output
+//     channels of one slot: the epilogue stores 8 bytes per lane straight from registers (no LDS
+//     staging), skipping gap / separator slots.
+//   * Four waves, one per SIMD; wave w owns M fragments w * WMF .. of the item's slots and all NF
+//     channel fragments: per tap WMF + NF reads for WMF * NF MFMAs.
+//   * Persistent: one block per CU walks items L, L + grid, ... (L = XCD-contiguous remap of the
+//     block id, so the blocks sharing an item's x or weights share an L2), as one continuous
+//     stream of stages: the next stage's DMAs -- the next item's first stage included -- ride on
+//     the current stage's taps, and an item's epilogue runs while its successor's first stage
+//     lands.
+#include "gemm_glds_common.h"
+
+#include <cstdlib>
+
+using namespace cxg;
+
+namespace cxg {
+void launch_db_reduce(const GEpi &E, int rows, hipStream_t s);
+}
+
+namespace {
+
+// One 1-KiB LDS-DMA (16 bytes per lane), inline asm so that hipcc neither waits for it before the
+// current stage's ds_reads nor reorders LDS reads across it; completion is counted by hand
+// (wait_vmcnt + barrier at the end of each stage).  M0 is saved and restored in the statement.
+__device__ __forceinline__ void dma16c(rsrc_t r, uint32_t lds_addr, uint32_t voff) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(r), "s"(lds_addr) : "memory");
+}
+
+// MFMA on an accumulator pinned to AGPRs: with the builtin, hipcc kept the loop-carried tile in
+// VGPRs and copied all of it into AGPRs and back every stage (2 x 96 v_accvgpr moves per stage)
+__device__ __forceinline__ void mfma_acc(f32x4 &acc, const bf16x8 &a, const bf16x8 &b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+constexpr int cd_fdiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+
+template <int H, int W, int KS, int IPB, int NF, int NW>
+struct Cd {
+  static constexpr int P = (KS - 1) / 2, T = KS * KS, PW = W + P, VR = H + P;
+  static constexpr int IMG = VR * PW;                             // slots per image
+  static constexpr int OS = (IPB * VR - P) * PW;                  // output slots that can hold pixels
+  static constexpr int WMF = ((OS + 15) / 16 + NW - 1) / NW;      // M fragments per wave
+  static constexpr int MS = 16 * NW * WMF;                        // output slots computed
+  static constexpr int NXS = (MS + (KS - 1) * (PW + 1) + 16 * NW - 1) / (16 * NW) * (16 * NW);  // staged x slots
+  static constexpr int NXP = NXS / 16;                            // x DMA pieces: 16 slots x 4 planes each
+  static constexpr int XB = NXP * 1024;                           // x image bytes
+  static constexpr int WB = T * NF * 1024;                        // weight image bytes
+  static constexpr int BUF = XB + WB;
+  static constexpr int NDX = NXP, ND = NDX + T * NF, NDPW = (ND + NW - 1) / NW;
+  static constexpr int XLEAD = P * PW + P;                        // staged slot of linear position 0
+  static_assert(2 * BUF <= 160 * 1024, "LDS");
+};
+
+// pixel (image-relative: (img H + row) W + col) of a linear slot position, -1 on gap / separator
+template <int H, int W, int KS, int IPB>
+__device__ __forceinline__ int cd_pixel(int lin) {
+  constexpr int P = (KS - 1) / 2, PW = W + P, VR = H + P;
+  const int vrow = cd_fdiv(lin, PW) ;
+  const int col = lin - vrow * PW;
+  const int img = cd_fdiv(vrow, VR);
+  const int row = vrow - img * VR;
+  if (lin < 0 || img >= IPB || row >= H || col >= W) return -1;
+  return (img * H + row) * W + col;
+}
+
+struct CdArgs {
+  const bf16_t *x;    // NHWC input (pixel stride ldx), group g's channels at g * Cg
+  const bf16_t *w;    // [groups * Cog][KS][KS][Cg]
+  const float *bias;  // EPI 0: [groups * Cog] or null
+  bf16_t *y;          // NHWC output (pixel stride ldy), group g's channels at g * Cog
+  float *dbp;         // EPI 2: bias-gradient partial rows [nig * NW][dbp_ld]
+  int N, ldx, ldy, Cg, Cog, groups, ncob, nitems, nst, relu, dbp_ld;
+};
+
+// EPI 0: + bias, optional relu (a.relu).  EPI 1: data gradient; with a.relu, y *= (y_old > 0)
+// (y holds relu(z) on entry).  EPI 2: EPI 1 plus the column sums of the stored values as partial
+// rows.
+template <int H, int W, int KS, int IPB, int NF, int NW, int EPI, int DBG = 0>
+__global__ void __launch_bounds__(64 * NW, 1) conv_direct(CdArgs a) {
+  using G = Cd<H, W, KS, IPB, NF, NW>;
+  constexpr int T = G::T, WMF = G::WMF, XB = G::XB, BUF = G::BUF;
+  constexpr int NDX = G::NDX, ND = G::ND, NDPW = G::NDPW, PW = G::PW, IMG = G::IMG, HW = H * W;
+  static_assert(NDX % NW == 0, "x pieces per wave");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lds0 =
+      __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void *)smem)));
+  const int nb = static_cast<int>(gridDim.x);
+  const int L = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
+  const int nmine = L < a.nitems ? (a.nitems - L + nb - 1) / nb : 0;
+  const int K = nmine * a.nst;  // stages of this block
+  if (K == 0) return;
+
+  // ---- per-lane DMA source offsets (bytes from the stage's descriptor base), fixed for the kernel
+  uint32_t voff[NDPW];
+#pragma unroll
+  for (int i = 0; i < NDPW; ++i) {
+    const int q = wave + NW * i;
+    uint32_t v = OOB;
+    if (q < NDX) {  // slots 16 q .. 16 q + 15, lane (plane lane >> 4, slot lane & 15)
+      const int pix = cd_pixel<H, W, KS, IPB>(16 * q + (lane & 15) - G::XLEAD);
+      if (pix >= 0) v = static_cast<uint32_t>((pix * a.ldx + 8 * (lane >> 4)) * 2);
+    } else if (q < ND) {
+      const int qw = q - NDX, t = qw / NF, f = qw - t * NF;
+      v = static_cast<uint32_t>((((16 * f + (lane & 15)) * T + t) * a.Cg + 8 * (lane >> 4)) * 2);
+    }
+    voff[i] = v;
+  }
+
+  auto item_of = [&](int k, int &ig, int &g, int &cob, int &s) __attribute__((always_inline)) {
+    const int j = k / a.nst;
+    s = k - j * a.nst;
+    const int it = L + j * nb;
+    const int r = it / a.ncob;
+    cob = it - r * a.ncob;
+    ig = r / a.groups;
+    g = r - ig * a.groups;
+  };
+  rsrc_t rx, rw;
+  // descriptors of stage k; past the last stage (k == K) empty ranges: the DMAs issued for it
+  // write zeros into the idle buffer, so the issue needs no branch
+  auto prep = [&](int k) __attribute__((always_inline)) {
+    if (k >= K) {
+      rx = make_rsrc(a.x, 0u);
+      rw = make_rsrc(a.w, 0u);
+      return;
+    }
+    int ig, g, cob, s;
+    item_of(k, ig, g, cob, s);
+    const int n0 = ig * IPB;
+    const int nimg = min(IPB, a.N - n0);
+    const long cx = static_cast<long>(g) * a.Cg + 32 * s;
+    rx = make_rsrc(a.x + static_cast<long>(n0) * HW * a.ldx + cx,
+                   static_cast<uint32_t>((static_cast<long>(nimg) * HW * a.ldx - cx) * 2));
+    const long co = static_cast<long>(g) * a.Cog + cob * 16 * NF;
+    rw = make_rsrc(a.w + co * T * a.Cg + 32 * s, static_cast<uint32_t>((16L * NF * T * a.Cg - 32 * s) * 2));
+  };
+  // DMA i of this wave is piece q = wave + NW i: x pieces for i < NDX / NW (NDX is a multiple of
+  // NW), weight pieces after them (only the last i may run past ND, for some waves)
+  auto issue_one = [&](auto ic, int b) __attribute__((always_inline)) {
+    constexpr int i = decltype(ic)::value;
+    const int q = wave + NW * i;
+    const uint32_t dst = lds0 + static_cast<uint32_t>(b * BUF + q * 1024);
+    if constexpr (i < NDX / NW) {
+      if constexpr (!(DBG & 1)) dma16c(rx, dst, voff[i]);
+    } else if constexpr (NW * (i + 1) <= ND) {
+      if constexpr (!(DBG & 2)) dma16c(rw, dst, voff[i]);
+    } else {
+      if constexpr (!(DBG & 2)) if (q < ND) dma16c(rw, dst, voff[i]);
+    }
+  };
+
+  // fragment read bases.  x image: 1-KiB slot groups [16 slots of plane 0][.. plane 1][.. 2][.. 3],
+  // 16 B per (slot, plane); lane (plane p = lane >> 4, l16 = lane & 15) of M fragment mi under a
+  // tap shift sh = 16 h + r reads slot s = 16 (mi + h) + l16 + r, at byte
+  // 1024 (mi + h + ((l16 + r) >> 4)) + 256 p + 16 ((l16 + r) & 15): per-lane offsets for the 16
+  // values of r, everything else an immediate.  Weight image (t, f): 16 bytes per lane.
+  const int l16 = lane & 15;
+  const int xrd = 1024 * wave * WMF + 256 * (lane >> 4);
+  auto xoff = [&](int r) __attribute__((always_inline)) {
+    return xrd + 1024 * ((l16 + r) >> 4) + 16 * ((l16 + r) & 15);
+  };
+  const int wrd = XB + 16 * lane;
+
+  f32x4 acc[WMF][NF];
+#pragma unroll
+  for (int i = 0; i < WMF; ++i)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto epilogue = [&](int k) __attribute__((always_inline)) {
+    int ig, g, cob, s;
+    item_of(k, ig, g, cob, s);
+    const int n0 = ig * IPB;
+    const int c0 = g * a.Cog + cob * 16 * NF + 4 * (lane >> 4);
+    int po[WMF];  // element offsets (< 2^30: cxn_conv_direct checks the extent)
+    bool ok[WMF];
+#pragma unroll
+    for (int i = 0; i < WMF; ++i) {
+      const int o = 16 * (wave * WMF + i) + (lane & 15);
+      const int img = o / IMG, ro = o - img * IMG;
+      const int r = ro / PW, c = ro - r * PW;
+      ok[i] = img < IPB && r < H && c < W && n0 + img < a.N;
+      po[i] = ((n0 + img) * HW + r * W + c) * a.ldy + c0;
+    }
+    if constexpr (EPI == 0) {
+      f32x4 bv[NF];
+#pragma unroll
+      for (int f = 0; f < NF; ++f)
+        bv[f] = a.bias ? f32x4{a.bias[c0 + 16 * f], a.bias[c0 + 16 * f + 1], a.bias[c0 + 16 * f + 2],
+                               a.bias[c0 + 16 * f + 3]}
+                       : f32x4{0.f, 0.f, 0.f, 0.f};  // (the bias may sit at any offset of the arena)
+#pragma unroll
+      for (int i = 0; i < WMF; ++i) {
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          f32x4 v = acc[i][f] + bv[f];
+          if (a.relu) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+          }
+          if (ok[i]) *reinterpret_cast<uint2 *>(a.y + po[i] + 16 * f) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        }
+      }
+    } else {
+      f32x4 sum[NF];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) sum[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // in halves of the M fragments: each half's old values are all loaded before its first store
+      constexpr int HM = (WMF + 1) / 2;
+#pragma unroll
+      for (int h = 0; h < WMF; h += HM) {
+        uint2 old[HM][NF];
+#pragma unroll
+        for (int i = 0; i < HM; ++i)
+#pragma unroll
+          for (int f = 0; f < NF; ++f)
+            old[i][f] = (a.relu && h + i < WMF && ok[h + i])
+                            ? *reinterpret_cast<const uint2 *>(a.y + po[h + i] + 16 * f)
+                            : make_uint2(0x3f803f80u, 0x3f803f80u);  // (no mask: all ones)
+#pragma unroll
+        for (int i = 0; i < HM; ++i) {
+          if (h + i >= WMF) continue;
+#pragma unroll
+          for (int f = 0; f < NF; ++f) {
+            const uint2 o2 = old[i][f];
+            // relu'(z) from relu(z) > 0: bf16 bits > 0 as signed shorts
+            const bool m0 = static_cast<short>(o2.x & 0xffffu) > 0, m1 = static_cast<short>(o2.x >> 16) > 0;
+            const bool m2 = static_cast<short>(o2.y & 0xffffu) > 0, m3 = static_cast<short>(o2.y >> 16) > 0;
+            const f32x4 v = acc[h + i][f];
+            const uint2 pk =
+                make_uint2(pack2(m0 ? v[0] : 0.f, m1 ? v[1] : 0.f), pack2(m2 ? v[2] : 0.f, m3 ? v[3] : 0.f));
+            if (ok[h + i]) *reinterpret_cast<uint2 *>(a.y + po[h + i] + 16 * f) = pk;
+            if constexpr (EPI == 2) {
+              if (ok[h + i]) {
+                sum[f][0] += __uint_as_float(pk.x << 16);
+                sum[f][1] += __uint_as_float(pk.x & 0xffff0000u);
+                sum[f][2] += __uint_as_float(pk.y << 16);
+                sum[f][3] += __uint_as_float(pk.y & 0xffff0000u);
+              }
+            }
+          }
+        }
+      }
+      if constexpr (EPI == 2) {
+        // sum over the 16 slots of a lane group (lane & 15), then lane (lane & 15) == 0 writes the
+        // wave's partial row (row = image group x wave, every column written exactly once)
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float v = sum[f][j];
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            v += __shfl_xor(v, 8);
+            sum[f][j] = v;
+          }
+        if ((lane & 15) == 0) {
+          float *row = a.dbp + static_cast<long>(ig * NW + wave) * a.dbp_ld + c0;
+#pragma unroll
+          for (int f = 0; f < NF; ++f) *reinterpret_cast<f32x4 *>(row + 16 * f) = sum[f];
+        }
+      }
+    }
+  };
+
+  // prologue: the first stage
+  prep(0);
+  static_for<NDPW>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    const int q = wave + NW * i;
+    if (q < ND) dma16c(i < NDX / NW ? rx : rw, lds0 + static_cast<uint32_t>(q * 1024), voff[i]);
+  });
+  wait_vmcnt<0>();
+  block_barrier();
+
+  // Per stage: tap t's fragments were read one tap ahead (register sets alternate by tap
+  // parity); the reads of tap t + 1 are issued before tap t's MFMAs, and sched_barriers keep the
+  // two groups apart, so each tap's 24 MFMAs cover the next tap's LDS latency.  The next stage's
+  // DMAs are issued over the first taps and land under the rest of the stage.
+  constexpr int DMA_TAPS = T < 4 ? T : 4;
+  bf16x8 xf[2][WMF], wf[2][NF];
+  // fragment r of tap t into register set st: r < NF the weight fragment r (every MFMA of the
+  // next tap's first row needs them), else the x fragment of M fragment r - NF, in MFMA order
+  auto read_one = [&](const char *buf, auto tc, auto sc, auto rc) __attribute__((always_inline)) {
+    constexpr int t = decltype(tc)::value, st = decltype(sc)::value, r = decltype(rc)::value;
+    constexpr int kh = t / KS, kw = t - kh * KS;
+    constexpr int sh = kh * PW + kw;
+    if constexpr (r < NF) {
+      wf[st][r] = *reinterpret_cast<const bf16x8 *>(buf + wrd + (t * NF + r) * 1024);
+    } else {
+      xf[st][r - NF] = *reinterpret_cast<const bf16x8 *>(buf + xoff(sh & 15) + 1024 * (r - NF + (sh >> 4)));
+    }
+  };
+  constexpr int NR = WMF + NF;  // fragment reads per tap
+  auto stage = [&](int k) __attribute__((always_inline)) {
+    const int b = k & 1;
+    prep(k + 1);
+    const char *buf = smem + b * BUF;
+    static_for<NR>([&](auto rc) { read_one(buf, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, rc); });
+    static_for<T>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      constexpr int st = t & 1;
+      // tap t's MFMAs with the NR reads of tap t + 1 spread between them (one per RS MFMAs):
+      // clumped, each wave's read burst held its MFMA pipe idle while four waves queued at the LDS
+      constexpr int NM = WMF * NF, RS = NM / NR > 0 ? NM / NR : 1;
+      static_for<NM>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        constexpr int i = q / NF, f = q % NF;
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_acc(acc[i][f], wf[st][f], xf[st][i]);
+        if constexpr (!(DBG & 8) && t + 1 < T && q % RS == RS - 1 && q / RS < NR) {
+          read_one(buf, std::integral_constant<int, t + 1>{}, std::integral_constant<int, st ^ 1>{},
+                   std::integral_constant<int, q / RS>{});
+        }
+        if constexpr (!(DBG & 8) && t + 1 < T && q == NM - 1 && NM / RS < NR) {  // reads left over
+          static_for<NR - NM / RS>([&](auto rc) {
+            read_one(buf, std::integral_constant<int, t + 1>{}, std::integral_constant<int, st ^ 1>{},
+                     std::integral_constant<int, NM / RS + decltype(rc)::value>{});
+          });
+        }
+      });
+      __builtin_amdgcn_sched_barrier(0);
+      static_for<NDPW>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (i * DMA_TAPS / NDPW == t) issue_one(ic, b ^ 1);
+      });
+    });
+    if constexpr (!(DBG & 16)) {
+      wait_vmcnt<0>();
+      asm volatile("" ::: "memory");
+      block_barrier();
+      asm volatile("" ::: "memory");
+    }
+  };
+  // items outer, stages inner: the accumulators stay in AGPRs across the stage loop (one flat
+  // loop with a conditional epilogue made hipcc carry them in VGPRs and copy them every stage)
+  for (int j = 0, k = 0; j < nmine; ++j) {
+#pragma unroll
+    for (int i = 0; i < WMF; ++i)
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+        asm volatile("" : "+a"(acc[i][f]));
+      }
+    for (int s = 0; s < a.nst; ++s, ++k) stage(k);
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // the last inline-asm MFMAs' results
+#pragma unroll
+    for (int i = 0; i < WMF; ++i)
+#pragma unroll
+      for (int f = 0; f < NF; ++f) asm volatile("" : "+a"(acc[i][f]));
+    epilogue(k - 1);
+  }
+}
+
+template <int H, int W, int KS, int IPB, int NF, int NW>
+int launch_cd(CdArgs a, int epi, float *db, hipStream_t s) {
+  using G = Cd<H, W, KS, IPB, NF, NW>;
+  (void)sizeof(G);
+  if (a.Cog % (16 * NF) || a.Cg % 32) return -1;
+  const int nig = (a.N + IPB - 1) / IPB;
+  a.ncob = a.Cog / (16 * NF);
+  a.nitems = nig * a.groups * a.ncob;
+  a.nst = a.Cg / 32;
+  const int grid = a.nitems < 256 ? a.nitems : 256;
+  static const int dbg = getenv("CXN_CD_DBG") ? atoi(getenv("CXN_CD_DBG")) : 0;
+  if (epi == 0 && dbg) {
+    switch (dbg) {
+      case 1: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 1>), dim3(grid), dim3(64 * NW), 0, s, a); break;
+      case 2: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 2>), dim3(grid), dim3(64 * NW), 0, s, a); break;
+      case 3: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 3>), dim3(grid), dim3(64 * NW), 0, s, a); break;
+      case 11: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 11>), dim3(grid), dim3(64 * NW), 0, s, a); break;
+      case 19: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 19>), dim3(grid), dim3(64 * NW), 0, s, a); break;
+      default: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 27>), dim3(grid), dim3(64 * NW), 0, s, a); break;
+    }
+  } else if (epi == 0) {
+    CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0>), dim3(grid), dim3(64 * NW), 0, s, a);
+  } else if (epi == 1) {
+    CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 1>), dim3(grid), dim3(64 * NW), 0, s, a);
+  } else {
+    CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 2>), dim3(grid), dim3(64 * NW), 0, s, a);
+    GEpi E{};
+    E.dbias = a.dbp;
+    E.part_ld = a.dbp_ld;
+    E.dbias_final = db;
+    launch_db_reduce(E, nig * NW, s);
+  }
+  return 0;
+}
+
+}  // namespace
+
+// Served: stride 1, "same" padding, K = 3 on 13 x 13 maps; Cg (input channels per group) a
+// multiple of 32, Cog (output channels per group) a multiple of 64, pixel strides multiples of 8.
+// epi 0: y = conv(x, w) + bias (relu optional).  epi 1: data gradient (x = dy, w = flipped
+// weights), with relu = 1 y *= relu'(y_old).  epi 2: epi 1 and db += column sums of the stored y (dbp: a
+// workspace of at least dbp_elems floats, db the fp32 bias gradient).  dbp == nullptr with
+// epi 2 asks for the workspace size (floats).  Returns -1 when the shape is not served.
+CXN_API long cxn_conv_direct(const void *x, int ldx, const void *w, const float *bias, void *y, int ldy, float *dbp,
+                             long dbp_elems, float *db, int N, int H, int W, int Cg, int Cog, int groups, int KS,
+                             int relu, int epi, void *stream) {
+  if (KS != 3 || H != 13 || W != 13) return -1;
+  if (Cg % 32 || Cog % 64 || ldx % 8 || ldy % 8 || groups < 1 || ldx < groups * Cg || ldy < groups * Cog) return -1;
+  if (static_cast<long>(N) * H * W * (ldx > ldy ? ldx : ldy) >= (1L << 30)) return -1;
+  constexpr int IPB = 2;
+  const long need = static_cast<long>((N + IPB - 1) / IPB) * 8 * groups * Cog;  // (rows: image group x wave)
+  if (epi == 2 && dbp == nullptr) return need;
+  if (epi == 2 && dbp_elems < need) return -4;
+  CdArgs a{};
+  a.x = static_cast<const bf16_t *>(x);
+  a.w = static_cast<const bf16_t *>(w);
+  a.bias = bias;
+  a.y = static_cast<bf16_t *>(y);
+  a.dbp = dbp;
+  a.N = N;
+  a.ldx = ldx;
+  a.ldy = ldy;
+  a.Cg = Cg;
+  a.Cog = Cog;
+  a.groups = groups;
+  a.relu = relu;
+  a.dbp_ld = groups * Cog;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  static const int nw = getenv("CXN_CD_NW") ? atoi(getenv("CXN_CD_NW")) : 4;
+  const int rc = nw == 8 ? launch_cd<13, 13, 3, IPB, 4, 8>(a, epi, db, s) : launch_cd<13, 13, 3, IPB, 4, 4>(a, epi, db, s);
+  if (rc != 0) return rc;
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}

@@ -33,7 +33,7 @@
 //     K slice) so each wave waits with one constant `s_waitcnt vmcnt(N)` for its own loads of
 //     the tile to read, then a raw s_barrier: DMAs of later tiles stay in flight across it;
 //   * 4 waves (wave grid WGM x WGN) of v_mfma_f32_16x16x32_bf16; small-LDS 2-stage tiles run
-//     2-5 blocks per CU, which is what hides the DMA latency best (profiles/r14_glds_tiles.jsonl);
+//     2-5 blocks per CU, which is what hides the DMA latency best (profiles/early-r14_glds_tiles.jsonl);
 //   * epilogues staged per wave through LDS so every global access is a contiguous row
 //     segment: bf16 (+bias, relu, relu'-mask of the old value), fp32 split-K slab, fp32 +=,
 //     fp32 atomics.

@@ -483,6 +483,10 @@ inline int ReadCoefCrop(const jpg::Api &J, const unsigned char *buf, size_t len,
     total += static_cast<long>(win[k][2]) * win[k][3];
   }
   const long blk0 = st.cursor.fetch_add(total);
+  // the reserved blocks get a valid window id before anything can fail (stage full below, or a
+  // libjpeg longjmp from access_virt_barray): a failed row keeps meta VALID = 0 and falls back
+  // to the host decoder, but its blocks stay in the uploaded range and the IDCT reads their ids
+  if (blk0 < st.cap_blocks) std::fill(st.bwin + blk0, st.bwin + std::min(blk0 + total, st.cap_blocks), row * 3);
   if (blk0 + total > st.cap_blocks) {
     J.abort_decompress(&cinfo);
     J.destroy_decompress(&cinfo);

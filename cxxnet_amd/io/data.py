@@ -27,8 +27,9 @@ class DevicePrefetch:
     the next one (40+ MB per AlexNet batch, about 1 ms of PCIe).  Sources should be pinned
     (asynchronous DMA).  ``take`` orders the current stream after the copies."""
 
-    def __init__(self, tensors, dev: torch.device):
+    def __init__(self, tensors, dev: torch.device, lo: int = 0):
         self.dev = dev
+        self.lo = lo  # first batch row the copied tensors hold
         with DEVICE_IO_LOCK:
             s = _copy_streams.get(dev.index)
             if s is None:
@@ -67,13 +68,23 @@ class U8Images:
         self.pix, self.prm, self.cm, self.mean, self.mode, self.scale = pix, prm, cm, mean, mode, float(scale)
         self.pf, self.rows = pf, rows  # DevicePrefetch of (pix, prm, cm) and the rows of it this view is
 
-    def prefetch(self, dev: torch.device):
-        self.pf, self.rows = DevicePrefetch([self.pix, self.prm, self.cm], dev), (0, self.pix.shape[0])
+    def prefetch(self, dev: torch.device, lo: int = 0, hi: Optional[int] = None):
+        """Copy rows [lo, hi) to `dev` ahead of the step (a data-parallel rank decodes and trains
+        only its own rows; the rest of the batch is never read on this rank)."""
+        hi = self.pix.shape[0] if hi is None else hi
+        self.pf = DevicePrefetch([self.pix[lo:hi], self.prm[lo:hi], self.cm[lo:hi]], dev, lo)
+        self.rows = (0, self.pix.shape[0])
 
     def on_device(self, dev):
-        """(pix, prm, cm) on `dev` from the prefetch, or None."""
-        got = self.pf.take(dev) if self.pf is not None else None
-        return None if got is None else [t[self.rows[0]:self.rows[1]] for t in got]
+        """(pix, prm, cm) on `dev` from the prefetch, or None (also when this view reaches
+        rows the prefetch did not copy)."""
+        if self.pf is None:
+            return None
+        r0, r1 = self.rows[0] - self.pf.lo, self.rows[1] - self.pf.lo
+        if r0 < 0 or r1 > self.pf.tensors[0].shape[0]:
+            return None
+        got = self.pf.take(dev)
+        return None if got is None else [t[r0:r1] for t in got]
 
     @property
     def shape(self):

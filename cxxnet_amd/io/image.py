@@ -243,6 +243,28 @@ class ImageBinXSource(ImageBinSource):
 
 
 # ----------------------------------------------------------------------------- batch iterator
+def consumer_device(dev: Optional[str]) -> Optional[torch.device]:
+    """The CUDA device the trainer configured by `dev` trains on, or None when the batches are
+    consumed on the host (NetTrainer._device's rule): 'cpu' -> None; under torch.distributed the
+    rank's device (LOCAL_RANK); 'gpu:N' -> cuda:N; no `dev` key seen -> the rank's GPU when one is
+    present."""
+    if not torch.cuda.is_available():
+        return None
+    if dev is None:
+        return input_device()
+    from ..nnet.trainer import parse_devices
+    kind, ids = parse_devices(dev)
+    if kind != "gpu":
+        return None
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            return input_device()
+    except Exception:  # noqa: BLE001
+        pass
+    return torch.device("cuda", ids[0] if ids else 0)
+
+
 def _dist_rows(batch_size: int) -> Tuple[int, int]:
     """Rows of the global batch this rank trains on (same rule as NetTrainer._slice)."""
     world, rank = 1, 0
@@ -294,6 +316,8 @@ class ImageBatchIterator(DataIterator):
         self.decode_native_threads = 0
         self.decode_gpu = -1
         self.prefetch_device = -1
+        self.dev = None  # the trainer's `dev` (global conf key): the device the batches feed
+        self._dev: Optional[torch.device] = None
         self._jpeg = None
         self._pool: Optional[ThreadPoolExecutor] = None
         self.mean: Optional[torch.Tensor] = None
@@ -331,6 +355,8 @@ class ImageBatchIterator(DataIterator):
             self.decode_gpu = int(val)
         elif name == "prefetch_device":
             self.prefetch_device = int(val)
+        elif name == "dev":
+            self.dev = val
 
     # ------------------------------------------------------------------ setup
     def init(self):
@@ -341,16 +367,19 @@ class ImageBatchIterator(DataIterator):
             self.decode_process = default_decode_process()
         if not shm_available():
             self.decode_process = 0
+        self._dev = consumer_device(self.dev)
         if self.prefetch_device < 0:
-            self.prefetch_device = int(torch.cuda.is_available())
+            self.prefetch_device = int(self._dev is not None)
+        elif self._dev is None:
+            self.prefetch_device = 0  # nothing on a GPU consumes the batches
         C, h, w = self.aug.shape
         if self.decode_native and h > 1 and C <= 3 and not self.aug.need_affine():
             rt = native.rt()
             if rt.JpegDecodePool.available():
                 n = self.decode_native_threads or default_native_threads()
                 self._jpeg = rt.JpegDecodePool(n)
-                if self.decode_gpu < 0:
-                    self.decode_gpu = int(torch.cuda.is_available())
+                if self.decode_gpu < 0:  # default: on only when a GPU consumes the batches
+                    self.decode_gpu = int(self._dev is not None)
             elif not self.silent:
                 print(f"native JPEG decoder unavailable ({rt.JpegDecodePool.error()}): decoding with Pillow")
         if self.aug.mean_value is not None and any(v > 0 for v in self.aug.mean_value):
@@ -479,7 +508,7 @@ class ImageBatchIterator(DataIterator):
         if self._jpeg is not None and self.decode_gpu > 0:
             data = self._stage_jpeg(rows, seeds, (B, h, w, C))
             if self.prefetch_device:
-                data.prefetch(input_device())
+                data.prefetch(self._dev)
             return DataBatch(data, label, index, padd)
         if self._jpeg is not None:
             pix = self._decode_native(rows, seeds, (B, h, w, C), prm, cm)
@@ -489,7 +518,7 @@ class ImageBatchIterator(DataIterator):
             pix = self._decode_threads(rows, seeds, (B, h, w, C), prm, cm)
         data = U8Images(pix, prm_t, cm_t, self.mean, self.mean_mode, self.aug.scale)
         if self.prefetch_device and h > 1:
-            data.prefetch(input_device())
+            data.prefetch(self._dev, lo, hi)  # only this rank's decoded rows cross PCIe
         return DataBatch(data, label, index, padd)
 
     @staticmethod

@@ -219,9 +219,11 @@ class NeuralNet:
                 ok = all(id(n) in nn for n in ins)
             else:
                 ok = False
-            if ok:
-                for n in conn.nodes_out:
+            for n in conn.nodes_out:
+                if ok:
                     nn.add(id(n))
+                else:  # a later writer (an in-place batch_norm / prelu / bias on a relu output) can make it negative
+                    nn.discard(id(n))
         for b, a in getattr(self, "aliases", {}).items():  # b = fused relu(a): a holds relu(z) too
             if b in nn:
                 nn.add(id(a))

@@ -169,13 +169,13 @@ _glds_cfg = {"on": os.environ.get("CXXNET_GEMM_GLDS", "1") != "0",
              # op classes routed to it: conv fwd, conv1-style row-gather fwd, conv dgrad, conv wgrad, fc fwd, fc wgrad
              "ops": set(os.environ.get("CXXNET_GLDS_OPS", "cf,cr,cd,cw,fc,fw").split(","))}
 # conv weight-grad ("cw"): on every AlexNet layer together the LDS-DMA form is 0.6% slower than the
-# register-staged split-K kernel (profiles/r14_ab_glds_ops.jsonl), but per layer it wins conv4
-# (0.3% of the step, profiles/r15_ab_cw_layers.jsonl, r15_ab_cw_tiles.jsonl), so the register
+# register-staged split-K kernel (profiles/early-r14_ab_glds_ops.jsonl), but per layer it wins conv4
+# (0.3% of the step, profiles/early-r15_ab_cw_layers.jsonl, early-r15_ab_cw_tiles.jsonl), so the register
 # kernel is a tuning candidate (REG) and the shipped table keeps it for conv2/3/5.  The
 # row-run weight-grad for few-channel convs ("cwr", conv1) is 3% faster as a kernel but its
-# padded-buffer zero + fold-back pass makes the whole step 1.1% slower (profiles/r15_ab_cwr.jsonl)
+# padded-buffer zero + fold-back pass makes the whole step 1.1% slower (profiles/early-r15_ab_cwr.jsonl)
 # Autotuning candidates: the 2-stage tiles that run 2-5 blocks per CU measured best on every
-# AlexNet shape (profiles/r14_glds_tiles.jsonl); 2 covers the fc weight-gradients; the 8-wave
+# AlexNet shape (profiles/early-r14_glds_tiles.jsonl); 2 covers the fc weight-gradients; the 8-wave
 # 128x256 / 64x256 tiles and the pipelined variants (30-41) win conv2/conv3 forward, fc6 forward
 # and several VGG shapes (profiles/r2_sweep_tiles.jsonl).
 GLDS_CANDS = (1, 7, 10, 15, 2, 17, 21, 25, 30, 31, 34, 37, 38, 39, 40, 41, 72, 75, 76, 77, 78, 79,
@@ -188,7 +188,7 @@ _HALO_DB = os.environ.get("CXXNET_HALO_DB", "1") != "0"
 _CW_TUNE = os.environ.get("CXXNET_CW_TUNE", "0") == "1"
 # Pseudo-tile: the register-staged kernel (gemm_mfma.hip) with its heuristic tile.  A candidate
 # for conv forward / data-grad / weight-grad, where it still wins some shapes (conv2 forward on
-# AlexNet timed alone: 172 vs 186 us, profiles/r15_glds_8wave.jsonl "old_us").
+# AlexNet timed alone: 172 vs 186 us, profiles/early-r15_glds_8wave.jsonl "old_us").
 REG = 99
 # Tuning database: {signature: tile}.  A shipped table for gfx950 (written by
 # benchmarks/tune_db.py on an MI355X) makes tile choice deterministic across runs and
@@ -457,7 +457,7 @@ def _gemm_bf16_out(a, b, amode, bmode, out, ldc, *, bias=None, relu=False, mask_
     fill the chip (the FC layers at batch 256: 64 tiles of 128x128 for fc6).  drop: see
     _finalize; returns True when the dropout was applied (only the split-K path fuses it)."""
     # fc data-grad (A MN-major) stays on the register-staged kernel: its LDS-DMA form measured
-    # slower on AlexNet's fc6-8 (profiles/r14_glds_tiles.jsonl)
+    # slower on AlexNet's fc6-8 (profiles/early-r14_glds_tiles.jsonl)
     if bmode == DIRECT_K and amode == DIRECT_K and alpha == 1.0 and _use("fc"):
         r = _fc_glds(a, b, GL_K, out, ldc, bias, relu, mask_relu, drop)
         if r is not None:
@@ -645,6 +645,8 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
             out = out.clamp_min(0)
         y.copy_(out.permute(0, 2, 3, 1))
         return
+    if conv_direct_forward(x, w, bias, y, g, relu=relu):
+        return
     cg = g.cg_in
     va = 8 if cg % 8 == 0 else 4
     if cg % va and not rowrun_ok(g):
@@ -775,6 +777,8 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False, wt_
     if not wt_ready:
         native.check(native.kernels().cxn_conv_weight_flip(w.data_ptr(), wt_buf.data_ptr(), g.groups, cg_out, g.KH,
                                                            g.KW, cg_in, _stream()), "conv_weight_flip")
+    if conv_direct_data(dy, wt_buf, dx, g, mask_relu=mask_relu, dbias=dbias):
+        return dbias is not None
     kd = g.KH * g.KW * cg_out
     A = _op(wt_buf, cg_in * kd, kd, cg_in, kd)
     B = _op(dy, cg_out, 0, g.N * g.H * g.W, kd, H=g.Ho, W=g.Wo, C=_pix(dy), Ho=g.H, Wo=g.W, KH=g.KH,
@@ -836,6 +840,69 @@ def conv_backward_data_add(dy, w, dx, add, g: ConvGeom, wt_buf, mask_relu=False,
         return False
     native.check(rc, "gemm_glds_add")
     LAST_GLDS[0] = t
+    return True
+
+
+# Direct small-map forward / data gradient (conv_direct.hip: gap-slot layout, taps as constant
+# LDS offsets, persistent blocks).  "auto" / "1": wherever it serves the shape; "0": off (the
+# implicit GEMMs run).
+_CD = os.environ.get("CXXNET_CONV_DIRECT", "auto")
+_cd_ws = {}
+
+
+def _cd_workspace(n, device):
+    buf = _cd_ws.get(str(device))
+    if buf is None or buf.numel() < n:
+        from .mode import retire
+        retire(buf)
+        buf = _cd_ws[str(device)] = torch.empty(max(n, 1 << 16), dtype=torch.float32, device=device)
+    return buf
+
+
+def _cd_ok(g: ConvGeom, *ts) -> bool:
+    if _CD == "0" or _glds_cfg["tile"] >= 0:  # (a forced LDS-DMA tile id means a test / probe wants that kernel)
+        return False
+    if g.stride != 1 or g.Ho != g.H or g.Wo != g.W or g.KH != g.KW or g.pad_y != (g.KH - 1) // 2 or g.pad_x != g.pad_y:
+        return False
+    return all(t.stride(-1) == 1 and (t.is_contiguous() or t.stride(-2) * t.shape[-2] == t.stride(-3))
+               for t in ts)
+
+
+def conv_direct_forward(x, w, bias, y, g: ConvGeom, relu=False) -> bool:
+    """y = conv(x, w) + bias (relu optional) on the direct small-map kernel; False when it does
+    not serve the shape."""
+    if not _cd_ok(g, x, y):
+        return False
+    rc = int(native.kernels().cxn_conv_direct(
+        x.data_ptr(), _pix(x), w.data_ptr(), bias.data_ptr() if bias is not None else None, y.data_ptr(), _pix(y),
+        None, 0, None, g.N, g.H, g.W, g.cg_in, g.cg_out, g.groups, g.KH, int(relu), 0, _stream()))
+    if rc == -1:
+        return False
+    native.check(rc, "conv_direct")
+    return True
+
+
+def conv_direct_data(dy, wt, dx, g: ConvGeom, mask_relu=False, dbias=None) -> bool:
+    """dx = conv_transpose(dy, w) (wt: the flipped weights), relu'-masked when mask_relu, and
+    dbias += the column sums of the stored dx; False when the kernel does not serve the shape."""
+    if not _cd_ok(g, dy, dx):
+        return False
+    k = native.kernels()
+    args = (g.N, g.H, g.W, g.cg_out, g.cg_in, g.groups, g.KH, int(mask_relu))
+    ws, n = None, 0
+    if dbias is not None:
+        need = int(k.cxn_conv_direct(None, _pix(dy), None, None, None, _pix(dx), None, 0, None, *args, 2, None))
+        if need <= 0:
+            return False
+        ws = _cd_workspace(need, dx.device)
+        n = ws.numel()
+    rc = int(k.cxn_conv_direct(dy.data_ptr(), _pix(dy), wt.data_ptr(), None, dx.data_ptr(), _pix(dx),
+                               ws.data_ptr() if ws is not None else None, n,
+                               dbias.data_ptr() if dbias is not None else None, *args,
+                               2 if dbias is not None else 1, _stream()))
+    if rc == -1:
+        return False
+    native.check(rc, "conv_direct")
     return True
 
 

@@ -54,6 +54,35 @@ input_shape = 3,12,12
     assert [p.input_nonneg for p in pools] == [False, True]
 
 
+def test_in_place_writer_after_relu_clears_the_mark():
+    """relu -> in-place batch_norm (a self-loop that can make values negative) -> max_pool: the
+    pool must take the float-compare path."""
+    from cxxnet_amd import native
+    conf = """
+netconfig=start
+layer[0->1] = conv:c1
+  kernel_size = 3
+  nchannel = 8
+layer[1->2] = relu
+layer[2->2] = batch_norm
+layer[2->3] = max_pooling
+  kernel_size = 2
+  stride = 2
+layer[3->4] = flatten
+layer[4->5] = fullc:f
+  nhidden = 4
+layer[5->5] = softmax
+netconfig=end
+input_shape = 3,12,12
+"""
+    tr = NetTrainer()
+    for k, v in list(native.rt().parse_config(conf)) + [("batch_size", "2"), ("dev", "cpu")]:
+        tr.set_param(k, v)
+    tr.init_model()
+    pools = [c.layer for c in tr.net.connections if type(c.layer).__name__ == "PoolingLayer"]
+    assert [p.input_nonneg for p in pools] == [False]
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("K,S,P,H", [(3, 2, 0, 27), (3, 1, 1, 14), (2, 2, 0, 28), (3, 2, 0, 13)])
 def test_integer_key_pool_matches_float_compare(K, S, P, H):
