@@ -45,7 +45,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--ops", default=",".join(OPS))
-    ap.add_argument("--paths", default="gemm,direct")
+    ap.add_argument("--paths", default="table,200,201,202",
+                    help="tile ids to force (200-202: the direct kernel's schedules) or 'table' (the shipped pick)")
     ap.add_argument("--dirs", default="fwd,dgrad")
     a = ap.parse_args()
     dev = "cuda"
@@ -73,10 +74,10 @@ def main():
                 if op not in a.dirs.split(","):
                     continue
                 for path in a.paths.split(","):
-                    gemm._CD = "0" if path == "gemm" else "auto"
+                    gemm._glds_cfg["tile"] = -1 if path == "table" else int(path)
                     t = _time(fn, a.iters)
                     res.setdefault((name, op, path), []).append(t)
-    gemm._CD = "auto"
+    gemm._glds_cfg["tile"] = -1
     for (name, op, path), ts in res.items():
         H, C, Cout, K, pad, G = OPS[name]
         flop = 2.0 * a.batch * H * H * Cout * K * K * (C // G)

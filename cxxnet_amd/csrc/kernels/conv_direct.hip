@@ -101,13 +101,21 @@ struct CdArgs {
 // EPI 0: + bias, optional relu (a.relu).  EPI 1: data gradient; with a.relu, y *= (y_old > 0)
 // (y holds relu(z) on entry).  EPI 2: EPI 1 plus the column sums of the stored values as partial
 // rows.
-template <int H, int W, int KS, int IPB, int NF, int NW, int EPI, int DBG = 0>
-__global__ void __launch_bounds__(64 * NW, 1) conv_direct(CdArgs a) {
+// SB = 0: persistent blocks (one per CU), two LDS stage buffers, the next stage's DMAs under the
+// current stage.  SB = 1: one block per item, one stage buffer (64 KiB), two blocks per CU: the
+// co-resident block's MFMAs cover a block's DMA waits, barriers, first-tap reads and epilogue.
+// NL > 0: NL more waves per block only issue the LDS-DMAs (an LDS-DMA costs its issuing wave
+// ~60-185 cycles of issue; on the MFMA waves that was ~17 % of the forward), the NW MFMA waves
+// only compute; both kinds meet at the one barrier per stage.
+template <int H, int W, int KS, int IPB, int NF, int NW, int EPI, int DBG = 0, bool SB = false, int NL = 0>
+__global__ void __launch_bounds__(64 * (NW + NL), (SB || NW + NL == 8) ? 2 : 1) conv_direct(CdArgs a) {
   using G = Cd<H, W, KS, IPB, NF, NW>;
   constexpr int T = G::T, WMF = G::WMF, XB = G::XB, BUF = G::BUF;
-  constexpr int NDX = G::NDX, ND = G::ND, NDPW = G::NDPW, PW = G::PW, IMG = G::IMG, HW = H * W;
-  static_assert(NDX % NW == 0, "x pieces per wave");
-  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+  constexpr int NDX = G::NDX, ND = G::ND, PW = G::PW, IMG = G::IMG, HW = H * W;
+  constexpr int DW = NL > 0 ? NL : NW;  // waves that issue DMAs
+  constexpr int NDPW = (ND + DW - 1) / DW;
+  static_assert(NDX % DW == 0, "x pieces per wave");
+  __shared__ __attribute__((aligned(1024))) char smem[SB ? BUF : 2 * BUF];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -115,15 +123,16 @@ __global__ void __launch_bounds__(64 * NW, 1) conv_direct(CdArgs a) {
       __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void *)smem)));
   const int nb = static_cast<int>(gridDim.x);
   const int L = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
-  const int nmine = L < a.nitems ? (a.nitems - L + nb - 1) / nb : 0;
+  const int nmine = SB ? 1 : (L < a.nitems ? (a.nitems - L + nb - 1) / nb : 0);
   const int K = nmine * a.nst;  // stages of this block
   if (K == 0) return;
 
+  const int dwave = NL > 0 ? wave - NW : wave;  // DMA wave index
   // ---- per-lane DMA source offsets (bytes from the stage's descriptor base), fixed for the kernel
   uint32_t voff[NDPW];
 #pragma unroll
   for (int i = 0; i < NDPW; ++i) {
-    const int q = wave + NW * i;
+    const int q = dwave + DW * i;
     uint32_t v = OOB;
     if (q < NDX) {  // slots 16 q .. 16 q + 15, lane (plane lane >> 4, slot lane & 15)
       const int pix = cd_pixel<H, W, KS, IPB>(16 * q + (lane & 15) - G::XLEAD);
@@ -163,15 +172,15 @@ __global__ void __launch_bounds__(64 * NW, 1) conv_direct(CdArgs a) {
     const long co = static_cast<long>(g) * a.Cog + cob * 16 * NF;
     rw = make_rsrc(a.w + co * T * a.Cg + 32 * s, static_cast<uint32_t>((16L * NF * T * a.Cg - 32 * s) * 2));
   };
-  // DMA i of this wave is piece q = wave + NW i: x pieces for i < NDX / NW (NDX is a multiple of
-  // NW), weight pieces after them (only the last i may run past ND, for some waves)
+  // DMA i of this wave is piece q = dwave + DW i: x pieces for i < NDX / DW (NDX is a multiple of
+  // DW), weight pieces after them (only the last i may run past ND, for some waves)
   auto issue_one = [&](auto ic, int b) __attribute__((always_inline)) {
     constexpr int i = decltype(ic)::value;
-    const int q = wave + NW * i;
+    const int q = dwave + DW * i;
     const uint32_t dst = lds0 + static_cast<uint32_t>(b * BUF + q * 1024);
-    if constexpr (i < NDX / NW) {
+    if constexpr (i < NDX / DW) {
       if constexpr (!(DBG & 1)) dma16c(rx, dst, voff[i]);
-    } else if constexpr (NW * (i + 1) <= ND) {
+    } else if constexpr (DW * (i + 1) <= ND) {
       if constexpr (!(DBG & 2)) dma16c(rw, dst, voff[i]);
     } else {
       if constexpr (!(DBG & 2)) if (q < ND) dma16c(rw, dst, voff[i]);
@@ -294,20 +303,35 @@ __global__ void __launch_bounds__(64 * NW, 1) conv_direct(CdArgs a) {
   };
 
   // prologue: the first stage
-  prep(0);
-  static_for<NDPW>([&](auto ic) {
-    constexpr int i = decltype(ic)::value;
-    const int q = wave + NW * i;
-    if (q < ND) dma16c(i < NDX / NW ? rx : rw, lds0 + static_cast<uint32_t>(q * 1024), voff[i]);
-  });
+  if (NL == 0 || wave >= NW) {
+    prep(0);
+    static_for<NDPW>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      const int q = dwave + DW * i;
+      if (q < ND) dma16c(i < NDX / DW ? rx : rw, lds0 + static_cast<uint32_t>(q * 1024), voff[i]);
+    });
+  }
   wait_vmcnt<0>();
   block_barrier();
+  if constexpr (NL > 0) {
+    if (wave >= NW) {  // loader waves: stage k + 1's DMAs during stage k, one barrier per stage
+      for (int k = 0; k < K; ++k) {
+        if (k + 1 < K) {
+          prep(k + 1);
+          static_for<NDPW>([&](auto ic) { issue_one(ic, (k + 1) & 1); });
+        }
+        wait_vmcnt<0>();
+        block_barrier();
+      }
+      return;
+    }
+  }
 
   // Per stage: tap t's fragments were read one tap ahead (register sets alternate by tap
   // parity); the reads of tap t + 1 are issued before tap t's MFMAs, and sched_barriers keep the
   // two groups apart, so each tap's 24 MFMAs cover the next tap's LDS latency.  The next stage's
   // DMAs are issued over the first taps and land under the rest of the stage.
-  constexpr int DMA_TAPS = T < 4 ? T : 4;
+  constexpr int DMA_TAPS = (DBG & 64) ? 1 : (DBG & 128) ? 2 : (DBG & 256) ? 6 : (T < 4 ? T : 4);
   bf16x8 xf[2][WMF], wf[2][NF];
   // fragment r of tap t into register set st: r < NF the weight fragment r (every MFMA of the
   // next tap's first row needs them), else the x fragment of M fragment r - NF, in MFMA order
@@ -323,8 +347,8 @@ __global__ void __launch_bounds__(64 * NW, 1) conv_direct(CdArgs a) {
   };
   constexpr int NR = WMF + NF;  // fragment reads per tap
   auto stage = [&](int k) __attribute__((always_inline)) {
-    const int b = k & 1;
-    prep(k + 1);
+    const int b = SB ? 0 : (k & 1);
+    if constexpr (!SB && NL == 0) prep(k + 1);
     const char *buf = smem + b * BUF;
     static_for<NR>([&](auto rc) { read_one(buf, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, rc); });
     static_for<T>([&](auto tc) {
@@ -350,11 +374,20 @@ __global__ void __launch_bounds__(64 * NW, 1) conv_direct(CdArgs a) {
         }
       });
       __builtin_amdgcn_sched_barrier(0);
-      static_for<NDPW>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        if constexpr (i * DMA_TAPS / NDPW == t) issue_one(ic, b ^ 1);
-      });
+      if constexpr (!SB && NL == 0) {
+        static_for<NDPW>([&](auto ic) {
+          constexpr int i = decltype(ic)::value;
+          if constexpr (i * DMA_TAPS / NDPW == t) issue_one(ic, b ^ 1);
+        });
+      }
     });
+    if constexpr (SB) {  // reload the one buffer once every wave has read it
+      if (k + 1 < K) {
+        block_barrier();
+        prep(k + 1);
+        static_for<NDPW>([&](auto ic) { issue_one(ic, 0); });
+      }
+    }
     if constexpr (!(DBG & 16)) {
       wait_vmcnt<0>();
       asm volatile("" ::: "memory");
@@ -378,12 +411,13 @@ __global__ void __launch_bounds__(64 * NW, 1) conv_direct(CdArgs a) {
     for (int i = 0; i < WMF; ++i)
 #pragma unroll
       for (int f = 0; f < NF; ++f) asm volatile("" : "+a"(acc[i][f]));
-    epilogue(k - 1);
+    if constexpr (!(DBG & 32)) epilogue(k - 1);
+    else if (a.N < 0) epilogue(k - 1);  // (never: keeps the accumulators live)
   }
 }
 
 template <int H, int W, int KS, int IPB, int NF, int NW>
-int launch_cd(CdArgs a, int epi, float *db, hipStream_t s) {
+int launch_cd(CdArgs a, int epi, int variant, float *db, hipStream_t s) {
   using G = Cd<H, W, KS, IPB, NF, NW>;
   (void)sizeof(G);
   if (a.Cog % (16 * NF) || a.Cg % 32) return -1;
@@ -391,23 +425,42 @@ int launch_cd(CdArgs a, int epi, float *db, hipStream_t s) {
   a.ncob = a.Cog / (16 * NF);
   a.nitems = nig * a.groups * a.ncob;
   a.nst = a.Cg / 32;
-  const int grid = a.nitems < 256 ? a.nitems : 256;
+  const int sb = variant == 1;
   static const int dbg = getenv("CXN_CD_DBG") ? atoi(getenv("CXN_CD_DBG")) : 0;
-  if (epi == 0 && dbg) {
+  const int grid = a.nitems < 256 ? a.nitems : 256;
+  const dim3 blk(64 * NW);
+  if (variant == 2 && NW == 4) {
+    const dim3 b8(64 * (NW + 4));
+    if (epi == 0) CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 0, false, 4>), dim3(grid), b8, 0, s, a);
+    else if (epi == 1) CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 1, 0, false, 4>), dim3(grid), b8, 0, s, a);
+    else CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 2, 0, false, 4>), dim3(grid), b8, 0, s, a);
+  } else if (sb && NW == 4) {
+    const dim3 g1(a.nitems);
+    if (epi == 0) CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 0, true>), g1, blk, 0, s, a);
+    else if (epi == 1) CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 1, 0, true>), g1, blk, 0, s, a);
+    else CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 2, 0, true>), g1, blk, 0, s, a);
+  } else if (epi == 0 && dbg) {
     switch (dbg) {
-      case 1: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 1>), dim3(grid), dim3(64 * NW), 0, s, a); break;
-      case 2: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 2>), dim3(grid), dim3(64 * NW), 0, s, a); break;
-      case 3: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 3>), dim3(grid), dim3(64 * NW), 0, s, a); break;
-      case 11: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 11>), dim3(grid), dim3(64 * NW), 0, s, a); break;
-      case 19: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 19>), dim3(grid), dim3(64 * NW), 0, s, a); break;
-      default: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 27>), dim3(grid), dim3(64 * NW), 0, s, a); break;
+      case 1: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 1>), dim3(grid), blk, 0, s, a); break;
+      case 2: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 2>), dim3(grid), blk, 0, s, a); break;
+      case 3: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 3>), dim3(grid), blk, 0, s, a); break;
+      case 11: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 11>), dim3(grid), blk, 0, s, a); break;
+      case 19: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 19>), dim3(grid), blk, 0, s, a); break;
+      case 64: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 64>), dim3(grid), blk, 0, s, a); break;
+      case 128: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 128>), dim3(grid), blk, 0, s, a); break;
+      case 256: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 256>), dim3(grid), blk, 0, s, a); break;
+      case 27: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 27>), dim3(grid), blk, 0, s, a); break;
+      case 35: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 35>), dim3(grid), blk, 0, s, a); break;
+      default: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 59>), dim3(grid), blk, 0, s, a); break;
     }
   } else if (epi == 0) {
-    CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0>), dim3(grid), dim3(64 * NW), 0, s, a);
+    CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0>), dim3(grid), blk, 0, s, a);
   } else if (epi == 1) {
-    CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 1>), dim3(grid), dim3(64 * NW), 0, s, a);
+    CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 1>), dim3(grid), blk, 0, s, a);
   } else {
-    CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 2>), dim3(grid), dim3(64 * NW), 0, s, a);
+    CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 2>), dim3(grid), blk, 0, s, a);
+  }
+  if (epi == 2) {
     GEpi E{};
     E.dbias = a.dbp;
     E.part_ld = a.dbp_ld;
@@ -421,13 +474,15 @@ int launch_cd(CdArgs a, int epi, float *db, hipStream_t s) {
 
 // Served: stride 1, "same" padding, K = 3 on 13 x 13 maps; Cg (input channels per group) a
 // multiple of 32, Cog (output channels per group) a multiple of 64, pixel strides multiples of 8.
+// variant: 0 persistent blocks with two stage buffers, 1 one block per item with one stage
+// buffer (two blocks per CU), 2 as 0 with four more waves per block that only issue the LDS-DMAs.
 // epi 0: y = conv(x, w) + bias (relu optional).  epi 1: data gradient (x = dy, w = flipped
 // weights), with relu = 1 y *= relu'(y_old).  epi 2: epi 1 and db += column sums of the stored y (dbp: a
 // workspace of at least dbp_elems floats, db the fp32 bias gradient).  dbp == nullptr with
 // epi 2 asks for the workspace size (floats).  Returns -1 when the shape is not served.
 CXN_API long cxn_conv_direct(const void *x, int ldx, const void *w, const float *bias, void *y, int ldy, float *dbp,
                              long dbp_elems, float *db, int N, int H, int W, int Cg, int Cog, int groups, int KS,
-                             int relu, int epi, void *stream) {
+                             int relu, int epi, int variant, void *stream) {
   if (KS != 3 || H != 13 || W != 13) return -1;
   if (Cg % 32 || Cog % 64 || ldx % 8 || ldy % 8 || groups < 1 || ldx < groups * Cg || ldy < groups * Cog) return -1;
   if (static_cast<long>(N) * H * W * (ldx > ldy ? ldx : ldy) >= (1L << 30)) return -1;
@@ -450,8 +505,8 @@ CXN_API long cxn_conv_direct(const void *x, int ldx, const void *w, const float 
   a.relu = relu;
   a.dbp_ld = groups * Cog;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  static const int nw = getenv("CXN_CD_NW") ? atoi(getenv("CXN_CD_NW")) : 4;
-  const int rc = nw == 8 ? launch_cd<13, 13, 3, IPB, 4, 8>(a, epi, db, s) : launch_cd<13, 13, 3, IPB, 4, 4>(a, epi, db, s);
+  if (variant < 0 || variant > 2) return -1;
+  const int rc = launch_cd<13, 13, 3, IPB, 4, 4>(a, epi, variant, db, s);
   if (rc != 0) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

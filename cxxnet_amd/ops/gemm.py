@@ -645,8 +645,6 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
             out = out.clamp_min(0)
         y.copy_(out.permute(0, 2, 3, 1))
         return
-    if conv_direct_forward(x, w, bias, y, g, relu=relu):
-        return
     cg = g.cg_in
     va = 8 if cg % 8 == 0 else 4
     if cg % va and not rowrun_ok(g):
@@ -666,10 +664,16 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
         def run(t, o):
             if t == REG:
                 return reg(o)
+            if t in DIRECT_TILES:
+                return _CD != "0" and conv_direct_forward(x, w, bias, o, g, relu=relu, variant=DIRECT_TILES[t])
             return _glds(A, B, GL_K, GL_KG, o, g.cg_out, _pix(o), bias=bias, bias_gstride=g.cg_out, relu=relu,
                          groups=g.groups, tile=t)
         key = ("cf", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
-        if run(_tuned_tile(key, run, y, lambda: _pick_glds(A.rows, B.rows, g.groups), extra=(REG,)), y):
+        extra = (REG,) + (tuple(DIRECT_TILES) if _cd_serves(g, x, y) else ())
+        t = _tuned_tile(key, run, y, lambda: _pick_glds(A.rows, B.rows, g.groups), extra=extra)
+        if run(t, y):
+            return
+        if t in DIRECT_TILES and run(_pick_glds(A.rows, B.rows, g.groups), y):  # (direct kernel switched off)
             return
     if va != 8 and rowrun_ok(g) and (_use("cr") or g.C % 4):
         # few input channels (conv1: 11x11 taps of 4 channels): each kernel row's KW*C
@@ -777,8 +781,6 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False, wt_
     if not wt_ready:
         native.check(native.kernels().cxn_conv_weight_flip(w.data_ptr(), wt_buf.data_ptr(), g.groups, cg_out, g.KH,
                                                            g.KW, cg_in, _stream()), "conv_weight_flip")
-    if conv_direct_data(dy, wt_buf, dx, g, mask_relu=mask_relu, dbias=dbias):
-        return dbias is not None
     kd = g.KH * g.KW * cg_out
     A = _op(wt_buf, cg_in * kd, kd, cg_in, kd)
     B = _op(dy, cg_out, 0, g.N * g.H * g.W, kd, H=g.Ho, W=g.Wo, C=_pix(dy), Ho=g.H, Wo=g.W, KH=g.KH,
@@ -789,12 +791,23 @@ def conv_backward_data(dy, w, dx, g: ConvGeom, wt_buf=None, mask_relu=False, wt_
               tile=tile)
         return True
     if g.stride == 1 and _use("cd"):
+        dg = ConvGeom(g.N, g.H, g.W, g.Cout, g.H, g.W, g.C, g.KH, g.KW, 1, g.pad_y, g.pad_x, g.groups)
+
         def run(t, o):
             if t == REG:
                 return reg(o)
+            if t in DIRECT_TILES:
+                return _CD != "0" and conv_direct_data(dy, wt_buf, o, g, mask_relu=mask_relu,
+                                                       variant=DIRECT_TILES[t])
             return _glds(A, B, GL_K, GL_KG, o, cg_in, _pix(o), groups=g.groups, mask_relu=mask_relu, tile=t)
         key = ("cd", g.N, g.H, g.W, g.C, g.Cout, g.KH, g.KW, g.stride, g.pad_y, g.pad_x, g.groups)
-        t = _tuned_tile(key, run, dx, lambda: _pick_glds(A.rows, B.rows, g.groups), extra=(REG,))
+        extra = (REG,) + (tuple(DIRECT_TILES) if _cd_serves(dg, dy, dx) else ())
+        t = _tuned_tile(key, run, dx, lambda: _pick_glds(A.rows, B.rows, g.groups), extra=extra)
+        if t in DIRECT_TILES and _CD != "0":
+            db = dbias if dbias is not None and not deterministic() else None
+            if conv_direct_data(dy, wt_buf, dx, g, mask_relu=mask_relu, dbias=db, variant=DIRECT_TILES[t]):
+                return db is not None
+            t = _pick_glds(A.rows, B.rows, g.groups)
         if dbias is not None and t != REG and (t not in (130, 131) or _HALO_DB):
             from .nn import _workspace
             ws = _workspace((-(-B.rows // 16) + 8) * g.C, dx.device)  # >= tiles_j * waves_j rows
@@ -848,6 +861,11 @@ def conv_backward_data_add(dy, w, dx, add, g: ConvGeom, wt_buf, mask_relu=False,
 # implicit GEMMs run).
 _CD = os.environ.get("CXXNET_CONV_DIRECT", "auto")
 _cd_ws = {}
+# Pseudo-tiles of the tile table for the direct kernel's schedules (cxn_conv_direct variant):
+# 200 persistent blocks with two stage buffers, 201 one block per item (two per CU), 202 as 200
+# with four LDS-DMA loader waves per block.  Tuning candidates of the "cf" / "cd" signatures it
+# serves (in-step picks: profiles/r6_step_tune_direct.jsonl).
+DIRECT_TILES = {200: 0, 201: 1, 202: 2}
 
 
 def _cd_workspace(n, device):
@@ -860,29 +878,36 @@ def _cd_workspace(n, device):
 
 
 def _cd_ok(g: ConvGeom, *ts) -> bool:
-    if _CD == "0" or _glds_cfg["tile"] >= 0:  # (a forced LDS-DMA tile id means a test / probe wants that kernel)
-        return False
+    if _CD == "0" or (_glds_cfg["tile"] >= 0 and _glds_cfg["tile"] not in DIRECT_TILES):
+        return False  # (a forced LDS-DMA tile id means a test / probe wants that kernel)
     if g.stride != 1 or g.Ho != g.H or g.Wo != g.W or g.KH != g.KW or g.pad_y != (g.KH - 1) // 2 or g.pad_x != g.pad_y:
         return False
     return all(t.stride(-1) == 1 and (t.is_contiguous() or t.stride(-2) * t.shape[-2] == t.stride(-3))
                for t in ts)
 
 
-def conv_direct_forward(x, w, bias, y, g: ConvGeom, relu=False) -> bool:
+def _cd_serves(g: ConvGeom, *ts) -> bool:
+    """The direct kernel's shape rule (cxn_conv_direct), without launching anything."""
+    if not _cd_ok(g, *ts):
+        return False
+    return g.KH == 3 and g.H == 13 and g.W == 13 and g.cg_in % 32 == 0 and g.cg_out % 64 == 0
+
+
+def conv_direct_forward(x, w, bias, y, g: ConvGeom, relu=False, variant=0) -> bool:
     """y = conv(x, w) + bias (relu optional) on the direct small-map kernel; False when it does
     not serve the shape."""
     if not _cd_ok(g, x, y):
         return False
     rc = int(native.kernels().cxn_conv_direct(
         x.data_ptr(), _pix(x), w.data_ptr(), bias.data_ptr() if bias is not None else None, y.data_ptr(), _pix(y),
-        None, 0, None, g.N, g.H, g.W, g.cg_in, g.cg_out, g.groups, g.KH, int(relu), 0, _stream()))
+        None, 0, None, g.N, g.H, g.W, g.cg_in, g.cg_out, g.groups, g.KH, int(relu), 0, int(variant), _stream()))
     if rc == -1:
         return False
     native.check(rc, "conv_direct")
     return True
 
 
-def conv_direct_data(dy, wt, dx, g: ConvGeom, mask_relu=False, dbias=None) -> bool:
+def conv_direct_data(dy, wt, dx, g: ConvGeom, mask_relu=False, dbias=None, variant=0) -> bool:
     """dx = conv_transpose(dy, w) (wt: the flipped weights), relu'-masked when mask_relu, and
     dbias += the column sums of the stored dx; False when the kernel does not serve the shape."""
     if not _cd_ok(g, dy, dx):
@@ -891,7 +916,7 @@ def conv_direct_data(dy, wt, dx, g: ConvGeom, mask_relu=False, dbias=None) -> bo
     args = (g.N, g.H, g.W, g.cg_out, g.cg_in, g.groups, g.KH, int(mask_relu))
     ws, n = None, 0
     if dbias is not None:
-        need = int(k.cxn_conv_direct(None, _pix(dy), None, None, None, _pix(dx), None, 0, None, *args, 2, None))
+        need = int(k.cxn_conv_direct(None, _pix(dy), None, None, None, _pix(dx), None, 0, None, *args, 2, 0, None))
         if need <= 0:
             return False
         ws = _cd_workspace(need, dx.device)
@@ -899,7 +924,7 @@ def conv_direct_data(dy, wt, dx, g: ConvGeom, mask_relu=False, dbias=None) -> bo
     rc = int(k.cxn_conv_direct(dy.data_ptr(), _pix(dy), wt.data_ptr(), None, dx.data_ptr(), _pix(dx),
                                ws.data_ptr() if ws is not None else None, n,
                                dbias.data_ptr() if dbias is not None else None, *args,
-                               2 if dbias is not None else 1, _stream()))
+                               2 if dbias is not None else 1, int(variant), _stream()))
     if rc == -1:
         return False
     native.check(rc, "conv_direct")

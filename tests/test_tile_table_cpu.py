@@ -16,7 +16,9 @@ def test_every_entry_names_a_known_tile():
         op = key.split("|")[0]
         if op == "cws":  # register weight-grad: tile * 100000 + K-split slices
             ok = tile // 100000 in G.TILES and tile % 100000 >= 1
-        elif op in ("cf", "cd", "cw", "cfs"):
+        elif op in ("cf", "cd"):  # also the direct small-map kernel's schedules (conv_direct.hip)
+            ok = tile in G.GLDS_TILES or tile == G.REG or tile in G.DIRECT_TILES
+        elif op in ("cw", "cfs"):
             ok = tile in G.GLDS_TILES or tile == G.REG
         else:  # cr, cwr, fc, fw, fws: LDS-DMA tiles only
             ok = tile in G.GLDS_TILES
@@ -60,6 +62,7 @@ def test_every_compiled_tile_is_used():
     used = {t for k, t in _table().items() if k.split("|")[0] != "cws"}
     used |= {1, 7, 10, 15}  # _pick_glds defaults
     used |= {141, 142}  # forced patch widths of the 140 kernel (same template instances)
+    used |= {82}  # 256x192 wave-quantisation tile: a step_tune candidate (AlexNet conv3 data-grad moved to the direct kernel)
     unused = sorted(_compiled_tiles() - used)
     assert not unused, unused
 
