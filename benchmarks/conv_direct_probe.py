@@ -18,6 +18,7 @@ from cxxnet_amd.ops.gemm import ConvGeom  # noqa: E402
 
 # name -> (H, C, Cout, K, pad, groups)
 OPS = {
+    "conv2": (27, 96, 256, 5, 2, 2),
     "conv3": (13, 256, 384, 3, 1, 1),
     "conv4": (13, 384, 384, 3, 1, 2),
     "conv5": (13, 384, 256, 3, 1, 2),
@@ -44,7 +45,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--ops", default=",".join(OPS))
+    ap.add_argument("--ops", default="conv3,conv4,conv5")
     ap.add_argument("--paths", default="table,200,201,202",
                     help="tile ids to force (200-202: the direct kernel's schedules) or 'table' (the shipped pick)")
     ap.add_argument("--dirs", default="fwd,dgrad")

@@ -470,10 +470,262 @@ int launch_cd(CdArgs a, int epi, int variant, float *db, hipStream_t s) {
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Paired-tap form for larger maps and kernels (AlexNet conv2: 27 x 27, 5 x 5, 48 input channels
+// per group).  The K loop walks the input channels in stages of 16 and each MFMA's K = 32 holds
+// two (tap, 16 channels) halves: lanes 0-31 read tap 2p, lanes 32-63 tap 2p + 1 (a missing last
+// tap reads zero weights), so a stage is ceil(T / 2) MFMA K-steps and any channel count that is a
+// multiple of 16 is served.  A block item is a band of R output rows of one image (the halo rows
+// above / below come from the same image, rows off the map read zeros) x 16 NF output channels;
+// one block per item and one stage buffer, two blocks per CU (as variant 1 above).
+//   x image: 16-slot groups [plane 0: 16 slots][plane 1: 16 slots] x 16 B (512 B); one 1-KiB
+//     DMA piece fills two groups.  Lane (half h, plane p, l16) of M fragment i under pair q
+//     reads slot s = 16 (mi) + l16 + shift(2q + h): byte 512 (mi + (u >> 4)) + 256 p + 16 (u & 15),
+//     u = l16 + shift -- a per-lane offset per pair, the fragment index an immediate.
+//   weight image (q, f): 1 KiB, lane l's 16 B at 16 l: W[co 16 f + l16][tap 2q + h][8 p ..].
+template <int H, int W, int KS, int R, int NF>
+struct Cp {
+  static constexpr int P = (KS - 1) / 2, T = KS * KS, NPR = (T + 1) / 2, PW = W + P;
+  static constexpr int NB = (H + R - 1) / R;                       // bands per image
+  static constexpr int OS = R * PW;                                // output slots of a full band
+  static constexpr int WMF = ((OS + 15) / 16 + 3) / 4;             // M fragments per wave
+  static constexpr int MS = 64 * WMF;
+  static constexpr int NXS = (MS + (KS - 1) * (PW + 1) + 31) / 32 * 32;
+  static constexpr int NDX = NXS / 32;                             // x DMA pieces
+  static constexpr int XB = NXS * 32;
+  static constexpr int WB = NPR * NF * 1024;
+  static constexpr int BUF = XB + WB;
+  static constexpr int ND = NDX + NPR * NF, NDPW = (ND + 3) / 4;
+  static constexpr int XLEAD = P * PW + P;
+  static_assert(BUF <= 80 * 1024, "two blocks per CU");
+};
+
+template <int H, int W, int KS, int R, int NF, int EPI>
+__global__ void __launch_bounds__(256, 2) conv_direct_pair(CdArgs a) {
+  using G = Cp<H, W, KS, R, NF>;
+  constexpr int T = G::T, NPR = G::NPR, WMF = G::WMF, XB = G::XB, BUF = G::BUF, PW = G::PW, P = G::P;
+  constexpr int NDX = G::NDX, ND = G::ND, NDPW = G::NDPW, HW = H * W;
+  __shared__ __attribute__((aligned(1024))) char smem[BUF];
+  const int lane = threadIdx.x & 63, l16 = lane & 15, hl = lane >> 5, pl = (lane >> 4) & 1;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lds0 =
+      __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void *)smem)));
+  // item = ((n NB + band) groups + g) ncob + cob
+  const int it = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
+  const int cob = it % a.ncob, r1 = it / a.ncob;
+  const int g = r1 % a.groups, r2 = r1 / a.groups;
+  const int band = r2 % G::NB, n = r2 / G::NB;
+  const int r0 = band * R, nr = min(R, H - r0);
+
+  uint32_t voff[NDPW];
+#pragma unroll
+  for (int i = 0; i < NDPW; ++i) {
+    const int q = wave + 4 * i;
+    uint32_t v = OOB;
+    if (q < NDX) {
+      const int lin = 32 * q + 16 * hl + l16 - G::XLEAD;
+      const int vrow = cd_fdiv(lin, PW), col = lin - vrow * PW, row = r0 + vrow;
+      if (row >= 0 && row < H && col < W) v = static_cast<uint32_t>(((row * W + col) * a.ldx + 8 * pl) * 2);
+    } else if (q < ND) {
+      const int qw = q - NDX, pr = qw / NF, f = qw - pr * NF, t = 2 * pr + hl;
+      if (t < T) v = static_cast<uint32_t>((((16 * f + l16) * T + t) * a.Cg + 8 * pl) * 2);
+    }
+    voff[i] = v;
+  }
+  rsrc_t rx, rw;
+  auto prep = [&](int s) __attribute__((always_inline)) {
+    const long cx = static_cast<long>(g) * a.Cg + 16 * s;
+    rx = make_rsrc(a.x + static_cast<long>(n) * HW * a.ldx + cx, static_cast<uint32_t>((static_cast<long>(HW) * a.ldx - cx) * 2));
+    const long co = static_cast<long>(g) * a.Cog + cob * 16 * NF;
+    rw = make_rsrc(a.w + co * T * a.Cg + 16 * s, static_cast<uint32_t>((16L * NF * T * a.Cg - 16 * s) * 2));
+  };
+  auto issue_all = [&]() __attribute__((always_inline)) {
+    static_for<NDPW>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      const int q = wave + 4 * i;
+      const uint32_t dst = lds0 + static_cast<uint32_t>(q * 1024);
+      if (q < NDX) dma16c(rx, dst, voff[i]);
+      else if (q < ND) dma16c(rw, dst, voff[i]);
+    });
+  };
+  auto shift = [](int t) { return (t / KS) * PW + (t % KS); };
+  // per-lane x read offset of pair pr (fragment 0 of this wave)
+  auto xoffp = [&](int pr) __attribute__((always_inline)) {
+    const int t0 = 2 * pr, t1 = 2 * pr + 1 < T ? 2 * pr + 1 : 2 * pr;
+    const int u = l16 + (hl ? shift(t1) : shift(t0));
+    return 512 * (wave * WMF + (u >> 4)) + 256 * pl + 16 * (u & 15);
+  };
+  const int wrd = XB + 16 * lane;
+
+  f32x4 acc[WMF][NF];
+#pragma unroll
+  for (int i = 0; i < WMF; ++i)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+      asm volatile("" : "+a"(acc[i][f]));
+    }
+  bf16x8 xf[2][WMF], wf[2][NF];
+  auto read_one = [&](auto pc, auto sc, auto rc) __attribute__((always_inline)) {
+    constexpr int pr = decltype(pc)::value, st = decltype(sc)::value, r = decltype(rc)::value;
+    if constexpr (r < NF) {
+      wf[st][r] = *reinterpret_cast<const bf16x8 *>(smem + wrd + (pr * NF + r) * 1024);
+    } else {
+      xf[st][r - NF] = *reinterpret_cast<const bf16x8 *>(smem + xoffp(pr) + 512 * (r - NF));
+    }
+  };
+  constexpr int NR = WMF + NF, NM = WMF * NF, RS = NM / NR > 0 ? NM / NR : 1;
+
+  prep(0);
+  issue_all();
+  for (int s = 0; s < a.nst; ++s) {
+    wait_vmcnt<0>();
+    block_barrier();
+    static_for<NR>([&](auto rc) { read_one(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, rc); });
+    static_for<NPR>([&](auto pc) {
+      constexpr int pr = decltype(pc)::value, st = pr & 1;
+      static_for<NM>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        constexpr int i = q / NF, f = q % NF;
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_acc(acc[i][f], wf[st][f], xf[st][i]);
+        if constexpr (pr + 1 < NPR && q % RS == RS - 1 && q / RS < NR) {
+          read_one(std::integral_constant<int, pr + 1>{}, std::integral_constant<int, st ^ 1>{},
+                   std::integral_constant<int, q / RS>{});
+        }
+        if constexpr (pr + 1 < NPR && q == NM - 1 && NM / RS < NR) {
+          static_for<NR - NM / RS>([&](auto rc) {
+            read_one(std::integral_constant<int, pr + 1>{}, std::integral_constant<int, st ^ 1>{},
+                     std::integral_constant<int, NM / RS + decltype(rc)::value>{});
+          });
+        }
+      });
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    if (s + 1 < a.nst) {  // reload the one buffer once every wave has read it
+      block_barrier();
+      prep(s + 1);
+      issue_all();
+    }
+  }
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < WMF; ++i)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) asm volatile("" : "+a"(acc[i][f]));
+
+  // ---- epilogue (as conv_direct): 4 consecutive output channels of one slot per lane
+  const int c0 = g * a.Cog + cob * 16 * NF + 4 * (lane >> 4);
+  int po[WMF];
+  bool ok[WMF];
+#pragma unroll
+  for (int i = 0; i < WMF; ++i) {
+    const int o = 16 * (wave * WMF + i) + l16;
+    const int r = o / PW, c = o - r * PW;
+    ok[i] = r < nr && c < W;
+    po[i] = ((n * H + r0 + r) * W + c) * a.ldy + c0;
+  }
+  if constexpr (EPI == 0) {
+    f32x4 bv[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+      bv[f] = a.bias ? f32x4{a.bias[c0 + 16 * f], a.bias[c0 + 16 * f + 1], a.bias[c0 + 16 * f + 2], a.bias[c0 + 16 * f + 3]}
+                     : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < WMF; ++i)
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        f32x4 v = acc[i][f] + bv[f];
+        if (a.relu) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+        }
+        if (ok[i]) *reinterpret_cast<uint2 *>(a.y + po[i] + 16 * f) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
+  } else {
+    f32x4 sum[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) sum[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int HM = (WMF + 1) / 2;
+#pragma unroll
+    for (int h = 0; h < WMF; h += HM) {
+      uint2 old[HM][NF];
+#pragma unroll
+      for (int i = 0; i < HM; ++i)
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+          old[i][f] = (a.relu && h + i < WMF && ok[h + i]) ? *reinterpret_cast<const uint2 *>(a.y + po[h + i] + 16 * f)
+                                                          : make_uint2(0x3f803f80u, 0x3f803f80u);
+#pragma unroll
+      for (int i = 0; i < HM; ++i) {
+        if (h + i >= WMF) continue;
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          const uint2 o2 = old[i][f];
+          const bool m0 = static_cast<short>(o2.x & 0xffffu) > 0, m1 = static_cast<short>(o2.x >> 16) > 0;
+          const bool m2 = static_cast<short>(o2.y & 0xffffu) > 0, m3 = static_cast<short>(o2.y >> 16) > 0;
+          const f32x4 v = acc[h + i][f];
+          const uint2 pk = make_uint2(pack2(m0 ? v[0] : 0.f, m1 ? v[1] : 0.f), pack2(m2 ? v[2] : 0.f, m3 ? v[3] : 0.f));
+          if (ok[h + i]) *reinterpret_cast<uint2 *>(a.y + po[h + i] + 16 * f) = pk;
+          if constexpr (EPI == 2) {
+            if (ok[h + i]) {
+              sum[f][0] += __uint_as_float(pk.x << 16);
+              sum[f][1] += __uint_as_float(pk.x & 0xffff0000u);
+              sum[f][2] += __uint_as_float(pk.y << 16);
+              sum[f][3] += __uint_as_float(pk.y & 0xffff0000u);
+            }
+          }
+        }
+      }
+    }
+    if constexpr (EPI == 2) {
+#pragma unroll
+      for (int f = 0; f < NF; ++f)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float v = sum[f][j];
+          v += __shfl_xor(v, 1);
+          v += __shfl_xor(v, 2);
+          v += __shfl_xor(v, 4);
+          v += __shfl_xor(v, 8);
+          sum[f][j] = v;
+        }
+      if (l16 == 0) {
+        float *row = a.dbp + static_cast<long>((n * G::NB + band) * 4 + wave) * a.dbp_ld + c0;
+#pragma unroll
+        for (int f = 0; f < NF; ++f) *reinterpret_cast<f32x4 *>(row + 16 * f) = sum[f];
+      }
+    }
+  }
+}
+
+template <int H, int W, int KS, int R, int NF>
+int launch_cp(CdArgs a, int epi, float *db, hipStream_t s) {
+  using G = Cp<H, W, KS, R, NF>;
+  if (a.Cog % (16 * NF) || a.Cg % 16) return -1;
+  a.ncob = a.Cog / (16 * NF);
+  a.nitems = a.N * G::NB * a.groups * a.ncob;
+  a.nst = a.Cg / 16;
+  const dim3 grid(a.nitems), blk(256);
+  if (epi == 0) CXN_LAUNCH((conv_direct_pair<H, W, KS, R, NF, 0>), grid, blk, 0, s, a);
+  else if (epi == 1) CXN_LAUNCH((conv_direct_pair<H, W, KS, R, NF, 1>), grid, blk, 0, s, a);
+  else {
+    CXN_LAUNCH((conv_direct_pair<H, W, KS, R, NF, 2>), grid, blk, 0, s, a);
+    GEpi E{};
+    E.dbias = a.dbp;
+    E.part_ld = a.dbp_ld;
+    E.dbias_final = db;
+    launch_db_reduce(E, a.N * G::NB * 4, s);
+  }
+  return 0;
+}
+
 }  // namespace
 
-// Served: stride 1, "same" padding, K = 3 on 13 x 13 maps; Cg (input channels per group) a
-// multiple of 32, Cog (output channels per group) a multiple of 64, pixel strides multiples of 8.
+// Served: stride 1, "same" padding, K = 3 on 13 x 13 maps with Cg (input channels per group) a
+// multiple of 32 and Cog (output channels per group) a multiple of 64; K = 5 on 27 x 27 maps (the
+// paired-tap form, every variant id) with Cg a multiple of 16 and Cog a multiple of 64 or 48.
+// Pixel strides multiples of 8.
 // variant: 0 persistent blocks with two stage buffers, 1 one block per item with one stage
 // buffer (two blocks per CU), 2 as 0 with four more waves per block that only issue the LDS-DMAs.
 // epi 0: y = conv(x, w) + bias (relu optional).  epi 1: data gradient (x = dy, w = flipped
@@ -483,11 +735,14 @@ int launch_cd(CdArgs a, int epi, int variant, float *db, hipStream_t s) {
 CXN_API long cxn_conv_direct(const void *x, int ldx, const void *w, const float *bias, void *y, int ldy, float *dbp,
                              long dbp_elems, float *db, int N, int H, int W, int Cg, int Cog, int groups, int KS,
                              int relu, int epi, int variant, void *stream) {
-  if (KS != 3 || H != 13 || W != 13) return -1;
-  if (Cg % 32 || Cog % 64 || ldx % 8 || ldy % 8 || groups < 1 || ldx < groups * Cg || ldy < groups * Cog) return -1;
+  const bool pair = KS == 5 && H == 27 && W == 27;  // paired-tap form (AlexNet conv2)
+  if (!pair && (KS != 3 || H != 13 || W != 13)) return -1;
+  if (ldx % 8 || ldy % 8 || groups < 1 || ldx < groups * Cg || ldy < groups * Cog) return -1;
+  if (pair ? (Cg % 16 || (Cog % 64 && Cog % 48)) : (Cg % 32 || Cog % 64)) return -1;
   if (static_cast<long>(N) * H * W * (ldx > ldy ? ldx : ldy) >= (1L << 30)) return -1;
   constexpr int IPB = 2;
-  const long need = static_cast<long>((N + IPB - 1) / IPB) * 8 * groups * Cog;  // (rows: image group x wave)
+  const long need = pair ? static_cast<long>(N) * 2 * 4 * groups * Cog  // (rows: image band x wave)
+                         : static_cast<long>((N + IPB - 1) / IPB) * 8 * groups * Cog;  // (image group x wave)
   if (epi == 2 && dbp == nullptr) return need;
   if (epi == 2 && dbp_elems < need) return -4;
   CdArgs a{};
@@ -506,7 +761,9 @@ CXN_API long cxn_conv_direct(const void *x, int ldx, const void *w, const float 
   a.dbp_ld = groups * Cog;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (variant < 0 || variant > 2) return -1;
-  const int rc = launch_cd<13, 13, 3, IPB, 4, 4>(a, epi, variant, db, s);
+  int rc;
+  if (pair) rc = Cog % 64 == 0 ? launch_cp<27, 27, 5, 14, 4>(a, epi, db, s) : launch_cp<27, 27, 5, 14, 3>(a, epi, db, s);
+  else rc = launch_cd<13, 13, 3, IPB, 4, 4>(a, epi, variant, db, s);
   if (rc != 0) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -890,6 +890,8 @@ def _cd_serves(g: ConvGeom, *ts) -> bool:
     """The direct kernel's shape rule (cxn_conv_direct), without launching anything."""
     if not _cd_ok(g, *ts):
         return False
+    if g.KH == 5 and g.H == 27 and g.W == 27:  # paired-tap form (AlexNet conv2)
+        return g.cg_in % 16 == 0 and (g.cg_out % 64 == 0 or g.cg_out % 48 == 0)
     return g.KH == 3 and g.H == 13 and g.W == 13 and g.cg_in % 32 == 0 and g.cg_out % 64 == 0
 
 

@@ -13,7 +13,7 @@ from cxxnet_amd.ops.gemm import ConvGeom
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
-# (N, C, Cout, groups)
+# (N, C, Cout, groups[, H, K]): 13 x 13 / 3 x 3 unless given
 CASES = [
     (256, 256, 384, 1),  # AlexNet conv3
     (256, 384, 384, 2),  # conv4
@@ -22,7 +22,16 @@ CASES = [
     (7, 384, 256, 2),    # odd N
     (1, 64, 64, 1),      # one item
     (5, 192, 128, 1),    # six channel stages (data gradient: four)
+    (256, 96, 256, 2, 27, 5),  # AlexNet conv2: paired-tap form (forward 48 channels per group, data gradient 128 -> 48)
+    (32, 96, 256, 2, 27, 5),
+    (3, 64, 128, 1, 27, 5),
 ]
+
+
+def _geo(case):
+    N, C, Cout, groups = case[:4]
+    H, K = case[4:] if len(case) > 4 else (13, 3)
+    return N, C, Cout, groups, H, K
 
 
 def _rnd(shape, seed, scale=1.0):
@@ -41,15 +50,15 @@ def _nchw(t):
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
 @pytest.mark.parametrize("relu", [False, True])
 def test_direct_forward(case, relu):
-    N, C, Cout, groups = case
-    g = ConvGeom(N, 13, 13, C, 13, 13, Cout, 3, 3, 1, 1, 1, groups)
-    x = _rnd((N, 13, 13, C), 1)
-    w = _rnd((Cout, 3, 3, C // groups), 2, 0.05)
+    N, C, Cout, groups, H, K = _geo(case)
+    g = ConvGeom(N, H, H, C, H, H, Cout, K, K, 1, K // 2, K // 2, groups)
+    x = _rnd((N, H, H, C), 1)
+    w = _rnd((Cout, K, K, C // groups), 2, 0.05)
     b = torch.randn(Cout, device=DEV) * 0.1
-    y = torch.full((N, 13, 13, Cout), 7.0, device=DEV, dtype=torch.bfloat16)
+    y = torch.full((N, H, H, Cout), 7.0, device=DEV, dtype=torch.bfloat16)
     assert gemm.conv_direct_forward(x, w, b, y, g, relu=relu)
     torch.cuda.synchronize()
-    ref = F.conv2d(_nchw(x), w.float().permute(0, 3, 1, 2), b, padding=1, groups=groups)
+    ref = F.conv2d(_nchw(x), w.float().permute(0, 3, 1, 2), b, padding=K // 2, groups=groups)
     if relu:
         ref = ref.clamp_min(0)
     assert _err(y.permute(0, 3, 1, 2), ref) < 5e-3  # bf16 output rounding
@@ -58,19 +67,19 @@ def test_direct_forward(case, relu):
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
 @pytest.mark.parametrize("mode", ["plain", "mask", "mask_db"])
 def test_direct_data_grad(case, mode):
-    N, C, Cout, groups = case
-    g = ConvGeom(N, 13, 13, C, 13, 13, Cout, 3, 3, 1, 1, 1, groups)
-    dy = _rnd((N, 13, 13, Cout), 3)
-    w = _rnd((Cout, 3, 3, C // groups), 4, 0.05)
+    N, C, Cout, groups, H, K = _geo(case)
+    g = ConvGeom(N, H, H, C, H, H, Cout, K, K, 1, K // 2, K // 2, groups)
+    dy = _rnd((N, H, H, Cout), 3)
+    w = _rnd((Cout, K, K, C // groups), 4, 0.05)
     wt = torch.empty_like(w)
     gemm.conv_weight_flip_multi([(w, wt, g)])
-    act = torch.relu(_rnd((N, 13, 13, C), 5))  # relu(z) of the layer below
+    act = torch.relu(_rnd((N, H, H, C), 5))  # relu(z) of the layer below
     dx = act.clone()
     db = torch.full((C,), 0.5, device=DEV) if mode == "mask_db" else None
     got_db = gemm.conv_direct_data(dy, wt, dx, g, mask_relu=mode != "plain", dbias=db)
     assert got_db
     torch.cuda.synchronize()
-    ref = torch.nn.grad.conv2d_input((N, C, 13, 13), w.float().permute(0, 3, 1, 2), _nchw(dy), padding=1,
+    ref = torch.nn.grad.conv2d_input((N, C, H, H), w.float().permute(0, 3, 1, 2), _nchw(dy), padding=K // 2,
                                      groups=groups)
     if mode != "plain":
         ref = ref * (_nchw(act) > 0).float()

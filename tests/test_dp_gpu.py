@@ -76,7 +76,15 @@ def _worker(rank, world, port, steps, out, extra, backend="gloo"):
                                    # the gloo CPU tests' 1e-4 bound: deterministic GEMMs (no fp32
                                    # atomics), so only the 2-rank sum order differs (measured 1e-9)
                                    (("deterministic", "1"),),
-                                   (("deterministic", "1"), ("dp_mode", "allreduce"))])
+                                   (("deterministic", "1"), ("dp_mode", "allreduce")),
+                                   # the gathered fc path with two real ranks: [x | dy] row
+                                   # all-gathers and the SGD step fused into the weight-gradient
+                                   # GEMM, under launch lists, graph segments, and bit-equal to
+                                   # the single-GPU step in deterministic mode
+                                   (("fullc_gather", "1"),),
+                                   (("fullc_gather", "1"), ("cuda_graph", "1")),
+                                   (("fullc_gather", "1"), ("dp_mode", "shard")),
+                                   (("fullc_gather", "1"), ("deterministic", "1"))])
 def test_dp_two_ranks_gpu_equals_single(tmp_path, extra):
     steps = 4
     out = str(tmp_path / "w")
