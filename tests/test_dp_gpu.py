@@ -68,6 +68,10 @@ def _worker(rank, world, port, steps, out, extra, backend="gloo"):
             (tr.net.updater.fused_offsets, [f._gathering() for f in fcs], list(tr._lists), list(tr._graphs))
     tr.reducer.sync_master()  # sharded: each rank updated only its slice of the fp32 masters
     torch.save(tr.net.arena.w.cpu(), out + f".r{rank}")
+    # per parameter too: with fullc_gather the arena pads the gathered layers' segments to
+    # world * ALIGN boundaries, so the flat layout differs from the single-process arena
+    a = tr.net.arena
+    torch.save([a.w[sp.offset:sp.offset + sp.numel].cpu() for _, sp in a.specs], out + f".p{rank}")
     dist.destroy_process_group()
 
 
@@ -82,6 +86,7 @@ def _worker(rank, world, port, steps, out, extra, backend="gloo"):
                                    # GEMM, under launch lists, graph segments, and bit-equal to
                                    # the single-GPU step in deterministic mode
                                    (("fullc_gather", "1"),),
+                                   (("fullc_gather", "1"), ("launch_replay", "0")),
                                    (("fullc_gather", "1"), ("cuda_graph", "1")),
                                    (("fullc_gather", "1"), ("dp_mode", "shard")),
                                    (("fullc_gather", "1"), ("deterministic", "1"))])
@@ -98,10 +103,12 @@ def test_dp_two_ranks_gpu_equals_single(tmp_path, extra):
     for _ in range(steps):
         tr.update(DataBatch(x.cuda(), y.cuda()))
     torch.cuda.synchronize()
-    w = tr.net.arena.w.cpu()
-    w0 = _make(8, list(extra)).net.arena.w.cpu()  # same seed: the initial weights
-    n = w.numel()
-    err = ((r0[:n] - w).norm() / (w - w0).norm()).item()  # relative to the distance trained
+    a = tr.net.arena
+    w = torch.cat([a.w[sp.offset:sp.offset + sp.numel].cpu() for _, sp in a.specs])
+    a0 = _make(8, list(extra)).net.arena  # same seed: the initial weights
+    w0 = torch.cat([a0.w[sp.offset:sp.offset + sp.numel].cpu() for _, sp in a0.specs])
+    p0 = torch.cat(torch.load(out + ".p0", weights_only=True))
+    err = ((p0 - w).norm() / (w - w0).norm()).item()  # relative to the distance trained
     print(f"dp 2-rank vs single, {extra}: err {err:.3g}")
     # default mode: fp32 atomics in the weight gradients make the summation order run-dependent,
     # and a 1-ulp flip of a bf16 weight shadow moves later activations by bf16 ulps
