@@ -864,7 +864,7 @@ _cd_ws = {}
 # Pseudo-tiles of the tile table for the direct kernel's schedules (cxn_conv_direct variant):
 # 200 persistent blocks with two stage buffers, 201 one block per item (two per CU), 202 as 200
 # with four LDS-DMA loader waves per block.  Tuning candidates of the "cf" / "cd" signatures it
-# serves (in-step picks: profiles/r6_step_tune_direct.jsonl).
+# serves (in-step picks at the strong-scaling batches: profiles/r6_step_tune_direct_b{32,64,128}.jsonl).
 DIRECT_TILES = {200: 0, 201: 1, 202: 2}
 
 
