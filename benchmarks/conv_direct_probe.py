@@ -46,7 +46,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--ops", default="conv3,conv4,conv5")
-    ap.add_argument("--paths", default="table,200,201,202",
+    ap.add_argument("--paths", default="table,200,201,202,203",
                     help="tile ids to force (200-202: the direct kernel's schedules) or 'table' (the shipped pick)")
     ap.add_argument("--dirs", default="fwd,dgrad")
     a = ap.parse_args()

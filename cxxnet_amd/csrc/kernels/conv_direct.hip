@@ -720,6 +720,330 @@ int launch_cp(CdArgs a, int epi, float *db, hipStream_t s) {
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Version 2 (tile 203): the paired-tap K walk of conv_direct_pair on persistent blocks of eight
+// waves -- two per SIMD, so one wave's LDS-read and DMA-issue stalls are covered by its partner's
+// MFMAs (a calibration loop with this fragment pattern: 75 % of the MFMA peak at one wave per
+// SIMD, 98 % at two) -- and double-buffered stages, so the next stage's DMAs land under the
+// current stage and an item's first stage lands under its predecessor's last.
+//   * Waves WM (along the slots) x WN (along the output channels); wave tile WMF x NFW fragments.
+//   * An item = IPB images stacked with separator rows (13 x 13) or a band of R virtual rows of
+//     one image (27 x 27) x 16 NFW WN output channels of one group.
+//   * Stage = (16-channel chunk, group of PPG tap pairs); the chunk's x image stays in its own
+//     double buffer for the chunk's NPG stages, the weight image of a stage in a second one.
+template <int H, int W, int KS, int IPB, int R, int WM, int WN, int NFW>
+struct C2 {
+  static constexpr int P = (KS - 1) / 2, T = KS * KS, NPR = (T + 1) / 2, PW = W + P, VR = H + P;
+  static constexpr int NB = (IPB * VR - P + R - 1) / R;           // bands per item stack
+  static constexpr int MF = (R * PW + 15) / 16;
+  static constexpr int WMF = (MF + WM - 1) / WM;
+  static constexpr int MS = 16 * WM * WMF;
+  static constexpr int NXS = (MS + (KS - 1) * (PW + 1) + 31) / 32 * 32;
+  static constexpr int NDX = NXS / 32;                             // x DMA pieces per chunk
+  static constexpr int XB = NXS * 32;
+  static constexpr int NFB = NFW * WN;                             // channel fragments per block
+  static constexpr int PPG_MAX = (160 * 1024 - 2 * XB) / (2 * NFB * 1024);
+  static constexpr int NPG = (NPR + PPG_MAX - 1) / PPG_MAX;        // pair groups (stages) per chunk
+  static constexpr int PPG = (NPR + NPG - 1) / NPG;                // pairs per stage
+  static constexpr int WBF = PPG * NFB * 1024;
+  static constexpr int NDW = PPG * NFB;                            // weight DMA pieces per stage
+  static constexpr int XLEAD = P * PW + P;
+  static constexpr int NDXW = (NDX + 7) / 8, NDWW = (NDW + 7) / 8; // per wave (8 waves)
+  static_assert(WM * WN == 8, "eight waves");
+  static_assert(PPG_MAX >= 1 && 2 * XB + 2 * WBF <= 160 * 1024, "LDS");
+};
+
+template <int H, int W, int KS, int IPB, int R, int WM, int WN, int NFW, int EPI>
+__global__ void __launch_bounds__(512, 2) conv_direct2(CdArgs a) {
+  using G = C2<H, W, KS, IPB, R, WM, WN, NFW>;
+  constexpr int T = G::T, NPR = G::NPR, WMF = G::WMF, XB = G::XB, WBF = G::WBF, PW = G::PW, VR = G::VR;
+  constexpr int NPG = G::NPG, PPG = G::PPG, NFB = G::NFB, NDX = G::NDX, NDW = G::NDW, NB = G::NB;
+  constexpr int HW = H * W;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * XB + 2 * WBF];
+  const int lane = threadIdx.x & 63, l16 = lane & 15, hl = lane >> 5, pl = (lane >> 4) & 1;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+  const uint32_t lds0 =
+      __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void *)smem)));
+  const int nb = static_cast<int>(gridDim.x);
+  const int L = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
+  const int nmine = L < a.nitems ? (a.nitems - L + nb - 1) / nb : 0;
+  const int SPI = a.nst * NPG;  // stages per item
+  const int K = nmine * SPI;
+  if (K == 0) return;
+
+  // item = ((ig NB + band) groups + g) ncob + cob
+  auto item_of = [&](int j, int &ig, int &band, int &g, int &cob) __attribute__((always_inline)) {
+    const int it = L + j * nb;
+    cob = it % a.ncob;
+    const int r1 = it / a.ncob;
+    g = r1 % a.groups;
+    const int r2 = r1 / a.groups;
+    band = r2 % NB;
+    ig = r2 / NB;
+  };
+  // x DMA offsets per band (NB <= 2: two sets), weight offsets of a stage's pairs (group 0)
+  static_assert(NB <= 2, "x offset sets");
+  uint32_t vx[NB][G::NDXW], vw[G::NDWW];
+#pragma unroll
+  for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+    for (int i = 0; i < G::NDXW; ++i) {
+      const int q = wave + 8 * i;
+      uint32_t v = OOB;
+      if (q < NDX) {
+        const int lin = 32 * q + 16 * hl + l16 - G::XLEAD;
+        const int vrow = cd_fdiv(lin, PW), col = lin - vrow * PW;
+        const int gv = bb * R + vrow, img = cd_fdiv(gv, VR), row = gv - img * VR;
+        if (img >= 0 && img < IPB && row < H && col < W)
+          v = static_cast<uint32_t>((((img * H + row) * W + col) * a.ldx + 8 * pl) * 2);
+      }
+      vx[bb][i] = v;
+    }
+#pragma unroll
+  for (int i = 0; i < G::NDWW; ++i) {
+    const int q = wave + 8 * i;
+    const int pp = q / NFB, f = q - pp * NFB;
+    vw[i] = q < NDW ? static_cast<uint32_t>((((16 * f + l16) * T + 2 * pp + hl) * a.Cg + 8 * pl) * 2) : OOB;
+  }
+
+  rsrc_t rx, rw;
+  int band_n = 0, npp_n = PPG, pr0_n = 0;  // of the stage being loaded
+  bool newx = true;
+  auto prep = [&](int k) __attribute__((always_inline)) {
+    const int j = k / SPI, r = k - j * SPI, c = r / NPG, h = r - c * NPG;
+    int ig, band, g, cob;
+    item_of(j, ig, band, g, cob);
+    const int n0 = ig * IPB, nimg = min(IPB, a.N - n0);
+    const long cx = static_cast<long>(g) * a.Cg + 16 * c;
+    rx = make_rsrc(a.x + static_cast<long>(n0) * HW * a.ldx + cx,
+                   static_cast<uint32_t>((static_cast<long>(nimg) * HW * a.ldx - cx) * 2));
+    const long co = static_cast<long>(g) * a.Cog + cob * 16 * NFB;
+    const long wofs = co * T * a.Cg + 16 * c + static_cast<long>(2 * h * PPG) * a.Cg;
+    rw = make_rsrc(a.w + wofs, static_cast<uint32_t>((static_cast<long>(16 * NFB) * T * a.Cg - (wofs - co * T * a.Cg)) * 2));
+    band_n = band;
+    pr0_n = h * PPG;
+    npp_n = min(PPG, NPR - h * PPG);
+    newx = h == 0;
+  };
+  // DMAs of stage k (prep'd) into W buffer wb and, at a chunk's first stage, x buffer xb
+  auto issue = [&](int wb, int xb) __attribute__((always_inline)) {
+    if (newx) {
+#pragma unroll
+      for (int i = 0; i < G::NDXW; ++i) {
+        const int q = wave + 8 * i;
+        if (q < NDX) {
+          const uint32_t off = (NB == 2 && band_n == 1) ? vx[NB - 1][i] : vx[0][i];
+          dma16c(rx, lds0 + static_cast<uint32_t>(xb * XB + q * 1024), off);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < G::NDWW; ++i) {
+      const int q = wave + 8 * i;
+      const int pp = q / NFB;
+      if (q < NDW && pp < npp_n) {
+        // the second half of an odd tap count's last pair reads zeros
+        const uint32_t off = (2 * (pr0_n + pp) + 1 >= T && hl) ? OOB : vw[i];
+        dma16c(rw, lds0 + static_cast<uint32_t>(2 * XB + wb * WBF + q * 1024), off);
+      }
+    }
+  };
+
+  auto shift = [](int t) { return (t / KS) * PW + (t % KS); };
+  f32x4 acc[WMF][NFW];
+  bf16x8 xf[2][WMF], wf[2][NFW];
+  constexpr int NR = WMF + NFW, NM = WMF * NFW, RS = NM / NR > 0 ? NM / NR : 1;
+
+  auto epilogue = [&](int j) __attribute__((always_inline)) {
+    int ig, band, g, cob;
+    item_of(j, ig, band, g, cob);
+    const int n0 = ig * IPB, r0 = band * R;
+    const int c0 = g * a.Cog + cob * 16 * NFB + wn * 16 * NFW + 4 * (lane >> 4);
+    int po[WMF];
+    bool ok[WMF];
+#pragma unroll
+    for (int i = 0; i < WMF; ++i) {
+      const int o = 16 * (wm * WMF + i) + l16;
+      const int vrow = o / PW, c = o - vrow * PW;
+      const int gv = r0 + vrow, img = gv / VR, row = gv - img * VR;
+      ok[i] = vrow < R && img < IPB && n0 + img < a.N && row < H && c < W;
+      po[i] = (((n0 + img) * H + row) * W + c) * a.ldy + c0;
+    }
+    if constexpr (EPI == 0) {
+      f32x4 bv[NFW];
+#pragma unroll
+      for (int f = 0; f < NFW; ++f)
+        bv[f] = a.bias ? f32x4{a.bias[c0 + 16 * f], a.bias[c0 + 16 * f + 1], a.bias[c0 + 16 * f + 2],
+                               a.bias[c0 + 16 * f + 3]}
+                       : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < WMF; ++i)
+#pragma unroll
+        for (int f = 0; f < NFW; ++f) {
+          f32x4 v = acc[i][f] + bv[f];
+          if (a.relu) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+          }
+          if (ok[i]) *reinterpret_cast<uint2 *>(a.y + po[i] + 16 * f) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        }
+    } else {
+      f32x4 sum[NFW];
+#pragma unroll
+      for (int f = 0; f < NFW; ++f) sum[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+      constexpr int HM = 2;  // (two M fragments at a time: registers)
+#pragma unroll
+      for (int hh = 0; hh < WMF; hh += HM) {
+        uint2 old[HM][NFW];
+#pragma unroll
+        for (int i = 0; i < HM; ++i)
+#pragma unroll
+          for (int f = 0; f < NFW; ++f)
+            old[i][f] = (a.relu && hh + i < WMF && ok[hh + i])
+                            ? *reinterpret_cast<const uint2 *>(a.y + po[hh + i] + 16 * f)
+                            : make_uint2(0x3f803f80u, 0x3f803f80u);
+#pragma unroll
+        for (int i = 0; i < HM; ++i) {
+          if (hh + i >= WMF) continue;
+#pragma unroll
+          for (int f = 0; f < NFW; ++f) {
+            const uint2 o2 = old[i][f];
+            const bool m0 = static_cast<short>(o2.x & 0xffffu) > 0, m1 = static_cast<short>(o2.x >> 16) > 0;
+            const bool m2 = static_cast<short>(o2.y & 0xffffu) > 0, m3 = static_cast<short>(o2.y >> 16) > 0;
+            const f32x4 v = acc[hh + i][f];
+            const uint2 pk =
+                make_uint2(pack2(m0 ? v[0] : 0.f, m1 ? v[1] : 0.f), pack2(m2 ? v[2] : 0.f, m3 ? v[3] : 0.f));
+            if (ok[hh + i]) *reinterpret_cast<uint2 *>(a.y + po[hh + i] + 16 * f) = pk;
+            if constexpr (EPI == 2) {
+              if (ok[hh + i]) {
+                sum[f][0] += __uint_as_float(pk.x << 16);
+                sum[f][1] += __uint_as_float(pk.x & 0xffff0000u);
+                sum[f][2] += __uint_as_float(pk.y << 16);
+                sum[f][3] += __uint_as_float(pk.y & 0xffff0000u);
+              }
+            }
+          }
+        }
+      }
+      if constexpr (EPI == 2) {
+#pragma unroll
+        for (int f = 0; f < NFW; ++f)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float v = sum[f][e];
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            v += __shfl_xor(v, 8);
+            sum[f][e] = v;
+          }
+        if (l16 == 0) {  // row = (image group, band) x wave along the slots
+          float *row = a.dbp + static_cast<long>((ig * NB + band) * WM + wm) * a.dbp_ld + c0;
+#pragma unroll
+          for (int f = 0; f < NFW; ++f) *reinterpret_cast<f32x4 *>(row + 16 * f) = sum[f];
+        }
+      }
+    }
+  };
+
+  // prologue: stage 0 into W buffer 0 / x buffer 0
+  prep(0);
+  issue(0, 0);
+  wait_vmcnt<0>();
+  block_barrier();
+  const int wrd = 16 * lane;
+  int xbuf = 0;
+  for (int j = 0, k = 0; j < nmine; ++j) {
+#pragma unroll
+    for (int i = 0; i < WMF; ++i)
+#pragma unroll
+      for (int f = 0; f < NFW; ++f) {
+        acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+        asm volatile("" : "+a"(acc[i][f]));
+      }
+    for (int r = 0; r < SPI; ++r, ++k) {
+      const int h = r % NPG;
+      const int wb = k & 1;
+      if (k + 1 < K) {  // the next stage's DMAs land under this one
+        prep(k + 1);
+        issue(wb ^ 1, newx ? (xbuf ^ 1) : xbuf);
+      }
+      const char *xs = smem + xbuf * XB + 512 * (wm * WMF);
+      const char *ws = smem + 2 * XB + wb * WBF + wn * NFW * 1024 + wrd;
+      const int pr0 = h * PPG, npp = min(PPG, NPR - pr0);
+      auto read_one = [&](int pr, int pp, auto sc, auto rc) __attribute__((always_inline)) {
+        constexpr int st = decltype(sc)::value, rr = decltype(rc)::value;
+        if constexpr (rr < NFW) {
+          wf[st][rr] = *reinterpret_cast<const bf16x8 *>(ws + (pp * NFB + rr) * 1024);
+        } else {
+          const int t0 = 2 * pr, t1 = 2 * pr + 1 < T ? 2 * pr + 1 : 2 * pr;
+          const int u = l16 + (hl ? shift(t1) : shift(t0));
+          xf[st][rr - NFW] = *reinterpret_cast<const bf16x8 *>(xs + 512 * (rr - NFW + (u >> 4)) + 256 * pl + 16 * (u & 15));
+        }
+      };
+      static_for<NR>([&](auto rc) { read_one(pr0, 0, std::integral_constant<int, 0>{}, rc); });
+      // pairs of this stage, two at a time (register sets alternate)
+      static_for<PPG>([&](auto pc) {
+        constexpr int pp = decltype(pc)::value, st = pp & 1;
+        if (pp < npp) {
+          static_for<NM>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            constexpr int i = q / NFW, f = q % NFW;
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_acc(acc[i][f], wf[st][f], xf[st][i]);
+            if constexpr (q % RS == RS - 1 && q / RS < NR) {
+              if (pp + 1 < npp)
+                read_one(pr0 + pp + 1, pp + 1, std::integral_constant<int, st ^ 1>{}, std::integral_constant<int, q / RS>{});
+            }
+            if constexpr (q == NM - 1 && NM / RS < NR) {
+              if (pp + 1 < npp)
+                static_for<NR - NM / RS>([&](auto rc) {
+                  read_one(pr0 + pp + 1, pp + 1, std::integral_constant<int, st ^ 1>{},
+                           std::integral_constant<int, NM / RS + decltype(rc)::value>{});
+                });
+            }
+          });
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      });
+      wait_vmcnt<0>();
+      asm volatile("" ::: "memory");
+      block_barrier();
+      asm volatile("" ::: "memory");
+      if (h == NPG - 1) xbuf ^= 1;  // the next chunk's x image
+    }
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < WMF; ++i)
+#pragma unroll
+      for (int f = 0; f < NFW; ++f) asm volatile("" : "+a"(acc[i][f]));
+    epilogue(j);
+  }
+}
+
+template <int H, int W, int KS, int IPB, int R, int WM, int WN, int NFW>
+int launch_c2(CdArgs a, int epi, float *db, hipStream_t s) {
+  using G = C2<H, W, KS, IPB, R, WM, WN, NFW>;
+  if (a.Cog % (16 * G::NFB) || a.Cg % 16) return -1;
+  const int nig = (a.N + IPB - 1) / IPB;
+  a.ncob = a.Cog / (16 * G::NFB);
+  a.nitems = nig * G::NB * a.groups * a.ncob;
+  a.nst = a.Cg / 16;
+  const int grid = a.nitems < 256 ? a.nitems : 256;
+  if (epi == 0) CXN_LAUNCH((conv_direct2<H, W, KS, IPB, R, WM, WN, NFW, 0>), dim3(grid), dim3(512), 0, s, a);
+  else if (epi == 1) CXN_LAUNCH((conv_direct2<H, W, KS, IPB, R, WM, WN, NFW, 1>), dim3(grid), dim3(512), 0, s, a);
+  else {
+    CXN_LAUNCH((conv_direct2<H, W, KS, IPB, R, WM, WN, NFW, 2>), dim3(grid), dim3(512), 0, s, a);
+    GEpi E{};
+    E.dbias = a.dbp;
+    E.part_ld = a.dbp_ld;
+    E.dbias_final = db;
+    launch_db_reduce(E, nig * G::NB * WM, s);
+  }
+  return 0;
+}
+
 }  // namespace
 
 // Served: stride 1, "same" padding, K = 3 on 13 x 13 maps with Cg (input channels per group) a
@@ -741,7 +1065,7 @@ CXN_API long cxn_conv_direct(const void *x, int ldx, const void *w, const float 
   if (pair ? (Cg % 16 || (Cog % 64 && Cog % 48)) : (Cg % 32 || Cog % 64)) return -1;
   if (static_cast<long>(N) * H * W * (ldx > ldy ? ldx : ldy) >= (1L << 30)) return -1;
   constexpr int IPB = 2;
-  const long need = pair ? static_cast<long>(N) * 2 * 4 * groups * Cog  // (rows: image band x wave)
+  const long need = pair ? static_cast<long>(N) * 2 * 8 * groups * Cog  // (rows: image band x wave)
                          : static_cast<long>((N + IPB - 1) / IPB) * 8 * groups * Cog;  // (image group x wave)
   if (epi == 2 && dbp == nullptr) return need;
   if (epi == 2 && dbp_elems < need) return -4;
@@ -760,10 +1084,23 @@ CXN_API long cxn_conv_direct(const void *x, int ldx, const void *w, const float 
   a.relu = relu;
   a.dbp_ld = groups * Cog;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (variant < 0 || variant > 2) return -1;
+  if (variant < 0 || variant > 3) return -1;
   int rc;
-  if (pair) rc = Cog % 64 == 0 ? launch_cp<27, 27, 5, 14, 4>(a, epi, db, s) : launch_cp<27, 27, 5, 14, 3>(a, epi, db, s);
-  else rc = launch_cd<13, 13, 3, IPB, 4, 4>(a, epi, variant, db, s);
+  if (variant == 3) {  // version 2: eight waves, paired taps, persistent double-buffered stages
+    if (pair) {
+      rc = Cog % 128 == 0 ? launch_c2<27, 27, 5, 1, 14, 4, 2, 4>(a, epi, db, s)
+         : Cog % 48 == 0  ? launch_c2<27, 27, 5, 1, 14, 8, 1, 3>(a, epi, db, s)
+                          : -1;
+    } else {
+      rc = Cog % 128 == 0 ? launch_c2<13, 13, 3, 2, 27, 4, 2, 4>(a, epi, db, s)
+         : Cog % 96 == 0  ? launch_c2<13, 13, 3, 2, 27, 4, 2, 3>(a, epi, db, s)
+                          : -1;
+    }
+  } else if (pair) {
+    rc = Cog % 64 == 0 ? launch_cp<27, 27, 5, 14, 4>(a, epi, db, s) : launch_cp<27, 27, 5, 14, 3>(a, epi, db, s);
+  } else {
+    rc = launch_cd<13, 13, 3, IPB, 4, 4>(a, epi, variant, db, s);
+  }
   if (rc != 0) return rc;
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

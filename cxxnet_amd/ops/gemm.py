@@ -863,9 +863,10 @@ _CD = os.environ.get("CXXNET_CONV_DIRECT", "auto")
 _cd_ws = {}
 # Pseudo-tiles of the tile table for the direct kernel's schedules (cxn_conv_direct variant):
 # 200 persistent blocks with two stage buffers, 201 one block per item (two per CU), 202 as 200
-# with four LDS-DMA loader waves per block.  Tuning candidates of the "cf" / "cd" signatures it
+# with four LDS-DMA loader waves per block, 203 version 2 (eight waves, two per SIMD, paired taps,
+# persistent double-buffered stages).  Tuning candidates of the "cf" / "cd" signatures it
 # serves (in-step picks at the strong-scaling batches: profiles/r6_step_tune_direct_b{32,64,128}.jsonl).
-DIRECT_TILES = {200: 0, 201: 1, 202: 2}
+DIRECT_TILES = {200: 0, 201: 1, 202: 2, 203: 3}
 
 
 def _cd_workspace(n, device):

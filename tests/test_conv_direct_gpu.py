@@ -47,16 +47,27 @@ def _nchw(t):
     return t.float().permute(0, 3, 1, 2)
 
 
+def _served(variant, C, Cout, groups, H):
+    """Version 2 (variant 3) serves channel blocks of 128 / 96 (13 x 13) or 128 / 48 (27 x 27)."""
+    if variant != 3:
+        return True
+    cog = Cout // groups
+    return cog % 128 == 0 or cog % (96 if H == 13 else 48) == 0
+
+
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
 @pytest.mark.parametrize("relu", [False, True])
-def test_direct_forward(case, relu):
+@pytest.mark.parametrize("variant", [0, 3])
+def test_direct_forward(case, relu, variant):
     N, C, Cout, groups, H, K = _geo(case)
+    if not _served(variant, C, Cout, groups, H):
+        pytest.skip("channel count not served by this variant")
     g = ConvGeom(N, H, H, C, H, H, Cout, K, K, 1, K // 2, K // 2, groups)
     x = _rnd((N, H, H, C), 1)
     w = _rnd((Cout, K, K, C // groups), 2, 0.05)
     b = torch.randn(Cout, device=DEV) * 0.1
     y = torch.full((N, H, H, Cout), 7.0, device=DEV, dtype=torch.bfloat16)
-    assert gemm.conv_direct_forward(x, w, b, y, g, relu=relu)
+    assert gemm.conv_direct_forward(x, w, b, y, g, relu=relu, variant=variant)
     torch.cuda.synchronize()
     ref = F.conv2d(_nchw(x), w.float().permute(0, 3, 1, 2), b, padding=K // 2, groups=groups)
     if relu:
@@ -66,8 +77,11 @@ def test_direct_forward(case, relu):
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
 @pytest.mark.parametrize("mode", ["plain", "mask", "mask_db"])
-def test_direct_data_grad(case, mode):
+@pytest.mark.parametrize("variant", [0, 1, 3])
+def test_direct_data_grad(case, mode, variant):
     N, C, Cout, groups, H, K = _geo(case)
+    if not _served(variant, Cout, C, groups, H):
+        pytest.skip("channel count not served by this variant")
     g = ConvGeom(N, H, H, C, H, H, Cout, K, K, 1, K // 2, K // 2, groups)
     dy = _rnd((N, H, H, Cout), 3)
     w = _rnd((Cout, K, K, C // groups), 4, 0.05)
@@ -76,7 +90,7 @@ def test_direct_data_grad(case, mode):
     act = torch.relu(_rnd((N, H, H, C), 5))  # relu(z) of the layer below
     dx = act.clone()
     db = torch.full((C,), 0.5, device=DEV) if mode == "mask_db" else None
-    got_db = gemm.conv_direct_data(dy, wt, dx, g, mask_relu=mode != "plain", dbias=db)
+    got_db = gemm.conv_direct_data(dy, wt, dx, g, mask_relu=mode != "plain", dbias=db, variant=variant)
     assert got_db
     torch.cuda.synchronize()
     ref = torch.nn.grad.conv2d_input((N, C, H, H), w.float().permute(0, 3, 1, 2), _nchw(dy), padding=K // 2,
