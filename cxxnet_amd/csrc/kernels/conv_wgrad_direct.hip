@@ -1,5 +1,5 @@
 // Direct stride-1 "same" convolution WEIGHT gradient for small maps (AlexNet conv3-5: 13 x 13,
-// 3 x 3, grouped), gfx950:  dW[co][kh][kw][ci] += sum_p dy[p][co] * x[p + (kh, kw) - pad][ci].
+// 3 x 3, grouped; conv2: 27 x 27, 5 x 5, grouped, tap-split form below), gfx950:  dW[co][kh][kw][ci] += sum_p dy[p][co] * x[p + (kh, kw) - pad][ci].
 // Reference: src/layer/convolution_layer-inl.hpp:121-138 (im2col + gemm into gwmat per group).
 //
 // Why.  The split-K implicit GEMM (gemm_mfma.hip GATHER_MN) rebuilds every pixel's im2col address
@@ -474,10 +474,284 @@ long ws_wd(int N, int Cg, int Cog, int groups, int splits) {
   return static_cast<long>(S) * npairs * (G::NACC * 256 + 64);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Tap-split form for larger maps / kernels (AlexNet conv2: 27 x 27, 5 x 5, 48 input channels
+// per group): 25 taps x 64 output channels x 32 input channels would be 200 accumulators per
+// wave.  Here a block tile is 16 CO_U output channels x 16 input channels x all taps, and the
+// four waves split the TAPS (wave w: taps w, w + 4, ...; 7 / 6 / 6 / 6 of 25) while each walks
+// every K-step, so a wave holds CO_U x 7 accumulators and reads CO_U dy + 7 x fragments per
+// K-step for 7 CO_U MFMAs.  A stage is a band of R output rows of one image (two bands for
+// 27 rows): dy rows of the band (rows past it read zeros, so a band's slots never count a
+// neighbour's pixels), x rows of the band plus the halo (rows off the map read zeros: two
+// per-lane offset sets, one per band).  LDS images and fragment reads as above
+// ([unit][slot][16 ch], ds_read_b64_tr_b16 pairs with the slot permutation of frag_d).
+template <int H, int W, int KS, int R, int CO_U, int NWV>
+struct Wt {
+  static constexpr int P = (KS - 1) / 2, T = KS * KS, PW = W + P;
+  static constexpr int NB = (H + R - 1) / R;
+  static constexpr int NK = (R * PW + 31) / 32;                    // K-steps per stage
+  static constexpr int NKS = NK * 32;
+  static constexpr int NX = (NKS + (KS - 1) * (PW + 1) + 31) / 32;
+  static constexpr int NXS = NX * 32;
+  static constexpr int XLEAD = P * PW + P;
+  static constexpr int DYB = CO_U * NKS * 32, XB = NXS * 32, BUF = DYB + XB;
+  static constexpr int NQD = CO_U * NK, NQ = NQD + NX, NQW = (NQ + NWV - 1) / NWV;  // DMA pieces
+  static constexpr int TPW = (T + 3) / 4;                          // taps per wave
+  static constexpr int NP = NWV / 4;                               // K-step interleave (wave groups)
+  static constexpr int NJ = (NK + NP - 1) / NP;                    // K-steps per wave and stage
+  static constexpr int NACC = CO_U * T;                            // accumulators of a block tile
+  static_assert(NWV == 4 || NWV == 8, "waves");
+  static_assert(2 * BUF <= 160 * 1024, "LDS");
+  static_assert(NB <= 2, "x offset sets");
+  static_assert(NJ >= 2, "DMA spread");
+};
+
+// NWV = 8: two waves per SIMD; waves w and w + 4 hold the same taps and take alternate K-steps
+// (summed through LDS at the end).  A stage's DMAs for the next one are spread over
+// this stage's K-steps (one or two after an MFMA) instead of a burst at the stage start.
+template <int H, int W, int KS, int R, int CO_U, int NWV>
+__global__ void __launch_bounds__(NWV * 64, 1)
+conv_wgrad_taps(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, float *__restrict__ ws, int N, int C,
+                int ldy, int Cg, int Cog, int npairs, int nciu, int ncob, int per, int nstages) {
+  using G = Wt<H, W, KS, R, CO_U, NWV>;
+  constexpr int T = G::T, NK = G::NK, NKS = G::NKS, PW = G::PW, P = G::P, NP = G::NP, NJ = G::NJ;
+  constexpr int BUF = G::BUF, DYB = G::DYB, NQD = G::NQD, NQ = G::NQ, NQW = G::NQW, TPW = G::TPW, NB = G::NB;
+  constexpr int HW = H * W;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+  const uint32_t L = xcd_remap(blockIdx.x, gridDim.x);
+  const int pair = static_cast<int>(L % static_cast<uint32_t>(npairs));
+  const int split = static_cast<int>(L / static_cast<uint32_t>(npairs));
+  const int per_g = ncob * nciu;
+  const int g = pair / per_g, rem = pair - g * per_g;
+  const int cob = rem / nciu, ciu = rem - cob * nciu;
+  const int ci0 = g * Cg + ciu * 16, co0 = g * Cog + cob * 16 * CO_U;
+  const int sb = split * per, se = min(nstages, sb + per);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tg = wave & 3, kpar = wave >> 2;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void *)smem)));
+
+  // per-lane DMA offsets: piece q = wave + NWV i; q < NQD: dy unit q / NK, slots 32 (q % NK) ..;
+  // else x slots 32 (q - NQD) .. (minus the lead); lane: slot lane >> 1, channels 8 (lane & 1) ..
+  // x rows are relative to the band's first halo row (band 1) or row 0 (band 0: rows above read 0)
+  uint32_t vq[NB][NQW];
+#pragma unroll
+  for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+    for (int i = 0; i < NQW; ++i) {
+      const int q = wave + NWV * i;
+      uint32_t v = OOB;
+      if (q < NQD) {
+        const int u = q / NK, sg = q - u * NK;
+        const int o = 32 * sg + (lane >> 1), vrow = o / PW, col = o - vrow * PW;
+        if (vrow < R && col < W) v = static_cast<uint32_t>(((vrow * W + col) * ldy + 16 * u + 8 * (lane & 1)) * 2);
+      } else if (q < NQ) {
+        const int lin = 32 * (q - NQD) + (lane >> 1) - G::XLEAD;
+        const int vrow = fdiv_floor(lin, PW), col = lin - vrow * PW;
+        const int rrel = bb == 0 ? vrow : vrow + P;  // row relative to the x base of this band
+        if (rrel >= 0 && col < W) v = static_cast<uint32_t>(((rrel * W + col) * C + 8 * (lane & 1)) * 2);
+      }
+      vq[bb][i] = v;
+    }
+  rsrc_t rd, rx;
+  int bsel = 0;
+  auto prep = [&](int st) __attribute__((always_inline)) {
+    const int n = st / NB, band = st - n * NB, r0 = band * R;
+    const int xr0 = band == 0 ? 0 : r0 - P;
+    const long pd = static_cast<long>(n) * HW + static_cast<long>(r0) * W;
+    rd = make_rsrc(dy + pd * ldy + co0, static_cast<uint32_t>((static_cast<long>(H - r0) * W * ldy - co0) * 2));
+    const long px = static_cast<long>(n) * HW + static_cast<long>(xr0) * W;
+    rx = make_rsrc(x + px * C + ci0, static_cast<uint32_t>((static_cast<long>(H - xr0) * W * C - ci0) * 2));
+    bsel = band;
+  };
+  auto issue_one = [&](int b, auto ic) __attribute__((always_inline)) {
+    constexpr int i = decltype(ic)::value;
+    const int q = wave + NWV * i;
+    const uint32_t off = (NB == 2 && bsel == 1) ? vq[NB - 1][i] : vq[0][i];
+    if (q < NQD) dma16d(rd, lds0 + static_cast<uint32_t>(b * BUF + q * 1024), off);
+    else if (q < NQ) dma16d(rx, lds0 + static_cast<uint32_t>(b * BUF + DYB + (q - NQD) * 1024), off);
+  };
+
+  // fragment read bases (frag_d's slot permutation); A = dy unit m at K-step k: (m NKS + 32 k) 32,
+  // B = x at K-step k under tap t: DYB + (32 k + shift(t)) 32
+  const int l16 = lane & 15, g4 = lane >> 4;
+  int bo[2];
+#pragma unroll
+  for (int hl = 0; hl < 2; ++hl) {
+    const int sl = ((g4 >> 1) << 4) | (hl << 3) | ((g4 & 1) << 2) | (l16 >> 2);
+    bo[hl] = sl * 32 + 8 * (l16 & 3);
+  }
+  f32x4 acc[CO_U][TPW];
+#pragma unroll
+  for (int m = 0; m < CO_U; ++m)
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt) {
+      acc[m][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      asm volatile("" : "+a"(acc[m][tt]));
+    }
+  const int ntap = tg + 4 * (TPW - 1) < T ? TPW : TPW - 1;  // this wave's tap count
+  bf16x8 fa[2][CO_U], fb[2][TPW];
+  constexpr int NR = CO_U + TPW, NM = CO_U * TPW, RS = NM / NR > 0 ? NM / NR : 1;
+  auto read_one = [&](const char *buf, int k, auto sc, auto rc) __attribute__((always_inline)) {
+    constexpr int st = decltype(sc)::value, r = decltype(rc)::value;
+    if constexpr (r < CO_U) {
+      const int off = (r * NKS + 32 * k) * 32;
+      fa[st][r] = frag_d(buf + bo[0] + off, buf + bo[1] + off);
+    } else {
+      constexpr int tt = r - CO_U;
+      const int t = tg + 4 * tt < T ? tg + 4 * tt : tg;  // (a missing tap reads anything finite)
+      const int off = DYB + (32 * k + (t / KS) * PW + (t % KS)) * 32;
+      fb[st][tt] = frag_d(buf + bo[0] + off, buf + bo[1] + off);
+    }
+  };
+
+  if (sb < se) {
+    prep(sb);
+    static_for<NQW>([&](auto ic) { issue_one(0, ic); });
+  }
+  for (int st = sb; st < se; ++st) {
+    const int b = (st - sb) & 1;
+    wait_vmcnt<0>();
+    block_barrier();
+    const bool more = st + 1 < se;  // the next stage's DMAs land under this one
+    if (more) prep(st + 1);
+    const char *buf = smem + b * BUF;
+    static_for<NR>([&](auto rc) { read_one(buf, kpar, std::integral_constant<int, 0>{}, rc); });
+    // this wave's K-steps k = kpar + NP j; register sets alternate with j; DMA piece i goes out in
+    // step i (NJ - 1) / NQW (never the last: a wave may have one step fewer)
+    static_for<NJ>([&](auto jc) {
+      constexpr int j = decltype(jc)::value, s0 = j & 1;
+      const int k = kpar + NP * j;
+      const bool valid = j < NJ - 1 || k < NK;
+      static_for<NM>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        constexpr int tt = q / CO_U, m = q % CO_U;
+        __builtin_amdgcn_sched_barrier(0);
+        if (valid && tt < ntap) mfma_d<true>(acc[m][tt], fa[s0][m], fb[s0][tt]);
+        static_for<NQW>([&](auto ic) {
+          constexpr int i = decltype(ic)::value;
+          constexpr int js = i * (NJ - 1) / NQW, first = (js * NQW + NJ - 2) / (NJ - 1);
+          if constexpr (js == j && q == 2 * (i - first) + 1) {
+            if (more) issue_one(b ^ 1, ic);
+          }
+        });
+        if constexpr (q % RS == RS - 1 && q / RS < NR) {
+          if (k + NP < NK) read_one(buf, k + NP, std::integral_constant<int, s0 ^ 1>{}, std::integral_constant<int, q / RS>{});
+        }
+        if constexpr (q == NM - 1 && NM / RS < NR) {
+          if (k + NP < NK)
+            static_for<NR - NM / RS>([&](auto rc) {
+              read_one(buf, k + NP, std::integral_constant<int, s0 ^ 1>{},
+                       std::integral_constant<int, NM / RS + decltype(rc)::value>{});
+            });
+        }
+      });
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    // (no barrier here: the next stage's starts with one, after which its DMAs go into this buffer)
+  }
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+  for (int m = 0; m < CO_U; ++m)
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt) pin_d<true>(acc[m][tt]);
+  if constexpr (NP == 2) {  // the odd-K-step waves hand their sums to the even ones through LDS
+    static_assert(4 * TPW * CO_U * 1024 <= 2 * BUF, "LDS combine");
+    block_barrier();  // every wave is done with the stage buffers
+    char *cb = smem + (tg * TPW * CO_U) * 1024 + 16 * lane;
+    if (kpar == 1) {
+#pragma unroll
+      for (int tt = 0; tt < TPW; ++tt)
+#pragma unroll
+        for (int m = 0; m < CO_U; ++m) *reinterpret_cast<f32x4 *>(cb + (tt * CO_U + m) * 1024) = acc[m][tt];
+    }
+    block_barrier();
+    if (kpar == 1) return;
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt)
+#pragma unroll
+      for (int m = 0; m < CO_U; ++m) acc[m][tt] += *reinterpret_cast<const f32x4 *>(cb + (tt * CO_U + m) * 1024);
+  }
+  // partial tile: ws[(split npairs + pair)][t][m][lane] (f32x4), this wave's taps
+  float *out = ws + (static_cast<long>(split) * npairs + pair) * (G::NACC * 256) + 4 * lane;
+#pragma unroll
+  for (int tt = 0; tt < TPW; ++tt) {
+    const int t = tg + 4 * tt;
+    if (t < T) {
+#pragma unroll
+      for (int m = 0; m < CO_U; ++m) *reinterpret_cast<f32x4 *>(out + (t * CO_U + m) * 256) = acc[m][tt];
+    }
+  }
+}
+
+// dW[co][t][ci] += alpha * sum over split slabs (fixed order); thread = (pair, t, m, lane)
+template <int T, int CO_U>
+__global__ void __launch_bounds__(256)
+conv_wgrad_taps_reduce(const float *__restrict__ ws, float *__restrict__ dw, int nsplit, int npairs, int nciu, int ncob,
+                       int Cg, int Cog, float alpha) {
+  constexpr int NACC = CO_U * T;
+  const long tid = static_cast<long>(blockIdx.x) * 256 + threadIdx.x;
+  if (tid >= static_cast<long>(npairs) * NACC * 64) return;
+  const int lane = static_cast<int>(tid & 63);
+  const long r = tid >> 6;
+  const int i = static_cast<int>(r % NACC), pair = static_cast<int>(r / NACC);
+  const long slab = static_cast<long>(npairs) * NACC * 256;
+  const float *p = ws + (static_cast<long>(pair) * NACC + i) * 256 + 4 * lane;
+  f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < nsplit; ++k) s += *reinterpret_cast<const f32x4 *>(p + k * slab);
+  const int per_g = ncob * nciu;
+  const int g = pair / per_g, rem = pair - g * per_g;
+  const int cob = rem / nciu, ciu = rem - cob * nciu;
+  const int t = i / CO_U, m = i - t * CO_U;
+  const int ci = ciu * 16 + (lane & 15);
+  const int co = g * Cog + cob * 16 * CO_U + 16 * m + 4 * (lane >> 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dw[(static_cast<long>(co + j) * T + t) * Cg + ci] += alpha * s[j];
+}
+
+// splits S (stage ranges) from the request (0: fill ~256 CUs); returns stages per split
+template <int H, int W, int KS, int R, int CO_U, int NWV>
+int wt_splits(int N, int npairs, int splits, int &S) {
+  using G = Wt<H, W, KS, R, CO_U, NWV>;
+  const int nstages = N * G::NB;
+  S = splits > 0 ? splits : 256 / npairs;
+  S = S < 1 ? 1 : (S > nstages ? nstages : S);
+  const int per = (nstages + S - 1) / S;
+  S = (nstages + per - 1) / per;
+  return per;
+}
+
+template <int H, int W, int KS, int R, int CO_U, int NWV>
+long ws_wt(int N, int Cg, int Cog, int groups, int splits) {
+  using G = Wt<H, W, KS, R, CO_U, NWV>;
+  const int npairs = groups * (Cg / 16) * (Cog / (16 * CO_U));
+  int S;
+  wt_splits<H, W, KS, R, CO_U, NWV>(N, npairs, splits, S);
+  return static_cast<long>(S) * npairs * G::NACC * 256;
+}
+
+template <int H, int W, int KS, int R, int CO_U, int NWV>
+int launch_wt(const bf16_t *x, const bf16_t *dy, float *dw, float *ws, long ws_floats, int N, int C, int ldy, int Cg,
+              int Cog, int groups, int splits, float alpha, hipStream_t s) {
+  using G = Wt<H, W, KS, R, CO_U, NWV>;
+  const int nciu = Cg / 16, ncob = Cog / (16 * CO_U);
+  const int npairs = groups * nciu * ncob;
+  int S;
+  const int per = wt_splits<H, W, KS, R, CO_U, NWV>(N, npairs, splits, S);
+  if (ws_floats < static_cast<long>(S) * npairs * G::NACC * 256) return -4;
+  CXN_LAUNCH((conv_wgrad_taps<H, W, KS, R, CO_U, NWV>), dim3(static_cast<unsigned>(npairs * S)), dim3(NWV * 64), 0, s,
+             x, dy, ws, N, C, ldy, Cg, Cog, npairs, nciu, ncob, per, N * G::NB);
+  const long blocks = (static_cast<long>(npairs) * G::NACC * 64 + 255) / 256;
+  CXN_LAUNCH((conv_wgrad_taps_reduce<G::T, CO_U>), dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, ws, dw, S,
+             npairs, nciu, ncob, Cg, Cog, alpha);
+  return 0;
+}
+
 }  // namespace
 
-// Served: stride 1, "same" padding (pad = (K - 1) / 2), K = 3, 13 x 13 maps; input channels per
-// group a multiple of 32, output channels per group a multiple of 64; x / dy pixel strides (C,
+// Served: stride 1, "same" padding (pad = (K - 1) / 2); K = 3 on 13 x 13 maps with input channels
+// per group a multiple of 32, or K = 5 on 27 x 27 maps (no db) with a multiple of 16; output
+// channels per group a multiple of 64; x / dy pixel strides (C,
 // ldy) multiples of 8.  ws == nullptr: returns the workspace size in floats (0: not served).
 // Otherwise launches the kernel and the split reduction into dw (fp32 [Cout][K][K][Cg], +=
 // alpha * gradient) and, when db is given, the bias gradient (fp32 [Cout], += alpha * sum of dy
@@ -487,10 +761,18 @@ CXN_API long cxn_conv_wgrad_direct(const void *x, const void *dy, float *dw, flo
                                    int W, int C, int ldy, int Cg, int Cog, int groups, int KH, int KW, int pad_h,
                                    int pad_w, int stride, int splits, float alpha, void *stream) {
   if (stride != 1 || KH != KW || pad_h != pad_w || pad_h != (KH - 1) / 2) return ws ? -1 : 0;
-  if (Cg % 32 || Cog % 64 || C % 8 || ldy % 8 || groups < 1 || C < groups * Cg || ldy < groups * Cog) return ws ? -1 : 0;
+  if (Cg % 16 || Cog % 64 || C % 8 || ldy % 8 || groups < 1 || C < groups * Cg || ldy < groups * Cog) return ws ? -1 : 0;
+  if (KH == 3 && Cg % 32) return ws ? -1 : 0;
   if (static_cast<long>(N) * H * W * (C > ldy ? C : ldy) >= (1L << 30)) return ws ? -1 : 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bf16_t *xb = static_cast<const bf16_t *>(x), *dyb = static_cast<const bf16_t *>(dy);
+  if (KH == 5 && H == 27 && W == 27 && db == nullptr && Cg % 16 == 0 && Cog % 64 == 0) {  // tap-split form (conv2)
+    // eight waves (2 per SIMD, K-steps alternating) over four: 119 vs 141 us at AlexNet b256
+    if (!ws) return ws_wt<27, 27, 5, 14, 4, 8>(N, Cg, Cog, groups, splits);
+    const int rc = launch_wt<27, 27, 5, 14, 4, 8>(xb, dyb, dw, ws, ws_floats, N, C, ldy, Cg, Cog, groups, splits, alpha, s);
+    if (rc != 0) return rc;
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+  }
   if (KH == 3 && H == 13 && W == 13) {
     if (!ws) return ws_wd<13, 13, 3, 2>(N, Cg, Cog, groups, splits);
     const int rc = launch_wd<13, 13, 3, 2>(xb, dyb, dw, db, ws, ws_floats, N, C, ldy, Cg, Cog, groups, splits, alpha, s);

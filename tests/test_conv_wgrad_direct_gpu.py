@@ -87,3 +87,34 @@ def test_wgrad_direct_declines_unserved_shapes():
     dy = _rnd((2, 13, 13, 64), 6)
     dw = torch.zeros((64, 3, 3, 48), device=DEV)
     assert not gemm.conv_wgrad_direct(x, dy, dw, ConvGeom(2, 13, 13, 48, 13, 13, 64, 3, 3, 1, 1, 1, 1))
+
+
+# AlexNet conv2 (27 x 27, 5 x 5, 48 input / 128 output channels per group): the tap-split form,
+# two 14 / 13-row bands per image, no bias gradient (conv2's comes from the pool behind it)
+CASES5 = [
+    (256, 96, 256, 2, 0),
+    (32, 96, 256, 2, 0),
+    (3, 48, 64, 1, 0),    # odd N, one channel pair
+    (5, 32, 128, 1, 3),   # two input-channel units, forced splits
+]
+
+
+@pytest.mark.parametrize("case", CASES5, ids=lambda c: "x".join(map(str, c)))
+def test_wgrad_direct_5x5_bands(case):
+    N, C, Cout, groups, splits = case
+    g = ConvGeom(N, 27, 27, C, 27, 27, Cout, 5, 5, 1, 2, 2, groups)
+    x = _rnd((N, 27, 27, C), 11)
+    dy = _rnd((N, 27, 27, Cout), 12)
+    dw = torch.full((Cout, 5, 5, C // groups), 0.5, device=DEV)
+    assert gemm.conv_wgrad_direct(x, dy, dw, g, splits=splits)
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (Cout, C // groups, 5, 5),
+                                      dy.float().permute(0, 3, 1, 2), stride=1, padding=2, groups=groups)
+    err = _err((dw - 0.5).permute(0, 3, 1, 2), ref)
+    assert err < 1e-5, err
+    dw2 = torch.full_like(dw, 0.5)
+    assert gemm.conv_wgrad_direct(x, dy, dw2, g, splits=splits)
+    torch.cuda.synchronize()
+    assert torch.equal(dw, dw2)  # fixed split order, no atomics
+    db = torch.zeros(Cout, device=DEV)
+    assert not gemm.conv_wgrad_direct(x, dy, dw2, g, splits=splits, db=db)  # no bias-gradient form: not served
