@@ -973,6 +973,28 @@ def conv_wgrad_direct(x, dy, dw, g: ConvGeom, splits: int = 0, db=None) -> bool:
     return True
 
 
+def conv_wgrad_rowrun(x, dy, dw, g: ConvGeom) -> bool:
+    """dw += the weight gradient of a few-channel pad-0 first layer (AlexNet conv1 class) on the
+    direct kernel-row-run kernel (conv_wgrad_direct.hip conv_wgrad_rowrun: transposed LDS reads
+    straight out of staged input rows, fixed-order partial sums); False when not served."""
+    if _WGD == "0" or _glds_cfg["tile"] >= 0 or not _native_t(x) or g.groups != 1 or g.pad_y or g.pad_x:
+        return False
+    if not x.is_contiguous() or _pix(x) != g.C or dy.stride(-1) != 1 or not dw.is_contiguous():
+        return False
+    k = native.kernels()
+    args = (g.N, g.H, g.W, g.C, g.Ho, g.Wo, g.Cout, _pix(dy), g.KH, g.KW, g.stride)
+    need = int(k.cxn_conv_wgrad_rowrun(None, None, None, None, 0, *args, 1.0, None))
+    if need <= 0:
+        return False
+    ws = _wgd_workspace(need, dw.device)
+    rc = int(k.cxn_conv_wgrad_rowrun(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), ws.data_ptr(), ws.numel(), *args, 1.0,
+                                     _stream()))
+    if rc == -1:
+        return False
+    native.check(rc, "conv_wgrad_rowrun")
+    return True
+
+
 def conv_backward_weight(x, dy, dw, g: ConvGeom, db=None) -> bool:
     """dw += sum over pixels of dy (x) im2col(x).  dw fp32 [Cout][KH][KW][Cg].  db (fp32 [Cout],
     optional): the kernel may also add the bias gradient (sum of dy over pixels); returns True
@@ -1012,6 +1034,8 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom, db=None) -> bool:
     rowrun = va != 8 and rowrun_ok(g)
     if conv_wgrad_direct(x, dy, dw, g, db=db):  # deterministic as well: no atomics, fixed split order
         return db is not None
+    if rowrun and conv_wgrad_rowrun(x, dy, dw, g):  # (likewise)
+        return False
     if _DET["on"] and not (rowrun and cg % va):
         # one fp32 slab per K slice, summed in slice order into dw: bitwise reproducible
         tile = _pick(WGRAD_TILES, kd, g.cg_out, g.groups, min_blocks=1)
