@@ -24,9 +24,15 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--groups", default="8", help="tile-order groups (ops.gemm.set_tile_group) to A/B")
+    ap.add_argument("--flush", type=int, default=1,
+                    help="overwrite 1 GB before every timed call (w / m then come from HBM, as in a training step)")
+    ap.add_argument("--ops", default="fc6,fc7")
     a = ap.parse_args()
+    junk = torch.empty(1 << 28, device="cuda") if a.flush else None
     B = a.batch
-    for name, nin, nout in (("fc6", 9216, 4096), ("fc7", 4096, 4096)):
+    for name, nin, nout in (("fc6", 9216, 4096), ("fc7", 4096, 4096), ("fc8", 4096, 1000)):
+        if name not in a.ops.split(","):
+            continue
         g = torch.Generator(device="cuda").manual_seed(1)
         x = torch.randn(B, nin, device="cuda", generator=g).to(torch.bfloat16)
         dy = torch.randn(B, nout, device="cuda", generator=g).to(torch.bfloat16)
@@ -43,15 +49,19 @@ def main():
                 G.set_tile_group(gi)
                 assert ops.fc_backward_weight_sgd(x, dy, w, m, wb, 1e-6, 0.0, 0.9, 0.0)
                 torch.cuda.synchronize()
-                s.record()
+                tot = 0.0
                 for _ in range(a.iters):
+                    if junk is not None:
+                        junk.fill_(1.0)
+                    s.record()
                     ops.fc_backward_weight_sgd(x, dy, w, m, wb, 1e-6, 0.0, 0.9, 0.0)
-                e.record()
-                e.synchronize()
-                times[arm].append(s.elapsed_time(e) * 1e3 / a.iters)
+                    e.record()
+                    e.synchronize()
+                    tot += s.elapsed_time(e) * 1e3
+                times[arm].append(tot / a.iters)
         G.set_glds(True, -1)
         G.set_tile_group(8)
-        rec = {"op": name, "batch": B}
+        rec = {"op": name, "batch": B, "mode": os.environ.get("CXN_SGD_MODE", "0"), "flush": a.flush}
         for (t, gi), v in times.items():
             us = statistics.median(v)
             tag = (f"t{t}" if t >= 0 else "tdef") + f"g{gi}"

@@ -28,58 +28,15 @@
 //     read the same images share an L2.  No atomics: each block stores its partial tile with
 //     plain coalesced 16-byte stores into a workspace, and conv_wgrad_direct_reduce sums the
 //     splits in a fixed order into dW (+=), so the result is bitwise reproducible.
-#include "gemm_glds_common.h"
+#include "direct_common.h"
 
 using namespace cxg;
+using namespace cxd;
 
 namespace {
 
-// One 1-KiB LDS-DMA (16 bytes per lane) as inline asm: hipcc cannot tell the LDS bytes it writes
-// from the ones the ds_reads of the current stage touch, and for the builtin it inserts a
-// vmcnt(0) before the first ds_read after the DMAs -- the next stage's loads would then be waited
-// for at the start of the current stage instead of landing under its MFMAs.  Completion is
-// counted by hand (wait_vmcnt + barrier at the end of the stage).  M0 is saved and restored in
-// the statement (compiler-reserved).
-__device__ __forceinline__ void dma16d(rsrc_t r, uint32_t lds_addr, uint32_t voff) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(voff), "s"(r), "s"(lds_addr) : "memory");
-}
-
-template <int N>
-__device__ __forceinline__ void wait_lgkm_d() {
-  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// accumulators beyond the 256-register AGPR file live in VGPRs (gfx950 MFMAs take either)
-template <bool AGPR>
-__device__ __forceinline__ void mfma_d(f32x4 &acc, const bf16x8 &a, const bf16x8 &b) {
-  if constexpr (AGPR) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-  else asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
-}
-// bias-gradient MFMA: its B operand (the ones fragment) lives in VGPRs that hipcc may have just
-// (re)written with a VALU move; "s_nop 1" covers the VALU-write -> MFMA-operand wait states hipcc
-// does not insert for inline asm
-__device__ __forceinline__ void mfma_db(f32x4 &acc, const bf16x8 &a, const bf16x8 &b) {
-  asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
-}
-template <bool AGPR>
-__device__ __forceinline__ void pin_d(f32x4 &acc) {
-  if constexpr (AGPR) asm volatile("" : "+a"(acc));
-  else asm volatile("" : "+v"(acc));
-}
 constexpr int NAGPR_ACC = 56;  // f32x4 accumulators kept in AGPRs (224 of the 256)
 
-// two transposed 8-byte reads (k-rows 8 g4 + q and 8 g4 + 4 + q) -> one 16x16x32 operand fragment
-__device__ __forceinline__ bf16x8 frag_d(const char *p0, const char *p1) {
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p0));
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p1));
-  typedef short s16x8 __attribute__((ext_vector_type(8)));
-  const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, r);
-}
-
-constexpr int fdiv_floor(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 
 template <int H, int W, int KS, int IPS>
 struct Wd {
@@ -748,260 +705,6 @@ int launch_wt(const bf16_t *x, const bf16_t *dy, float *dw, float *ws, long ws_f
 }
 
 
-// ---------------------------------------------------------------------------------------------
-// Few-channel, pad-0, strided first layer (AlexNet conv1: 3 channels on 228-pixel rows, 11 x 11 /
-// 4, 96 outputs), weight gradient  dW[co][kh][kw c] = sum_p dy[p][co] x[S oy + kh][S ox + kw][c].
-// The GEMM's N index is (kernel row kh, position j of the row's KW C run): for one output pixel
-// the KW C values of kernel row kh are CONTIGUOUS in the input row, at byte 2 S C ox.  A
-// transposed LDS read (ds_read_b64_tr_b16) takes per lane one address of 4 consecutive N
-// elements of one K row (pixel), so the B operand is read straight out of staged input rows:
-// address = row(S oy_local + kh) + 2 S C ox + 8 j4 (j4: 4-element chunk of the run, runs padded
-// to NCH chunks; the pad elements read the next pixel's values and their dW columns are
-// dropped).  No im2col, no row-padded buffers.
-//   * Work item = RG output rows of one image: its S (RG - 1) + KH input rows are one
-//     contiguous span of x and its RG Wo dy pixels another; both land by LDS-DMA in a double
-//     buffer (next item's pieces spread over this item's K-steps).  Past the image end the
-//     descriptors return zeros (a short last row group).
-//   * dy image [pixel][COUT] with each pixel's 16-byte channel chunks rotated by 2 on pixels with
-//     bit 2 set: the 8 pixels of a transposed read's half-wave then hit 8 distinct bank groups.
-//   * Block = 8 waves (2 per SIMD), tile = all COUT x all KH NCH 4 columns; wave (m half, n
-//     quarter) holds MT/2 x ~NTN/4 accumulators.  Persistent: a block walks a contiguous item
-//     range, stores its partial tile once; two fixed-order passes sum the partials into dW.
-template <int KH, int KW, int C, int S, int WP, int WO, int COUT, int RG>
-struct Rr {
-  static constexpr int ROWB = WP * C * 2;                          // input row bytes
-  static constexpr int XROWS = S * (RG - 1) + KH;                  // input rows per item
-  static constexpr int NXQ = (XROWS * ROWB + 1023) / 1024, XB = NXQ * 1024;
-  static constexpr int PIX = RG * WO;                              // output pixels per item
-  static constexpr int NK = (PIX + 31) / 32;                       // K-steps per item
-  static constexpr int PB = COUT * 2;                              // dy bytes per pixel
-  static constexpr int NDQ = (NK * 32 * PB + 1023) / 1024, DB = NDQ * 1024;
-  static constexpr int BUF = XB + DB;
-  static constexpr int NQ = NXQ + NDQ, NQW = (NQ + 7) / 8;         // DMA pieces (per wave)
-  static constexpr int NCH = (KW * C + 3) / 4;                     // 4-element chunks per kernel row
-  static constexpr int NTN = (KH * NCH + 3) / 4;                   // 16-column N tiles
-  static constexpr int MT = COUT / 16, MTW = MT / 2;               // M tiles (per wave)
-  static constexpr int TPW = (NTN + 3) / 4;                        // N tiles per wave (max)
-  static constexpr int SLAB = MT * NTN * 256;                      // floats per partial tile
-  static_assert(COUT % 32 == 0 && PB % 16 == 0 && ROWB % 8 == 0 && (S * C * 2) % 8 == 0, "alignment");
-  static_assert(2 * BUF <= 160 * 1024, "LDS");
-  static_assert(NK >= 3, "DMA spread");
-  static_assert(S * C * 2 * (WO - 1) + 8 * NCH <= ROWB, "runs stay inside a staged row");
-};
-
-template <int KH, int KW, int C, int S, int WP, int WO, int COUT, int RG>
-__global__ void __launch_bounds__(512, 1)
-conv_wgrad_rowrun(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, float *__restrict__ ws, int H, int Ho,
-                  int ldy, int nitems, int per) {
-  using G = Rr<KH, KW, C, S, WP, WO, COUT, RG>;
-  constexpr int NK = G::NK, BUF = G::BUF, XB = G::XB, NXQ = G::NXQ, NQ = G::NQ, NQW = G::NQW;
-  constexpr int NCH = G::NCH, NTN = G::NTN, MTW = G::MTW, TPW = G::TPW, PB = G::PB, ROWB = G::ROWB;
-  constexpr int IG = 0;  // (unused)
-  (void)IG;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int mh = wave & 1, nq = wave >> 1;
-  const int groups_per_img = (Ho + RG - 1) / RG;
-  const int ib = blockIdx.x * per, ie = min(nitems, ib + per);
-  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void *)smem)));
-
-  // DMA: piece q = wave + 8 i; q < NXQ: x bytes 1024 q + 16 lane of the item's span; else dy
-  // LDS bytes b = 1024 (q - NXQ) + 16 lane: pixel b / PB, stored chunk (b % PB) / 16 holding
-  // channel chunk (stored - rot) mod (PB / 16), rot = 2 on pixels with bit 2 set
-  uint32_t vq[NQW];
-#pragma unroll
-  for (int i = 0; i < NQW; ++i) {
-    const int q = wave + 8 * i;
-    uint32_t v = OOB;
-    if (q < NXQ) {
-      v = static_cast<uint32_t>(1024 * q + 16 * lane);
-    } else if (q < NQ) {
-      const int b = 1024 * (q - NXQ) + 16 * lane, pix = b / PB, st = (b % PB) / 16;
-      const int cc = (st - 2 * ((pix >> 2) & 1) + PB / 16) % (PB / 16);
-      if (pix < G::PIX) v = static_cast<uint32_t>((pix * ldy + 8 * cc) * 2);
-    }
-    vq[i] = v;
-  }
-  rsrc_t rx, rd;
-  auto prep = [&](int it) __attribute__((always_inline)) {
-    const int n = it / groups_per_img, oy0 = (it - n * groups_per_img) * RG;
-    const long xrow = static_cast<long>(n) * H + static_cast<long>(S) * oy0;
-    rx = make_rsrc(reinterpret_cast<const char *>(x) + xrow * ROWB, static_cast<uint32_t>((H - S * oy0) * ROWB));
-    const long dpix = (static_cast<long>(n) * Ho + oy0) * WO;
-    rd = make_rsrc(dy + dpix * ldy, static_cast<uint32_t>(static_cast<long>(Ho - oy0) * WO * ldy * 2));
-  };
-  auto issue_one = [&](int b, auto ic) __attribute__((always_inline)) {
-    constexpr int i = decltype(ic)::value;
-    const int q = wave + 8 * i;
-    if (q < NXQ) dma16d(rx, lds0 + static_cast<uint32_t>(b * BUF + q * 1024), vq[i]);
-    else if (q < NQ) dma16d(rd, lds0 + static_cast<uint32_t>(b * BUF + XB + (q - NXQ) * 1024), vq[i]);
-  };
-
-  // fragment addresses: K row (pixel) of lane for read hl: sl (frag_d's permutation), columns 4 p..
-  const int l16 = lane & 15, g4 = lane >> 4, p4 = l16 & 3;
-  int pa[NK][2];  // x: row(S oy_local) + 2 S C ox of pixel 32 k + sl
-#pragma unroll
-  for (int k = 0; k < NK; ++k)
-#pragma unroll
-    for (int hl = 0; hl < 2; ++hl) {
-      int pix = 32 * k + (((g4 >> 1) << 4) | (hl << 3) | ((g4 & 1) << 2) | (l16 >> 2));
-      pix = pix < G::PIX ? pix : G::PIX - 1;  // pad pixels (zero dy) read any staged pixel
-      const int oyl = pix / WO, ox = pix - oyl * WO;
-      pa[k][hl] = S * oyl * ROWB + S * C * 2 * ox;
-    }
-  int ca[TPW];  // x: row(kh) + 8 j4 of the lane's chunk in N tile nq + 4 tt
-#pragma unroll
-  for (int tt = 0; tt < TPW; ++tt) {
-    int c = 4 * (nq + 4 * tt) + p4;
-    c = c < KH * NCH ? c : KH * NCH - 1;
-    ca[tt] = (c / NCH) * ROWB + 8 * (c % NCH);
-  }
-  int da[MTW][2];  // dy: pixel sl, channel chunk (16 mt + 4 p4) / 8 rotated, half p4 & 1
-#pragma unroll
-  for (int j = 0; j < MTW; ++j)
-#pragma unroll
-    for (int hl = 0; hl < 2; ++hl) {
-      const int sl = ((g4 >> 1) << 4) | (hl << 3) | ((g4 & 1) << 2) | (l16 >> 2);
-      const int mt = mh * MTW + j, cc = (2 * mt + (p4 >> 1) + 2 * (g4 & 1)) % (PB / 16);
-      da[j][hl] = XB + sl * PB + cc * 16 + 8 * (p4 & 1);
-    }
-  const int ntn = nq + 4 * (TPW - 1) < NTN ? TPW : TPW - 1;  // this wave's N tiles
-
-  f32x4 acc[MTW][TPW];
-#pragma unroll
-  for (int j = 0; j < MTW; ++j)
-#pragma unroll
-    for (int tt = 0; tt < TPW; ++tt) {
-      acc[j][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      asm volatile("" : "+a"(acc[j][tt]));
-    }
-  bf16x8 fa[2][MTW], fb[2][TPW];
-  constexpr int NR = MTW + TPW, NM = MTW * TPW, RS = NM / NR > 0 ? NM / NR : 1;
-  auto read_one = [&](const char *buf, auto kc, auto sc, auto rc) __attribute__((always_inline)) {
-    constexpr int k = decltype(kc)::value, st = decltype(sc)::value, r = decltype(rc)::value;
-    if constexpr (r < MTW) {
-      fa[st][r] = frag_d(buf + da[r][0] + 32 * k * PB, buf + da[r][1] + 32 * k * PB);
-    } else {
-      constexpr int tt = r - MTW;
-      fb[st][tt] = frag_d(buf + pa[k][0] + ca[tt], buf + pa[k][1] + ca[tt]);
-    }
-  };
-
-  if (ib < ie) {
-    prep(ib);
-    static_for<NQW>([&](auto ic) { issue_one(0, ic); });
-  }
-  for (int it = ib; it < ie; ++it) {
-    const int b = (it - ib) & 1;
-    wait_vmcnt<0>();
-    block_barrier();
-    const bool more = it + 1 < ie;
-    if (more) prep(it + 1);
-    const char *buf = smem + b * BUF;
-    static_for<NR>([&](auto rc) { read_one(buf, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, rc); });
-    static_for<NK>([&](auto kc) {
-      constexpr int k = decltype(kc)::value, s0 = k & 1;
-      static_for<NM>([&](auto qc) {
-        constexpr int q = decltype(qc)::value;
-        constexpr int tt = q / MTW, j = q % MTW;
-        __builtin_amdgcn_sched_barrier(0);
-        if (tt < ntn) mfma_d<true>(acc[j][tt], fa[s0][j], fb[s0][tt]);
-        static_for<NQW>([&](auto ic) {
-          constexpr int i = decltype(ic)::value;
-          constexpr int js = i * (NK - 1) / NQW, first = (js * NQW + NK - 2) / (NK - 1);
-          if constexpr (js == k && q == 2 * (i - first) + 1) {
-            if (more) issue_one(b ^ 1, ic);
-          }
-        });
-        if constexpr (k + 1 < NK) {
-          if constexpr (q % RS == RS - 1 && q / RS < NR)
-            read_one(buf, std::integral_constant<int, k + 1>{}, std::integral_constant<int, s0 ^ 1>{},
-                     std::integral_constant<int, q / RS>{});
-          if constexpr (q == NM - 1 && NM / RS < NR)
-            static_for<NR - NM / RS>([&](auto rc) {
-              read_one(buf, std::integral_constant<int, k + 1>{}, std::integral_constant<int, s0 ^ 1>{},
-                       std::integral_constant<int, NM / RS + decltype(rc)::value>{});
-            });
-        }
-      });
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  }
-  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-#pragma unroll
-  for (int j = 0; j < MTW; ++j)
-#pragma unroll
-    for (int tt = 0; tt < TPW; ++tt) pin_d<true>(acc[j][tt]);
-  // partial tile: ws[block][mt][nt][lane] (f32x4)
-  float *out = ws + static_cast<long>(blockIdx.x) * G::SLAB + 4 * lane;
-#pragma unroll
-  for (int tt = 0; tt < TPW; ++tt)
-    if (tt < ntn) {
-#pragma unroll
-      for (int j = 0; j < MTW; ++j)
-        *reinterpret_cast<f32x4 *>(out + ((mh * MTW + j) * NTN + nq + 4 * tt) * 256) = acc[j][tt];
-    }
-}
-
-// fixed-order sums of the partial tiles: pass 1 (final == 0) sums groups of GS slabs into
-// out[group]; pass 2 sums the groups and adds alpha x the (kh, j < KW C) columns into dW
-template <int KH, int KW, int C, int MT, int NTN>
-__global__ void __launch_bounds__(256)
-conv_wgrad_rowrun_reduce(const float *__restrict__ in, int nslab, int gs, float *__restrict__ out, float *__restrict__ dw,
-                         float alpha, int final) {
-  constexpr int NCH = (KW * C + 3) / 4, NE = MT * NTN * 64;  // f32x4 units per slab
-  constexpr long SLAB = static_cast<long>(NE) * 4;
-  const long tid = static_cast<long>(blockIdx.x) * 256 + threadIdx.x;
-  const int grp = static_cast<int>(tid / NE), e = static_cast<int>(tid - static_cast<long>(grp) * NE);
-  if (grp * gs >= nslab) return;
-  const int s1 = min(nslab, grp * gs + gs);
-  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int sl = grp * gs; sl < s1; ++sl) acc += *reinterpret_cast<const f32x4 *>(in + sl * SLAB + 4L * e);
-  if (!final) {
-    *reinterpret_cast<f32x4 *>(out + grp * SLAB + 4L * e) = acc;
-    return;
-  }
-  const int lane = e & 63, t = e >> 6, mt = t / NTN, nt = t - mt * NTN;
-  const int c = 4 * nt + (lane & 15) / 4, jj = 4 * (c % NCH) + (lane & 3), kh = c / NCH;
-  if (kh >= KH || jj >= KW * C) return;
-  const int co = 16 * mt + 4 * (lane >> 4);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) dw[static_cast<long>(co + i) * KH * KW * C + kh * KW * C + jj] += alpha * acc[i];
-}
-
-template <int KH, int KW, int C, int S, int WP, int WO, int COUT, int RG>
-struct RrLaunch {
-  using G = Rr<KH, KW, C, S, WP, WO, COUT, RG>;
-  static constexpr int GS = 16;
-  static void plan(int N, int Ho, int &nitems, int &per, int &nblk) {
-    nitems = N * ((Ho + RG - 1) / RG);
-    per = (nitems + 255) / 256;
-    nblk = (nitems + per - 1) / per;
-  }
-  static long ws(int N, int Ho) {
-    int nitems, per, nblk;
-    plan(N, Ho, nitems, per, nblk);
-    return static_cast<long>(nblk + (nblk + GS - 1) / GS) * G::SLAB;
-  }
-  static int run(const bf16_t *x, const bf16_t *dy, float *dw, float *ws_, long ws_floats, int N, int H, int Ho, int ldy,
-                 float alpha, hipStream_t s) {
-    int nitems, per, nblk;
-    plan(N, Ho, nitems, per, nblk);
-    const int ngrp = (nblk + GS - 1) / GS;
-    if (ws_floats < static_cast<long>(nblk + ngrp) * G::SLAB) return -4;
-    CXN_LAUNCH((conv_wgrad_rowrun<KH, KW, C, S, WP, WO, COUT, RG>), dim3(static_cast<unsigned>(nblk)), dim3(512), 0, s, x,
-               dy, ws_, H, Ho, ldy, nitems, per);
-    float *part = ws_ + static_cast<long>(nblk) * G::SLAB;
-    constexpr int NE = G::MT * G::NTN * 64;
-    CXN_LAUNCH((conv_wgrad_rowrun_reduce<KH, KW, C, G::MT, G::NTN>), dim3(static_cast<unsigned>((ngrp * NE + 255) / 256)),
-               dim3(256), 0, s, ws_, nblk, GS, part, nullptr, 0.f, 0);
-    CXN_LAUNCH((conv_wgrad_rowrun_reduce<KH, KW, C, G::MT, G::NTN>), dim3(static_cast<unsigned>((NE + 255) / 256)),
-               dim3(256), 0, s, part, ngrp, ngrp, nullptr, dw, alpha, 1);
-    return 0;
-  }
-};
-
 }  // namespace
 
 // Served: stride 1, "same" padding (pad = (K - 1) / 2); K = 3 on 13 x 13 maps with input channels
@@ -1037,22 +740,3 @@ CXN_API long cxn_conv_wgrad_direct(const void *x, const void *dy, float *dw, flo
   return ws ? -1 : 0;
 }
 
-// Few-channel first layer weight gradient (conv_wgrad_rowrun above).  Served: the AlexNet conv1
-// class -- 3 channels on rows of 228 pixels (x contiguous, [N][H][228][3]), 11 x 11 / 4, pad 0,
-// 55 output columns, 96 outputs, one group; dy pixel stride ldy a multiple of 8.  dw fp32
-// [96][11][11][3] += alpha * gradient.  ws == nullptr: workspace floats (0: not served); else -1
-// not served, -4 workspace too small.
-CXN_API long cxn_conv_wgrad_rowrun(const void *x, const void *dy, float *dw, float *ws, long ws_floats, int N, int H,
-                                   int W, int C, int Ho, int Wo, int Cout, int ldy, int KH, int KW, int stride,
-                                   float alpha, void *stream) {
-  using L = RrLaunch<11, 11, 3, 4, 228, 55, 96, 4>;
-  const bool ok = C == 3 && W == 228 && Wo == 55 && Cout == 96 && KH == 11 && KW == 11 && stride == 4 && N > 0 &&
-                  Ho > 0 && H >= 4 * (Ho - 1) + 11 && ldy >= Cout && ldy % 8 == 0 &&
-                  static_cast<long>(H) * 228 * 3 * 2 < (1L << 31) && static_cast<long>(Ho) * Wo * ldy * 2 < (1L << 31);
-  if (!ok) return ws ? -1 : 0;
-  if (!ws) return L::ws(N, Ho);
-  const int rc = L::run(static_cast<const bf16_t *>(x), static_cast<const bf16_t *>(dy), dw, ws, ws_floats, N, H, Ho, ldy,
-                        alpha, static_cast<hipStream_t>(stream));
-  if (rc != 0) return rc;
-  return hipGetLastError() == hipSuccess ? 0 : -3;
-}

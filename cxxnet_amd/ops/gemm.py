@@ -607,6 +607,9 @@ _FEWC = os.environ.get("CXXNET_FEWC", "1") != "0"
 # direct row-run forward (conv_rowrun.hip: input rows staged once per 4 output rows) for the
 # few-channel pad-0 first layer (AlexNet conv1) instead of the K_ROWGATHER GEMM
 _ROWRUN_DIRECT = os.environ.get("CXXNET_ROWRUN_DIRECT", "1") != "0"
+# the AlexNet conv1 class on conv_rowrun_direct.hip's forward (flattened pixels x (kernel row,
+# 4-element chunk) GEMM out of staged input rows, no row-padded weight copy) ahead of both
+_ROWRUN_FWD2 = os.environ.get("CXXNET_ROWRUN_FWD2", "1") != "0"
 
 
 def fewc_ok(x, g: ConvGeom) -> bool:
@@ -678,6 +681,14 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
     if va != 8 and rowrun_ok(g) and (_use("cr") or g.C % 4):
         # few input channels (conv1: 11x11 taps of 4 channels): each kernel row's KW*C
         # elements are contiguous in NHWC; the GEMM reads them as zero-padded runs
+        if _ROWRUN_FWD2 and x.is_contiguous() and w.is_contiguous() and _pix(y) % 4 == 0 and y.stride(-1) == 1:
+            rc = native.kernels().cxn_conv_rowrun_fwd2(
+                x.data_ptr(), w.data_ptr(), bias.data_ptr() if bias is not None else None, y.data_ptr(), g.N, g.H, g.W,
+                g.C, g.Ho, g.Wo, g.Cout, _pix(y), g.KH, g.KW, g.stride, int(relu), _stream())
+            if rc == 0:
+                return
+            if rc != -1:
+                native.check(rc, "conv_rowrun_fwd2")
         wp, lp = _row_padded_weights(w, g)
         if _ROWRUN_DIRECT and x.is_contiguous() and y.shape[-1] == _pix(y):
             rc = native.kernels().cxn_conv_rowrun_fwd(

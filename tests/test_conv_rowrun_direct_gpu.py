@@ -1,8 +1,10 @@
-"""Few-channel first-layer weight gradient (conv_wgrad_direct.hip conv_wgrad_rowrun: AlexNet
-conv1, 3 channels on 228-pixel rows, 11 x 11 / 4, 96 outputs) against fp32 torch: the 1-GPU batch,
+"""Few-channel first-layer direct kernels (conv_rowrun_direct.hip: AlexNet conv1, 3 channels on
+228-pixel rows, 11 x 11 / 4, 96 outputs) against fp32 torch.  Weight gradient: the 1-GPU batch,
 the 8-GPU strong-scaling batch, odd image counts, a map whose last row group is short (14 output
 rows = 3 groups of 4 + 2), a channel-sliced dy, accumulation into dw, bitwise repeatability and
-the shapes it must refuse."""
+the shapes it must refuse.  Forward: the same batches and maps, bias / relu, an output channel
+slice of a wider buffer (nothing outside it written), and the conv_forward dispatch."""
+import torch.nn.functional as F
 import pytest
 import torch
 
@@ -75,3 +77,40 @@ def test_rowrun_wgrad_refuses(change):
     dy = _rnd((N, kw["Ho"], kw["Wo"], kw["Cout"]), 6)
     dw = torch.zeros((kw["Cout"], 11, 11, 3), device=DEV)
     assert not gemm.conv_wgrad_rowrun(x, dy, dw, g)
+
+
+@pytest.mark.parametrize("N,H,ldc,relu,bias", [(256, 227, 96, True, True), (32, 227, 96, False, True),
+                                               (3, 227, 96, True, False), (5, 63, 96, True, True),
+                                               (2, 63, 128, False, True)])
+def test_rowrun_fwd2(N, H, ldc, relu, bias):
+    from cxxnet_amd import native
+    g = _geo(N, H)
+    x = _rnd((N, H, 228, 3), 7)
+    w = (_rnd((96, 11, 11, 3), 8).float() * 0.05).to(torch.bfloat16)
+    b = torch.randn(96, device=DEV) if bias else None
+    yb = torch.full((N, g.Ho, 55, ldc), 7.0, device=DEV, dtype=torch.bfloat16)
+    y = yb[..., :96]
+    rc = native.kernels().cxn_conv_rowrun_fwd2(x.data_ptr(), w.data_ptr(), b.data_ptr() if bias else None, y.data_ptr(),
+                                               N, H, 228, 3, g.Ho, 55, 96, ldc, 11, 11, 4, int(relu),
+                                               torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, stride=4)
+    if relu:
+        ref = ref.clamp_min(0)
+    got = y.float().permute(0, 3, 1, 2)
+    assert ((got - ref).norm() / ref.norm()).item() < 5e-3
+    if ldc > 96:
+        assert torch.all(yb[..., 96:] == 7.0)  # nothing outside the slice
+
+
+def test_rowrun_fwd2_through_conv_forward():
+    g = _geo(4, 227)
+    x = _rnd((4, 227, 228, 3), 9)
+    w = (_rnd((96, 11, 11, 3), 10).float() * 0.05).to(torch.bfloat16)
+    b = torch.randn(96, device=DEV)
+    y = torch.empty((4, 55, 55, 96), device=DEV, dtype=torch.bfloat16)
+    gemm.conv_forward(x, w, b, y, g, relu=True)
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, stride=4).clamp_min(0)
+    assert ((y.float().permute(0, 3, 1, 2) - ref).norm() / ref.norm()).item() < 5e-3
