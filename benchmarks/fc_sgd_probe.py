@@ -24,8 +24,9 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--groups", default="8", help="tile-order groups (ops.gemm.set_tile_group) to A/B")
-    ap.add_argument("--flush", type=int, default=1,
-                    help="overwrite 1 GB before every timed call (w / m then come from HBM, as in a training step)")
+    ap.add_argument("--flush", type=int, default=0,
+                    help="overwrite 1 GB before every timed call (w / m then come from HBM; the fill's dirty lines "
+                         "are written back during the call, so times read high)")
     ap.add_argument("--ops", default="fc6,fc7")
     a = ap.parse_args()
     junk = torch.empty(1 << 28, device="cuda") if a.flush else None
@@ -61,7 +62,7 @@ def main():
                 times[arm].append(tot / a.iters)
         G.set_glds(True, -1)
         G.set_tile_group(8)
-        rec = {"op": name, "batch": B, "mode": os.environ.get("CXN_SGD_MODE", "0"), "flush": a.flush}
+        rec = {"op": name, "batch": B, "flush": a.flush}
         for (t, gi), v in times.items():
             us = statistics.median(v)
             tag = (f"t{t}" if t >= 0 else "tdef") + f"g{gi}"

@@ -201,26 +201,6 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
 #pragma unroll
     for (int e = 0; e < 8; ++e) bias8[e] = (bias && ibase + il_b + e < Mi) ? bias[ibase + il_b + e] : 0.f;
   }
-  // (experiment) SGD epilogue mode 2: every pass's w / m loads issued before the first pass
-  constexpr int SG_LPR = WM / 4, SG_RPI = 64 / SG_LPR, SG_NJL = (16 + SG_RPI - 1) / SG_RPI;
-  f32x4 pw[EPI == EPI_F32_SGD ? NR : 1][SG_NJL], pm[EPI == EPI_F32_SGD ? NR : 1][SG_NJL];
-  if constexpr (EPI == EPI_F32_SGD) {
-    const int il = (lane % SG_LPR) * 4, i = ibase + il;
-    const int jl0 = lane < SG_LPR * SG_RPI ? lane / SG_LPR : 16;
-    if (E.sgd_mode == 2 && ((E.ldc & 3) == 0) && (i + 4 <= Mi)) {
-#pragma unroll
-      for (int n = 0; n < NR; ++n)
-#pragma unroll
-        for (int r = 0; r < SG_NJL; ++r) {
-          const int jl = jl0 + r * SG_RPI, j = jbase + n * 16 + jl;
-          if (jl < 16 && j < Nj) {
-            const long idx = static_cast<long>(j) * E.ldc + i;
-            pw[n][r] = *reinterpret_cast<const f32x4 *>(E.sgd_w + idx);
-            pm[n][r] = *reinterpret_cast<const f32x4 *>(E.sgd_m + idx);
-          }
-        }
-    }
-  }
 #pragma unroll
   for (int n = 0; n < NR; ++n) {
 #pragma unroll
@@ -339,22 +319,13 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
       const int jl0 = lane < LPR * RPI ? lane / LPR : 16;
       if (((E.ldc & 3) == 0) && (i + 4 <= Mi)) {
         f32x4 wv[NJL], mv[NJL];
-        const int mode = E.sgd_mode;
 #pragma unroll
         for (int r = 0; r < NJL; ++r) {
           const int jl = jl0 + r * RPI, j = jbase + n * 16 + jl;
           if (jl < 16 && j < Nj) {
             const long idx = static_cast<long>(j) * E.ldc + i;
-            if (mode == 2) {
-              wv[r] = pw[n][r];
-              mv[r] = pm[n][r];
-            } else if (mode == 1) {
-              wv[r] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(E.sgd_w + idx));
-              mv[r] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(E.sgd_m + idx));
-            } else {
-              wv[r] = *reinterpret_cast<const f32x4 *>(E.sgd_w + idx);
-              mv[r] = *reinterpret_cast<const f32x4 *>(E.sgd_m + idx);
-            }
+            wv[r] = *reinterpret_cast<const f32x4 *>(E.sgd_w + idx);
+            mv[r] = *reinterpret_cast<const f32x4 *>(E.sgd_m + idx);
           }
         }
 #pragma unroll
@@ -370,17 +341,9 @@ gemm_glds(GOperand A, GOperand B, GEpi E, int tiles_i, int tiles_j, int ksplit_t
               w4[e] = sgd_step(hy, v[e], mm, w4[e]);
               m4[e] = mm;
             }
-            if (mode == 1) {
-              __builtin_nontemporal_store(w4, reinterpret_cast<f32x4 *>(E.sgd_w + idx));
-              __builtin_nontemporal_store(m4, reinterpret_cast<f32x4 *>(E.sgd_m + idx));
-              typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-              __builtin_nontemporal_store(u32x2{pack2(w4[0], w4[1]), pack2(w4[2], w4[3])},
-                                          reinterpret_cast<u32x2 *>(E.sgd_wb + idx));
-            } else {
-              *reinterpret_cast<f32x4 *>(E.sgd_w + idx) = w4;
-              *reinterpret_cast<f32x4 *>(E.sgd_m + idx) = m4;
-              *reinterpret_cast<uint2 *>(E.sgd_wb + idx) = make_uint2(pack2(w4[0], w4[1]), pack2(w4[2], w4[3]));
-            }
+            *reinterpret_cast<f32x4 *>(E.sgd_w + idx) = w4;
+            *reinterpret_cast<f32x4 *>(E.sgd_m + idx) = m4;
+            *reinterpret_cast<uint2 *>(E.sgd_wb + idx) = make_uint2(pack2(w4[0], w4[1]), pack2(w4[2], w4[3]));
           }
         }
       } else {
@@ -737,8 +700,6 @@ CXN_API int cxn_gemm_glds_sgd(const CxnOperandG *a, const CxnOperandG *b, int ld
   fill(B, b, MN_DIRECT);
   GEpi E{nullptr, 0, ldc, alpha, nullptr, 0, 0, 0, 0, w, m, static_cast<bf16_t *>(wb), lr, wd, mom, clip, nullptr, 0, 0, nullptr,
          g_gemm_group_i, hyp};
-  static const int sgd_mode = [] { const char *e = getenv("CXN_SGD_MODE"); return e ? atoi(e) : 0; }();
-  E.sgd_mode = sgd_mode;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int rc = dispatch(MN_DIRECT, MN_DIRECT, EPI_F32_SGD, tile, A, B, E, 1, 1, s);
   if (rc != 0) return rc;

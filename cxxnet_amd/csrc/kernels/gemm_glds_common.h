@@ -64,7 +64,6 @@ struct GEpi {
   // out like out (same gstride / ldc) -- a data-gradient GEMM summing a second gradient into its
   // node instead of a separate add pass (the split after a sibling group, NeuralNet._fuse_siblings)
   const bf16_t *add;
-  int sgd_mode;  // (experiment) EPI_F32_SGD access variant
 };
 
 }  // namespace cxg
