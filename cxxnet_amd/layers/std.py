@@ -48,6 +48,7 @@ class FullConnectLayer(Layer):
         self._rows = 0
         self._gbuf = {}      # persistent gather sources / outputs (graph-capturable)
         self._xwork = None   # the forward's all-gather of x, waited in backprop
+        self._dywork = None  # world > 1: backprop's dy all-gather in flight
 
     def set_param(self, name, val):
         super().set_param(name, val)
@@ -155,14 +156,20 @@ class FullConnectLayer(Layer):
         drop = (d.seed, self.ctx.step_counter, 1.0 - d.threshold) if (d is not None and is_train) else None
         ops.fc_forward(x, self.w.wb, bias, nodes_out[0].mat(), relu=self.fuse_relu, drop=drop)
 
-    def _fused_sgd(self, x, dy, prop_grad, nodes_in, xw=None, dyw=None) -> bool:
+    def _dx_scratch(self, x):
+        if self._dx is None or self._dx.shape[0] < x.shape[0] or self._dx.shape[1] != x.shape[1]:
+            self._dx = torch.empty_like(x)
+        return self._dx[:x.shape[0]]
+
+    def _fused_sgd(self, x, dy, prop_grad, nodes_in, xw=None, dyw=None, gx=None) -> bool:
         """SGD step of the weights fused into the weight-gradient GEMM (ctx.sgd_fuse = the
         arena updater, set by the trainer when eligible): one GPU, or -- under data
         parallelism -- a fullc_gather layer, whose gradient is formed from the all-gathered
         rows (xw, dyw) and is the same global gradient on every rank.  The data gradient reads
         the OLD shadow weights, so it runs first, into a scratch buffer (x, which the
         weight-gradient still needs, lives where it goes); the scratch is copied back (with
-        relu' when fused) after the update."""
+        relu' when fused) after the update.  gx: that data gradient, already computed (the
+        gathered path runs it while the dy all-gather is in flight)."""
         upd = getattr(self.ctx, "sgd_fuse", None)
         if upd is None or not (getattr(self.ctx, "grad_overwrite", False) and self.w.overwrite) or not self.ctx.is_gpu:
             return False
@@ -178,6 +185,28 @@ class FullConnectLayer(Layer):
         a = upd.arena
         m = a.m1[spec.offset:spec.offset + spec.numel].view(spec.shape)
         side = getattr(self.ctx, "fc_side", None)
+        if side is not None and xw is not None:
+            # data parallel, gathered rows: the data gradient (local rows, old shadow weights) on
+            # the main stream, then the fused step on `side` -- it reads only the gathered copies,
+            # so the conv backward below runs beside it (joined at the end of NeuralNet.backprop)
+            if prop_grad and gx is None:
+                gx = self._dx_scratch(x)
+                ops.fc_backward_data(dy, spec.wb, gx, alpha=self.grad_alpha)
+            ready = torch.cuda.Event()
+            ready.record()
+            side.wait_event(ready)
+            with torch.cuda.stream(side):
+                ok = ops.fc_backward_weight_sgd(xw, dyw, spec.w, m, spec.wb, lr, wd, mom, clip, hyp)
+            self.ctx.fc_side_used = True
+            if ok:
+                upd.fused_offsets.add(spec.offset)
+            else:
+                torch.cuda.current_stream().wait_stream(side)
+                ops.fc_backward_weight(xw, dyw, spec.g, overwrite=True)
+            if gx is not None:
+                dst = nodes_in[0].gmat()
+                ops.channel_copy(gx, 0, dst, 0, dst.shape[1], mask_relu=self.grad_mask_relu)
+            return True
         if side is not None and xw is None:
             # side stream: x is copied aside (its buffer receives the data gradient), the data
             # gradient reads the old shadow weights on the main stream, then the fused step runs
@@ -205,11 +234,8 @@ class FullConnectLayer(Layer):
                 torch.cuda.current_stream().wait_stream(side)
                 ops.fc_backward_weight(self._xs, dy, spec.g, overwrite=True)
             return True
-        gx = None
-        if prop_grad:
-            if self._dx is None or self._dx.shape[0] < x.shape[0] or self._dx.shape[1] != x.shape[1]:
-                self._dx = torch.empty_like(x)
-            gx = self._dx[:x.shape[0]]
+        if prop_grad and gx is None:
+            gx = self._dx_scratch(x)
             ops.fc_backward_data(dy, spec.wb, gx, alpha=self.grad_alpha)
         xg, dyg = (x, dy) if xw is None else (xw, dyw)
         if ops.fc_backward_weight_sgd(xg, dyg, spec.w, m, spec.wb, lr, wd, mom, clip, hyp):
@@ -232,19 +258,42 @@ class FullConnectLayer(Layer):
             import torch.distributed as dist
             dsrc, dyw = self._gather_io("dy", dy, nodes_out[0].shape[0])
             x_all = self._gbuf["x"][1]
+            # world > 1: the dy all-gather runs while the data gradient (local rows, old weights)
+            # is formed into a scratch buffer -- x's buffer, where it goes, may still be the x
+            # gather's source; at world 1 there is nothing to overlap and the extra segment cut
+            # of a recorded step costs more (profiles/r5_dp_world1.md), so the gather comes first
+            early = dist.get_world_size() > 1
+            gx = None
+            if early:
+                def gather_dy_async():
+                    self._dywork = dist.all_gather_into_tensor(dyw, dsrc, async_op=True)
+                self._collective(gather_dy_async)
+                if prop_grad:
+                    gx = self._dx_scratch(x)
+                    ops.fc_backward_data(dy, self.w.wb, gx, alpha=self.grad_alpha)
 
             def gather_dy():
                 # the compute stream waits for both gathers (no host block)
-                dist.all_gather_into_tensor(dyw, dsrc)
+                if early:
+                    self._dywork.wait()
+                    self._dywork = None
+                else:
+                    dist.all_gather_into_tensor(dyw, dsrc)
                 if self._xwork is not None:
                     self._xwork.wait()
                     self._xwork = None
             self._collective(gather_dy)
-            if self._fused_sgd(x, dy, prop_grad, nodes_in, xw=x_all, dyw=dyw):
+            if self._fused_sgd(x, dy, prop_grad, nodes_in, xw=x_all, dyw=dyw, gx=gx):
                 if self.b is not None:
                     self.ctx.bias_grad(dy, self.b.g)
                 return
             ops.fc_backward_weight(x_all, dyw, self.w.g, overwrite=overwrite)
+            if gx is not None:
+                if self.b is not None:
+                    self.ctx.bias_grad(dy, self.b.g)
+                dst = nodes_in[0].gmat()
+                ops.channel_copy(gx, 0, dst, 0, dst.shape[1], mask_relu=self.grad_mask_relu)
+                return
         else:
             ops.fc_backward_weight(x, dy, self.w.g, overwrite=overwrite)
         if self.b is not None:

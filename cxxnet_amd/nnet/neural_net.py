@@ -735,8 +735,10 @@ class NeuralNet:
             self.ctx.flipped = seen
         side = self._bias_stream() if defer and hook is None else None
         # fused fc SGD steps (memory-bound: w / m / shadow streams) on a side stream, overlapping
-        # the compute-bound conv backward below them; joined at the end of the pass
-        self.ctx.fc_side = self._fc_side_stream() if self.ctx.is_gpu and hook is None else None
+        # the compute-bound conv backward below them; joined at the end of the pass.  Under data
+        # parallelism (a bucket hook) only the fullc_gather layers fuse, from their gathered rows
+        # (FullConnectLayer._fused_sgd)
+        self.ctx.fc_side = self._fc_side_stream(dp=hook is not None) if self.ctx.is_gpu else None
         self.ctx.fc_side_used = False
         with _BatchView(self):
             for i in range(len(self.connections) - 1, -1, -1):
@@ -774,15 +776,19 @@ class NeuralNet:
             self._side = torch.cuda.Stream(device=self.device)
         return self._side
 
-    def _fc_side_stream(self):
-        """Side stream of the fc weight-gradient GEMMs with the fused SGD step
-        (CXXNET_FC_SGD_SIDE=1): they stream each fc layer's fp32 master, momentum and bf16
-        shadow (18 B / parameter, AlexNet fc6: 680 MB) and so are HBM-bound, while the conv
-        backward that follows is MFMA-bound.  None (the default) keeps them on the main stream:
-        interleaved A/B on one MI355X, AlexNet b256 2.320 -> 2.375 ms and VGG-16 b64 9.40 ->
-        9.41 ms with the side stream (profiles/r3_ab_fc_sgd_side.jsonl) -- the concurrent HBM
-        stream slows the GEMMs it overlaps by more than it hides.  Not under HIP-graph capture."""
-        if os.environ.get("CXXNET_FC_SGD_SIDE", "0") != "1" or frozen():
+    def _fc_side_stream(self, dp=False):
+        """Side stream of the fc weight-gradient GEMMs with the fused SGD step: they stream
+        each fc layer's fp32 master, momentum and bf16 shadow (18 B / parameter, AlexNet fc6:
+        680 MB) and so are HBM-bound, while the conv backward that follows is MFMA-bound.
+        One GPU: off unless CXXNET_FC_SGD_SIDE=1 -- AlexNet b256 2.320 -> 2.375 ms and VGG-16 b64
+        9.40 -> 9.41 ms with it in round 3 (profiles/r3_ab_fc_sgd_side.jsonl), 1.801 / 1.806 vs
+        1.813 / 1.796 ms in round 6: the concurrent HBM stream slows the GEMMs it overlaps by as
+        much as it hides.  Data parallel (the fullc_gather layers' step from the gathered rows,
+        8x the GEMM work at world 8): on unless CXXNET_FC_SGD_SIDE=0 -- RCCL forced at world 1,
+        AlexNet b256 2.072 -> 2.014-2.024 ms (profiles/r6_dp_world1.md).  Not under HIP-graph
+        capture."""
+        env = os.environ.get("CXXNET_FC_SGD_SIDE", "")
+        if frozen() or env == "0" or (env != "1" and not dp):
             return None
         if getattr(self, "_fc_side", None) is None:
             self._fc_side = torch.cuda.Stream(device=self.device)

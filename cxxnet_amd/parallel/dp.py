@@ -62,6 +62,7 @@ class Bucket:
         self.agin = None      # sharded: all-gather source
         self.ready = False
         self.done = None      # event on the side stream: bucket reduced, updated (and gathered)
+        self.final = None     # event on the compute stream: the bucket's gradients are final
         self.pending = False  # done recorded but not yet waited for by the compute stream
 
     def own(self, rank, world):
@@ -226,6 +227,7 @@ class GradReducer:
         self.side = torch.cuda.Stream(device=self.arena.g.device)
         for b in self.buckets:
             b.done = torch.cuda.Event()
+            b.final = torch.cuda.Event()  # gradients final on the compute stream (reused every step)
         return True
 
     # ------------------------------------------------------------------ per step
@@ -266,9 +268,9 @@ class GradReducer:
             self._launch(b)
         if self.update_fn is None:
             return
-        ev = torch.cuda.current_stream().record_event()
+        b.final.record()
         with torch.cuda.stream(self.side):
-            self.side.wait_event(ev)
+            self.side.wait_event(b.final)
             if self.active:
                 b.work.wait()  # the side stream waits for the collective (no host block)
                 if self.shard and not self.inplace:
