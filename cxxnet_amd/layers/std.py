@@ -452,8 +452,13 @@ class ConvolutionLayer(Layer):
             ops.conv_forward(nodes_in[0].data, S["w_all"], S["b_all"], S["H"][:self.geo.N], self._sib_geo(S["ctot"]),
                              relu=self.fuse_relu)
             return
-        # few-channel stride-1 first layers (VGG conv1_1): the direct kernel pads on the
-        # fly; the zero-bordered copy is then built by the weight-gradient pass that needs it
+        # few-channel first layers on direct kernels that pad on the fly (GoogLeNet conv1: the
+        # row-run forward; VGG conv1_1: conv_fewc); a zero-bordered copy is then built only by a
+        # weight-gradient pass that needs it
+        if self.geo.C <= 4 and ops.gemm.conv_rowrun_fwd2(nodes_in[0].data, self.w.wb, bias, nodes_out[0].data,
+                                                         self.geo, relu=self.fuse_relu):
+            self._xpad_stale = True
+            return
         if ops.gemm.fewc_preferred(self.geo) and ops.gemm.conv_forward_fewc(
                 nodes_in[0].data, self.w.wb, bias, nodes_out[0].data, self.geo, relu=self.fuse_relu):
             self._xpad_stale = True
@@ -487,10 +492,13 @@ class ConvolutionLayer(Layer):
                         return
                 ops.conv_backward_data(H, S["w_all"], S["dx_node"].gdst, gall, S["wt"], wt_ready=ready)
             return
-        xw, geo = self._padded(x, getattr(self, "_xpad_stale", False))
-        self._xpad_stale = False
         want_db = self.b is not None and not self.bias_done and self.ctx.is_gpu
-        db_done = ops.conv_backward_weight(xw, dy, self.w.g, geo, db=self.b.g if want_db else None)
+        if self.geo.C <= 4 and self.ctx.is_gpu and ops.gemm.conv_wgrad_rowrun(x, dy, self.w.g, self.geo):
+            db_done = False  # (few-channel first layer, padding staged on the fly: no bordered copy)
+        else:
+            xw, geo = self._padded(x, getattr(self, "_xpad_stale", False))
+            self._xpad_stale = False
+            db_done = ops.conv_backward_weight(xw, dy, self.w.g, geo, db=self.b.g if want_db else None)
         if self.bias_done:  # summed by the max-pool behind this conv (NeuralNet._fuse_pool_bias)
             self.bias_done = False
         elif self.b is not None and not db_done:  # (db_done: summed by the weight-gradient kernel)

@@ -139,8 +139,8 @@ _SIGS = {
     "cxn_rec_free": [_P],
     "cxn_copy_d2d": [_P, _P, _L, _P],
     "cxn_conv_wgrad_direct": [_P, _P, _P, _P, _P, _L] + [_I] * 14 + [_F, _P],
-    "cxn_conv_wgrad_rowrun": [_P, _P, _P, _P, _L] + [_I] * 11 + [_F, _P],
-    "cxn_conv_rowrun_fwd2": [_P, _P, _P, _P] + [_I] * 12 + [_P],
+    "cxn_conv_wgrad_rowrun": [_P, _P, _P, _P, _L] + [_I] * 12 + [_F, _P],
+    "cxn_conv_rowrun_fwd2": [_P, _P, _P, _P] + [_I] * 13 + [_P],
     "cxn_conv_direct": [_P, _I, _P, _P, _P, _I, _P, _L, _P] + [_I] * 10 + [_P],
 }
 _RESTYPE = {"cxn_rec_end": ctypes.c_void_p, "cxn_rec_free": None, "cxn_conv_wgrad_direct": ctypes.c_long,

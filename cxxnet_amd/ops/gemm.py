@@ -621,6 +621,22 @@ _ROWRUN_DIRECT = os.environ.get("CXXNET_ROWRUN_DIRECT", "1") != "0"
 _ROWRUN_FWD2 = os.environ.get("CXXNET_ROWRUN_FWD2", "1") != "0"
 
 
+def conv_rowrun_fwd2(x, w, bias, y, g: ConvGeom, relu=False) -> bool:
+    """y = conv(x, w) + bias (relu) for a few-channel first layer on conv_rowrun_direct.hip's
+    forward (flattened pixels x (kernel row, 4-element chunk) GEMM out of staged input rows, no
+    row-padded weight copy): the AlexNet / GoogLeNet conv1 classes.  False when not served."""
+    if not (_ROWRUN_FWD2 and _native_t(x) and g.groups == 1 and g.pad_y == g.pad_x and x.is_contiguous()
+            and w.is_contiguous() and _pix(y) % 4 == 0 and y.stride(-1) == 1 and _pix(x) == g.C):
+        return False
+    rc = native.kernels().cxn_conv_rowrun_fwd2(
+        x.data_ptr(), w.data_ptr(), bias.data_ptr() if bias is not None else None, y.data_ptr(), g.N, g.H, g.W,
+        g.C, g.Ho, g.Wo, g.Cout, _pix(y), g.KH, g.KW, g.stride, g.pad_y, int(relu), _stream())
+    if rc == -1:
+        return False
+    native.check(rc, "conv_rowrun_fwd2")
+    return True
+
+
 def fewc_ok(x, g: ConvGeom) -> bool:
     """Few-channel first-layer forward kernel (conv_fewc.hip): 4-channel NHWC input, one group,
     16..128 output channels (multiple of 16), at most 64 taps, any stride / padding."""
@@ -659,6 +675,8 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
         return
     cg = g.cg_in
     va = 8 if cg % 8 == 0 else 4
+    if g.C == 4 and conv_rowrun_fwd2(x, w, bias, y, g, relu):  # padded 4-channel first layers (GoogLeNet conv1)
+        return
     if cg % va and not rowrun_ok(g):
         raise ValueError(f"conv: channels per group ({cg}) must be a multiple of 4 on the GPU path")
     kd = g.kdim
@@ -690,14 +708,8 @@ def conv_forward(x, w, bias, y, g: ConvGeom, relu=False):
     if va != 8 and rowrun_ok(g) and (_use("cr") or g.C % 4):
         # few input channels (conv1: 11x11 taps of 4 channels): each kernel row's KW*C
         # elements are contiguous in NHWC; the GEMM reads them as zero-padded runs
-        if _ROWRUN_FWD2 and x.is_contiguous() and w.is_contiguous() and _pix(y) % 4 == 0 and y.stride(-1) == 1:
-            rc = native.kernels().cxn_conv_rowrun_fwd2(
-                x.data_ptr(), w.data_ptr(), bias.data_ptr() if bias is not None else None, y.data_ptr(), g.N, g.H, g.W,
-                g.C, g.Ho, g.Wo, g.Cout, _pix(y), g.KH, g.KW, g.stride, int(relu), _stream())
-            if rc == 0:
-                return
-            if rc != -1:
-                native.check(rc, "conv_rowrun_fwd2")
+        if conv_rowrun_fwd2(x, w, bias, y, g, relu):
+            return
         wp, lp = _row_padded_weights(w, g)
         if _ROWRUN_DIRECT and x.is_contiguous() and y.shape[-1] == _pix(y):
             rc = native.kernels().cxn_conv_rowrun_fwd(
@@ -994,15 +1006,15 @@ def conv_wgrad_direct(x, dy, dw, g: ConvGeom, splits: int = 0, db=None) -> bool:
 
 
 def conv_wgrad_rowrun(x, dy, dw, g: ConvGeom) -> bool:
-    """dw += the weight gradient of a few-channel pad-0 first layer (AlexNet conv1 class) on the
-    direct kernel-row-run kernel (conv_wgrad_direct.hip conv_wgrad_rowrun: transposed LDS reads
-    straight out of staged input rows, fixed-order partial sums); False when not served."""
-    if _WGD == "0" or _glds_cfg["tile"] >= 0 or not _native_t(x) or g.groups != 1 or g.pad_y or g.pad_x:
+    """dw += the weight gradient of a few-channel first layer (AlexNet / GoogLeNet conv1 class) on
+    the direct kernel-row-run kernel (conv_rowrun_direct.hip conv_wgrad_rowrun: transposed LDS
+    reads straight out of staged input rows, fixed-order partial sums); False when not served."""
+    if _WGD == "0" or _glds_cfg["tile"] >= 0 or not _native_t(x) or g.groups != 1 or g.pad_y != g.pad_x:
         return False
     if not x.is_contiguous() or _pix(x) != g.C or dy.stride(-1) != 1 or not dw.is_contiguous():
         return False
     k = native.kernels()
-    args = (g.N, g.H, g.W, g.C, g.Ho, g.Wo, g.Cout, _pix(dy), g.KH, g.KW, g.stride)
+    args = (g.N, g.H, g.W, g.C, g.Ho, g.Wo, g.Cout, _pix(dy), g.KH, g.KW, g.stride, g.pad_y)
     need = int(k.cxn_conv_wgrad_rowrun(None, None, None, None, 0, *args, 1.0, None))
     if need <= 0:
         return False
@@ -1054,7 +1066,7 @@ def conv_backward_weight(x, dy, dw, g: ConvGeom, db=None) -> bool:
     rowrun = va != 8 and rowrun_ok(g)
     if conv_wgrad_direct(x, dy, dw, g, db=db):  # deterministic as well: no atomics, fixed split order
         return db is not None
-    if rowrun and conv_wgrad_rowrun(x, dy, dw, g):  # (likewise)
+    if g.C <= 4 and conv_wgrad_rowrun(x, dy, dw, g):  # few-channel first layers (likewise deterministic)
         return False
     if _DET["on"] and not (rowrun and cg % va):
         # one fp32 slab per K slice, summed in slice order into dw: bitwise reproducible

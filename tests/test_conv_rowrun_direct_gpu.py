@@ -1,5 +1,6 @@
 """Few-channel first-layer direct kernels (conv_rowrun_direct.hip: AlexNet conv1, 3 channels on
-228-pixel rows, 11 x 11 / 4, 96 outputs) against fp32 torch.  Weight gradient: the 1-GPU batch,
+228-pixel rows, 11 x 11 / 4, 96 outputs; GoogLeNet conv1, 4-channel NHWC 224 x 224, 7 x 7 / 2,
+pad 3, 64 outputs -- padding staged on the fly) against fp32 torch.  Weight gradient: the 1-GPU batch,
 the 8-GPU strong-scaling batch, odd image counts, a map whose last row group is short (14 output
 rows = 3 groups of 4 + 2), a channel-sliced dy, accumulation into dw, bitwise repeatability and
 the shapes it must refuse.  Forward: the same batches and maps, bias / relu, an output channel
@@ -91,7 +92,7 @@ def test_rowrun_fwd2(N, H, ldc, relu, bias):
     yb = torch.full((N, g.Ho, 55, ldc), 7.0, device=DEV, dtype=torch.bfloat16)
     y = yb[..., :96]
     rc = native.kernels().cxn_conv_rowrun_fwd2(x.data_ptr(), w.data_ptr(), b.data_ptr() if bias else None, y.data_ptr(),
-                                               N, H, 228, 3, g.Ho, 55, 96, ldc, 11, 11, 4, int(relu),
+                                               N, H, 228, 3, g.Ho, 55, 96, ldc, 11, 11, 4, 0, int(relu),
                                                torch.cuda.current_stream().cuda_stream)
     assert rc == 0
     torch.cuda.synchronize()
@@ -113,4 +114,42 @@ def test_rowrun_fwd2_through_conv_forward():
     gemm.conv_forward(x, w, b, y, g, relu=True)
     torch.cuda.synchronize()
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, stride=4).clamp_min(0)
+    assert ((y.float().permute(0, 3, 1, 2) - ref).norm() / ref.norm()).item() < 5e-3
+
+
+def _ggeo(N, H=224):
+    Ho = (H + 6 - 7) // 2 + 1
+    return ConvGeom(N, H, 224, 4, Ho, 112, 64, 7, 7, 2, 3, 3, 1)
+
+
+@pytest.mark.parametrize("N,H", [(128, 224), (32, 224), (3, 224), (2, 20)])
+def test_rowrun_googlenet_wgrad(N, H):
+    g = _ggeo(N, H)
+    x = _rnd((N, H, 224, 4), 21)
+    dy = _rnd((N, g.Ho, 112, 64), 22)
+    dw = torch.full((64, 7, 7, 4), 0.25, device=DEV)
+    assert gemm.conv_wgrad_rowrun(x, dy, dw, g)
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (64, 4, 7, 7), dy.float().permute(0, 3, 1, 2),
+                                      stride=2, padding=3)
+    err = (((dw - 0.25).permute(0, 3, 1, 2) - ref).norm() / ref.norm()).item()
+    assert err < 1e-5, err
+    dw2 = torch.full_like(dw, 0.25)
+    assert gemm.conv_wgrad_rowrun(x, dy, dw2, g)
+    torch.cuda.synchronize()
+    assert torch.equal(dw, dw2)
+
+
+@pytest.mark.parametrize("N,H,relu", [(128, 224, True), (32, 224, False), (3, 224, True), (2, 20, True)])
+def test_rowrun_googlenet_fwd(N, H, relu):
+    g = _ggeo(N, H)
+    x = _rnd((N, H, 224, 4), 23)
+    w = (_rnd((64, 7, 7, 4), 24).float() * 0.05).to(torch.bfloat16)
+    b = torch.randn(64, device=DEV)
+    y = torch.full((N, g.Ho, 112, 64), 7.0, device=DEV, dtype=torch.bfloat16)
+    assert gemm.conv_rowrun_fwd2(x, w, b, y, g, relu=relu)
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, stride=2, padding=3)
+    if relu:
+        ref = ref.clamp_min(0)
     assert ((y.float().permute(0, 3, 1, 2) - ref).norm() / ref.norm()).item() < 5e-3
