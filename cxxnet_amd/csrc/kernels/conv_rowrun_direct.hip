@@ -241,8 +241,10 @@ conv_wgrad_rowrun(const bf16_t *__restrict__ x, const bf16_t *__restrict__ dy, f
         if (tt < ntn) mfma_d<true>(acc[j][tt], fa[s0][j], fb[s0][tt]);
         static_for<NQW>([&](auto ic) {
           constexpr int i = decltype(ic)::value;
-          constexpr int js = i * (NK - 1) / NQW, first = (js * NQW + NK - 2) / (NK - 1);
-          if constexpr (js == k && q == 2 * (i - first) + 1) {
+          // the next item's DMAs go out during the first K-step (one after each MFMA): its
+          // compute is short against their latency (AlexNet b256 1.814 / 1.819 -> 1.800 / 1.806 ms
+          // against spreading them over the K-steps; GoogLeNet b128 unchanged)
+          if constexpr (k == 0 && q == i % NM) {
             if (more) issue_one(b ^ 1, ic);
           }
         });
@@ -504,8 +506,10 @@ conv_rowrun_fwd2(const bf16_t *__restrict__ x, const bf16_t *__restrict__ w, con
         else mfma_d<true>(acc[j][tt], av, fb[s0][tt]);
         static_for<NQW>([&](auto ic) {
           constexpr int i = decltype(ic)::value;
-          constexpr int js = i * (NK - 1) / NQW, first = (js * NQW + NK - 2) / (NK - 1);
-          if constexpr (js == k && q == 2 * (i - first) + 1) {
+          // the next item's DMAs go out during the first K-step (one after each MFMA): its
+          // compute is short against their latency (AlexNet b256 1.814 / 1.819 -> 1.800 / 1.806 ms
+          // against spreading them over the K-steps; GoogLeNet b128 unchanged)
+          if constexpr (k == 0 && q == i % NM) {
             if (more) issue_one(b ^ 1, ic);
           }
         });
