@@ -83,7 +83,7 @@ def main():
         H, C, Cout, K, pad, G = OPS[name]
         flop = 2.0 * a.batch * H * H * Cout * K * K * (C // G)
         t = sorted(ts)[len(ts) // 2]
-        print(json.dumps({"op": f"{name}_{op}", "path": path, "dbg": os.environ.get("CXN_CD_DBG", "0"), "batch": a.batch, "us": round(t, 1),
+        print(json.dumps({"op": f"{name}_{op}", "path": path, "batch": a.batch, "us": round(t, 1),
                           "tflops": round(flop / t / 1e6, 1), "rounds_us": [round(v, 1) for v in ts]}))
 
 

@@ -107,6 +107,8 @@ struct CdArgs {
 // NL > 0: NL more waves per block only issue the LDS-DMAs (an LDS-DMA costs its issuing wave
 // ~60-185 cycles of issue; on the MFMA waves that was ~17 % of the forward), the NW MFMA waves
 // only compute; both kinds meet at the one barrier per stage.
+// DBG: compile-time ablation bits used while tuning (1 / 2: skip the x / weight DMAs, 8: skip the
+// fragment reads, 16 / 32: skip the MFMAs / epilogue, 64-256: DMA tap spread); 0 in every launch.
 template <int H, int W, int KS, int IPB, int NF, int NW, int EPI, int DBG = 0, bool SB = false, int NL = 0>
 __global__ void __launch_bounds__(64 * (NW + NL), (SB || NW + NL == 8) ? 2 : 1) conv_direct(CdArgs a) {
   using G = Cd<H, W, KS, IPB, NF, NW>;
@@ -426,7 +428,6 @@ int launch_cd(CdArgs a, int epi, int variant, float *db, hipStream_t s) {
   a.nitems = nig * a.groups * a.ncob;
   a.nst = a.Cg / 32;
   const int sb = variant == 1;
-  static const int dbg = getenv("CXN_CD_DBG") ? atoi(getenv("CXN_CD_DBG")) : 0;
   const int grid = a.nitems < 256 ? a.nitems : 256;
   const dim3 blk(64 * NW);
   if (variant == 2 && NW == 4) {
@@ -439,20 +440,6 @@ int launch_cd(CdArgs a, int epi, int variant, float *db, hipStream_t s) {
     if (epi == 0) CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 0, true>), g1, blk, 0, s, a);
     else if (epi == 1) CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 1, 0, true>), g1, blk, 0, s, a);
     else CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 2, 0, true>), g1, blk, 0, s, a);
-  } else if (epi == 0 && dbg) {
-    switch (dbg) {
-      case 1: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 1>), dim3(grid), blk, 0, s, a); break;
-      case 2: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 2>), dim3(grid), blk, 0, s, a); break;
-      case 3: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 3>), dim3(grid), blk, 0, s, a); break;
-      case 11: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 11>), dim3(grid), blk, 0, s, a); break;
-      case 19: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 19>), dim3(grid), blk, 0, s, a); break;
-      case 64: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 64>), dim3(grid), blk, 0, s, a); break;
-      case 128: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 128>), dim3(grid), blk, 0, s, a); break;
-      case 256: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 256>), dim3(grid), blk, 0, s, a); break;
-      case 27: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 27>), dim3(grid), blk, 0, s, a); break;
-      case 35: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 35>), dim3(grid), blk, 0, s, a); break;
-      default: CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0, 59>), dim3(grid), blk, 0, s, a); break;
-    }
   } else if (epi == 0) {
     CXN_LAUNCH((conv_direct<H, W, KS, IPB, NF, NW, 0>), dim3(grid), blk, 0, s, a);
   } else if (epi == 1) {
