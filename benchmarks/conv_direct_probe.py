@@ -22,6 +22,10 @@ OPS = {
     "conv3": (13, 256, 384, 3, 1, 1),
     "conv4": (13, 384, 384, 3, 1, 2),
     "conv5": (13, 384, 256, 3, 1, 2),
+    # VGG-16 conv5_x (batch 64) and GoogLeNet inception 4c / 4e 3 x 3 (batch 128)
+    "vgg_c5": (14, 512, 512, 3, 1, 1),
+    "goog_4c": (14, 128, 256, 3, 1, 1),
+    "goog_4e": (14, 160, 320, 3, 1, 1),
 }
 
 

@@ -1047,7 +1047,8 @@ CXN_API long cxn_conv_direct(const void *x, int ldx, const void *w, const float 
                              long dbp_elems, float *db, int N, int H, int W, int Cg, int Cog, int groups, int KS,
                              int relu, int epi, int variant, void *stream) {
   const bool pair = KS == 5 && H == 27 && W == 27;  // paired-tap form (AlexNet conv2)
-  if (!pair && (KS != 3 || H != 13 || W != 13)) return -1;
+  const bool m14 = KS == 3 && H == 14 && W == 14;    // VGG-16 conv5, GoogLeNet's 14 x 14 3 x 3 convs
+  if (!pair && !m14 && (KS != 3 || H != 13 || W != 13)) return -1;
   if (ldx % 8 || ldy % 8 || groups < 1 || ldx < groups * Cg || ldy < groups * Cog) return -1;
   if (pair ? (Cg % 16 || (Cog % 64 && Cog % 48)) : (Cg % 32 || Cog % 64)) return -1;
   if (static_cast<long>(N) * H * W * (ldx > ldy ? ldx : ldy) >= (1L << 30)) return -1;
@@ -1073,7 +1074,10 @@ CXN_API long cxn_conv_direct(const void *x, int ldx, const void *w, const float 
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (variant < 0 || variant > 3) return -1;
   int rc;
-  if (variant == 3) {  // version 2: eight waves, paired taps, persistent double-buffered stages
+  if (m14) {
+    if (variant == 3) return -1;
+    rc = launch_cd<14, 14, 3, IPB, 4, 4>(a, epi, variant, db, s);
+  } else if (variant == 3) {  // version 2: eight waves, paired taps, persistent double-buffered stages
     if (pair) {
       rc = Cog % 128 == 0 ? launch_c2<27, 27, 5, 1, 14, 4, 2, 4>(a, epi, db, s)
          : Cog % 48 == 0  ? launch_c2<27, 27, 5, 1, 14, 8, 1, 3>(a, epi, db, s)

@@ -925,7 +925,7 @@ def _cd_serves(g: ConvGeom, *ts) -> bool:
         return False
     if g.KH == 5 and g.H == 27 and g.W == 27:  # paired-tap form (AlexNet conv2)
         return g.cg_in % 16 == 0 and (g.cg_out % 64 == 0 or g.cg_out % 48 == 0)
-    return g.KH == 3 and g.H == 13 and g.W == 13 and g.cg_in % 32 == 0 and g.cg_out % 64 == 0
+    return g.KH == 3 and g.H == g.W and g.H in (13, 14) and g.cg_in % 32 == 0 and g.cg_out % 64 == 0
 
 
 def conv_direct_forward(x, w, bias, y, g: ConvGeom, relu=False, variant=0) -> bool:

@@ -25,6 +25,8 @@ CASES = [
     (256, 96, 256, 2, 27, 5),  # AlexNet conv2: paired-tap form (forward 48 channels per group, data gradient 128 -> 48)
     (32, 96, 256, 2, 27, 5),
     (3, 64, 128, 1, 27, 5),
+    (64, 512, 512, 1, 14, 3),  # VGG-16 conv5_x (14 x 14)
+    (5, 128, 256, 1, 14, 3),   # GoogLeNet inception 4c's 3 x 3, odd N
 ]
 
 
@@ -48,9 +50,12 @@ def _nchw(t):
 
 
 def _served(variant, C, Cout, groups, H):
-    """Version 2 (variant 3) serves channel blocks of 128 / 96 (13 x 13) or 128 / 48 (27 x 27)."""
+    """Version 2 (variant 3) serves channel blocks of 128 / 96 (13 x 13) or 128 / 48 (27 x 27), not
+    14 x 14 maps."""
     if variant != 3:
         return True
+    if H == 14:
+        return False
     cog = Cout // groups
     return cog % 128 == 0 or cog % (96 if H == 13 else 48) == 0
 
