@@ -58,8 +58,7 @@ struct Wd {
   static constexpr int NQD = CO_U * NK / 4;              // dy DMA instructions per wave
   static constexpr int NQX = (CI_U * NX + 3) / 4;        // x DMA instructions per wave (last maybe idle)
   static constexpr int NACC = CO_U * CI_U * T;           // f32x4 accumulators per wave
-  static_assert(2 * BUF <= 160 * 1024, "LDS");
-  static_assert(4 * NACC * 64 * 16 / 2 <= 2 * BUF, "epilogue staging fits the stage buffers");
+  static_assert(2 * BUF <= 160 * 1024, "LDS");  // (the epilogue's chunked combine checks its own fit)
 };
 
 // (image, row, col) of a linear position in a stage's virtual slot space; -1 when it is padding
@@ -707,7 +706,7 @@ int launch_wt(const bf16_t *x, const bf16_t *dy, float *dw, float *ws, long ws_f
 
 }  // namespace
 
-// Served: stride 1, "same" padding (pad = (K - 1) / 2); K = 3 on 13 x 13 maps with input channels
+// Served: stride 1, "same" padding (pad = (K - 1) / 2); K = 3 on 13 x 13 or 14 x 14 maps with input channels
 // per group a multiple of 32, or K = 5 on 27 x 27 maps (no db) with a multiple of 16; output
 // channels per group a multiple of 64; x / dy pixel strides (C,
 // ldy) multiples of 8.  ws == nullptr: returns the workspace size in floats (0: not served).
@@ -734,6 +733,12 @@ CXN_API long cxn_conv_wgrad_direct(const void *x, const void *dy, float *dw, flo
   if (KH == 3 && H == 13 && W == 13) {
     if (!ws) return ws_wd<13, 13, 3, 2>(N, Cg, Cog, groups, splits);
     const int rc = launch_wd<13, 13, 3, 2>(xb, dyb, dw, db, ws, ws_floats, N, C, ldy, Cg, Cog, groups, splits, alpha, s);
+    if (rc != 0) return rc;
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+  }
+  if (KH == 3 && H == 14 && W == 14) {  // (VGG-16 conv5_x, GoogLeNet 4c / 4e): one image per stage
+    if (!ws) return ws_wd<14, 14, 3, 1>(N, Cg, Cog, groups, splits);
+    const int rc = launch_wd<14, 14, 3, 1>(xb, dyb, dw, db, ws, ws_floats, N, C, ldy, Cg, Cog, groups, splits, alpha, s);
     if (rc != 0) return rc;
     return hipGetLastError() == hipSuccess ? 0 : -3;
   }

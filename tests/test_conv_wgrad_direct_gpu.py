@@ -1,5 +1,6 @@
 """Direct small-map weight gradient (csrc/kernels/conv_wgrad_direct.hip) against fp32 torch:
-AlexNet's 13 x 13 layers (conv3 256->384, grouped conv4 / conv5), an odd image count (the last
+AlexNet's 13 x 13 layers (conv3 256->384, grouped conv4 / conv5), 14 x 14 (VGG-16 conv5_x,
+GoogLeNet 4c / 4e), an odd image count (the last
 stage holds one image: the missing one must read as zeros), forced split counts, a dy channel
 slice, accumulation into a non-zero dW (+=), and bitwise reproducibility."""
 import pytest
@@ -20,6 +21,9 @@ CASES = [
     (2, 32, 128, 1, 1),    # two co blocks, one split
     (32, 256, 384, 1, 0),  # the per-GPU batch of 8-GPU strong scaling
     (4, 64, 192, 1, 2),    # three co blocks, 2 ci blocks: bias K-steps k % 2 per ci block
+    (64, 512, 512, 1, 0, 14),  # VGG-16 conv5_x: 14 x 14, one image per stage
+    (5, 128, 256, 1, 0, 14),   # GoogLeNet inception 4c's 3 x 3, odd N
+    (3, 160, 320, 1, 2, 14),   # GoogLeNet 4e, forced splits
 ]
 
 
@@ -40,10 +44,11 @@ def _err(got, ref):
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
 def test_wgrad_direct(case):
-    N, C, Cout, groups, splits = case
-    g = ConvGeom(N, 13, 13, C, 13, 13, Cout, 3, 3, 1, 1, 1, groups)
-    x = _rnd((N, 13, 13, C), 1)
-    dy = _rnd((N, 13, 13, Cout), 2)
+    N, C, Cout, groups, splits = case[:5]
+    H = case[5] if len(case) > 5 else 13
+    g = ConvGeom(N, H, H, C, H, H, Cout, 3, 3, 1, 1, 1, groups)
+    x = _rnd((N, H, H, C), 1)
+    dy = _rnd((N, H, H, Cout), 2)
     dw = torch.full((Cout, 3, 3, C // groups), 0.5, device=DEV)
     db = torch.full((Cout,), 0.25, device=DEV)
     assert gemm.conv_wgrad_direct(x, dy, dw, g, splits=splits, db=db)
@@ -79,10 +84,10 @@ def test_wgrad_direct_dy_slice_and_accumulate():
 
 
 def test_wgrad_direct_declines_unserved_shapes():
-    x = _rnd((2, 14, 14, 64), 5)
-    dy = _rnd((2, 14, 14, 64), 6)
+    x = _rnd((2, 12, 12, 64), 5)  # (13 x 13 and 14 x 14 are served, 12 x 12 is not)
+    dy = _rnd((2, 12, 12, 64), 6)
     dw = torch.zeros((64, 3, 3, 64), device=DEV)
-    assert not gemm.conv_wgrad_direct(x, dy, dw, ConvGeom(2, 14, 14, 64, 14, 14, 64, 3, 3, 1, 1, 1, 1))
+    assert not gemm.conv_wgrad_direct(x, dy, dw, ConvGeom(2, 12, 12, 64, 12, 12, 64, 3, 3, 1, 1, 1, 1))
     x = _rnd((2, 13, 13, 48), 5)
     dy = _rnd((2, 13, 13, 64), 6)
     dw = torch.zeros((64, 3, 3, 48), device=DEV)
