@@ -18,7 +18,9 @@ from cxxnet_amd import ops  # noqa: E402
 from cxxnet_amd.ops.gemm import ConvGeom, conv_out_size  # noqa: E402
 
 N = 256
-CONVS = {"conv1": (4, 227, 96, 11, 4, 0, 1), "conv2": (96, 27, 256, 5, 1, 2, 2), "conv3": (256, 13, 384, 3, 1, 1, 1),
+# conv1 as the model runs it: 3 channels on rows padded to 228 pixels (NeuralNet._pad_input_channels)
+PHYS_W = {"conv1": 228}
+CONVS = {"conv1": (3, 227, 96, 11, 4, 0, 1), "conv2": (96, 27, 256, 5, 1, 2, 2), "conv3": (256, 13, 384, 3, 1, 1, 1),
          "conv4": (384, 13, 384, 3, 1, 1, 2), "conv5": (384, 13, 256, 3, 1, 1, 2)}
 FCS = {"fc6": (9216, 4096), "fc7": (4096, 4096), "fc8": (4096, 1000)}
 # VGG-16 (batch 64): the distinct 3x3 / pad 1 conv shapes (C, H, Cout) and its fc layers
@@ -59,9 +61,10 @@ def main():
     bf = torch.bfloat16
     dev = "cuda"
     for name, (C, H, Cout, K, s, p, g) in ({} if a.fc_only else CONVS).items():
-        Ho, Wo = conv_out_size(H, H, K, K, s, p, p)
-        geo = ConvGeom(N, H, H, C, Ho, Wo, Cout, K, K, s, p, p, g)
-        x = torch.randn(N, H, H, C, device=dev).to(bf)
+        Wp = PHYS_W.get(name, H) if a.model == "alexnet" else H
+        Ho, Wo = conv_out_size(H, Wp, K, K, s, p, p)
+        geo = ConvGeom(N, H, Wp, C, Ho, Wo, Cout, K, K, s, p, p, g)
+        x = torch.randn(N, H, Wp, C, device=dev).to(bf)
         w = (torch.randn(Cout, K, K, C // g, device=dev) * 0.05).to(bf)
         y = torch.randn(N, Ho, Wo, Cout, device=dev).to(bf)
         dw = torch.zeros(Cout, K, K, C // g, device=dev)
