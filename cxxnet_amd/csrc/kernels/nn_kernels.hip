@@ -137,11 +137,19 @@ __global__ void image_u8c3_nhwc4(const uint32_t *__restrict__ pix, const float *
 // image row and every 4-pixel group starts 8-byte aligned): one thread per 4 output pixels of a
 // padded row, three 8-byte stores; the pad columns (x >= w) get zeros.  mode 0/1.  The 12 source
 // bytes of a group start at any byte (rows of w*3 bytes): 4 aligned dword loads + alignbyte.
-__global__ void image_u8c3_nhwc3p(const uint32_t *__restrict__ pix, long ndw, const float *__restrict__ cm,
-                                  const float *__restrict__ mean, FastDiv fd_qpr, FastDiv fd_h, int w, int Wp,
-                                  int mode, float scale, uint32_t total, uint2 *__restrict__ y) {
-  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= total) return;
+// Consecutive groups are consecutive 24-byte pieces of y (Wp % 4 == 0), so a full wave's output is
+// one 1536-byte run: it goes through LDS and out as 16-byte stores (two per lane, the second on
+// half the lanes) instead of three 8-byte stores at a 24-byte lane stride.
+__global__ void __launch_bounds__(NT)
+image_u8c3_nhwc3p(const uint32_t *__restrict__ pix, long ndw, const float *__restrict__ cm,
+                  const float *__restrict__ mean, FastDiv fd_qpr, FastDiv fd_h, int w, int Wp,
+                  int mode, float scale, uint32_t total, uint2 *__restrict__ y) {
+  __shared__ uint2 stage[NT * 3];
+  const uint32_t q0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u);  // first group of this wave
+  const uint32_t q = q0 + (threadIdx.x & 63u);
+  if (q0 >= total) return;  // whole wave past the end
+  const bool full = q0 + 64 <= total;
+  if (!full && q >= total) return;  // (a partial wave stores directly below)
   const uint32_t row = fdiv(q, fd_qpr);
   const int x0 = static_cast<int>(q - row * fd_qpr.d) * 4;
   float ct = 1.f, il = 0.f;
@@ -172,13 +180,28 @@ __global__ void image_u8c3_nhwc3p(const uint32_t *__restrict__ pix, long ndw, co
       }
       out[3 * k + c] = v;
     }
-  {
+  if (!full) {
     uint2 *dst = y + (static_cast<long>(row) * Wp + x0) * 3 / 4;  // 4 pixels = 24 bytes = three uint2
 #pragma unroll
     for (int t = 0; t < 3; ++t)
       dst[t] = make_uint2(pack2(out[4 * t], out[4 * t + 1]),
                           pack2(out[4 * t + 2], out[4 * t + 3]));
+    return;
   }
+  const int lane = threadIdx.x & 63;
+  uint2 *const ws = stage + (threadIdx.x >> 6) * 192;  // this wave's 1536 bytes
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+    ws[3 * lane + t] = make_uint2(pack2(out[4 * t], out[4 * t + 1]), pack2(out[4 * t + 2], out[4 * t + 3]));
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // the wave's run starts at y + q0 * 3 uint2 (q0 % 64 == 0: 16-byte aligned when y is)
+  uint4 *const dst = reinterpret_cast<uint4 *>(y + static_cast<long>(q0) * 3);
+  const uint4 *const src = reinterpret_cast<const uint4 *>(ws);
+  dst[lane] = src[lane];
+  if (lane < 32) dst[64 + lane] = src[64 + lane];
 }
 
 // x: NHWC bf16 [N][H][Wp][Cp] -> y: NCHW fp32 [N][C][H][W]
@@ -2233,7 +2256,7 @@ CXN_API int cxn_image_u8_to_nhwc_bf16(const void *pix, const int *prm, const flo
   if (C > 8) return -2;
   const long npix = static_cast<long>(B) * h * w;
   const long nq = static_cast<long>(B) * h * (Wp / 4);
-  if (C == 3 && Cp == 3 && mode <= 1 && Wp % 4 == 0 && reinterpret_cast<uintptr_t>(y) % 8 == 0 &&
+  if (C == 3 && Cp == 3 && mode <= 1 && Wp % 4 == 0 && reinterpret_cast<uintptr_t>(y) % 16 == 0 &&
       reinterpret_cast<uintptr_t>(pix) % 4 == 0 && npix * 3 >= 16 && nq < (1L << 31)) {
     CXN_LAUNCH((image_u8c3_nhwc3p), cdiv(nq, NT), NT, 0, S_, (const uint32_t *)pix, (npix * 3 + 3) / 4, cm, mean,
                                                     make_fastdiv(static_cast<uint32_t>(Wp / 4)),
