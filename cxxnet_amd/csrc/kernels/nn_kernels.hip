@@ -1211,6 +1211,74 @@ __global__ void lrn_bwd_shfl(const bf16_t *x, const bf16_t *__restrict__ dy, bf1
   *reinterpret_cast<uint4 *>(dx + off) = pack8(out);
 }
 
+// lrn_bwd_shfl plus the bias gradient of the conv in front (GoogLeNet conv2 -> relu -> norm2: the
+// LRN's input gradient is that conv's output gradient): a grid-stride walk over the same
+// (4 waves x whole pixels) groups, each lane summing the bf16 values it stores; the block's lanes
+// meet in LDS in a fixed order and add one value per channel to db (not used in deterministic mode).
+template <int H>
+__global__ void __launch_bounds__(NT)
+lrn_bwd_db(const bf16_t *x, const bf16_t *__restrict__ dy, bf16_t *dx, long npix, int C, float salpha, float beta,
+           float knorm, int mask_relu, long ngroups, float *__restrict__ db, float *__restrict__ part) {
+  __shared__ float red[NT * 8];
+  LrnLane L;
+  L.tpp = C / 8;
+  const int ppw = 64 / L.tpp;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int pl = lane / L.tpp;
+  L.cv = lane - pl * L.tpp;
+  float bs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bs[e] = 0.f;
+  for (long gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {  // block-uniform: every lane shuffles
+    L.pix = (gi * (NT / 64) + wave) * ppw + pl;
+    L.active = pl < ppw && L.pix < npix;
+    const long off = L.pix * C + L.cv * 8;
+    float xv[8], gv[8], sq[8], sw[8];
+    if (L.active) {
+      unpack8(*reinterpret_cast<const uint4 *>(x + off), xv);
+      unpack8(*reinterpret_cast<const uint4 *>(dy + off), gv);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xv[e] = gv[e] = 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sq[e] = xv[e] * xv[e];
+    lrn_window_sum<H>(sq, L, sw);
+    float ng[8], t[8], ts[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float lg = lrn_log2(knorm + salpha * sw[e]);
+      const float pw = lrn_exp2(-beta * lg);
+      ng[e] = gv[e] * pw;
+      t[e] = gv[e] * xv[e] * pw * lrn_exp2(-lg);
+    }
+    lrn_window_sum<H>(t, L, ts);
+    if (!L.active) continue;
+    float out[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      out[e] = ng[e] - 2.f * beta * salpha * xv[e] * ts[e];
+      if (mask_relu && !(xv[e] > 0.f)) out[e] = 0.f;
+    }
+    const uint4 pk = pack8(out);
+    *reinterpret_cast<uint4 *>(dx + off) = pk;
+    unpack8(pk, out);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bs[e] += out[e];
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[threadIdx.x * 8 + e] = bs[e];
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += NT) {
+    const int cv = c >> 3, e = c & 7;
+    float s = 0.f;
+    for (int w = 0; w < NT / 64; ++w)
+      for (int p = 0; p < ppw; ++p) s += red[(w * 64 + p * L.tpp + cv) * 8 + e];
+    if (part != nullptr) part[static_cast<long>(blockIdx.x) * C + c] = s;  // summed by part_rows_colsum
+    else atomicAdd(db + c, s);
+  }
+}
+
 // ------------------------------------------------------------------ fused max-pool -> LRN
 // AlexNet's pool1 -> lrn1 and pool2 -> lrn2 (reference pooling_layer-inl.hpp:45-86 and
 // lrn_layer-inl.hpp:53-74) as one kernel per direction.  Lanes are laid out as the shuffle LRN
@@ -2558,6 +2626,34 @@ CXN_API int cxn_lrn_pool_bwd(const void *P, const void *dY, const void *arg, voi
   }
   if (hipGetLastError() != hipSuccess) return -3;
   return blocks;
+}
+// LRN backward plus db += the column sums of the stored dx (lrn_bwd_db): the shuffle form's
+// shapes (C % 8 == 0, C / 8 <= 64, local_size <= 9); -1 otherwise (nothing launched).  part (fp32,
+// part_floats >= 4096 * C): up to 4096 blocks store per-block sums there and part_rows_colsum
+// adds them up; without it 1024 blocks add theirs with one atomic each per channel.
+CXN_API int cxn_lrn_bwd_db(const void *x, const void *dy, void *dx, long npix, int C, int nsize, float alpha,
+                           float beta, float knorm, int mask_relu, float *db, float *part, long part_floats,
+                           void *stream) {
+  if (C % 8 != 0 || C / 8 > 64 || nsize / 2 > 4 || db == nullptr || npix <= 0) return -1;
+  const int tpp = C / 8, half = nsize / 2;
+  const long waves = (npix + 64 / tpp - 1) / (64 / tpp);
+  const long ngroups = (waves + NT / 64 - 1) / (NT / 64);
+  if (part != nullptr && part_floats < 4096L * C) part = nullptr;
+  const int blocks = static_cast<int>(std::min<long>(ngroups, part != nullptr ? 4096 : 1024));
+  const float sa = alpha / nsize;
+#define CXN_LDB(HV) CXN_LAUNCH((lrn_bwd_db<HV>), blocks, NT, 0, S_, (const bf16_t *)x, (const bf16_t *)dy, (bf16_t *)dx, \
+                               npix, C, sa, beta, knorm, mask_relu, ngroups, db, part)
+  switch (half) {
+    case 0: CXN_LDB(0); break;
+    case 1: CXN_LDB(1); break;
+    case 2: CXN_LDB(2); break;
+    case 3: CXN_LDB(3); break;
+    default: CXN_LDB(4); break;
+  }
+#undef CXN_LDB
+  if (part != nullptr)
+    CXN_LAUNCH((part_rows_colsum), dim3((C + 31) / 32, (blocks + 31) / 32), NT, 0, S_, part, blocks, C, db, 32);
+  RET;
 }
 CXN_API int cxn_lrn_bwd(const void *x, const void *dy, void *dx, long npix, int C, int nsize, float alpha, float beta,
                         float knorm, int mask_relu, void *stream) {

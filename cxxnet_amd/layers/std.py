@@ -740,6 +740,8 @@ class LRNLayer(Layer):
         self.beta = 0.0
         self.knorm = 1.0
         self.tmp = None
+        # the conv in front whose bias gradient this layer's backward sums (NeuralNet._fuse_lrn_bias)
+        self.bias_of = None
 
     def set_param(self, name, val):
         super().set_param(name, val)
@@ -768,6 +770,12 @@ class LRNLayer(Layer):
         if not prop_grad or self.fused_with_pool:
             return
         x = nodes_in[0].data
+        conv = self.bias_of
+        if conv is not None and conv.b is not None and self.ctx.is_gpu and not deterministic():
+            if ops.lrn_backward_bias(x, nodes_out[0].data, nodes_in[0].gdst, self.nsize, self.alpha, self.beta,
+                                     self.knorm, conv.b.g, mask_relu=self.grad_mask_relu):
+                conv.bias_done = True
+                return
         # in place: the LDS-staged kernel reads a pixel's whole channel row before writing it
         ops.lrn_backward(x, nodes_out[0].data, nodes_in[0].gdst, self.nsize, self.alpha, self.beta, self.knorm,
                          mask_relu=self.grad_mask_relu)

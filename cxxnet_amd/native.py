@@ -111,6 +111,7 @@ _SIGS = {
     "cxn_pool_bwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _L, _P],
     "cxn_lrn_fwd": [_P, _P, _L, _I, _I, _F, _F, _F, _P],
     "cxn_lrn_bwd": [_P, _P, _P, _L, _I, _I, _F, _F, _F, _I, _P],
+    "cxn_lrn_bwd_db": [_P, _P, _P, _L, _I, _I, _F, _F, _F, _I, _P, _P, _L, _P],
     "cxn_pool_lrn_fwd": [_P, _P, _P, _P] + [_I] * 8 + [_F, _F, _F, _P],
     "cxn_lrn_pool_bwd": [_P, _P, _P, _P] + [_I] * 8 + [_F, _F, _F, _P, _P, _L, _I, _P],
     "cxn_act_fwd": [_P, _P, _P, _L, _I, _F, _P],

@@ -199,6 +199,7 @@ class NeuralNet:
         self._fuse_pool_bias(producers, consumers)
         self._fuse_dgrad_bias(producers, consumers)
         self._fuse_pool_lrn(producers, consumers)
+        self._fuse_lrn_bias(producers, consumers)
         self._mark_nonneg()
 
     def _mark_nonneg(self):
@@ -297,6 +298,32 @@ class NeuralNet:
             if src is not node and len(consumers.get(id(node), [])) != 1:
                 continue
             conn.layer.bias_below = p.layer
+
+    def _fuse_lrn_bias(self, producers, consumers):
+        """Bias gradient of a conv whose output (through a fused relu) is read by an LRN alone
+        (GoogLeNet conv2 -> relu -> norm2): the LRN's input gradient is that conv's output
+        gradient, so the LRN backward sums it per channel as it stores it
+        (ops.lrn_backward_bias) instead of the column-sum pass re-reading it.  GPU only, not in
+        deterministic mode (the layer checks both).  CXXNET_LRN_BIAS=0 turns it off."""
+        if os.environ.get("CXXNET_LRN_BIAS", "1") == "0":
+            return
+        for conn in self.connections:
+            lay = conn.layer
+            if conn.type != K_LRN or conn.shared or len(conn.nodes_in) != 1 or getattr(lay, "fused_with_pool", False):
+                continue
+            node = conn.nodes_in[0]
+            src = self.aliases.get(id(node), node)
+            prod = producers.get(id(src), [])
+            if len(prod) != 1:
+                continue
+            p = self.connections[prod[0]]
+            if p.type != K_CONV or p.shared or len(consumers.get(id(src), [])) != 1:
+                continue
+            if getattr(p.layer, "sib", None) or getattr(p.layer, "sib_member", False):
+                continue  # a sibling group sums its biases together
+            if src is not node and len(consumers.get(id(node), [])) != 1:
+                continue
+            lay.bias_of = p.layer
 
     def _fuse_pool_bias(self, producers, consumers):
         """Bias gradient of a conv that feeds a max-pool, taken from the pool's OUTPUT gradient:

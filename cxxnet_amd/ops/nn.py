@@ -404,6 +404,24 @@ def lrn_forward(x, y, nsize, alpha, beta, knorm):
                                   float(knorm), _stream()), "lrn_fwd")
 
 
+def lrn_backward_bias(x, dy, dx, nsize, alpha, beta, knorm, dbias, mask_relu=False) -> bool:
+    """lrn_backward plus dbias (fp32 [C]) += the column sums of the stored dx: the bias gradient
+    of the conv in front, summed on the way out instead of by a later column-sum pass (per-block
+    sums in a scratch, added into dbias with atomics: not for deterministic mode).  False when the kernel does not
+    serve the shape (nothing was done)."""
+    if not _native_t(x):
+        return False
+    N, H, W, C = x.shape
+    part = _workspace(4096 * C, x.device)  # per-block sums, added up by a second launch
+    rc = _k().cxn_lrn_bwd_db(x.data_ptr(), dy.data_ptr(), dx.data_ptr(), N * H * W, C, nsize, float(alpha),
+                             float(beta), float(knorm), int(bool(mask_relu)), dbias.data_ptr(), part.data_ptr(),
+                             part.numel(), _stream())
+    if rc == -1:
+        return False
+    native.check(rc, "lrn_bwd_db")
+    return True
+
+
 def lrn_backward(x, dy, dx, nsize, alpha, beta, knorm, mask_relu=False):
     """dx = d LRN / dx (dx may alias x; it must not alias dy).  mask_relu: x is relu(z) of a
     fused producer, so dx is also multiplied by relu'(z) = (x > 0)."""

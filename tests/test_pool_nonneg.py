@@ -101,3 +101,15 @@ def test_integer_key_pool_matches_float_compare(K, S, P, H):
         out[nn] = (y.float(), st.clone())
     assert torch.equal(out[False][0], out[True][0])
     assert torch.equal(out[False][1], out[True][1])
+
+
+def test_lrn_bias_fusion_targets(monkeypatch):
+    """NeuralNet._fuse_lrn_bias: GoogLeNet's norm2 sums conv2's bias gradient (conv2 -> relu ->
+    norm2, the relu fused); AlexNet's LRNs follow max-pools and take no conv."""
+    monkeypatch.setenv("CXXNET_FUSE", "2")  # the GPU's graph fusion on a CPU net
+    goog = _net("inception_v1", 2)
+    lrns = [c.layer for c in goog.connections if type(c.layer).__name__ == "LRNLayer"]
+    tied = [l for l in lrns if l.bias_of is not None]
+    assert len(tied) == 1 and tied[0].bias_of.b is not None and tied[0].bias_of.geo.KH == 3
+    alex = _net("alexnet", 2)
+    assert all(c.layer.bias_of is None for c in alex.connections if type(c.layer).__name__ == "LRNLayer")
