@@ -278,16 +278,24 @@ class NeuralNet:
         """Bias gradient of a conv whose output (through a fused relu) is read by one other conv
         alone: that conv's data-gradient GEMM writes exactly this gradient, and its epilogue sums
         it per channel on the way out (ops.conv_backward_data(dbias=...)), so the gradient is not
-        re-read by the column-sum pass.  Off by default (CXXNET_DGRAD_BIAS=1 turns it on): the
-        epilogue sums, the per-wave partial rows and one reduce launch per fused conv cost about
-        what the saved read does -- interleaved A/B VGG-16 -0.2 %, AlexNet +0.6 %, GoogLeNet +2.9 %
-        (profiles/r2_ab_dgrad_bias.jsonl)."""
-        if os.environ.get("CXXNET_DGRAD_BIAS", "0") != "1":
+        re-read by the column-sum pass.  The epilogue sums, the per-wave partial rows and one
+        reduce launch per fused conv cost about what the saved read does on small layers (every
+        layer fused: AlexNet +2 %, VGG-16 +1.4 %, GoogLeNet +17 %,
+        profiles/r6_ab_dgrad_bias_negative.jsonl), so by default ("auto") only layers whose
+        gradient is at least CXXNET_DGRAD_BIAS_MIN_MB (150) MB are fused: VGG-16's conv1_1 and
+        conv2_1 at batch 64, -0.5 % (profiles/r6_ab_dgrad_bias_min_mb.jsonl).  CXXNET_DGRAD_BIAS=1
+        fuses every eligible layer, 0 none."""
+        mode = os.environ.get("CXXNET_DGRAD_BIAS", "auto")
+        if mode == "0":
             return
+        min_mb = float(os.environ.get("CXXNET_DGRAD_BIAS_MIN_MB", "150" if mode == "auto" else "0"))
         for conn in self.connections:
             if conn.type != K_CONV or conn.shared or len(conn.nodes_in) != 1:
                 continue
             node = conn.nodes_in[0]
+            b, c, h, w = node.shape
+            if b * c * h * w * 2 < min_mb * 1e6:
+                continue
             src = self.aliases.get(id(node), node)
             prod = producers.get(id(src), [])
             if len(prod) != 1:

@@ -882,29 +882,31 @@ def test_conv_dgrad_epilogue_bias_sum(geo_args, mask):
         assert torch.equal(db, torch.full_like(db, 0.25))
 
 
-def test_dgrad_fused_bias_grads_match_unfused(monkeypatch):
+@pytest.mark.parametrize("model,batch,nfused", [("alexnet", 16, 2), ("vgg16", 2, 8)])
+def test_dgrad_fused_bias_grads_match_unfused(monkeypatch, model, batch, nfused):
     """conv -> relu -> conv: the lower conv's bias gradient from the upper conv's data-gradient
-    epilogue (NeuralNet._fuse_dgrad_bias) equals the column-sum pass, on AlexNet (conv3, conv4)."""
+    epilogue (NeuralNet._fuse_dgrad_bias, every eligible layer) equals the column-sum pass, on
+    AlexNet (conv3, conv4: the direct kernels) and VGG-16 (the halo and LDS-DMA epilogues)."""
     from cxxnet_amd.io.data import DataBatch
     from cxxnet_amd.models import load_conf
     from cxxnet_amd.nnet import NetTrainer
 
     grads = []
     for fused in ("1", "0"):
-        monkeypatch.setenv("CXXNET_DGRAD_BIAS", fused)  # the fusion is opt-in
-        pairs = load_conf("alexnet", [("batch_size", "16"), ("dev", "gpu"), ("eval_train", "0"), ("silent", "1"),
-                                      ("update_period", "2")])
+        monkeypatch.setenv("CXXNET_DGRAD_BIAS", fused)
+        pairs = load_conf(model, [("batch_size", str(batch)), ("dev", "gpu"), ("eval_train", "0"), ("silent", "1"),
+                                  ("update_period", "2")])
         tr = NetTrainer()
         for k, v in pairs:
             if not k.startswith("metric"):
                 tr.set_param(k, v)
         tr.init_model()
         below = [c.layer.bias_below for c in tr.net.connections if getattr(c.layer, "bias_below", None) is not None]
-        assert len(below) == (2 if fused == "1" else 0)
+        assert len(below) == (nfused if fused == "1" else 0)
         c, h, w = tr.net_cfg.input_shape
         g = torch.Generator().manual_seed(6)
-        x = torch.randn(16, c, h, w, generator=g).to(DEV)
-        y = torch.randint(0, 1000, (16, 1), generator=g).float().to(DEV)
+        x = torch.randn(batch, c, h, w, generator=g).to(DEV)
+        y = torch.randint(0, 1000, (batch, 1), generator=g).float().to(DEV)
         tr.update(DataBatch(x, y))
         torch.cuda.synchronize()
         grads.append([cn.layer.b.g.clone() for cn in tr.net.connections

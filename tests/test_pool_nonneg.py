@@ -113,3 +113,15 @@ def test_lrn_bias_fusion_targets(monkeypatch):
     assert len(tied) == 1 and tied[0].bias_of.b is not None and tied[0].bias_of.geo.KH == 3
     alex = _net("alexnet", 2)
     assert all(c.layer.bias_of is None for c in alex.connections if type(c.layer).__name__ == "LRNLayer")
+
+
+@pytest.mark.parametrize("model,batch,expect", [("vgg16", 64, 2), ("alexnet", 256, 0), ("inception_v1", 128, 0)])
+def test_dgrad_bias_auto_takes_only_large_layers(monkeypatch, model, batch, expect):
+    """NeuralNet._fuse_dgrad_bias in its default ("auto") mode: only a conv whose output
+    gradient is >= 150 MB has its bias summed by the upper conv's data-gradient epilogue --
+    VGG-16's conv1_1 and conv2_1 at batch 64, nothing in AlexNet or GoogLeNet."""
+    monkeypatch.setenv("CXXNET_FUSE", "2")
+    monkeypatch.delenv("CXXNET_DGRAD_BIAS", raising=False)
+    net = _net(model, batch)
+    below = [c.layer.bias_below for c in net.connections if getattr(c.layer, "bias_below", None) is not None]
+    assert len(below) == expect
