@@ -303,6 +303,8 @@ class NeuralNet:
             p = self.connections[prod[0]]
             if p.type != K_CONV or p.shared or p is conn or len(consumers.get(id(src), [])) != 1:
                 continue
+            if getattr(p.layer, "sib", None) or getattr(p.layer, "sib_member", False):
+                continue  # a sibling group sums its biases together (it would count twice)
             if src is not node and len(consumers.get(id(node), [])) != 1:
                 continue
             conn.layer.bias_below = p.layer
@@ -355,6 +357,8 @@ class NeuralNet:
             p = self.connections[prod[0]]
             if p.type != K_CONV or p.shared or len(consumers.get(id(src), [])) != 1:
                 continue
+            if getattr(p.layer, "sib", None) or getattr(p.layer, "sib_member", False):
+                continue  # a sibling group sums its biases together
             if src is not node and len(consumers.get(id(node), [])) != 1:
                 continue
             lay.bias_of = p.layer

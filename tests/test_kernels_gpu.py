@@ -916,6 +916,43 @@ def test_dgrad_fused_bias_grads_match_unfused(monkeypatch, model, batch, nfused)
         assert relerr(a, b) < 1e-2, relerr(a, b)
 
 
+def test_dgrad_bias_auto_with_siblings_matches_unfused(monkeypatch):
+    """GoogLeNet with the sibling 1x1 groups on and the dgrad-bias fusion in "auto" mode at a 0 MB
+    threshold (every eligible conv): no sibling member becomes a bias target (the group sums its
+    biases over its shared buffer -- a member's bias would count twice), and every conv bias
+    gradient matches the run without the fusion."""
+    from cxxnet_amd.io.data import DataBatch
+    from cxxnet_amd.models import load_conf
+    from cxxnet_amd.nnet import NetTrainer
+
+    grads = []
+    for mode in ("auto", "0"):
+        monkeypatch.setenv("CXXNET_DGRAD_BIAS", mode)
+        monkeypatch.setenv("CXXNET_DGRAD_BIAS_MIN_MB", "0")
+        pairs = load_conf("inception_v1", [("batch_size", "4"), ("dev", "gpu"), ("eval_train", "0"),
+                                           ("silent", "1"), ("update_period", "2")])
+        tr = NetTrainer()
+        for k, v in pairs:
+            if not k.startswith("metric"):
+                tr.set_param(k, v)
+        tr.init_model()
+        assert tr.net.sib_groups  # the sibling groups stay on
+        below = [c.layer.bias_below for c in tr.net.connections if getattr(c.layer, "bias_below", None) is not None]
+        assert not any(b.sib is not None or b.sib_member for b in below)
+        if mode == "auto":
+            assert below  # conv2_reduce -> conv2 at least
+        c, h, w = tr.net_cfg.input_shape
+        g = torch.Generator().manual_seed(8)
+        x = torch.randn(4, c, h, w, generator=g).to(DEV)
+        y = torch.randint(0, 1000, (4, 1), generator=g).float().to(DEV)
+        tr.update(DataBatch(x, y))
+        torch.cuda.synchronize()
+        grads.append([(i, s.g.clone()) for i, s in tr.net.arena.specs if s.tag == "bias"])
+    for (i, a), (j, b) in zip(*grads):
+        assert i == j
+        assert relerr(a, b) < 1e-2, (i, relerr(a, b))
+
+
 FEWC_CASES = [
     # N, H, W, Cout, K, stride, pad, relu, bias, ldc_extra
     (2, 224, 224, 64, 3, 1, 1, True, True, 0),    # VGG conv1_1

@@ -125,3 +125,16 @@ def test_dgrad_bias_auto_takes_only_large_layers(monkeypatch, model, batch, expe
     net = _net(model, batch)
     below = [c.layer.bias_below for c in net.connections if getattr(c.layer, "bias_below", None) is not None]
     assert len(below) == expect
+
+
+def test_bias_fusions_skip_sibling_groups(monkeypatch):
+    """A sibling group (GoogLeNet's 1x1 convs on one input) sums its biases over its shared
+    buffer, so no other layer may take a member's bias: with every dgrad-bias fusion forced on,
+    no pool / LRN / conv names a sibling member or lead as its bias target."""
+    monkeypatch.setenv("CXXNET_FUSE", "2")
+    monkeypatch.setenv("CXXNET_DGRAD_BIAS", "1")
+    net = _net("inception_v1", 2)
+    targets = [t for c in net.connections for t in (getattr(c.layer, "bias_below", None),
+                                                     getattr(c.layer, "bias_of", None)) if t is not None]
+    assert targets
+    assert not any(getattr(t, "sib", None) or getattr(t, "sib_member", False) for t in targets)
